@@ -1,0 +1,9 @@
+"""nexus_supervisor_amd — a job supervisor for Kubernetes clusters of AMD MI355X GPUs.
+
+Same capabilities, config surface and ``nexus.checkpoints`` schema as
+SneaksAndData/nexus-supervisor (reference snapshot at ``/root/reference``),
+re-designed: asyncio control plane, native C++ CQL wire codec, amd-smi GPU
+attribution (HBM-OOM vs host-OOM on 288 GB HBM3E), RCCL/xGMI rank topology in
+the trace row, keyed work pipeline, leader election and pprof-format profiling.
+"""
+__version__ = "0.1.0"

@@ -1,0 +1,357 @@
+"""Failure-reason classifier: K8s Events / Pod status / Job status → decisions.
+
+Three rule sets:
+
+* **R-EVT** — the reference event table, byte-exact
+  (``/root/reference/services/supervisor.go:137-259``; :mod:`.reference_rules`).
+* **R-POD / R-JOB** — status-based rules the reference lacks (it registers no
+  Pod/Job handlers, ``supervisor.go:124-128``): OOMKilled, HBM-OOM, Evicted,
+  ImagePullBackOff/ErrImagePull, CreateContainerConfigError, CrashLoopBackOff,
+  Unschedulable, and Job ``Failed`` conditions (so a lost Event — K8s events
+  are best-effort — no longer loses the decision).
+* **R-GPU** — every failing decision is enriched with the rank topology
+  (:mod:`..gpu.topology`), node-agent GPU evidence (pod annotation) and the
+  HBM-vs-host OOM verdict (:mod:`..gpu.oom`).
+
+Everything here is pure and synchronous: it runs on the informer dispatch path
+and never does I/O.
+"""
+from __future__ import annotations
+
+import json
+import time
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+from ..config.schema import GpuConfig, LabelConfig, RulesConfig
+from ..gpu import oom as oom_mod
+from ..gpu.topology import merge_process_ranks, topology_from_pod
+from ..models import kube
+from ..models.decisions import DecisionAction as A
+from ..models.decisions import FailureClass as F
+from ..models.decisions import RunStatusAnalysisResult
+from . import reference_rules as R
+
+IGNORED = "ignored"        # not a Nexus run object / uninteresting kind
+STALE = "stale"            # involved object not in cache (yet)
+NOOP = "noop"              # Nexus event with a reason we do not act on
+DECIDED = "decided"
+EVIDENCE = "evidence"      # recorded for later enrichment, no decision
+
+MSG_HOST_OOM = "Algorithm container was OOMKilled: host memory limit exceeded."
+MSG_HBM_OOM = "Algorithm ran out of GPU memory (HBM) on an AMD Instinct GPU."
+MSG_EVICTED = "Algorithm pod was evicted from its node."
+MSG_IMAGE_PULL = "Unable to pull the algorithm container image."
+MSG_CONFIG = "Unable to create the algorithm container - please review configuration and try again."
+MSG_CRASH_LOOP = "Algorithm container is crash-looping."
+MSG_UNSCHEDULABLE = "Algorithm pod could not be scheduled on the target cluster."
+MSG_GPU_FAULT = "Algorithm hit a GPU fault."
+
+IMAGE_PULL_WAITING = ("ErrImagePull", "ImagePullBackOff", "InvalidImageName", "ErrImageNeverPull")
+CONFIG_WAITING = ("CreateContainerConfigError", "CreateContainerError", "RunContainerError")
+EVICTION_EVENT_REASONS = ("Evicted", "Preempted", "Preempting", "TaintManagerEviction")
+JOB_FAILED_CONDITION_REASONS = ("DeadlineExceeded", "BackoffLimitExceeded", "PodFailurePolicy",
+                                "MaxFailedIndexesExceeded", "FailedIndexes")
+
+
+class ObjectLookup:
+    """What the classifier needs from the informer caches (namespace already bound)."""
+
+    def get(self, kind: str, name: str) -> Optional[Dict[str, Any]]:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def pods_of_job(self, job_name: str) -> List[Dict[str, Any]]:  # pragma: no cover - interface
+        return []
+
+
+@dataclass
+class EvidenceBook:
+    """Bounded per-run memory of non-decisive observations (evictions, exit codes,
+    unschedulable periods) used to enrich the eventual terminal decision."""
+
+    capacity: int = 50_000
+    _data: "OrderedDict[Tuple[str, str], List[Dict[str, Any]]]" = field(default_factory=OrderedDict)
+
+    def add(self, key: Tuple[str, str], item: Dict[str, Any]) -> None:
+        lst = self._data.get(key)
+        if lst is None:
+            lst = self._data[key] = []
+            if len(self._data) > self.capacity:
+                self._data.popitem(last=False)
+        else:
+            self._data.move_to_end(key)
+        if item not in lst:
+            lst.append(item)
+            del lst[:-16]
+
+    def get(self, key) -> List[Dict[str, Any]]:
+        return list(self._data.get(key, ()))
+
+    def pop(self, key) -> List[Dict[str, Any]]:
+        return self._data.pop(key, [])
+
+    def __len__(self):
+        return len(self._data)
+
+
+class Classifier:
+    def __init__(self, labels: Optional[LabelConfig] = None, rules: Optional[RulesConfig] = None,
+                 gpu: Optional[GpuConfig] = None, clock: Callable[[], float] = time.monotonic):
+        self.labels = labels or LabelConfig()
+        self.rules = rules or RulesConfig()
+        self.gpu = gpu or GpuConfig()
+        self.evidence = EvidenceBook()
+        self.clock = clock
+
+    # ------------------------------------------------------------ helpers
+    def is_nexus(self, obj: Optional[Dict[str, Any]]) -> bool:
+        """nexus-core ``resolvers.IsNexusRunEvent`` label check."""
+        if not obj:
+            return False
+        return kube.labels_of(obj).get(self.labels.nexus_component_label) == self.labels.algorithm_run_value
+
+    def _algorithm(self, obj) -> str:
+        return kube.labels_of(obj).get(self.labels.job_template_name_key, "")
+
+    def _pod_request_id(self, pod) -> str:
+        return kube.labels_of(pod).get(self.labels.job_name_label, "")
+
+    def _result(self, action, message, trace, involved, request_id, algorithm, reason, fclass, source, event_uid="") -> RunStatusAnalysisResult:
+        r = RunStatusAnalysisResult(
+            action=action, run_status_message=message, run_status_trace=trace or "",
+            object_uid=(involved or {}).get("uid", "") or "", object_kind=(involved or {}).get("kind", "") or "",
+            request_id=request_id, algorithm=algorithm, reason=reason, failure_class=fclass, event_uid=event_uid,
+        )
+        r.evidence["source"] = source
+        return r
+
+    # ------------------------------------------------------------ R-EVT
+    def classify_event(self, event: Dict[str, Any], lookup: ObjectLookup) -> Tuple[str, List[RunStatusAnalysisResult]]:
+        inv = event.get("involvedObject") or {}
+        kind = inv.get("kind", "")
+        if kind not in ("Job", "Pod"):
+            return IGNORED, []
+        obj = lookup.get(kind, inv.get("name", ""))
+        if obj is None:
+            return STALE, []
+        if not self.is_nexus(obj):
+            return IGNORED, []
+        reason = event.get("reason", "")
+        message = event.get("message", "") or ""
+        ev_uid = kube.uid_of(event)
+        if kind == "Job":
+            rule = R.JOB_EVENT_RULES.get(reason)
+            if rule is None:
+                return NOOP, []
+            action, msg, fclass = rule
+            res = self._result(action, msg, message, inv, inv.get("name", ""), self._algorithm(obj), reason, fclass, "event", ev_uid)
+            self._enrich(res, pods=lookup.pods_of_job(inv.get("name", "")), texts=[message])
+            return DECIDED, [res]
+        # Pod
+        request_id = self._pod_request_id(obj)
+        algorithm = self._algorithm(obj)
+        rule = R.POD_EVENT_RULES.get(reason)
+        if rule is not None:
+            action, fclass = rule
+            if reason == "BackOff" and "pulling image" in message.lower():
+                fclass = F.IMAGE_PULL
+            elif reason == "BackOff" and "restarting failed container" in message.lower():
+                fclass = F.CRASH_LOOP
+            elif reason == "Failed" and ("image" in message.lower()):
+                fclass = F.IMAGE_PULL
+            res = self._result(action, reason, message, inv, request_id, algorithm, reason, fclass, "event", ev_uid)
+            if action != A.TO_RUNNING:
+                self._enrich(res, pods=[obj], texts=[message])
+            return DECIDED, [res]
+        if reason in EVICTION_EVENT_REASONS:
+            item = {"kind": "evicted", "reason": reason, "message": message, "pod": kube.name_of(obj)}
+            if self.rules.evicted_policy == "fail":
+                res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_EVICTED, message, inv, request_id, algorithm, reason, F.EVICTED, "event", ev_uid)
+                self._enrich(res, pods=[obj], texts=[message])
+                return DECIDED, [res]
+            self.evidence.add((algorithm, request_id), item)
+            return EVIDENCE, []
+        if reason == "FailedScheduling":
+            self.evidence.add((algorithm, request_id), {"kind": "unschedulable", "message": message})
+            return EVIDENCE, []
+        return NOOP, []
+
+    # ------------------------------------------------------------ R-POD
+    def classify_pod(self, pod: Dict[str, Any], old: Optional[Dict[str, Any]] = None) -> List[RunStatusAnalysisResult]:
+        if not self.rules.pod_status_rules or not self.is_nexus(pod):
+            return []
+        if old is not None and kube.resource_version(old) == kube.resource_version(pod) and kube.resource_version(pod):
+            return []  # resync replay of an unchanged object
+        request_id = self._pod_request_id(pod)
+        if not request_id:
+            return []
+        algorithm = self._algorithm(pod)
+        key = (algorithm, request_id)
+        inv = {"kind": "Pod", "name": kube.name_of(pod), "uid": kube.uid_of(pod)}
+        status = pod.get("status") or {}
+        current_terms = [t for t in kube.terminated_states(pod) if t["which"] == "state"]
+        # 1. OOM (host cgroup OOMKilled or HIP OOM signature on a terminated container)
+        failed_terms = [t for t in current_terms if t.get("exitCode", 0) != 0 or t.get("reason") == "OOMKilled"]
+        if failed_terms:
+            verdict = self._oom(pod, [t.get("message", "") for t in failed_terms], failed_terms)
+            if verdict.kind:
+                hbm = verdict.kind == "hbm"
+                t0 = failed_terms[0]
+                res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_HBM_OOM if hbm else MSG_HOST_OOM,
+                                   t0.get("message") or t0.get("reason") or "", inv, request_id, algorithm,
+                                   t0.get("reason") or "Error", F.HBM_OOM if hbm else F.HOST_OOM, "pod-status")
+                self._enrich(res, pods=[pod], verdict=verdict)
+                return [res]
+            for t in failed_terms:
+                self.evidence.add(key, {"kind": "exit", "container": t.get("container"), "exitCode": t.get("exitCode"),
+                                        "reason": t.get("reason"), "message": (t.get("message") or "")[-512:]})
+        # 2. eviction
+        if status.get("reason") == "Evicted" or self._disruption(pod):
+            msg = status.get("message", "") or (self._disruption(pod) or {}).get("message", "")
+            if self.rules.evicted_policy == "fail":
+                res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_EVICTED, msg, inv, request_id, algorithm,
+                                   status.get("reason") or "DisruptionTarget", F.EVICTED, "pod-status")
+                self._enrich(res, pods=[pod], texts=[msg])
+                return [res]
+            self.evidence.add(key, {"kind": "evicted", "message": msg, "pod": kube.name_of(pod)})
+            return []
+        # 3./4./5. waiting states
+        for w in kube.waiting_states(pod):
+            wr = w.get("reason", "")
+            if wr in IMAGE_PULL_WAITING:
+                res = self._result(A.TO_FAIL_STUCK_IN_PENDING, MSG_IMAGE_PULL, w.get("message", ""), inv, request_id, algorithm, wr, F.IMAGE_PULL, "pod-status")
+                self._enrich(res, pods=[pod])
+                return [res]
+            if wr in CONFIG_WAITING:
+                res = self._result(A.TO_FAIL_STUCK_IN_PENDING, MSG_CONFIG, w.get("message", ""), inv, request_id, algorithm, wr, F.CONFIG, "pod-status")
+                self._enrich(res, pods=[pod])
+                return [res]
+            if wr == "CrashLoopBackOff":
+                texts = [t.get("message", "") for t in kube.terminated_states(pod)]
+                res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_CRASH_LOOP, w.get("message", ""), inv, request_id, algorithm, wr, F.CRASH_LOOP, "pod-status")
+                self._enrich(res, pods=[pod], texts=texts)
+                return [res]
+        # 6. unschedulable
+        sched = kube.condition(pod, "PodScheduled")
+        if sched and sched.get("status") == "False" and sched.get("reason") == "Unschedulable":
+            self.evidence.add(key, {"kind": "unschedulable", "message": sched.get("message", "")})
+            if self.rules.unschedulable_timeout > 0 and self._pending_for(pod) >= self.rules.unschedulable_timeout:
+                res = self._result(A.TO_FAIL_STUCK_IN_PENDING, MSG_UNSCHEDULABLE, sched.get("message", ""), inv, request_id, algorithm,
+                                   "Unschedulable", F.SCHEDULING, "pod-status")
+                self._enrich(res, pods=[pod])
+                return [res]
+            return []
+        # 7. running (backup for a lost "Started" event)
+        if status.get("phase") == "Running" and any(
+            (cs.get("state") or {}).get("running") for cs in (status.get("containerStatuses") or [])
+        ):
+            res = self._result(A.TO_RUNNING, "Started", "", inv, request_id, algorithm, "Running", F.NONE, "pod-status")
+            return [res]
+        return []
+
+    def _disruption(self, pod) -> Optional[Dict[str, Any]]:
+        c = kube.condition(pod, "DisruptionTarget")
+        if c and c.get("status") == "True":
+            return c
+        return None
+
+    def _pending_for(self, pod) -> float:
+        import datetime as dt
+        ts = kube.meta(pod).get("creationTimestamp")
+        if not ts:
+            return 0.0
+        try:
+            t = dt.datetime.fromisoformat(ts.replace("Z", "+00:00"))
+        except ValueError:
+            return 0.0
+        return (dt.datetime.now(dt.timezone.utc) - t).total_seconds()
+
+    # ------------------------------------------------------------ R-JOB
+    def classify_job(self, job: Dict[str, Any], old: Optional[Dict[str, Any]], lookup: ObjectLookup) -> List[RunStatusAnalysisResult]:
+        if not self.rules.pod_status_rules or not self.is_nexus(job):
+            return []
+        if old is not None and kube.resource_version(old) == kube.resource_version(job) and kube.resource_version(job):
+            return []
+        cond = kube.condition(job, "Failed")
+        if not cond or cond.get("status") != "True":
+            return []
+        if old is not None:
+            oc = kube.condition(old, "Failed")
+            if oc and oc.get("status") == "True":
+                return []  # already failed before this update
+        reason = cond.get("reason", "")
+        rule = R.JOB_EVENT_RULES.get(reason)
+        if rule is None:
+            if reason not in JOB_FAILED_CONDITION_REASONS:
+                return []
+            rule = (A.TO_FAIL_FATAL_ERROR, R.MSG_FATAL, F.FATAL)
+        action, msg, fclass = rule
+        name = kube.name_of(job)
+        inv = {"kind": "Job", "name": name, "uid": kube.uid_of(job)}
+        res = self._result(action, msg, cond.get("message", ""), inv, name, self._algorithm(job), reason, fclass, "job-status")
+        self._enrich(res, pods=lookup.pods_of_job(name), texts=[cond.get("message", "")])
+        return [res]
+
+    # ------------------------------------------------------------ R-GPU enrichment
+    def _gpu_evidence(self, pod) -> Optional[Dict[str, Any]]:
+        raw = kube.annotations_of(pod).get(self.gpu.evidence_annotation)
+        if not raw:
+            return None
+        try:
+            ev = json.loads(raw)
+        except (TypeError, ValueError):
+            return None
+        return ev if isinstance(ev, dict) else None
+
+    def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
+        topo = topology_from_pod(pod, self.gpu.gpu_resource_name)
+        return oom_mod.analyze(texts, terms, self._gpu_evidence(pod), topo.get("expected_gpu"),
+                               self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+
+    def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
+        if not self.gpu.attribution_enabled:
+            return
+        pods = [p for p in pods if p]
+        key = res.key
+        if pods:
+            pod = pods[-1]
+            topo = topology_from_pod(pod, self.gpu.gpu_resource_name)
+            gev = self._gpu_evidence(pod)
+            topo = merge_process_ranks(topo, gev)
+            if topo:
+                res.evidence["topology"] = topo
+            if gev:
+                res.evidence["gpu"] = gev
+            if verdict is None and res.action != A.TO_RUNNING:
+                terms = [t for p in pods for t in kube.terminated_states(p)]
+                verdict = oom_mod.analyze(list(texts) + [t.get("message", "") for t in terms], terms, gev,
+                                          topo.get("expected_gpu"), self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+        elif verdict is None and res.action != A.TO_RUNNING and any(texts):
+            verdict = oom_mod.analyze(texts, (), None, None, self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+        if verdict is not None and verdict.kind:
+            res.evidence["oom"] = verdict.as_dict()
+            if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.CRASH_LOOP):
+                res.failure_class = F.HBM_OOM if verdict.kind == "hbm" else F.HOST_OOM
+        if res.action != A.TO_RUNNING:
+            prior = self.evidence.get(key)
+            if prior:
+                res.evidence["history"] = prior
+                if res.failure_class == F.BACKOFF_LIMIT and any(p.get("kind") == "evicted" for p in prior):
+                    res.failure_class = F.EVICTED
+
+
+def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
+    """Trace column (``algorithm_failure_details``) for a decision.
+
+    ``raw`` — the event/status message, as the reference (``supervisor.go:299``);
+    ``json`` — message + reason + failure class + evidence; ``auto`` — json only
+    when there is evidence beyond the message.
+    """
+    extra = {k: v for k, v in res.evidence.items() if k != "source"}
+    if fmt == "raw" or (fmt == "auto" and not extra and res.failure_class in (F.NONE, F.SCHEDULING, F.DEADLINE, F.FATAL, F.BACKOFF_LIMIT)):
+        return res.run_status_trace
+    doc = {"message": res.run_status_trace, "reason": res.reason, "class": res.failure_class,
+           "source": res.evidence.get("source", "")}
+    doc.update(extra)
+    return json.dumps(doc, sort_keys=True, separators=(",", ":"), default=str)

@@ -1,0 +1,206 @@
+"""Typed configuration schema.
+
+Reference keys are kept byte-identical (``/root/reference/app/app_config.go:8-25``;
+``/root/reference/appconfig.local.yaml:1-19``).  Defaults equal the Helm chart
+defaults (``/root/reference/.helm/values.yaml:119-165``) instead of Go's zero
+values, so an empty ``workers: ""`` no longer silently means zero workers
+(SURVEY §5.6).  Everything under a key the reference does not have is an
+extension of this build and documented in ``docs/CONFIG.md``.
+
+Each dataclass field carries ``metadata={"key": "<kebab-key>"}``; durations are
+float seconds tagged ``"kind": "duration"``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List
+
+
+def _k(key: str, kind: str | None = None, **extra):
+    md = {"key": key}
+    if kind:
+        md["kind"] = kind
+    md.update(extra)
+    return md
+
+
+CQL_STORE_ASTRA = "astra"
+CQL_STORE_SCYLLA = "scylla"
+CQL_STORE_MEMORY = "memory"  # extension: in-process store for tests / dry runs
+CQL_STORE_TYPES = (CQL_STORE_ASTRA, CQL_STORE_SCYLLA, CQL_STORE_MEMORY)
+
+
+@dataclass
+class AstraBundleConfig:
+    """``request.AstraBundleConfig`` (``/root/reference/appconfig.local.yaml:1-4``)."""
+
+    secure_connection_bundle_base64: str = field(default="", metadata=_k("secure-connection-bundle-base64", secret=True))
+    gateway_user: str = field(default="", metadata=_k("gateway-user"))
+    gateway_password: str = field(default="", metadata=_k("gateway-password", secret=True))
+    # extensions
+    keyspace: str = field(default="nexus", metadata=_k("keyspace"))
+    table: str = field(default="checkpoints", metadata=_k("table"))
+    consistency: str = field(default="LOCAL_QUORUM", metadata=_k("consistency"))
+    request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))
+
+
+@dataclass
+class ScyllaCqlStoreConfig:
+    """``request.ScyllaCqlStoreConfig`` (``/root/reference/appconfig.local.yaml:5-10``)."""
+
+    hosts: List[str] = field(default_factory=list, metadata=_k("hosts", "list"))
+    port: int = field(default=9042, metadata=_k("port"))
+    user: str = field(default="", metadata=_k("user"))
+    password: str = field(default="", metadata=_k("password", secret=True))
+    local_dc: str = field(default="", metadata=_k("local-dc"))
+    # extensions
+    keyspace: str = field(default="nexus", metadata=_k("keyspace"))
+    table: str = field(default="checkpoints", metadata=_k("table"))
+    consistency: str = field(default="LOCAL_QUORUM", metadata=_k("consistency"))
+    connections_per_host: int = field(default=2, metadata=_k("connections-per-host"))
+    request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))
+    connect_timeout: float = field(default=5.0, metadata=_k("connect-timeout", "duration"))
+    token_aware: bool = field(default=True, metadata=_k("token-aware"))
+
+
+@dataclass
+class CompatConfig:
+    """Switches for reference quirks; defaults keep observable parity
+    where it is harmless and fix the hazards."""
+
+    # "Algorithm encountered a fatal error during execution: Algorithm encountered ..."
+    # (/root/reference/services/supervisor.go:198,325)
+    doubled_fatal_cause: bool = field(default=True, metadata=_k("doubled-fatal-cause"))
+    # full-row INSERT (reference) vs owned-columns UPDATE (this build's default)
+    full_row_upsert: bool = field(default=False, metadata=_k("full-row-upsert"))
+    # delete the Job when the checkpoint read fails (supervisor.go:265-273)
+    delete_on_read_error: bool = field(default=False, metadata=_k("delete-on-read-error"))
+    # NotFound on Job DELETE counts as success (fixes retry hazard)
+    delete_not_found_ok: bool = field(default=True, metadata=_k("delete-not-found-ok"))
+    # conditional write: only move rows that are still unfinished (LWT)
+    conditional_update: bool = field(default=False, metadata=_k("conditional-update"))
+
+
+@dataclass
+class LabelConfig:
+    """Label keys of nexus-core ``checkpoint/models`` (values unverified offline,
+    SURVEY §8 q2) — configurable so a deployment can pin the real strings."""
+
+    nexus_component_label: str = field(default="science.sneaksanddata.com/nexus-component", metadata=_k("nexus-component"))
+    algorithm_run_value: str = field(default="algorithm-run", metadata=_k("algorithm-run-value"))
+    job_template_name_key: str = field(default="science.sneaksanddata.com/algorithm-template-name", metadata=_k("job-template-name"))
+    job_name_label: str = field(default="batch.kubernetes.io/job-name", metadata=_k("job-name"))
+
+
+@dataclass
+class RulesConfig:
+    """Classifier extensions beyond the reference decision table (SURVEY §2.9.1 gaps)."""
+
+    handle_event_updates: bool = field(default=True, metadata=_k("handle-event-updates"))
+    pod_status_rules: bool = field(default=True, metadata=_k("pod-status-rules"))
+    # Evicted pods: "fail" the run immediately, or "observe" (record evidence, let the
+    # Job controller retry and enrich the terminal Job event)
+    evicted_policy: str = field(default="observe", metadata=_k("evicted-policy"))
+    # FailedScheduling (e.g. insufficient amd.com/gpu): fail after this long unschedulable; 0 = never
+    unschedulable_timeout: float = field(default=0.0, metadata=_k("unschedulable-timeout", "duration"))
+    # keep events whose involved object is not cached yet this long before dropping as stale
+    stale_event_grace: float = field(default=2.0, metadata=_k("stale-event-grace", "duration"))
+    # trace column format: raw (reference: event message), json, or auto (json when extra evidence exists)
+    trace_format: str = field(default="auto", metadata=_k("trace-format"))
+
+
+@dataclass
+class GpuConfig:
+    """MI355X attribution (north star in BASELINE.json)."""
+
+    attribution_enabled: bool = field(default=True, metadata=_k("attribution-enabled"))
+    hbm_capacity_gb: float = field(default=288.0, metadata=_k("hbm-capacity-gb"))
+    hbm_oom_fraction: float = field(default=0.97, metadata=_k("hbm-oom-fraction"))
+    evidence_annotation: str = field(default="nexus.amd.com/gpu-evidence", metadata=_k("evidence-annotation"))
+    gpu_resource_name: str = field(default="amd.com/gpu", metadata=_k("gpu-resource-name"))
+    backend: str = field(default="auto", metadata=_k("backend"))  # auto | amdsmi | fake | none
+    sample_interval: float = field(default=0.5, metadata=_k("sample-interval", "duration"))
+
+
+@dataclass
+class LeaderElectionConfig:
+    enabled: bool = field(default=False, metadata=_k("enabled"))
+    lease_name: str = field(default="nexus-supervisor-leader", metadata=_k("lease-name"))
+    lease_duration: float = field(default=15.0, metadata=_k("lease-duration", "duration"))
+    renew_deadline: float = field(default=10.0, metadata=_k("renew-deadline", "duration"))
+    retry_period: float = field(default=2.0, metadata=_k("retry-period", "duration"))
+    identity: str = field(default="", metadata=_k("identity"))
+
+
+@dataclass
+class ShardingConfig:
+    """Consistent-hash sharding of runs across active replicas (0/1 shard = off)."""
+
+    shards: int = field(default=1, metadata=_k("shards"))
+    shard_index: int = field(default=0, metadata=_k("shard-index"))
+
+
+@dataclass
+class ObservabilityConfig:
+    statsd_name: str = field(default="nexus_supervisor", metadata=_k("statsd-name"))
+    http_port: int = field(default=0, metadata=_k("http-port"))  # /metrics /healthz /readyz /debug/pprof; 0 = off
+    http_host: str = field(default="0.0.0.0", metadata=_k("http-host"))
+    profiler_hz: int = field(default=97, metadata=_k("profiler-hz"))
+    stage_timestamps: bool = field(default=True, metadata=_k("stage-timestamps"))
+
+
+@dataclass
+class SupervisorConfig:
+    """``app.SupervisorConfig`` (``/root/reference/app/app_config.go:8-20``) + extensions."""
+
+    astra_cql_store: AstraBundleConfig = field(default_factory=AstraBundleConfig, metadata=_k("astra-cql-store"))
+    scylla_cql_store: ScyllaCqlStoreConfig = field(default_factory=ScyllaCqlStoreConfig, metadata=_k("scylla-cql-store"))
+    cql_store_type: str = field(default=CQL_STORE_ASTRA, metadata=_k("cql-store-type"))
+    kube_config_path: str = field(default="", metadata=_k("kube-config-path"))
+    resource_namespace: str = field(default="nexus", metadata=_k("resource-namespace"))
+    log_level: str = field(default="INFO", metadata=_k("log-level"))
+    failure_rate_base_delay: float = field(default=0.1, metadata=_k("failure-rate-base-delay", "duration"))
+    failure_rate_max_delay: float = field(default=1.0, metadata=_k("failure-rate-max-delay", "duration"))
+    rate_limit_elements_per_second: float = field(default=10, metadata=_k("rate-limit-elements-per-second", "number"))
+    rate_limit_elements_burst: int = field(default=100, metadata=_k("rate-limit-elements-burst"))
+    workers: int = field(default=2, metadata=_k("workers"))
+    # ---- extensions ----
+    resync_period: float = field(default=30.0, metadata=_k("resync-period", "duration"))
+    max_retries: int = field(default=16, metadata=_k("max-retries"))  # 0 = retry forever
+    compat: CompatConfig = field(default_factory=CompatConfig, metadata=_k("compat"))
+    labels: LabelConfig = field(default_factory=LabelConfig, metadata=_k("labels"))
+    rules: RulesConfig = field(default_factory=RulesConfig, metadata=_k("rules"))
+    gpu: GpuConfig = field(default_factory=GpuConfig, metadata=_k("gpu"))
+    leader_election: LeaderElectionConfig = field(default_factory=LeaderElectionConfig, metadata=_k("leader-election"))
+    sharding: ShardingConfig = field(default_factory=ShardingConfig, metadata=_k("sharding"))
+    observability: ObservabilityConfig = field(default_factory=ObservabilityConfig, metadata=_k("observability"))
+
+
+class ConfigError(ValueError):
+    pass
+
+
+def validate(cfg: SupervisorConfig) -> SupervisorConfig:
+    if cfg.cql_store_type not in CQL_STORE_TYPES:
+        raise ConfigError(f"unknown store type {cfg.cql_store_type}")
+    if cfg.workers < 1:
+        raise ConfigError(f"workers must be >= 1, got {cfg.workers}")
+    if cfg.rate_limit_elements_per_second < 0:
+        raise ConfigError("rate-limit-elements-per-second must be >= 0 (0 = unlimited)")
+    if cfg.rate_limit_elements_burst < 1:
+        raise ConfigError("rate-limit-elements-burst must be >= 1")
+    if cfg.failure_rate_base_delay < 0 or cfg.failure_rate_max_delay < cfg.failure_rate_base_delay:
+        raise ConfigError("failure-rate-max-delay must be >= failure-rate-base-delay >= 0")
+    if cfg.rules.evicted_policy not in ("fail", "observe"):
+        raise ConfigError("rules.evicted-policy must be fail|observe")
+    if cfg.rules.trace_format not in ("raw", "json", "auto"):
+        raise ConfigError("rules.trace-format must be raw|json|auto")
+    if cfg.sharding.shards < 1 or not 0 <= cfg.sharding.shard_index < cfg.sharding.shards:
+        raise ConfigError("sharding.shard-index must be in [0, shards)")
+    if not 0 < cfg.gpu.hbm_oom_fraction <= 1:
+        raise ConfigError("gpu.hbm-oom-fraction must be in (0, 1]")
+    if cfg.leader_election.enabled:
+        le = cfg.leader_election
+        if not le.lease_duration > le.renew_deadline > le.retry_period > 0:
+            raise ConfigError("leader-election: lease-duration > renew-deadline > retry-period > 0 required")
+    return cfg

@@ -1,0 +1,166 @@
+"""HBM-OOM vs host-OOM attribution (north star).
+
+Scored-evidence model — every signal adds weight to one hypothesis and is
+recorded, so the trace row says *why*:
+
+host-OOM
+  * container ``terminated.reason == "OOMKilled"`` (cgroup OOM, exit 137)  +1.0
+  * bare exit 137 (SIGKILL) without reason                                  +0.35
+  * in-process host allocation failure (``MemoryError``, ``std::bad_alloc``,
+    ``Cannot allocate memory``)                                             +0.6
+HBM-OOM (288 GB HBM3E per MI355X)
+  * HIP OOM signature in the termination / event message
+    (``hipErrorOutOfMemory``, ``HIP out of memory``, torch
+    ``OutOfMemoryError``, RCCL/hipMalloc allocation failures)              +1.0
+  * agent-sampled VRAM peak ≥ ``hbm_oom_fraction`` × capacity on the rank's GPU +0.5
+  * VM-fault / queue-eviction event on that GPU                             +0.25
+
+A verdict needs ≥0.5; the larger score wins, with a cgroup OOMKill (a hard
+kernel fact about *host* memory) winning ties.
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass, field
+from typing import Any, Dict, Iterable, List, Optional
+
+HBM_PATTERNS = [
+    re.compile(r"hipErrorOutOfMemory", re.I),
+    re.compile(r"\bHIP out of memory", re.I),
+    re.compile(r"\bCUDA out of memory", re.I),  # torch wording on some ROCm builds
+    re.compile(r"OutOfMemoryError", re.I),
+    re.compile(r"hipMalloc(?:Managed|Async)?\b[^\n]{0,80}(?:fail|out of memory|error)", re.I),
+    re.compile(r"(?:NCCL|RCCL)[^\n]{0,120}out of memory", re.I),
+    re.compile(r"HSA_STATUS_ERROR_OUT_OF_RESOURCES", re.I),
+    re.compile(r"\bGPU\b[^\n]{0,40}out of memory", re.I),
+    re.compile(r"RESOURCE_EXHAUSTED: Out of memory while trying to allocate", re.I),
+]
+HOST_PATTERNS = [
+    re.compile(r"\bMemoryError\b"),
+    re.compile(r"std::bad_alloc"),
+    re.compile(r"Cannot allocate memory", re.I),
+    re.compile(r"Memory cgroup out of memory", re.I),
+    re.compile(r"\bOOMKilled\b"),
+]
+_TORCH_GPU = re.compile(r"GPU (\d+) has a total capacity of ([\d.]+) (GiB|MiB|GB|MB)", re.I)
+_TORCH_REQ = re.compile(r"Tried to allocate ([\d.]+) (GiB|MiB|GB|MB|KiB)", re.I)
+_UNIT = {"gib": 1 << 30, "gb": 1 << 30, "mib": 1 << 20, "mb": 1 << 20, "kib": 1 << 10}
+
+
+@dataclass
+class OomVerdict:
+    kind: Optional[str] = None  # "hbm" | "host" | None
+    hbm_score: float = 0.0
+    host_score: float = 0.0
+    signals: List[str] = field(default_factory=list)
+    gpu_index: Optional[int] = None
+    requested_bytes: Optional[int] = None
+    capacity_bytes: Optional[int] = None
+    peak_vram_bytes: Optional[int] = None
+
+    def as_dict(self) -> Dict[str, Any]:
+        d: Dict[str, Any] = {"kind": self.kind, "hbm_score": round(self.hbm_score, 3),
+                             "host_score": round(self.host_score, 3), "signals": self.signals}
+        for k in ("gpu_index", "requested_bytes", "capacity_bytes", "peak_vram_bytes"):
+            v = getattr(self, k)
+            if v is not None:
+                d[k] = v
+        return d
+
+
+def hbm_signature(text: str) -> Optional[str]:
+    for p in HBM_PATTERNS:
+        m = p.search(text)
+        if m:
+            return m.group(0)
+    return None
+
+
+def host_signature(text: str) -> Optional[str]:
+    for p in HOST_PATTERNS:
+        m = p.search(text)
+        if m:
+            return m.group(0)
+    return None
+
+
+def analyze(
+    texts: Iterable[str] = (),
+    terminated: Iterable[Dict[str, Any]] = (),
+    gpu_evidence: Optional[Dict[str, Any]] = None,
+    expected_gpu: Optional[str] = None,
+    hbm_capacity_gb: float = 288.0,
+    hbm_oom_fraction: float = 0.97,
+) -> OomVerdict:
+    v = OomVerdict()
+    texts = [t for t in texts if t]
+    for t in terminated:
+        reason = t.get("reason") or ""
+        code = t.get("exitCode")
+        if reason == "OOMKilled":
+            v.host_score += 1.0
+            v.signals.append(f"container {t.get('container', '')!s} OOMKilled (cgroup, exit {code})")
+        elif code == 137:
+            v.host_score += 0.35
+            v.signals.append(f"container {t.get('container', '')!s} exit 137 (SIGKILL)")
+        if t.get("message"):
+            texts.append(t["message"])
+    hbm_hit = host_hit = False
+    for text in texts:
+        s = hbm_signature(text)
+        if s and not hbm_hit:
+            hbm_hit = True
+            v.hbm_score += 1.0
+            v.signals.append(f"HIP OOM signature: {s!r}")
+        h = host_signature(text)
+        if h and not host_hit and h != "OOMKilled":
+            host_hit = True
+            v.host_score += 0.6
+            v.signals.append(f"host allocation failure: {h!r}")
+        m = _TORCH_GPU.search(text)
+        if m and v.gpu_index is None:
+            v.gpu_index = int(m.group(1))
+            v.capacity_bytes = int(float(m.group(2)) * _UNIT[m.group(3).lower()])
+        r = _TORCH_REQ.search(text)
+        if r and v.requested_bytes is None:
+            v.requested_bytes = int(float(r.group(1)) * _UNIT[r.group(2).lower()])
+    if gpu_evidence:
+        cap = int(hbm_capacity_gb * (1 << 30))
+        for g in _candidate_gpus(gpu_evidence, expected_gpu, v.gpu_index):
+            total = int(g.get("vram_total_mb") or 0) * (1 << 20) or cap
+            peak = int(g.get("vram_peak_mb") or g.get("vram_used_mb") or 0) * (1 << 20)
+            if peak and peak >= hbm_oom_fraction * total:
+                v.hbm_score += 0.5
+                v.signals.append(f"GPU {g.get('index')} VRAM peak {peak / (1 << 30):.1f} GiB of {total / (1 << 30):.1f} GiB")
+                v.peak_vram_bytes = peak
+                if v.gpu_index is None:
+                    v.gpu_index = g.get("index")
+            faults = [e for e in g.get("events", []) if e.get("type") in ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET")]
+            if faults:
+                v.hbm_score += 0.25
+                v.signals.append(f"GPU {g.get('index')} events: {sorted({e['type'] for e in faults})}")
+                if v.gpu_index is None:
+                    v.gpu_index = g.get("index")
+            if v.capacity_bytes is None and g.get("vram_total_mb"):
+                v.capacity_bytes = int(g["vram_total_mb"]) * (1 << 20)
+    if v.hbm_score >= 0.5 or v.host_score >= 0.5:
+        if v.host_score >= 1.0 and v.host_score >= v.hbm_score:
+            v.kind = "host"
+        elif v.hbm_score >= v.host_score:
+            v.kind = "hbm"
+        else:
+            v.kind = "host"
+    return v
+
+
+def _candidate_gpus(ev: Dict[str, Any], expected: Optional[str], idx: Optional[int]):
+    gpus = ev.get("gpus") or []
+    if idx is not None:
+        sel = [g for g in gpus if g.get("index") == idx]
+        if sel:
+            return sel
+    if expected is not None:
+        sel = [g for g in gpus if str(g.get("index")) == str(expected) or g.get("uuid") == expected]
+        if sel:
+            return sel
+    return gpus

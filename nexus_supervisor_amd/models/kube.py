@@ -1,0 +1,187 @@
+"""Kubernetes object views used by the supervisor.
+
+Objects stay plain JSON dicts (what the watch stream decodes to) but are
+*slimmed* by a per-kind transform before they enter the informer cache — the
+equivalent of client-go's ``TransformFunc``.  At 10k concurrent jobs the pod
+and job caches then hold only the fields the classifier and the GPU
+attribution read (labels, container env, ``amd.com/gpu`` resources, container
+termination state), not full pod specs.
+
+The reference caches full objects via shared informers
+(``/root/reference/services/supervisor.go:73-75``) and reads only labels
+(``:181,231-232``).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Iterable, List, Optional
+
+_KEEP_ANNOTATIONS_PREFIXES = ("nexus.amd.com/", "batch.kubernetes.io/job-completion-index")
+
+
+def meta(obj: Dict[str, Any]) -> Dict[str, Any]:
+    return obj.get("metadata") or {}
+
+
+def name_of(obj) -> str:
+    return meta(obj).get("name", "")
+
+
+def namespace_of(obj) -> str:
+    return meta(obj).get("namespace", "")
+
+
+def uid_of(obj) -> str:
+    return meta(obj).get("uid", "")
+
+
+def labels_of(obj) -> Dict[str, str]:
+    return meta(obj).get("labels") or {}
+
+
+def annotations_of(obj) -> Dict[str, str]:
+    return meta(obj).get("annotations") or {}
+
+
+def resource_version(obj) -> str:
+    return meta(obj).get("resourceVersion", "")
+
+
+def object_key(obj) -> str:
+    """``namespace/name`` (client-go ``cache.MetaNamespaceKeyFunc``)."""
+    ns = namespace_of(obj)
+    return f"{ns}/{name_of(obj)}" if ns else name_of(obj)
+
+
+def _slim_meta(m: Dict[str, Any], keep_labels=True) -> Dict[str, Any]:
+    out = {k: m[k] for k in ("name", "namespace", "uid", "resourceVersion", "creationTimestamp", "deletionTimestamp") if k in m}
+    if keep_labels and m.get("labels"):
+        out["labels"] = m["labels"]
+    ann = m.get("annotations")
+    if ann:
+        kept = {k: v for k, v in ann.items() if k.startswith(_KEEP_ANNOTATIONS_PREFIXES)}
+        if kept:
+            out["annotations"] = kept
+    if m.get("ownerReferences"):
+        out["ownerReferences"] = [{"kind": o.get("kind"), "name": o.get("name"), "uid": o.get("uid")} for o in m["ownerReferences"]]
+    return out
+
+
+def slim_event(ev: Dict[str, Any]) -> Dict[str, Any]:
+    out = {"metadata": _slim_meta(meta(ev), keep_labels=False)}
+    for k in ("involvedObject", "reason", "message", "type", "count", "firstTimestamp", "lastTimestamp", "eventTime", "series", "reportingComponent"):
+        if k in ev:
+            out[k] = ev[k]
+    src = ev.get("source")
+    if src:
+        out["source"] = src
+    return out
+
+
+def _slim_container(c: Dict[str, Any]) -> Dict[str, Any]:
+    out: Dict[str, Any] = {"name": c.get("name", "")}
+    env = c.get("env")
+    if env:
+        out["env"] = [{"name": e.get("name"), "value": e.get("value")} for e in env if "value" in e]
+    res = c.get("resources")
+    if res:
+        out["resources"] = {k: dict(v) for k, v in res.items() if isinstance(v, dict)}
+    return out
+
+
+def _slim_status(cs: Dict[str, Any]) -> Dict[str, Any]:
+    return {k: cs[k] for k in ("name", "state", "lastState", "restartCount", "ready", "started") if k in cs}
+
+
+def slim_pod(pod: Dict[str, Any]) -> Dict[str, Any]:
+    spec = pod.get("spec") or {}
+    status = pod.get("status") or {}
+    out = {"metadata": _slim_meta(meta(pod))}
+    s: Dict[str, Any] = {}
+    if spec.get("nodeName"):
+        s["nodeName"] = spec["nodeName"]
+    if spec.get("containers"):
+        s["containers"] = [_slim_container(c) for c in spec["containers"]]
+    out["spec"] = s
+    st: Dict[str, Any] = {}
+    for k in ("phase", "reason", "message", "hostIP", "podIP", "startTime"):
+        if k in status:
+            st[k] = status[k]
+    for k in ("containerStatuses", "initContainerStatuses"):
+        if status.get(k):
+            st[k] = [_slim_status(c) for c in status[k]]
+    if status.get("conditions"):
+        st["conditions"] = [{kk: c.get(kk) for kk in ("type", "status", "reason", "message") if kk in c} for c in status["conditions"]]
+    out["status"] = st
+    return out
+
+
+def slim_job(job: Dict[str, Any]) -> Dict[str, Any]:
+    spec = job.get("spec") or {}
+    status = job.get("status") or {}
+    out = {"metadata": _slim_meta(meta(job))}
+    out["spec"] = {k: spec[k] for k in ("backoffLimit", "activeDeadlineSeconds", "completions", "parallelism", "completionMode") if k in spec}
+    st = {k: status[k] for k in ("active", "failed", "succeeded", "startTime", "completionTime") if k in status}
+    if status.get("conditions"):
+        st["conditions"] = [{kk: c.get(kk) for kk in ("type", "status", "reason", "message") if kk in c} for c in status["conditions"]]
+    out["status"] = st
+    return out
+
+
+def slim_lease(lease: Dict[str, Any]) -> Dict[str, Any]:
+    return lease
+
+
+SLIMMERS = {"Event": slim_event, "Pod": slim_pod, "Job": slim_job, "Lease": slim_lease}
+
+
+# ----------------------------------------------------------------- pod helpers
+def container_statuses(pod) -> List[Dict[str, Any]]:
+    st = pod.get("status") or {}
+    return list(st.get("initContainerStatuses") or []) + list(st.get("containerStatuses") or [])
+
+
+def terminated_states(pod) -> Iterable[Dict[str, Any]]:
+    """Yield ``state.terminated`` / ``lastState.terminated`` dicts (with container name)."""
+    for cs in container_statuses(pod):
+        for which in ("state", "lastState"):
+            t = (cs.get(which) or {}).get("terminated")
+            if t:
+                yield dict(t, container=cs.get("name", ""), which=which)
+
+
+def waiting_states(pod) -> Iterable[Dict[str, Any]]:
+    for cs in container_statuses(pod):
+        w = (cs.get("state") or {}).get("waiting")
+        if w:
+            yield dict(w, container=cs.get("name", ""), restartCount=cs.get("restartCount", 0))
+
+
+def pod_env(pod) -> Dict[str, str]:
+    """Merged literal env of all containers (first definition wins)."""
+    out: Dict[str, str] = {}
+    for c in (pod.get("spec") or {}).get("containers") or []:
+        for e in c.get("env") or []:
+            n = e.get("name")
+            if n and n not in out and e.get("value") is not None:
+                out[n] = e["value"]
+    return out
+
+
+def gpu_request(pod, resource: str = "amd.com/gpu") -> int:
+    total = 0
+    for c in (pod.get("spec") or {}).get("containers") or []:
+        res = c.get("resources") or {}
+        v = (res.get("limits") or {}).get(resource) or (res.get("requests") or {}).get(resource)
+        if v is not None:
+            try:
+                total += int(str(v))
+            except ValueError:
+                pass
+    return total
+
+
+def condition(obj, ctype: str) -> Optional[Dict[str, Any]]:
+    for c in (obj.get("status") or {}).get("conditions") or []:
+        if c.get("type") == ctype:
+            return c
+    return None

@@ -1,0 +1,99 @@
+"""Structured logging with klog-style verbosity.
+
+The reference logs through slog bridged into klog (``/root/reference/main.go:15,19``)
+with V(0) for decisions and errors, V(1) for no-op events and V(4) for every
+raw event (``/root/reference/services/supervisor.go:138,162,256``).
+``log-level`` (``NEXUS__LOG_LEVEL``, Helm default ``INFO``) maps to a max
+verbosity: ERROR/WARN/INFO → V(0), DEBUG → V(4), TRACE → V(9).  Lines are JSON
+objects with the reference's structured keys (``requestId``, ``algorithm``,
+``reason``, ``message``).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import sys
+import time
+from typing import Any, Dict, Optional
+
+_LEVELS = {"TRACE": (logging.DEBUG, 9), "DEBUG": (logging.DEBUG, 4), "INFO": (logging.INFO, 0),
+           "WARN": (logging.WARNING, 0), "WARNING": (logging.WARNING, 0), "ERROR": (logging.ERROR, 0)}
+
+
+class JsonFormatter(logging.Formatter):
+    def __init__(self, static: Optional[Dict[str, Any]] = None):
+        super().__init__()
+        self.static = dict(static or {})
+
+    def format(self, record: logging.LogRecord) -> str:
+        doc: Dict[str, Any] = {"time": time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(record.created)) + f".{int(record.msecs):03d}Z",
+                               "level": record.levelname, "logger": record.name, "msg": record.getMessage()}
+        v = getattr(record, "v", None)
+        if v:
+            doc["v"] = v
+        kv = getattr(record, "kv", None)
+        if kv:
+            doc.update(kv)
+        if record.exc_info:
+            doc["error"] = self.formatException(record.exc_info)
+        doc.update(self.static)
+        return json.dumps(doc, default=str)
+
+
+class KLogger:
+    """``logger.v(4).info("event received", object=...)`` on top of :mod:`logging`."""
+
+    def __init__(self, name: str = "nexus_supervisor_amd", verbosity: int = 0):
+        self._log = logging.getLogger(name)
+        self.verbosity = verbosity
+
+    def v(self, level: int) -> "_V":
+        return _V(self, level)
+
+    def enabled(self, level: int) -> bool:
+        return level <= self.verbosity
+
+    def info(self, msg: str, **kv) -> None:
+        if self._log.isEnabledFor(logging.INFO):
+            self._log.info(msg, extra={"kv": kv})
+
+    def warning(self, msg: str, **kv) -> None:
+        self._log.warning(msg, extra={"kv": kv})
+
+    def error(self, err: Optional[BaseException], msg: str, **kv) -> None:
+        if err is not None:
+            kv = dict(kv, err=str(err))
+        self._log.error(msg, extra={"kv": kv})
+
+
+class _V:
+    __slots__ = ("parent", "level")
+
+    def __init__(self, parent: KLogger, level: int):
+        self.parent = parent
+        self.level = level
+
+    def info(self, msg: str, **kv) -> None:
+        if self.level <= self.parent.verbosity:
+            self.parent._log.info(msg, extra={"kv": kv, "v": self.level})
+
+    def error(self, err: Optional[BaseException], msg: str, **kv) -> None:
+        self.parent.error(err, msg, **kv)
+
+    @property
+    def enabled(self) -> bool:
+        return self.level <= self.parent.verbosity
+
+
+def configure_logging(level: str = "INFO", stream=None, static: Optional[Dict[str, Any]] = None) -> KLogger:
+    """Configure the root ``nexus_supervisor_amd`` logger (telemetry.ConfigureLogger analog,
+    ``/root/reference/main.go:15``)."""
+    pylevel, verbosity = _LEVELS.get((level or "INFO").strip().upper(), (logging.INFO, 0))
+    root = logging.getLogger("nexus_supervisor_amd")
+    root.setLevel(pylevel)
+    root.handlers[:] = []
+    h = logging.StreamHandler(stream or sys.stdout)
+    h.setFormatter(JsonFormatter(static))
+    root.addHandler(h)
+    root.propagate = False
+    return KLogger("nexus_supervisor_amd", verbosity)

@@ -1,0 +1,50 @@
+"""Checkpoint store protocol.
+
+nexus-core ``request.CqlStore`` exposes ``ReadCheckpoint(algorithm, id)`` and
+``UpsertCheckpoint(*CheckpointedRequest)`` (call sites
+``/root/reference/services/supervisor.go:264,301,328,353,364``).  This build
+keeps both and adds :meth:`CheckpointStore.update_status`, an owned-columns
+write (``UPDATE … SET lifecycle_stage, algorithm_failure_cause,
+algorithm_failure_details, last_modified``) that cannot clobber columns other
+Nexus components own, optionally conditional on the row still
+being unfinished (lightweight transaction).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+from typing import Iterable, Optional
+
+from ..models.checkpoint import CheckpointedRequest
+
+
+class StoreError(Exception):
+    """Transient or permanent store failure (the pipeline retries it)."""
+
+
+class CheckpointStore:
+    async def read_checkpoint(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
+        raise NotImplementedError
+
+    async def upsert_checkpoint(self, checkpoint: CheckpointedRequest) -> None:
+        raise NotImplementedError
+
+    async def update_status(
+        self,
+        algorithm: str,
+        request_id: str,
+        lifecycle_stage: str,
+        failure_cause: Optional[str],
+        failure_details: Optional[str],
+        last_modified: _dt.datetime,
+        only_if_stages: Optional[Iterable[str]] = None,
+        set_failure: bool = True,
+    ) -> bool:
+        """Write the owned columns. With ``only_if_stages`` the write is a CAS
+        (``IF lifecycle_stage IN (...)``); returns whether it was applied."""
+        raise NotImplementedError
+
+    async def connect(self) -> None:
+        return None
+
+    async def close(self) -> None:
+        return None

@@ -1,0 +1,446 @@
+"""The supervisor domain service: informers → classify → keyed pipeline → actuate.
+
+Parity map to ``/root/reference/services/supervisor.go``:
+
+==========================  ===================================================
+reference                   here
+==========================  ===================================================
+``NewSupervisor`` :69-103   :class:`Supervisor` ``__init__`` (namespaced factory,
+                            Event/Pod/Job informers, injectable sync predicate)
+``Init`` :106-135           :meth:`Supervisor.init` (pipeline + handlers)
+``onEvent`` :137-259        :meth:`Supervisor._on_event_add` → :class:`Classifier`
+``superviseAction`` :261    :meth:`Supervisor.supervise_action`
+``Start`` :376-388          :meth:`Supervisor.start` (workers, then informers +
+                            cache sync as the post-start hook)
+==========================  ===================================================
+
+Beyond the reference: pod/job status rules, Event Update handling (repeat
+counts), parking of events whose object is not cached yet, per-run-key
+serialization, NotFound-tolerant deletes, owned-columns writes, a
+decided-stage cache that suppresses duplicate work, sharding/leader gating and
+per-stage timestamps for the pod-fail → checkpoint latency metric.
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as _dt
+import time
+import zlib
+from collections import OrderedDict
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+from .classify import DECIDED, STALE, Classifier, ObjectLookup, render_trace
+from .classify import reference_rules as R
+from .config.schema import SupervisorConfig
+from .informer import InformerFactory, label_index
+from .kube.errors import NotFound
+from .models import kube
+from .models.checkpoint import FINISHED_STAGES, LifecycleStage
+from .models.decisions import Decision, DecisionAction as A, RunStatusAnalysisResult
+from .obs.logging import KLogger
+from .obs.metrics import Metrics
+from .parallel.pipeline import PipelineStage
+from .store.base import CheckpointStore
+
+STAGE_FOR_ACTION = {
+    A.TO_FAIL_STUCK_IN_PENDING: lambda: LifecycleStage.SCHEDULING_FAILED,
+    A.TO_FAIL_FATAL_ERROR: lambda: LifecycleStage.FAILED,
+    A.TO_FAIL_DEADLINE_EXCEEDED: lambda: LifecycleStage.DEADLINE_EXCEEDED,
+    A.TO_RUNNING: lambda: LifecycleStage.RUNNING,
+}
+
+
+class JobClient:
+    """What the actuator needs from the K8s API."""
+
+    async def delete_job(self, namespace: str, name: str, propagation_policy: str = "Background") -> None:  # pragma: no cover
+        raise NotImplementedError
+
+
+class CasConflict(Exception):
+    """Conditional write lost a race; the item is retried (re-read + re-decide)."""
+
+
+def parse_k8s_time(ts: Optional[str]) -> Optional[float]:
+    """RFC3339 / MicroTime → epoch seconds."""
+    if not ts:
+        return None
+    try:
+        if ts.endswith("Z"):
+            ts = ts[:-1] + "+00:00"
+        return _dt.datetime.fromisoformat(ts).timestamp()
+    except ValueError:
+        return None
+
+
+class _Lookup(ObjectLookup):
+    __slots__ = ("sup",)
+
+    def __init__(self, sup: "Supervisor"):
+        self.sup = sup
+
+    def get(self, kind, name):
+        inf = self.sup.pod_informer if kind == "Pod" else self.sup.job_informer if kind == "Job" else None
+        if inf is None:
+            return None
+        return inf.indexer.get_by_name(self.sup.namespace, name)
+
+    def pods_of_job(self, job_name):
+        return self.sup.pod_informer.indexer.by_index("job-name", job_name)
+
+
+class Supervisor:
+    def __init__(
+        self,
+        cfg: SupervisorConfig,
+        store: CheckpointStore,
+        jobs: JobClient,
+        factory: InformerFactory,
+        logger: Optional[KLogger] = None,
+        metrics: Optional[Metrics] = None,
+        sync_state: Optional[Callable[[], bool]] = None,
+        wall: Callable[[], float] = time.time,
+    ):
+        self.cfg = cfg
+        self.namespace = cfg.resource_namespace
+        self.store = store
+        self.jobs = jobs
+        self.factory = factory
+        self.log = logger or KLogger()
+        self.metrics = metrics or Metrics(cfg.observability.statsd_name)
+        self.wall = wall
+        self.sync_state = sync_state
+        self.classifier = Classifier(cfg.labels, cfg.rules, cfg.gpu)
+        self.event_informer = factory.informer("Event")
+        self.pod_informer = factory.informer("Pod", indexers={"job-name": label_index(cfg.labels.job_name_label)})
+        self.job_informer = factory.informer("Job")
+        self.lookup = _Lookup(self)
+        self.pipeline: Optional[PipelineStage] = None
+        self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
+        self._applied_cap = 200_000
+        self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
+        self._sweeper: Optional[asyncio.Task] = None
+        self.decision_hooks: List[Callable[[Decision], None]] = []
+        self.active = not cfg.leader_election.enabled  # leader gating flips this
+        self._unfinished_cache: Optional[Tuple[str, ...]] = None
+        m = self.metrics
+        m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
+        m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
+
+    # ------------------------------------------------------------------ Init
+    def init(self) -> None:
+        c = self.cfg
+        self.pipeline = PipelineStage(
+            "supervisor",
+            self.supervise_action,
+            workers=c.workers,
+            elements_per_second=c.rate_limit_elements_per_second,
+            burst=c.rate_limit_elements_burst,
+            base_delay=c.failure_rate_base_delay,
+            max_delay=c.failure_rate_max_delay,
+            max_retries=c.max_retries,
+            key_fn=lambda r: (r.algorithm, r.request_id),
+            coalesce_key=lambda r: r.action,
+            on_dead_letter=self._dead_letter,
+            on_done=self._done,
+            tags={},
+        )
+        self.event_informer.add_event_handler(on_add=self._on_event_add, on_update=self._on_event_update)
+        self.pod_informer.add_event_handler(on_add=self._on_pod_add, on_update=self._on_pod_update)
+        self.job_informer.add_event_handler(on_add=self._on_job_add, on_update=self._on_job_update)
+
+    # ------------------------------------------------------------------ Start / stop
+    async def start(self, wait_sync_timeout: Optional[float] = None) -> None:
+        if self.pipeline is None:
+            self.init()
+
+        async def post_start():
+            self.factory.start()
+            if self.sync_state is not None:
+                ok = self.sync_state()
+            else:
+                ok = await self.factory.wait_for_cache_sync(wait_sync_timeout)
+            if not ok:
+                raise RuntimeError("failed to wait for pod informer caches to sync")
+            self.log.info("resource informers synced")
+
+        await self.pipeline.start(post_start)
+        self._sweeper = asyncio.create_task(self._sweep_parked(), name="stale-event-sweeper")
+
+    async def stop(self, drain: bool = True, timeout: float = 10.0) -> None:
+        if self._sweeper:
+            self._sweeper.cancel()
+            try:
+                await self._sweeper
+            except (asyncio.CancelledError, Exception):
+                pass
+        await self.factory.stop()
+        if self.pipeline is not None:
+            await self.pipeline.stop(drain=drain, timeout=timeout)
+
+    def set_active(self, active: bool) -> None:
+        """Leader gating: on gaining leadership replay the caches (idempotent) so nothing
+        decided while standby is lost (SURVEY §5.3 'replay on restart')."""
+        was = self.active
+        self.active = active
+        if active and not was:
+            self.replay()
+
+    def replay(self) -> None:
+        for ev in self.event_informer.indexer.values():
+            self._on_event_add(ev)
+        for job in self.job_informer.indexer.values():
+            self._on_job_add(job)
+        for pod in self.pod_informer.indexer.values():
+            self._on_pod_add(pod)
+
+    # ------------------------------------------------------------------ ownership
+    def owns(self, key: Tuple[str, str]) -> bool:
+        s = self.cfg.sharding
+        if s.shards <= 1:
+            return True
+        h = zlib.crc32(f"{key[0]}\x00{key[1]}".encode())
+        return h % s.shards == s.shard_index
+
+    # ------------------------------------------------------------------ handlers
+    def _on_event_add(self, ev: Dict[str, Any]) -> None:
+        recv = self.wall()
+        if self.log.enabled(4):
+            self.log.v(4).info("event received", object=kube.object_key(ev), reason=ev.get("reason"))
+        self.metrics.inc("events_received")
+        if not self.active:
+            return
+        status, results = self.classifier.classify_event(ev, self.lookup)
+        if status == STALE:
+            self._park(ev, recv)
+            return
+        if status != DECIDED:
+            if status == "noop":
+                self.log.v(1).info("no-op event, ignoring", reason=ev.get("reason"), message=ev.get("message"))
+            return
+        origin = parse_k8s_time(ev.get("eventTime")) or parse_k8s_time(ev.get("lastTimestamp")) or recv
+        for r in results:
+            if r.action != A.TO_RUNNING:
+                self.log.info("Algorithm run failed", requestId=r.request_id, algorithm=r.algorithm, reason=r.reason,
+                              message=r.run_status_trace)
+            self._submit(r, origin, recv)
+
+    def _on_event_update(self, old: Dict[str, Any], new: Dict[str, Any]) -> None:
+        if not self.cfg.rules.handle_event_updates or old is new:
+            return
+        if kube.resource_version(old) == kube.resource_version(new):
+            return
+        if old.get("count") == new.get("count") and old.get("reason") == new.get("reason") and old.get("series") == new.get("series"):
+            return
+        self._on_event_add(new)
+
+    def _on_pod_add(self, pod):
+        self._unpark("Pod", kube.name_of(pod))
+        self._on_pod_update(None, pod)
+
+    def _on_pod_update(self, old, pod):
+        if not self.active or old is pod:
+            return
+        recv = self.wall()
+        for r in self.classifier.classify_pod(pod, old):
+            self._submit(r, recv, recv)
+
+    def _on_job_add(self, job):
+        self._unpark("Job", kube.name_of(job))
+        self._on_job_update(None, job)
+
+    def _on_job_update(self, old, job):
+        if not self.active or old is job:
+            return
+        recv = self.wall()
+        for r in self.classifier.classify_job(job, old, self.lookup):
+            self._submit(r, recv, recv)
+
+    # ------------------------------------------------------------------ stale-event parking
+    def _park(self, ev, recv):
+        inv = ev.get("involvedObject") or {}
+        grace = self.cfg.rules.stale_event_grace
+        if grace <= 0:
+            self.log.info("Algorithm object not found - stale event", requestId=inv.get("name"), reason=ev.get("reason"),
+                          message=ev.get("message"))
+            self.metrics.inc("events_stale")
+            return
+        key = (inv.get("kind", ""), inv.get("name", ""))
+        lst = self._parked.setdefault(key, [])
+        lst.append((time.monotonic() + grace, ev, recv))
+        self.metrics.inc("events_parked")
+
+    def _unpark(self, kind, name):
+        if not self._parked:
+            return
+        lst = self._parked.pop((kind, name), None)
+        if lst:
+            for _deadline, ev, _recv in lst:
+                self._on_event_add(ev)
+
+    async def _sweep_parked(self):
+        while True:
+            await asyncio.sleep(max(0.05, min(1.0, self.cfg.rules.stale_event_grace / 4 or 1.0)))
+            now = time.monotonic()
+            for key in list(self._parked):
+                lst = [p for p in self._parked[key] if p[0] > now]
+                dropped = len(self._parked[key]) - len(lst)
+                if dropped:
+                    self.metrics.inc("events_stale", dropped)
+                    self.log.info("Algorithm object not found - stale event", kind=key[0], requestId=key[1])
+                if lst:
+                    self._parked[key] = lst
+                else:
+                    del self._parked[key]
+
+    # ------------------------------------------------------------------ submit
+    def _submit(self, r: RunStatusAnalysisResult, origin: float, recv: float) -> None:
+        key = (r.algorithm, r.request_id)
+        if not r.request_id:
+            self.metrics.inc("decisions_unkeyed")
+            return
+        if not self.owns(key):
+            return
+        applied = self._applied.get(key)
+        if applied is not None and (applied in FINISHED_STAGES or (r.action == A.TO_RUNNING and applied == LifecycleStage.RUNNING)):
+            self.metrics.inc("decisions_suppressed")
+            return
+        if self.cfg.observability.stage_timestamps:
+            r.stamps["origin"] = origin
+            r.stamps["receive"] = recv
+            r.stamps["enqueue"] = self.wall()
+        self.metrics.inc("decisions", labels={"action": r.action})
+        self.pipeline.receive(r)
+
+    # ------------------------------------------------------------------ actuate
+    def _unfinished_stages(self):
+        return tuple(s for s in (LifecycleStage.NEW, LifecycleStage.BUFFERED, LifecycleStage.RUNNING) if s not in FINISHED_STAGES)
+
+    async def _delete_job(self, name: str) -> bool:
+        try:
+            await self.jobs.delete_job(self.namespace, name, "Background")
+            self.metrics.inc("jobs_deleted")
+            return True
+        except NotFound:
+            if self.cfg.compat.delete_not_found_ok:
+                return False
+            raise
+
+    async def supervise_action(self, r: RunStatusAnalysisResult) -> Decision:
+        """Reference ``superviseAction`` (``supervisor.go:261-374``) with the fixes of SURVEY §7.5."""
+        wall = self.wall
+        compat = self.cfg.compat
+        r.attempts += 1
+        stamps = r.stamps
+        if stamps is not None and "dequeue" not in stamps:
+            stamps["dequeue"] = wall()
+        failing = r.action in A.FAILING
+        if r.action not in STAGE_FOR_ACTION:
+            raise ValueError(f"unknown analysis result action: {r.action}")
+        try:
+            cp = await self.store.read_checkpoint(r.algorithm, r.request_id)
+        except Exception as exc:
+            self.log.error(exc, "no checkpoint exists for the provided request, job will be deleted without metadata saved",
+                           requestId=r.request_id, algorithm=r.algorithm)
+            if compat.delete_on_read_error and failing:
+                try:
+                    await self._delete_job(r.request_id)
+                except Exception:
+                    pass
+            raise
+        stamps["read"] = wall()
+        key = (r.algorithm, r.request_id)
+        if cp is None:
+            self.log.info("no checkpoint exists for the provided request, skipping", requestId=r.request_id, algorithm=r.algorithm)
+            deleted = False
+            if compat.delete_on_read_error and failing:
+                deleted = await self._delete_job(r.request_id)
+            self.metrics.inc("decisions_missing_checkpoint")
+            return Decision(r, "skipped-missing", None, deleted)
+        if cp.is_finished():
+            self.log.info("algorithm run completed, skipping action", algorithm=r.algorithm, requestId=r.request_id)
+            deleted = False
+            if r.pending_delete:
+                deleted = await self._delete_job(r.request_id)
+                r.pending_delete = False
+            self._remember(key, cp.lifecycle_stage)
+            self.metrics.inc("decisions_skipped_finished")
+            return Decision(r, "skipped-finished", cp.lifecycle_stage, deleted)
+        stage = STAGE_FOR_ACTION[r.action]()
+        now_dt = _dt.datetime.fromtimestamp(wall(), _dt.timezone.utc)
+        if r.action == A.TO_RUNNING:
+            if cp.lifecycle_stage == LifecycleStage.RUNNING and not compat.full_row_upsert:
+                self._remember(key, stage)
+                return Decision(r, "skipped-already-running", stage, False)
+            await self._write(cp, stage, None, None, now_dt, set_failure=False)
+            stamps["ack"] = wall()
+            self._observe(r)
+            self._remember(key, stage)
+            return Decision(r, "applied", stage, False)
+        cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
+        details = render_trace(r, self.cfg.rules.trace_format)
+        # The reference deletes, then upserts (2 sequential RTTs after the read). Both are
+        # idempotent, so they are issued concurrently; a failed delete is remembered on the
+        # item so the retry still deletes after it sees the (now finished) row.
+        del_res, write_res = await asyncio.gather(
+            self._delete_job(r.request_id),
+            self._write(cp, stage, cause, details, now_dt, set_failure=True),
+            return_exceptions=True,
+        )
+        if isinstance(del_res, BaseException):
+            self.log.error(del_res, "failed to delete an algorithm submission", requestId=r.request_id, algorithm=r.algorithm)
+            r.pending_delete = True
+            raise del_res
+        if isinstance(write_res, BaseException):
+            self.log.error(write_res, "failed to update algorithm submission status", requestId=r.request_id, algorithm=r.algorithm)
+            raise write_res
+        stamps["ack"] = wall()
+        self._observe(r)
+        self._remember(key, stage)
+        self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
+        return Decision(r, "applied", stage, bool(del_res))
+
+    async def _write(self, cp, stage, cause, details, now_dt, set_failure):
+        compat = self.cfg.compat
+        if compat.full_row_upsert:
+            clone = cp.deep_copy()
+            clone.lifecycle_stage = stage
+            if set_failure:
+                clone.algorithm_failure_cause = cause
+                clone.algorithm_failure_details = details
+            clone.last_modified = now_dt
+            await self.store.upsert_checkpoint(clone)
+            return True
+        only_if = (cp.lifecycle_stage,) if compat.conditional_update else None
+        applied = await self.store.update_status(cp.algorithm, cp.id, stage, cause, details, now_dt,
+                                                 only_if_stages=only_if, set_failure=set_failure)
+        if only_if is not None and not applied:
+            raise CasConflict(f"checkpoint {cp.algorithm}/{cp.id} changed concurrently")
+        return True
+
+    def _remember(self, key, stage):
+        self._applied[key] = stage
+        self._applied.move_to_end(key)
+        if len(self._applied) > self._applied_cap:
+            self._applied.popitem(last=False)
+
+    def _observe(self, r: RunStatusAnalysisResult):
+        s = r.stamps
+        ack = s.get("ack")
+        if ack is None:
+            return
+        if "origin" in s:
+            self.metrics.observe_seconds("event_to_checkpoint", ack - s["origin"])
+        if "receive" in s:
+            self.metrics.observe_seconds("receive_to_checkpoint", ack - s["receive"])
+
+    def _done(self, r: RunStatusAnalysisResult, decision: Decision) -> None:
+        for h in self.decision_hooks:
+            h(decision)
+
+    def _dead_letter(self, r: RunStatusAnalysisResult, exc: BaseException) -> None:
+        self.metrics.inc("decisions_dead_lettered")
+        self.log.error(exc, "giving up on decision", requestId=r.request_id, algorithm=r.algorithm, action=r.action)
+        d = Decision(r, "dead-letter", None, False)
+        for h in self.decision_hooks:
+            h(d)

@@ -1,0 +1,80 @@
+"""HBM-OOM vs host-OOM scoring and RCCL/xGMI topology parsing (CPU-only)."""
+import json
+
+from nexus_supervisor_amd.gpu import oom
+from nexus_supervisor_amd.gpu.topology import expected_gpu, merge_process_ranks, rank_env_from_environ, topology_from_env
+
+# verbatim message produced by torch on an MI355X box (profiles/box_probe_r1.json)
+TORCH_HBM_OOM = ("torch.OutOfMemoryError: HIP out of memory. Tried to allocate 431.98 GiB. GPU 0 has a total capacity "
+                 "of 287.98 GiB of which 287.37 GiB is free. Of the allocated memory 0 bytes is allocated by PyTorch")
+
+
+def test_torch_hip_oom_is_hbm():
+    v = oom.analyze([TORCH_HBM_OOM])
+    assert v.kind == "hbm"
+    assert v.gpu_index == 0
+    assert v.capacity_bytes == int(287.98 * (1 << 30))
+    assert v.requested_bytes == int(431.98 * (1 << 30))
+
+
+def test_cgroup_oomkilled_is_host():
+    v = oom.analyze([], [{"reason": "OOMKilled", "exitCode": 137, "container": "algo"}])
+    assert v.kind == "host" and v.host_score >= 1.0
+
+
+def test_oomkilled_wins_tie_with_hip_message():
+    v = oom.analyze([TORCH_HBM_OOM], [{"reason": "OOMKilled", "exitCode": 137}])
+    assert v.kind == "host"
+
+
+def test_vram_peak_evidence_alone_is_hbm_and_attributes_gpu():
+    ev = {"gpus": [{"index": 3, "vram_total_mb": 294896, "vram_peak_mb": 294000},
+                   {"index": 4, "vram_total_mb": 294896, "vram_peak_mb": 1000}]}
+    v = oom.analyze(["RuntimeError: something failed"], [{"exitCode": 1}], ev, expected_gpu="3")
+    assert v.kind == "hbm" and v.gpu_index == 3
+
+
+def test_plain_failure_is_not_oom():
+    v = oom.analyze(["ValueError: bad input"], [{"exitCode": 1, "reason": "Error"}])
+    assert v.kind is None
+
+
+def test_host_memoryerror():
+    v = oom.analyze(["Traceback...\nMemoryError"], [{"exitCode": 1}])
+    assert v.kind == "host"
+
+
+def test_hip_error_variants():
+    for msg in ["hipErrorOutOfMemory: out of memory", "RCCL WARN Cuda failure 'out of memory'",
+                "hipMalloc failed with error 2", "HSA_STATUS_ERROR_OUT_OF_RESOURCES"]:
+        assert oom.analyze([msg]).kind == "hbm", msg
+
+
+def test_topology_from_torchrun_env():
+    env = {"RANK": "5", "WORLD_SIZE": "16", "LOCAL_RANK": "5", "LOCAL_WORLD_SIZE": "8", "MASTER_ADDR": "10.0.0.1",
+           "MASTER_PORT": "29500", "HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7", "NCCL_SOCKET_IFNAME": "eth0",
+           "RCCL_MSCCL_ENABLE": "0", "UNRELATED": "x"}
+    t = topology_from_env(env, gpus_requested=8, node="mi355x-07")
+    assert t["rank"] == 5 and t["world_size"] == 16 and t["local_rank"] == 5
+    assert t["master_addr"] == "10.0.0.1" and t["master_port"] == 29500
+    assert t["expected_gpu"] == "5"
+    assert t["xgmi"] == {"local_gpus": 8, "links_per_gpu": 7, "fully_connected": True}
+    assert t["collective_env"] == {"NCCL_SOCKET_IFNAME": "eth0", "RCCL_MSCCL_ENABLE": "0"}
+    assert t["backend"] == "rccl" and t["node"] == "mi355x-07"
+    json.dumps(t)
+
+
+def test_topology_indexed_job_and_single_gpu():
+    t = topology_from_env({"JOB_COMPLETION_INDEX": "3", "ROCR_VISIBLE_DEVICES": "6"}, gpus_requested=1)
+    assert t["rank"] == 3 and t["expected_gpu"] == "6" and t["visible_devices_var"] == "ROCR_VISIBLE_DEVICES"
+    assert expected_gpu({"visible_devices": ["0", "1"], "local_rank": 9}) is None
+    assert topology_from_env({}) == {}
+
+
+def test_merge_process_ranks_and_environ():
+    ev = {"gpus": [{"index": 2, "procs": [{"pid": 11, "rank": 1, "local_rank": 1}]},
+                   {"index": 1, "procs": [{"pid": 10, "rank": 0, "local_rank": 0}]}]}
+    t = merge_process_ranks({"rank": 0}, ev)
+    assert [e["gpu"] for e in t["rank_map"]] == [1, 2]
+    env = rank_env_from_environ(["RANK=3", "PATH=/bin", "LOCAL_RANK=1", "HIP_VISIBLE_DEVICES=1"])
+    assert env == {"RANK": "3", "LOCAL_RANK": "1", "HIP_VISIBLE_DEVICES": "1"}
