@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""North-star benchmark: pod-fail → checkpoint latency (p50/p99) and events/s at
+10k concurrent jobs (BASELINE.json ``metric``), one supervised GPU-job slot per rank.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--jobs 10000] [--events 1000]
+                    [--transport wire|inproc] [--profile uncapped|reference]
+
+One process per GPU (``torch.distributed.run`` for N>1).  Each rank runs one
+supervisor replica that owns the shard of runs hashed to it (``sharding``), with
+its GPU-job slot's telemetry on ``cuda:LOCAL_RANK`` (native amd-smi monitor; the
+HIP OOM message and VRAM peak of a real HBM-OOM on that GPU seed the synthetic
+hbm-oom failures).  Per-rank work is fixed (weak scaling): ``--jobs`` live runs,
+``--events`` pod failures per step.
+
+A *step* = ``--events`` pod failures (plus replacement-run churn) pushed through
+the watch → informer → classify → keyed pipeline → checkpoint store path, timed
+until the last of them is acknowledged by the store.  ``--transport wire`` (the
+default) runs the real protocols: a fake kube-apiserver streams the watch over
+HTTP and the native CQL server (``nexus-cqlsrv``) holds ``nexus.checkpoints``;
+``inproc`` feeds informers directly and uses the in-memory store.
+
+Rank 0 prints one JSON line; ``value`` = total events/s over all ranks
+(total events ÷ max rank time), ``vs_baseline`` against the reference's derived
+10 decisions/s ceiling (Helm defaults: 10 eps, burst 100, 2 workers).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+REFERENCE_EPS = 10.0  # derived throughput ceiling at Helm defaults
+METRIC = "pod-fail→checkpoint p50/p99 latency + events/sec at 10k concurrent jobs"
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--jobs", type=int, default=10_000, help="concurrent live jobs per rank")
+    ap.add_argument("--events", type=int, default=1000, help="pod-fail events per step per rank")
+    ap.add_argument("--transport", choices=("wire", "inproc"), default="inproc")
+    ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
+                    help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
+    ap.add_argument("--workers", type=int, default=256)
+    ap.add_argument("--no-real-oom", action="store_true", help="skip the real HBM-OOM on the rank's GPU")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args(argv)
+
+
+def real_hbm_oom(local_rank: int, workdir: str):
+    """Run the HIP stress workload to a real HBM OOM on this rank's GPU; returns its
+    termination message (None when unavailable)."""
+    try:
+        from nexus_supervisor_amd._build import binary
+
+        exe = binary("gpu_stress")
+    except Exception as exc:  # noqa: BLE001
+        print(f"[bench] gpu_stress unavailable: {exc}", file=sys.stderr)
+        return None
+    log = os.path.join(workdir, f"termination-{local_rank}.log")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=str(local_rank))
+    try:
+        p = subprocess.run([exe, "hbm-oom", "--chunk-gib", "8", "--linger", "0.6", "--termination-log", log,
+                            "--max-gib", "400"], env=env, capture_output=True, text=True, timeout=120)
+    except subprocess.TimeoutExpired:
+        print("[bench] gpu_stress hbm-oom timed out", file=sys.stderr)
+        return None
+    if p.returncode != 1 or not os.path.exists(log):
+        print(f"[bench] gpu_stress rc={p.returncode}: {p.stderr[-400:]}", file=sys.stderr)
+        return None
+    with open(log) as f:
+        return f.read().strip()
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    has_gpu = torch.cuda.is_available()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        backend = "nccl" if has_gpu else "gloo"
+        if has_gpu:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+    device = torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")
+
+    from nexus_supervisor_amd.bench.runner import BenchConfig, run_rank
+
+    workdir = tempfile.mkdtemp(prefix=f"nexus-bench-r{rank}-")
+    hip_msg = None
+    if has_gpu and not args.no_real_oom:
+        hip_msg = real_hbm_oom(local_rank, workdir)
+
+    def barrier_sync():
+        if dist is not None:
+            if has_gpu:
+                dist.barrier(device_ids=[local_rank])
+            else:
+                dist.barrier()
+        if has_gpu:
+            torch.cuda.synchronize(device)
+
+    cfg = BenchConfig(rank=rank, world=world, local_rank=local_rank, jobs=args.jobs, events=args.events,
+                      steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
+                      workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
+                      workdir=workdir)
+    res = asyncio.run(run_rank(cfg, barrier_sync))
+
+    elapsed = res["elapsed"]
+    stats = torch.tensor([elapsed, float(res["events"]), float(res["errors"])], dtype=torch.float64, device=device)
+    lat = torch.tensor(res["latencies_ms"], dtype=torch.float64, device=device)
+    if dist is not None:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([lat.numel()], dtype=torch.int64, device=device))
+        mlen = int(max(s.item() for s in sizes))
+        padded = torch.full((mlen,), float("nan"), dtype=torch.float64, device=device)
+        padded[: lat.numel()] = lat
+        gathered = [torch.empty(mlen, dtype=torch.float64, device=device) for _ in range(world)]
+        dist.all_gather(gathered, padded)
+        allat = torch.cat(gathered)
+        allat = allat[~torch.isnan(allat)]
+        max_elapsed, total_events, total_errors = mx[0].item(), sm[1].item(), sm[2].item()
+    else:
+        allat = lat
+        max_elapsed, total_events, total_errors = elapsed, float(res["events"]), float(res["errors"])
+    allat = allat.cpu()
+
+    if rank == 0:
+        eps = total_events / max_elapsed if max_elapsed > 0 else 0.0
+        q = torch.quantile(allat, torch.tensor([0.5, 0.99], dtype=torch.float64)).tolist() if allat.numel() else [None, None]
+        out = {
+            "metric": METRIC,
+            "value": round(eps, 2),
+            "unit": "events/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * max_elapsed / max(args.steps, 1), 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(eps / REFERENCE_EPS, 2),
+            "dtype": "n/a (control plane, no GPU compute)",
+            "data": "synthetic pod-failure events, random job ids (no cluster / dataset)",
+            "p50_ms": round(q[0], 3) if q[0] is not None else None,
+            "p99_ms": round(q[1], 3) if q[1] is not None else None,
+            "errors": int(total_errors),
+            "config": {
+                "model": "nexus-supervisor (informer→classify→CQL write), 1 replica-shard per GPU-job slot",
+                "global_batch": args.events * world,
+                "seq_len": None,
+                "parallelism": f"shard{world}",
+                "concurrent_jobs_per_rank": args.jobs,
+                "events_per_step_per_rank": args.events,
+                "transport": args.transport,
+                "profile": args.profile,
+                "store": res.get("store"),
+                "workers": res.get("workers"),
+                "rate_limit_eps": res.get("eps"),
+                "gpu_telemetry": res.get("telemetry"),
+                "real_hbm_oom": bool(hip_msg),
+                "baseline": "reference derived ceiling 10 decisions/s (Helm defaults; BASELINE.md)",
+            },
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

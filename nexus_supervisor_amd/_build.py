@@ -1,0 +1,142 @@
+"""Build the native components in-tree (no pip install; the .so files travel with
+the repo snapshot to GPU boxes).
+
+=====================  ======================================  ==================
+artefact               sources                                 toolchain
+=====================  ======================================  ==================
+``_cql_native``        ``csrc/cql/cql_native.cpp`` (+ proto)   g++ + pybind11
+``_amdsmi_monitor``    ``csrc/amdsmi/gpu_monitor.cpp``         g++ + libamd_smi
+``bin/nexus-cqlsrv``   ``csrc/cqlsrv/*.cpp`` (+ proto)         g++ (epoll)
+``bin/gpu_stress``     ``csrc/stress/gpu_stress.hip``          hipcc gfx950
+=====================  ======================================  ==================
+
+``python -m nexus_supervisor_amd._build [--force] [--only NAME] [--sanitize thread|address]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from typing import Dict, List, Optional
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(ROOT, "csrc")
+BIN = os.path.join(PKG, "bin")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _pybind_includes() -> List[str]:
+    import pybind11
+
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _cxx() -> str:
+    return os.environ.get("CXX", "g++")
+
+
+def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
+    common = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-fvisibility=hidden"]
+    san = [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"] if sanitize else []
+    proto = os.path.join(CSRC, "cql", "cql_proto.hpp")
+    return {
+        "cql_native": {
+            "out": os.path.join(PKG, "_cql_native" + EXT),
+            "srcs": [os.path.join(CSRC, "cql", "cql_native.cpp")],
+            "deps": [proto],
+            "cmd": lambda out, srcs: [_cxx(), *common, "-shared", "-fPIC", *_pybind_includes(), *srcs, "-o", out],
+        },
+        "amdsmi_monitor": {
+            "out": os.path.join(PKG, "_amdsmi_monitor" + EXT),
+            "srcs": [os.path.join(CSRC, "amdsmi", "gpu_monitor.cpp")],
+            "deps": [],
+            "cmd": lambda out, srcs: [_cxx(), *common, "-shared", "-fPIC", *_pybind_includes(), f"-I{ROCM}/include", *srcs,
+                                      f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib", "-pthread", "-o", out],
+            "requires": os.path.join(ROCM, "include", "amd_smi", "amdsmi.h"),
+        },
+        "cqlsrv": {
+            "out": os.path.join(BIN, "nexus-cqlsrv" + (f"-{sanitize}" if sanitize else "")),
+            "srcs": [os.path.join(CSRC, "cqlsrv", "cqlsrv.cpp")],
+            "deps": [proto],
+            "cmd": lambda out, srcs: [_cxx(), *common, *san, "-pthread", f"-I{os.path.join(CSRC, 'cql')}", *srcs, "-o", out],
+        },
+        "gpu_stress": {
+            "out": os.path.join(BIN, "gpu_stress"),
+            "srcs": [os.path.join(CSRC, "stress", "gpu_stress.hip")],
+            "deps": [],
+            "cmd": lambda out, srcs: [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17",
+                                      *srcs, "-o", out],
+            "requires": os.path.join(ROCM, "bin", "hipcc"),
+        },
+    }
+
+
+def _stale(t: Dict) -> bool:
+    out = t["out"]
+    if not os.path.exists(out):
+        return True
+    m = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > m for s in t["srcs"] + t["deps"] + [__file__])
+
+
+def build_one(name: str, t: Dict, force: bool = False, verbose: bool = False) -> str:
+    if t.get("requires") and not os.path.exists(t["requires"]):
+        return f"{name}: skipped (missing {t['requires']})"
+    missing = [s for s in t["srcs"] if not os.path.exists(s)]
+    if missing:
+        return f"{name}: skipped (no sources {missing})"
+    if not force and not _stale(t):
+        return f"{name}: up to date"
+    os.makedirs(os.path.dirname(t["out"]), exist_ok=True)
+    tmp = t["out"] + ".tmp"
+    cmd = t["cmd"](tmp, t["srcs"])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"{name}: build failed\n$ {' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+    os.replace(tmp, t["out"])
+    return f"{name}: built {os.path.relpath(t['out'], ROOT)}"
+
+
+def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optional[str] = None, verbose: bool = False) -> List[str]:
+    ts = targets(sanitize)
+    names = [n for n in ts if not only or n in only]
+    if sanitize:
+        names = [n for n in names if n == "cqlsrv"]
+    with cf.ThreadPoolExecutor(max_workers=min(4, len(names) or 1)) as ex:
+        futs = {ex.submit(build_one, n, ts[n], force, verbose): n for n in names}
+        return [f.result() for f in cf.as_completed(futs)]
+
+
+def binary(name: str) -> str:
+    """Path of a built helper binary, building it on demand."""
+    ts = targets()
+    key = {"nexus-cqlsrv": "cqlsrv", "gpu_stress": "gpu_stress"}[name]
+    t = ts[key]
+    if _stale(t):
+        build_one(key, t)
+    return t["out"]
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", action="append")
+    ap.add_argument("--sanitize", choices=("thread", "address", "undefined"))
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    for line in build(a.force, a.only, a.sanitize, a.verbose):
+        print(line)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -103,6 +103,9 @@ class Classifier:
         self.gpu = gpu or GpuConfig()
         self.evidence = EvidenceBook()
         self.clock = clock
+        # Live GPU evidence for pods without an agent annotation (supervisor co-located
+        # with the GPUs, or a node agent in-process): pod -> evidence record or None.
+        self.evidence_provider: Optional[Callable[[Dict[str, Any]], Optional[Dict[str, Any]]]] = None
 
     # ------------------------------------------------------------ helpers
     def is_nexus(self, obj: Optional[Dict[str, Any]]) -> bool:
@@ -297,6 +300,11 @@ class Classifier:
     def _gpu_evidence(self, pod) -> Optional[Dict[str, Any]]:
         raw = kube.annotations_of(pod).get(self.gpu.evidence_annotation)
         if not raw:
+            if self.evidence_provider is not None:
+                try:
+                    return self.evidence_provider(pod)
+                except Exception:  # evidence is advisory; never fail a decision on it
+                    return None
             return None
         try:
             ev = json.loads(raw)

@@ -1,0 +1,289 @@
+"""GPU telemetry backends and the per-pod evidence record.
+
+:class:`AmdSmiTelemetry` wraps the native monitor (``csrc/amdsmi/gpu_monitor.cpp``
+→ ``_amdsmi_monitor``): amd-smi VRAM/process sampling + the GPU event listener,
+all in native threads.  :class:`FakeTelemetry` is the programmable stand-in used
+on CPU-only hosts and in tests (the sandbox has no ``/dev/kfd``).
+
+:func:`evidence_for` folds a telemetry snapshot into the JSON record the
+classifier consumes (``nexus.amd.com/gpu-evidence``, see
+:mod:`nexus_supervisor_amd.gpu.oom`): the GPUs the pod's processes ran on, each
+with the device-wide VRAM peak *while those processes lived*, the processes'
+ranks (from their environment) and GPU events (VM faults, queue evictions,
+resets) in that window.
+
+The reference has no GPU awareness (``/root/reference/services/supervisor.go``
+classifies on event reasons only); this is the north-star extension.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Any, Dict, Iterable, List, Optional
+
+from .topology import _int
+
+ATTRIBUTION_EVENTS = ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET", "GPU_POST_RESET", "THERMAL_THROTTLE")
+
+
+class TelemetryUnavailable(RuntimeError):
+    pass
+
+
+class GpuTelemetry:
+    """Backend protocol. All methods are cheap and non-blocking (snapshots of native state)."""
+
+    name = "none"
+    interval = 0.25
+
+    def start(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def stop(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def devices(self) -> List[Dict[str, Any]]:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def snapshot(self, include_exited: bool = True) -> List[Dict[str, Any]]:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def drain_events(self) -> List[Dict[str, Any]]:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+def native_monitor_module():
+    """Import the native monitor; raises :class:`TelemetryUnavailable` with the build hint."""
+    try:
+        from .. import _amdsmi_monitor  # type: ignore
+
+        return _amdsmi_monitor
+    except ImportError as exc:  # pragma: no cover - exercised on hosts without the build
+        raise TelemetryUnavailable(
+            "native amd-smi monitor not built: run `python -m nexus_supervisor_amd._build`") from exc
+
+
+class AmdSmiTelemetry(GpuTelemetry):
+    name = "amdsmi"
+
+    def __init__(self, interval: float = 0.25, events: bool = True, retain: float = 600.0, read_proc: bool = True):
+        mod = native_monitor_module()
+        self.interval = interval
+        self._m = mod.GpuMonitor(int(interval * 1000), events, retain, read_proc)
+        self._started = False
+
+    def start(self) -> None:
+        if not self._started:
+            self._m.start()
+            self._started = True
+
+    def stop(self) -> None:
+        if self._started:
+            self._m.stop()
+            self._started = False
+
+    def devices(self):
+        return self._m.devices()
+
+    def snapshot(self, include_exited: bool = True):
+        return self._m.snapshot(include_exited)
+
+    def drain_events(self):
+        return self._m.drain_events()
+
+    def inject_event(self, gpu: int, etype: str, message: str = "") -> None:
+        self._m.inject_event(gpu, etype, message)
+
+    def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:
+        return int(self._m.peak_between(gpu_index, t0, t1))
+
+    @property
+    def samples(self) -> int:
+        return self._m.samples
+
+
+class FakeTelemetry(GpuTelemetry):
+    """In-memory node model: N MI355X GPUs (288 GB HBM3E each), programmable processes,
+    VRAM usage and events — same snapshot format as the native monitor."""
+
+    name = "fake"
+
+    def __init__(self, n_gpus: int = 8, vram_total_mb: int = 294896, clock=time.time):
+        self.clock = clock
+        self._lock = threading.Lock()
+        self._gpus = [{"index": i, "uuid": f"fake-{i:04d}", "hip_uuid": f"GPU-fake{i:012d}", "bdf": f"0000:{0x0a + i:02x}:00.0",
+                       "vram_total_mb": vram_total_mb, "vram_used_mb": 0, "vram_peak_mb": 0,
+                       "ecc_correctable": 0, "ecc_uncorrectable": 0} for i in range(n_gpus)]
+        self._hist: List[List] = [[] for _ in range(n_gpus)]
+        self._procs: Dict[tuple, Dict[str, Any]] = {}
+        self._events: List[Dict[str, Any]] = []
+        self._pending: List[Dict[str, Any]] = []
+
+    def start(self):
+        return None
+
+    def stop(self):
+        return None
+
+    def devices(self):
+        with self._lock:
+            return [{k: g[k] for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb")} | {"hip_id": g["index"],
+                    "market_name": "AMD Instinct MI355X (fake)", "events": True} for g in self._gpus]
+
+    # ---- programming API
+    def set_vram(self, gpu: int, used_mb: int, t: Optional[float] = None) -> None:
+        with self._lock:
+            g = self._gpus[gpu]
+            g["vram_used_mb"] = used_mb
+            g["vram_peak_mb"] = max(g["vram_peak_mb"], used_mb)
+            self._hist[gpu].append((self.clock() if t is None else t, used_mb))
+
+    def add_process(self, pid: int, gpu: int, vram_bytes: int = 0, env: Optional[Dict[str, str]] = None,
+                    pod_uid: str = "", name: str = "python3") -> None:
+        now = self.clock()
+        with self._lock:
+            self._procs[(gpu, pid)] = {"pid": pid, "name": name, "vram_bytes": vram_bytes, "peak_vram_bytes": vram_bytes,
+                                       "cu_occupancy": 0, "alive": True, "first_seen": now, "last_seen": now,
+                                       "pod_uid": pod_uid, "env": dict(env or {}), "gpu": gpu}
+
+    def update_process(self, pid: int, gpu: int, vram_bytes: int) -> None:
+        with self._lock:
+            p = self._procs[(gpu, pid)]
+            p["vram_bytes"] = vram_bytes
+            p["peak_vram_bytes"] = max(p["peak_vram_bytes"], vram_bytes)
+            p["last_seen"] = self.clock()
+
+    def end_process(self, pid: int, gpu: int) -> None:
+        with self._lock:
+            p = self._procs[(gpu, pid)]
+            p["alive"] = False
+            p["last_seen"] = self.clock()
+        self.inject_event(gpu, "PROCESS_END", f"pid {pid}")
+
+    def inject_event(self, gpu: int, etype: str, message: str = "") -> None:
+        e = {"gpu": gpu, "type": etype, "message": message, "t": self.clock()}
+        with self._lock:
+            self._events.append(e)
+            self._pending.append(e)
+
+    # ---- protocol
+    def snapshot(self, include_exited: bool = True):
+        with self._lock:
+            out = []
+            for g in self._gpus:
+                d = dict(g)
+                d["procs"] = [{k: v for k, v in p.items() if k != "gpu"} for p in self._procs.values()
+                              if p["gpu"] == g["index"] and (p["alive"] or include_exited)]
+                d["events"] = [dict(e) for e in self._events if e["gpu"] == g["index"]][-256:]
+                out.append(d)
+            return out
+
+    def drain_events(self):
+        with self._lock:
+            out, self._pending = self._pending, []
+            return out
+
+    def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:
+        with self._lock:
+            return max((u for t, u in self._hist[gpu_index] if t0 <= t <= t1), default=0)
+
+
+def has_amd_gpu() -> bool:
+    return os.path.exists("/dev/kfd")
+
+
+def make_telemetry(backend: str = "auto", interval: float = 0.25) -> Optional[GpuTelemetry]:
+    """``auto``: native amd-smi when a GPU is present (fails loudly if the extension is
+    missing there), else none; ``amdsmi``/``fake``/``none`` force a backend."""
+    if backend == "none":
+        return None
+    if backend == "fake":
+        return FakeTelemetry()
+    if backend == "amdsmi" or (backend == "auto" and has_amd_gpu()):
+        return AmdSmiTelemetry(interval=interval)
+    return None
+
+
+def _rank_fields(env: Dict[str, str]) -> Dict[str, Any]:
+    out: Dict[str, Any] = {}
+    for var, key in (("RANK", "rank"), ("LOCAL_RANK", "local_rank"), ("WORLD_SIZE", "world_size"),
+                     ("LOCAL_WORLD_SIZE", "local_world_size")):
+        v = _int(env.get(var))
+        if v is not None:
+            out[key] = v
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        if env.get(var):
+            out["visible_devices"] = env[var]
+            break
+    return out
+
+
+def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterable[int] = (), pids: Iterable[int] = (),
+                 lookback: float = 300.0, now: Optional[float] = None, node: str = "",
+                 snapshot: Optional[List[Dict[str, Any]]] = None) -> Optional[Dict[str, Any]]:
+    """Evidence record for one pod (matched by cgroup pod UID, PIDs or explicit GPU indices)."""
+    snap = snapshot if snapshot is not None else telemetry.snapshot(True)
+    now = time.time() if now is None else now
+    pids = set(pids)
+    wanted = set(int(i) for i in gpu_indices)
+    grace = 2 * max(telemetry.interval, 0.05)
+    gpus = []
+    for g in snap:
+        procs = [p for p in g.get("procs", [])
+                 if (pod_uid and p.get("pod_uid") == pod_uid) or (p.get("pid") in pids)]
+        if not procs and g["index"] not in wanted:
+            continue
+        if procs:
+            t0 = min(p["first_seen"] for p in procs) - grace
+            t1 = max(p["last_seen"] for p in procs) + grace
+        else:
+            t0, t1 = now - lookback, now
+        peak = telemetry.peak_between(g["index"], t0, t1) or 0
+        rec: Dict[str, Any] = {"index": g["index"], "uuid": g.get("hip_uuid") or g.get("uuid"),
+                               "bdf": g.get("bdf"), "vram_total_mb": g.get("vram_total_mb"),
+                               "vram_used_mb": g.get("vram_used_mb"), "vram_peak_mb": peak,
+                               "window": [round(t0, 3), round(t1, 3)]}
+        if g.get("ecc_uncorrectable"):
+            rec["ecc_uncorrectable"] = g["ecc_uncorrectable"]
+        rec["procs"] = [dict({"pid": p["pid"], "vram_bytes": p.get("vram_bytes", 0),
+                              "peak_vram_bytes": p.get("peak_vram_bytes", 0), "alive": p.get("alive", False)},
+                             **_rank_fields(p.get("env") or {})) for p in procs]
+        evs = [{"type": e["type"], "t": round(e["t"], 3), "message": (e.get("message") or "")[:200]}
+               for e in g.get("events", []) if e["type"] in ATTRIBUTION_EVENTS and t0 <= e["t"] <= t1 + grace]
+        if evs:
+            rec["events"] = evs
+        gpus.append(rec)
+    if not gpus:
+        return None
+    out: Dict[str, Any] = {"source": telemetry.name, "t": round(now, 3), "gpus": gpus}
+    if node:
+        out["node"] = node
+    if pod_uid:
+        out["pod_uid"] = pod_uid
+    return out
+
+
+def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/gpu", node: str = "",
+                          lookback: float = 300.0):
+    """Classifier hook (``Classifier.evidence_provider``): live evidence for a pod from a
+    co-located telemetry backend, matched by pod UID (cgroup) or the pod's expected GPU
+    (``visible_devices[local_rank]`` from its env)."""
+    from ..models import kube
+    from .topology import topology_from_pod
+
+    def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+        topo = topology_from_pod(pod, gpu_resource)
+        gpus = []
+        exp = topo.get("expected_gpu")
+        if exp is not None and str(exp).isdigit():
+            gpus.append(int(exp))
+        elif topo.get("visible_devices"):
+            gpus.extend(int(d) for d in topo["visible_devices"] if str(d).isdigit())
+        return evidence_for(telemetry, pod_uid=kube.uid_of(pod), gpu_indices=gpus, lookback=lookback,
+                            node=node or (pod.get("spec") or {}).get("nodeName", ""))
+
+    return provider
