@@ -48,13 +48,15 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--jobs", type=int, default=10_000, help="concurrent live jobs per rank")
     ap.add_argument("--events", type=int, default=1000, help="pod-fail events per step per rank")
-    ap.add_argument("--transport", choices=("wire", "inproc"), default="inproc")
+    ap.add_argument("--transport", choices=("wire", "inproc"), default="wire")
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--no-real-oom", action="store_true", help="skip the real HBM-OOM on the rank's GPU")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--pprof-out", default="", help="write a pprof profile of the timed steps (rank 0)")
+    ap.add_argument("--cql-latency-us", type=int, default=0, help="inject CQL server response latency")
     return ap.parse_args(argv)
 
 
@@ -121,7 +123,8 @@ def main(argv=None) -> int:
     cfg = BenchConfig(rank=rank, world=world, local_rank=local_rank, jobs=args.jobs, events=args.events,
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
-                      workdir=workdir)
+                      workdir=workdir, cql_latency_us=args.cql_latency_us,
+                      pprof_out=args.pprof_out if rank == 0 else "")
     res = asyncio.run(run_rank(cfg, barrier_sync))
 
     elapsed = res["elapsed"]
@@ -180,6 +183,8 @@ def main(argv=None) -> int:
                 "rate_limit_eps": res.get("eps"),
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
+                "cql_latency_us": args.cql_latency_us,
+                "stages_ms": res.get("stages"),
                 "baseline": "reference derived ceiling 10 decisions/s (Helm defaults; BASELINE.md)",
             },
         }

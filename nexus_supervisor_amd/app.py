@@ -1,0 +1,163 @@
+"""Composition root: config → store, kube client, informers, supervisor, GPU
+telemetry, leader election, HTTP observability.
+
+Mirrors the reference's process entry and DI builder
+(``/root/reference/main.go:12-43``; ``/root/reference/app/app_dependencies.go:12-85``):
+store selection by ``cql-store-type`` (unknown → exit 1, ``main.go:28-36``),
+kube client from ``kube-config-path`` (empty → in-cluster), supervisor wiring,
+then ``Init`` + ``Start``.  Added: SIGTERM drain (the reference has none,
+SURVEY §3E), leader election / sharding gating, GPU attribution and the
+``/metrics`` ``/healthz`` ``/readyz`` ``/debug/pprof`` endpoints.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import signal
+import socket
+import sys
+from typing import Optional
+
+from . import __version__
+from .config import load_config, redacted
+from .config.schema import CQL_STORE_MEMORY, SupervisorConfig
+from .informer import InformerFactory
+from .obs.logging import KLogger, configure_logging
+from .obs.metrics import DogStatsd, Metrics
+from .store.base import CheckpointStore
+from .supervisor import JobClient, Supervisor
+
+
+def build_store(cfg: SupervisorConfig) -> CheckpointStore:
+    if cfg.cql_store_type == CQL_STORE_MEMORY:
+        from .store.memory import MemoryStore
+
+        return MemoryStore()
+    from .store.cql import CqlCheckpointStore
+
+    return CqlCheckpointStore.from_config(cfg)
+
+
+def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
+    from .kube.client import KubeListWatch
+
+    ns = cfg.resource_namespace
+    sel = f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}" if cfg.informer_label_selector else ""
+
+    def lw(kind: str):
+        return KubeListWatch(client, kind, ns, label_selector=sel if kind in ("Pod", "Job") else "",
+                             watch_timeout=int(cfg.watch_timeout))
+
+    return InformerFactory(lw, resync_period=cfg.resync_period)
+
+
+class Application:
+    def __init__(self, cfg: SupervisorConfig, *, kube=None, store: Optional[CheckpointStore] = None,
+                 jobs: Optional[JobClient] = None, factory: Optional[InformerFactory] = None, telemetry=None,
+                 logger: Optional[KLogger] = None, metrics: Optional[Metrics] = None):
+        self.cfg = cfg
+        self.log = logger or KLogger()
+        self.metrics = metrics or Metrics(cfg.observability.statsd_name, {"version": __version__})
+        if kube is None and (factory is None or jobs is None):
+            from .kube.client import KubeClient, KubeConfig
+
+            kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+        self.kube = kube
+        self.store = store if store is not None else build_store(cfg)
+        self.factory = factory if factory is not None else build_factory(cfg, kube)
+        self.supervisor = Supervisor(cfg, self.store, jobs if jobs is not None else kube, self.factory,
+                                     logger=self.log, metrics=self.metrics)
+        self.telemetry = telemetry
+        self.elector = None
+        self.http = None
+        self._stopped = asyncio.Event()
+
+    async def start(self) -> None:
+        cfg = self.cfg
+        self.log.info("Starting Nexus Supervisor", version=__version__, namespace=cfg.resource_namespace,
+                      store=cfg.cql_store_type)
+        await self.store.connect()
+        if self.telemetry is None and cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry:
+            from .gpu.telemetry import make_telemetry
+
+            self.telemetry = make_telemetry(cfg.gpu.backend, cfg.gpu.sample_interval)
+        if self.telemetry is not None:
+            from .gpu.telemetry import pod_evidence_provider
+
+            self.telemetry.start()
+            self.supervisor.classifier.evidence_provider = pod_evidence_provider(
+                self.telemetry, cfg.gpu.gpu_resource_name, node=os.environ.get("NODE_NAME", ""))
+        self.supervisor.init()
+        if cfg.observability.http_port:
+            from .obs.http import ObsServer
+
+            self.http = ObsServer(self)
+            await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
+        if cfg.leader_election.enabled:
+            from .ha.leader import LeaderElector, LeaseLock
+
+            le = cfg.leader_election
+            identity = le.identity or os.environ.get("POD_NAME") or f"{socket.gethostname()}-{os.getpid()}"
+            self.supervisor.active = False
+            self.elector = LeaderElector(
+                LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, identity),
+                lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
+                on_started_leading=lambda: self.supervisor.set_active(True),
+                on_stopped_leading=lambda: self.supervisor.set_active(False), metrics=self.metrics)
+        await self.supervisor.start()
+        if self.elector is not None:
+            self.elector.start()
+
+    def ready(self) -> bool:
+        return self.factory is not None and all(i.has_synced() for i in self.factory.informers.values())
+
+    async def stop(self, drain_timeout: float = 10.0) -> None:
+        if self.elector is not None:
+            await self.elector.stop(release=True)
+        await self.supervisor.stop(drain=True, timeout=drain_timeout)
+        if self.http is not None:
+            await self.http.stop()
+        if self.telemetry is not None:
+            self.telemetry.stop()
+        await self.store.close()
+        if self.kube is not None:
+            await self.kube.close()
+        self._stopped.set()
+
+    async def run(self, stop: asyncio.Event) -> None:
+        await self.start()
+        await stop.wait()
+        self.log.info("shutting down: draining in-flight decisions")
+        await self.stop()
+
+
+def main(argv=None) -> int:
+    """Process entry (``/root/reference/main.go:12-43``)."""
+    cfg = load_config()
+    log = configure_logging(cfg.log_level, static={"service": "nexus-supervisor"})
+    metrics = Metrics(cfg.observability.statsd_name, {"version": __version__})
+    metrics.statsd = DogStatsd.from_env(cfg.observability.statsd_name)
+    log.v(1).info("configuration", config=redacted(cfg))
+
+    async def amain() -> int:
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            loop.add_signal_handler(sig, stop.set)
+        try:
+            app = Application(cfg, logger=log, metrics=metrics)
+        except Exception as exc:  # noqa: BLE001 - fatal init (klog.FlushAndExit analog)
+            log.error(exc, "failed to initialise application services")
+            return 1
+        try:
+            await app.run(stop)
+        except Exception as exc:  # noqa: BLE001
+            log.error(exc, "supervisor failed")
+            return 1
+        return 0
+
+    return asyncio.run(amain())
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,116 @@
+"""Synthetic cluster process for the wire-mode benchmark.
+
+Runs, in its own process (so its CPU does not count against the supervisor's
+event loop): the fake kube-apiserver, the :class:`~.workload.Workload`
+generator, and the "receiver" role that inserts each new run's checkpoint row
+into the CQL store before the run's pods exist (what nexus's receiver does
+upstream of the supervisor).  A small control API drives it:
+
+``POST /bench/init {"jobs": N, "seed": s, ...}``  create the live runs (+ rows)
+``POST /bench/step {"events": E}``                fail E runs, replace them; returns
+                                                    ``{"rids": [...], "t_push": monotonic}``
+
+``python -m nexus_supervisor_amd.bench.cluster_proc --ready-file F --cql HOST:PORT``
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+from aiohttp import web
+
+
+async def amain(args) -> None:
+    from ..store.cql import CqlCheckpointStore, CqlSession
+    from ..testing.fake_apiserver import FakeApiServer
+    from .workload import DEFAULT_HIP_OOM, Workload
+
+    api = FakeApiServer(history=args.history, bookmark_interval=2.0)
+    host, _, port = args.cql.partition(":")
+    store = CqlCheckpointStore(CqlSession([(host, int(port))], connections_per_host=2, consistency="ONE"), consistency="ONE")
+    await store.connect()
+    state = {"wl": None}
+
+    async def write_rows(rows):
+        sem = asyncio.Semaphore(512)
+
+        async def one(r):
+            async with sem:
+                await store.upsert_checkpoint(r)
+
+        await asyncio.gather(*(one(r) for r in rows))
+
+    async def h_init(req):
+        p = await req.json()
+        wl = Workload(p.get("jobs", 10_000), rank=p.get("rank", 0), world=p.get("world", 1), seed=p.get("seed", 0),
+                      hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=p.get("shards", 1),
+                      shard_index=p.get("shard_index", 0))
+        objs, rows = wl.initial()
+        await write_rows(rows)
+        for o in objs:
+            api.create(o)
+        state["wl"] = wl
+        return web.json_response({"objects": len(objs), "rows": len(rows), "rv": api.rv})
+
+    async def h_step(req):
+        p = await req.json()
+        wl = state["wl"]
+        failed, traffic, rows = wl.step(int(p["events"]))
+        await write_rows(rows)
+        t_push = time.monotonic()
+        for etype, obj in traffic:
+            if etype == "ADDED":
+                api.create(obj)
+            else:
+                api.update(obj)
+        return web.json_response({"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}})
+
+    async def h_stats(req):
+        return web.json_response({"requests": api.requests, "watch_requests": api.watch_requests, "rv": api.rv,
+                                  "deleted": len(api.deleted)})
+
+    url = await api.start(args.host, args.port)
+    # control routes live on a second tiny app (the apiserver app is frozen once started)
+    ctl = web.Application(client_max_size=64 << 20)
+    ctl.router.add_post("/bench/init", h_init)
+    ctl.router.add_post("/bench/step", h_step)
+    ctl.router.add_get("/bench/stats", h_stats)
+    runner = web.AppRunner(ctl, access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, args.host, 0)
+    await site.start()
+    ctl_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+    tmp = args.ready_file + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump({"api": url, "ctl": f"http://{args.host}:{ctl_port}", "pid": os.getpid()}, f)
+    os.replace(tmp, args.ready_file)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    import signal
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    await stop.wait()
+    await runner.cleanup()
+    await api.stop()
+    await store.close()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--cql", required=True)
+    ap.add_argument("--ready-file", required=True)
+    ap.add_argument("--history", type=int, default=400_000)
+    args = ap.parse_args(argv)
+    asyncio.run(amain(args))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

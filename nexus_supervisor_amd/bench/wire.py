@@ -1,0 +1,110 @@
+"""Wire-mode benchmark harness: supervisor (this process) ↔ fake kube-apiserver over
+HTTP watch (cluster process) and ↔ native CQL server over TCP.
+
+Process layout per rank::
+
+    nexus-cqlsrv  ◄── CQL v4 ──  supervisor (rank process)  ── HTTP list/watch/DELETE ──►  cluster_proc
+         ▲                                                                                  (apiserver +
+         └──────────────────────────── CQL v4 (receiver inserts new rows) ───────────────── workload)
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import time
+from typing import List, Tuple
+
+import aiohttp
+
+from ..app import Application
+from ..config.schema import SupervisorConfig
+from ..kube.client import KubeClient, KubeConfig
+from ..models.checkpoint import create_index_cql, create_table_cql
+from ..store.cql import CqlCheckpointStore, CqlSession
+from ..testing.cqlsrv import CqlServer
+
+
+def schema_statements(ks: str = "nexus", table: str = "checkpoints") -> List[str]:
+    return ([f"CREATE KEYSPACE IF NOT EXISTS {ks} WITH replication = {{'class': 'SimpleStrategy', 'replication_factor': 1}}",
+             create_table_cql(ks, table)] + list(create_index_cql(ks, table)))
+
+
+class WireHarness:
+    store_name = "cql (nexus-cqlsrv over TCP)"
+
+    def __init__(self, sc: SupervisorConfig, cfg, workdir: str):
+        self.sc = sc
+        self.cfg = cfg
+        self.workdir = workdir
+        self.cql: CqlServer = None
+        self.proc: subprocess.Popen = None
+        self.app: Application = None
+        self.ctl = ""
+        self.http: aiohttp.ClientSession = None
+
+    async def start(self) -> None:
+        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=self.cfg.cql_latency_us).start()
+        ready = os.path.join(self.workdir, "cluster.ready")
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
+        self._log = open(os.path.join(self.workdir, "cluster.log"), "ab")
+        self.proc = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd.bench.cluster_proc", "--cql",
+                                      f"127.0.0.1:{self.cql.port}", "--ready-file", ready], env=env,
+                                     stdout=self._log, stderr=self._log, start_new_session=True)
+        deadline = time.monotonic() + 120
+        while not os.path.exists(ready):
+            if self.proc.poll() is not None or time.monotonic() > deadline:
+                raise RuntimeError(f"cluster process failed to start (rc={self.proc.poll()})")
+            await asyncio.sleep(0.05)
+        with open(ready) as f:
+            info = json.load(f)
+        self.ctl = info["ctl"]
+        self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=600))
+        async with self.http.post(self.ctl + "/bench/init", json={
+                "jobs": self.cfg.jobs, "seed": self.cfg.seed, "rank": self.cfg.rank, "world": self.cfg.world,
+                "shards": self.cfg.world, "shard_index": self.cfg.rank,
+                "hip_oom_message": self.cfg.hip_oom_message}) as r:
+            r.raise_for_status()
+            await r.json()
+        sc = self.sc
+        sc.cql_store_type = "scylla"
+        sc.scylla_cql_store.hosts = [f"127.0.0.1:{self.cql.port}"]
+        sc.scylla_cql_store.consistency = "LOCAL_QUORUM"
+        kube = KubeClient(KubeConfig(info["api"]), max_connections=64)
+        store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql.port)],
+                                              connections_per_host=sc.scylla_cql_store.connections_per_host))
+        self.app = Application(sc, kube=kube, store=store)
+        await self.app.start()
+        ok = await self.app.factory.wait_for_cache_sync(120)
+        if not ok:
+            raise RuntimeError("informer caches did not sync")
+
+    @property
+    def supervisor(self):
+        return self.app.supervisor
+
+    async def step(self, events: int) -> Tuple[List[str], float]:
+        async with self.http.post(self.ctl + "/bench/step", json={"events": events}) as r:
+            r.raise_for_status()
+            doc = await r.json()
+        return doc["rids"], doc["t_push"]
+
+    async def stop(self) -> None:
+        try:
+            if self.app is not None:
+                await self.app.stop(drain_timeout=5)
+        finally:
+            if self.http is not None:
+                await self.http.close()
+            if self.proc is not None and self.proc.poll() is None:
+                self.proc.terminate()
+                try:
+                    self.proc.wait(10)
+                except subprocess.TimeoutExpired:
+                    self.proc.kill()
+            if self.cql is not None:
+                self.cql.stop()
+            if getattr(self, "_log", None):
+                self._log.close()

@@ -120,6 +120,11 @@ class GpuConfig:
     gpu_resource_name: str = field(default="amd.com/gpu", metadata=_k("gpu-resource-name"))
     backend: str = field(default="auto", metadata=_k("backend"))  # auto | amdsmi | fake | none
     sample_interval: float = field(default=0.5, metadata=_k("sample-interval", "duration"))
+    # read GPUs of the node this process runs on (in-node supervisor / bench); the cluster
+    # deployment instead reads the node agents' pod annotations
+    local_telemetry: bool = field(default=False, metadata=_k("local-telemetry"))
+    # node agent: how often to publish evidence, and whether to annotate failed pods
+    agent_publish: bool = field(default=True, metadata=_k("agent-publish"))
 
 
 @dataclass
@@ -166,6 +171,9 @@ class SupervisorConfig:
     workers: int = field(default=2, metadata=_k("workers"))
     # ---- extensions ----
     resync_period: float = field(default=30.0, metadata=_k("resync-period", "duration"))
+    # server-side label selector on the Pod/Job informers (only Nexus runs are cached)
+    informer_label_selector: bool = field(default=True, metadata=_k("informer-label-selector"))
+    watch_timeout: float = field(default=300.0, metadata=_k("watch-timeout", "duration"))
     max_retries: int = field(default=16, metadata=_k("max-retries"))  # 0 = retry forever
     compat: CompatConfig = field(default_factory=CompatConfig, metadata=_k("compat"))
     labels: LabelConfig = field(default_factory=LabelConfig, metadata=_k("labels"))

@@ -1,0 +1,319 @@
+"""Minimal asyncio Kubernetes REST client: LIST + WATCH, DELETE, PATCH, Leases.
+
+Replaces client-go's clientset + reflectors in the reference
+(``/root/reference/app/app_dependencies.go:36-53`` builds the clientset from
+``kube-config-path`` — empty means in-cluster; ``services/supervisor.go:70-75``
+builds namespaced Event/Pod/Job informers; ``:262-291`` deletes Jobs with
+``PropagationPolicy=Background``).  The Python ``kubernetes`` package is not
+available offline, so the REST + watch protocol is spoken directly:
+
+* auth: in-cluster service-account token (re-read periodically — projected
+  tokens rotate) + CA, or a kubeconfig (token, client cert/key, basic auth,
+  CA data or file, ``insecure-skip-tls-verify``);
+* LIST with ``limit``/``continue`` pagination; WATCH from the list's
+  ``resourceVersion`` with ``allowWatchBookmarks`` and a server timeout, decoded
+  line-by-line from the chunked stream; ``410 Gone`` surfaces as an ERROR event
+  (the informer re-lists);
+* ``ListWatch`` adapter for :mod:`..informer`.
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import json
+import logging
+import os
+import ssl
+import tempfile
+import time
+from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
+
+import aiohttp
+
+from ..informer.informer import ListWatch
+from .errors import ApiError, from_status
+
+log = logging.getLogger("nexus_supervisor_amd.kube")
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+# kind -> (api prefix, plural)
+RESOURCES: Dict[str, Tuple[str, str]] = {
+    "Event": ("/api/v1", "events"),
+    "Pod": ("/api/v1", "pods"),
+    "Job": ("/apis/batch/v1", "jobs"),
+    "Lease": ("/apis/coordination.k8s.io/v1", "leases"),
+    "Node": ("/api/v1", "nodes"),
+}
+
+
+def resource_path(kind: str, namespace: Optional[str], name: Optional[str] = None) -> str:
+    prefix, plural = RESOURCES[kind]
+    p = f"{prefix}/namespaces/{namespace}/{plural}" if namespace else f"{prefix}/{plural}"
+    return f"{p}/{name}" if name else p
+
+
+class KubeConfig:
+    def __init__(self, server: str, token: str = "", token_file: str = "", ca_data: Optional[bytes] = None,
+                 ca_file: str = "", cert_data: Optional[bytes] = None, key_data: Optional[bytes] = None,
+                 insecure: bool = False, username: str = "", password: str = "", namespace: str = ""):
+        self.server = server.rstrip("/")
+        self.token = token
+        self.token_file = token_file
+        self.ca_data, self.ca_file = ca_data, ca_file
+        self.cert_data, self.key_data = cert_data, key_data
+        self.insecure = insecure
+        self.username, self.password = username, password
+        self.namespace = namespace
+        self._token_read = 0.0
+
+    @classmethod
+    def in_cluster(cls) -> "KubeConfig":
+        host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        if not host:
+            raise ApiError(0, "ConfigError", "not running in a cluster (KUBERNETES_SERVICE_HOST unset) and no kube-config-path")
+        if ":" in host and not host.startswith("["):
+            host = f"[{host}]"
+        ns = ""
+        try:
+            with open(os.path.join(SA_DIR, "namespace")) as f:
+                ns = f.read().strip()
+        except OSError:
+            pass
+        return cls(f"https://{host}:{port}", token_file=os.path.join(SA_DIR, "token"),
+                   ca_file=os.path.join(SA_DIR, "ca.crt"), namespace=ns)
+
+    @classmethod
+    def from_file(cls, path: str, context: Optional[str] = None) -> "KubeConfig":
+        import yaml
+
+        with open(path) as f:
+            doc = yaml.safe_load(f) or {}
+        base = os.path.dirname(os.path.abspath(path))
+        ctx_name = context or doc.get("current-context")
+        ctxs = {c["name"]: c.get("context", {}) for c in doc.get("contexts", [])}
+        ctx = ctxs.get(ctx_name) or (next(iter(ctxs.values())) if ctxs else {})
+        clusters = {c["name"]: c.get("cluster", {}) for c in doc.get("clusters", [])}
+        users = {u["name"]: u.get("user", {}) for u in doc.get("users", [])}
+        cl = clusters.get(ctx.get("cluster"), next(iter(clusters.values()), {}))
+        us = users.get(ctx.get("user"), {})
+
+        def data(d, key):
+            if d.get(f"{key}-data"):
+                return base64.b64decode(d[f"{key}-data"])
+            p = d.get(key)
+            if p:
+                p = p if os.path.isabs(p) else os.path.join(base, p)
+                with open(p, "rb") as fh:
+                    return fh.read()
+            return None
+
+        token = us.get("token", "")
+        token_file = us.get("tokenFile", "")
+        return cls(cl.get("server", ""), token=token, token_file=token_file, ca_data=data(cl, "certificate-authority"),
+                   cert_data=data(us, "client-certificate"), key_data=data(us, "client-key"),
+                   insecure=bool(cl.get("insecure-skip-tls-verify")), username=us.get("username", ""),
+                   password=us.get("password", ""), namespace=ctx.get("namespace", ""))
+
+    @classmethod
+    def load(cls, kube_config_path: str = "") -> "KubeConfig":
+        """``kube-config-path`` semantics of the reference: empty → in-cluster
+        (``/root/reference/app/app_dependencies.go:39``)."""
+        return cls.from_file(kube_config_path) if kube_config_path else cls.in_cluster()
+
+    def bearer(self) -> str:
+        if self.token_file and (not self.token or time.monotonic() - self._token_read > 60):
+            try:
+                with open(self.token_file) as f:
+                    self.token = f.read().strip()
+                self._token_read = time.monotonic()
+            except OSError as exc:
+                log.warning("cannot read service account token %s: %s", self.token_file, exc)
+        return self.token
+
+    def ssl_context(self) -> Optional[ssl.SSLContext]:
+        if not self.server.startswith("https"):
+            return None
+        ctx = ssl.create_default_context()
+        if self.insecure:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        elif self.ca_data:
+            ctx = ssl.create_default_context(cadata=self.ca_data.decode())
+        elif self.ca_file and os.path.exists(self.ca_file):
+            ctx = ssl.create_default_context(cafile=self.ca_file)
+        if self.cert_data and self.key_data:
+            with tempfile.TemporaryDirectory() as d:
+                cp, kp = os.path.join(d, "c"), os.path.join(d, "k")
+                with open(cp, "wb") as f:
+                    f.write(self.cert_data)
+                with open(kp, "wb") as f:
+                    f.write(self.key_data)
+                ctx.load_cert_chain(cp, kp)
+        return ctx
+
+
+class KubeClient:
+    def __init__(self, config: KubeConfig, *, request_timeout: float = 30.0, max_connections: int = 32,
+                 user_agent: str = "nexus-supervisor-amd/0.1"):
+        self.config = config
+        self.request_timeout = request_timeout
+        self.max_connections = max_connections
+        self.user_agent = user_agent
+        self._session: Optional[aiohttp.ClientSession] = None
+        self.requests = 0
+
+    async def _s(self) -> aiohttp.ClientSession:
+        if self._session is None or self._session.closed:
+            conn = aiohttp.TCPConnector(limit=self.max_connections, ssl=self.config.ssl_context() or False,
+                                        enable_cleanup_closed=True)
+            self._session = aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None, sock_connect=10),
+                                                  headers={"User-Agent": self.user_agent, "Accept": "application/json"},
+                                                  json_serialize=json.dumps)
+        return self._session
+
+    def _headers(self, extra: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+        h: Dict[str, str] = {}
+        tok = self.config.bearer()
+        if tok:
+            h["Authorization"] = f"Bearer {tok}"
+        elif self.config.username:
+            raw = f"{self.config.username}:{self.config.password}".encode()
+            h["Authorization"] = "Basic " + base64.b64encode(raw).decode()
+        if extra:
+            h.update(extra)
+        return h
+
+    async def close(self) -> None:
+        if self._session is not None:
+            await self._session.close()
+            self._session = None
+
+    async def request(self, method: str, path: str, *, params: Optional[Dict[str, Any]] = None, body: Any = None,
+                      content_type: str = "application/json", timeout: Optional[float] = None) -> Dict[str, Any]:
+        s = await self._s()
+        self.requests += 1
+        data = json.dumps(body) if body is not None else None
+        async with s.request(method, self.config.server + path, params=params, data=data,
+                             headers=self._headers({"Content-Type": content_type} if data is not None else None),
+                             timeout=aiohttp.ClientTimeout(total=timeout or self.request_timeout)) as r:
+            raw = await r.read()
+            try:
+                doc = json.loads(raw) if raw else {}
+            except ValueError:
+                doc = {"message": raw[:500].decode("utf-8", "replace")}
+            if r.status >= 400:
+                raise from_status(r.status, doc)
+            return doc
+
+    # ------------------------------------------------------------------ typed helpers
+    async def list(self, kind: str, namespace: Optional[str], *, label_selector: str = "", field_selector: str = "",
+                   limit: int = 500) -> Tuple[List[Dict[str, Any]], str]:
+        items: List[Dict[str, Any]] = []
+        cont = ""
+        rv = ""
+        while True:
+            params: Dict[str, Any] = {"limit": str(limit)}
+            if label_selector:
+                params["labelSelector"] = label_selector
+            if field_selector:
+                params["fieldSelector"] = field_selector
+            if cont:
+                params["continue"] = cont
+            doc = await self.request("GET", resource_path(kind, namespace), params=params)
+            api_version, k = doc.get("apiVersion", ""), kind
+            for it in doc.get("items") or []:
+                it.setdefault("kind", k)
+                if api_version:
+                    it.setdefault("apiVersion", api_version)
+                items.append(it)
+            meta = doc.get("metadata") or {}
+            rv = meta.get("resourceVersion", rv)
+            cont = meta.get("continue", "")
+            if not cont:
+                return items, rv
+
+    async def watch(self, kind: str, namespace: Optional[str], resource_version: str, *, label_selector: str = "",
+                    field_selector: str = "", timeout_seconds: int = 300) -> AsyncIterator[Tuple[str, Dict[str, Any]]]:
+        s = await self._s()
+        params = {"watch": "1", "resourceVersion": resource_version, "allowWatchBookmarks": "true",
+                  "timeoutSeconds": str(timeout_seconds)}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        self.requests += 1
+        async with s.get(self.config.server + resource_path(kind, namespace), params=params, headers=self._headers(),
+                         timeout=aiohttp.ClientTimeout(total=timeout_seconds + 30, sock_read=timeout_seconds + 30)) as r:
+            if r.status >= 400:
+                doc = {}
+                try:
+                    doc = json.loads(await r.read())
+                except ValueError:
+                    pass
+                if r.status == 410:
+                    yield "ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": doc.get("message", "")}
+                    return
+                raise from_status(r.status, doc)
+            loads = json.loads
+            buf = b""
+            async for chunk in r.content.iter_any():
+                buf += chunk
+                if b"\n" not in buf:
+                    continue
+                lines = buf.split(b"\n")
+                buf = lines.pop()
+                for line in lines:
+                    if not line.strip():
+                        continue
+                    ev = loads(line)
+                    obj = ev.get("object") or {}
+                    if kind != "Status" and obj.get("kind") is None:
+                        obj["kind"] = kind
+                    yield ev.get("type", ""), obj
+            if buf.strip():
+                ev = loads(buf)
+                yield ev.get("type", ""), ev.get("object") or {}
+
+    async def get(self, kind: str, namespace: Optional[str], name: str) -> Dict[str, Any]:
+        return await self.request("GET", resource_path(kind, namespace, name))
+
+    async def create(self, kind: str, namespace: Optional[str], obj: Dict[str, Any]) -> Dict[str, Any]:
+        return await self.request("POST", resource_path(kind, namespace), body=obj)
+
+    async def replace(self, kind: str, namespace: Optional[str], name: str, obj: Dict[str, Any]) -> Dict[str, Any]:
+        return await self.request("PUT", resource_path(kind, namespace, name), body=obj)
+
+    async def patch_merge(self, kind: str, namespace: Optional[str], name: str, patch: Dict[str, Any]) -> Dict[str, Any]:
+        return await self.request("PATCH", resource_path(kind, namespace, name), body=patch,
+                                  content_type="application/merge-patch+json")
+
+    async def delete(self, kind: str, namespace: Optional[str], name: str, propagation_policy: str = "Background") -> Dict[str, Any]:
+        body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
+        return await self.request("DELETE", resource_path(kind, namespace, name), body=body)
+
+    # JobClient protocol (Supervisor actuator)
+    async def delete_job(self, namespace: str, name: str, propagation_policy: str = "Background") -> None:
+        await self.delete("Job", namespace, name, propagation_policy)
+
+
+class KubeListWatch(ListWatch):
+    """Informer transport over :class:`KubeClient` (one kind, one namespace)."""
+
+    def __init__(self, client: KubeClient, kind: str, namespace: Optional[str], *, label_selector: str = "",
+                 field_selector: str = "", watch_timeout: int = 300, page_size: int = 500):
+        self.client = client
+        self.kind = kind
+        self.namespace = namespace
+        self.label_selector = label_selector
+        self.field_selector = field_selector
+        self.watch_timeout = watch_timeout
+        self.page_size = page_size
+
+    async def list(self):
+        return await self.client.list(self.kind, self.namespace, label_selector=self.label_selector,
+                                      field_selector=self.field_selector, limit=self.page_size)
+
+    def watch(self, resource_version: str):
+        return self.client.watch(self.kind, self.namespace, resource_version, label_selector=self.label_selector,
+                                 field_selector=self.field_selector, timeout_seconds=self.watch_timeout)

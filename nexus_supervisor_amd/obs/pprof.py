@@ -1,0 +1,249 @@
+"""Sampling profiler that writes pprof ``profile.proto`` (gzip).
+
+The north star says the hot path (informer → classify → CQL write) is
+"profiled with pprof rather than rocprof"; the reference itself exposes no
+profiling (no ``net/http/pprof``, no HTTP server).  This sampler
+walks the target thread's Python stack ``hz`` times a second from a background
+thread and emits the standard pprof format (samples/count + cpu/nanoseconds,
+function + line locations) so ``go tool pprof`` / ``pprof -top`` read it
+directly.  The protobuf is hand-encoded (no generated code needed).
+"""
+from __future__ import annotations
+
+import gzip
+import sys
+import threading
+import time
+from collections import Counter
+from typing import Dict, List, Optional, Tuple
+
+Frame = Tuple[str, str, int, int]  # (filename, function, first line, line)
+
+
+def _varint(v: int) -> bytes:
+    v &= (1 << 64) - 1
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _key(field: int, wt: int) -> bytes:
+    return _varint((field << 3) | wt)
+
+
+def _f_varint(field: int, v: int) -> bytes:
+    return _key(field, 0) + _varint(v)
+
+
+def _f_bytes(field: int, b: bytes) -> bytes:
+    return _key(field, 2) + _varint(len(b)) + b
+
+
+def _f_packed(field: int, vals) -> bytes:
+    return _f_bytes(field, b"".join(_varint(v) for v in vals))
+
+
+class Profile:
+    """Aggregated stacks → profile.proto."""
+
+    def __init__(self, period_ns: int):
+        self.period_ns = period_ns
+        self.stacks: Counter = Counter()
+        self.start_ns = time.time_ns()
+        self.duration_ns = 0
+
+    def add(self, stack: Tuple[Frame, ...], n: int = 1) -> None:
+        self.stacks[stack] += n
+
+    def encode(self) -> bytes:
+        strings: List[str] = [""]
+        sidx: Dict[str, int] = {"": 0}
+
+        def s(x: str) -> int:
+            i = sidx.get(x)
+            if i is None:
+                i = sidx[x] = len(strings)
+                strings.append(x)
+            return i
+
+        funcs: Dict[Tuple[str, str, int], int] = {}
+        locs: Dict[Tuple[int, int], int] = {}
+        out = bytearray()
+        # sample_type: samples/count, cpu/nanoseconds
+        out += _f_bytes(1, _f_varint(1, s("samples")) + _f_varint(2, s("count")))
+        out += _f_bytes(1, _f_varint(1, s("cpu")) + _f_varint(2, s("nanoseconds")))
+        func_msgs = bytearray()
+        loc_msgs = bytearray()
+        for stack, n in self.stacks.items():
+            loc_ids = []
+            for filename, name, first, line in stack:  # leaf first
+                fk = (filename, name, first)
+                fid = funcs.get(fk)
+                if fid is None:
+                    fid = funcs[fk] = len(funcs) + 1
+                    func_msgs += _f_bytes(5, _f_varint(1, fid) + _f_varint(2, s(name)) + _f_varint(3, s(name))
+                                          + _f_varint(4, s(filename)) + _f_varint(5, first))
+                lk = (fid, line)
+                lid = locs.get(lk)
+                if lid is None:
+                    lid = locs[lk] = len(locs) + 1
+                    line_msg = _f_varint(1, fid) + _f_varint(2, line)
+                    loc_msgs += _f_bytes(4, _f_varint(1, lid) + _f_bytes(4, line_msg))
+                loc_ids.append(lid)
+            out += _f_bytes(2, _f_packed(1, loc_ids) + _f_packed(2, [n, n * self.period_ns]))
+        out += loc_msgs
+        out += func_msgs
+        for st in strings:
+            out += _f_bytes(6, st.encode())
+        out += _f_varint(9, self.start_ns)
+        out += _f_varint(10, self.duration_ns)
+        out += _f_bytes(11, _f_varint(1, sidx["cpu"]) + _f_varint(2, sidx["nanoseconds"]))
+        out += _f_varint(12, self.period_ns)
+        out += _f_varint(14, sidx["cpu"])
+        return bytes(out)
+
+    def encode_gz(self) -> bytes:
+        return gzip.compress(self.encode())
+
+    def top(self, n: int = 25) -> str:
+        """Flat + cumulative table (what ``pprof -top`` shows), for committed summaries."""
+        total = sum(self.stacks.values()) or 1
+        flat: Counter = Counter()
+        cum: Counter = Counter()
+        for stack, c in self.stacks.items():
+            if stack:
+                flat[_fmt(stack[0])] += c
+            for fr in set(_fmt(f) for f in stack):
+                cum[fr] += c
+        lines = [f"samples: {total}  period: {self.period_ns / 1e6:.2f} ms  duration: {self.duration_ns / 1e9:.2f} s",
+                 f"{'flat':>8} {'flat%':>6} {'cum':>8} {'cum%':>6}  function"]
+        for fn, c in flat.most_common(n):
+            lines.append(f"{c:8d} {100 * c / total:5.1f}% {cum[fn]:8d} {100 * cum[fn] / total:5.1f}%  {fn}")
+        lines.append("")
+        lines.append("top cumulative:")
+        for fn, c in cum.most_common(n):
+            lines.append(f"{c:8d} {100 * c / total:5.1f}%  {fn}")
+        return "\n".join(lines)
+
+
+def _fmt(fr: Frame) -> str:
+    filename, name, _first, _line = fr
+    short = filename.rsplit("/site-packages/", 1)[-1].rsplit("/repo/", 1)[-1]
+    return f"{name} ({short})"
+
+
+class Sampler:
+    """Samples one thread's stack at ``hz`` into a :class:`Profile`."""
+
+    def __init__(self, hz: int = 97, thread_id: Optional[int] = None, max_depth: int = 64):
+        self.hz = max(1, hz)
+        self.thread_id = thread_id if thread_id is not None else threading.main_thread().ident
+        self.max_depth = max_depth
+        self.profile = Profile(int(1e9 / self.hz))
+        self._stop = threading.Event()
+        self._t: Optional[threading.Thread] = None
+        self._t0 = 0.0
+
+    def start(self) -> "Sampler":
+        self._t0 = time.monotonic()
+        self._t = threading.Thread(target=self._loop, name="pprof-sampler", daemon=True)
+        self._t.start()
+        return self
+
+    def stop(self) -> Profile:
+        self._stop.set()
+        if self._t is not None:
+            self._t.join()
+        self.profile.duration_ns = int((time.monotonic() - self._t0) * 1e9)
+        return self.profile
+
+    def _loop(self) -> None:
+        period = 1.0 / self.hz
+        nxt = time.monotonic()
+        tid = self.thread_id
+        while not self._stop.is_set():
+            frame = sys._current_frames().get(tid)  # noqa: SLF001
+            if frame is not None:
+                stack = []
+                f = frame
+                while f is not None and len(stack) < self.max_depth:
+                    co = f.f_code
+                    stack.append((co.co_filename, co.co_name, co.co_firstlineno, f.f_lineno or 0))
+                    f = f.f_back
+                self.profile.add(tuple(stack))
+            del frame
+            nxt += period
+            delay = nxt - time.monotonic()
+            if delay > 0:
+                self._stop.wait(delay)
+            else:
+                nxt = time.monotonic()
+
+
+def profile_for(seconds: float, hz: int = 97, thread_id: Optional[int] = None) -> Profile:
+    s = Sampler(hz, thread_id).start()
+    time.sleep(seconds)
+    return s.stop()
+
+
+def decode_profile(data: bytes) -> Dict[str, object]:
+    """Minimal protobuf reader for tests: string table + sample count + locations."""
+    if data[:2] == b"\x1f\x8b":
+        data = gzip.decompress(data)
+
+    def read_varint(b, i):
+        shift = v = 0
+        while True:
+            c = b[i]
+            i += 1
+            v |= (c & 0x7F) << shift
+            if not c & 0x80:
+                return v, i
+            shift += 7
+
+    def fields(b):
+        i = 0
+        while i < len(b):
+            k, i = read_varint(b, i)
+            f, wt = k >> 3, k & 7
+            if wt == 0:
+                v, i = read_varint(b, i)
+                yield f, v
+            elif wt == 2:
+                ln, i = read_varint(b, i)
+                yield f, b[i:i + ln]
+                i += ln
+            else:
+                raise ValueError(f"unsupported wire type {wt}")
+
+    strings, samples, locations, functions = [], 0, 0, 0
+    values = 0
+    period = 0
+    for f, v in fields(data):
+        if f == 6:
+            strings.append(v.decode())
+        elif f == 2:
+            samples += 1
+            for sf, sv in fields(v):
+                if sf == 2:
+                    j = 0
+                    first = True
+                    while j < len(sv):
+                        x, j = read_varint(sv, j)
+                        if first:
+                            values += x
+                            first = False
+        elif f == 4:
+            locations += 1
+        elif f == 5:
+            functions += 1
+        elif f == 12:
+            period = v
+    return {"strings": strings, "samples": samples, "sample_count": values, "locations": locations,
+            "functions": functions, "period": period}

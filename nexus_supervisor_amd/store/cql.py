@@ -1,0 +1,776 @@
+"""Asyncio CQL v4 client and the Scylla / Astra checkpoint store.
+
+Replaces nexus-core's gocqlx-based ``request.CqlStore`` (constructed at
+``/root/reference/app/app_dependencies.go:18-34``; used for ``ReadCheckpoint`` /
+``UpsertCheckpoint`` at ``/root/reference/services/supervisor.go:264,301,328,353,364``).
+
+Design:
+
+* **native codec** — frames are built and responses split + decoded by the C++
+  extension ``_cql_native`` (``csrc/cql``); Python only matches stream ids.
+* **multiplexed connections** — up to 32k in-flight requests per connection on
+  stream ids; writes issued in the same loop tick are coalesced into one
+  ``send`` (the supervisor's workers issue hundreds of requests concurrently).
+* **prepared statements** — prepared once per query, re-prepared transparently
+  on ``UNPREPARED`` (server restart), result metadata cached so responses are
+  requested with ``skip_metadata``.
+* **token-aware, DC-aware routing** — the ring comes from ``system.local`` /
+  ``system.peers``; the partition key ``((algorithm, id))`` is hashed with
+  Cassandra's Murmur3 (native) and the request goes straight to the owner in
+  ``local-dc`` (one network hop, no coordinator forwarding).
+* **retries** — idempotent requests are retried on another host after
+  connection loss, ``Overloaded``, ``Unavailable`` or timeouts; hosts that fail
+  are reconnected in the background with exponential backoff.
+* **Astra** — the Secure Connect Bundle (base64 zip: ``config.json``,
+  ``ca.crt``, ``cert``, ``key``) gives a mutual-TLS context and the SNI proxy;
+  node connections go through the proxy with the host id as SNI.
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import bisect
+import datetime as _dt
+import io
+import json
+import logging
+import random
+import ssl
+import time
+import zipfile
+from dataclasses import dataclass, field
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
+
+from ..models.checkpoint import COLUMN_NAMES, COLUMNS, KEYSPACE, TABLE, CheckpointedRequest
+from .base import CheckpointStore, StoreError
+
+log = logging.getLogger("nexus_supervisor_amd.cql")
+
+try:
+    from .. import _cql_native as N  # type: ignore
+except ImportError as _exc:  # pragma: no cover - build hint
+    N = None
+    _IMPORT_ERROR = _exc
+
+EPOCH = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc)
+
+
+def _ms_to_dt(ms: int) -> _dt.datetime:
+    return EPOCH + _dt.timedelta(milliseconds=ms)
+
+
+def _native():
+    if N is None:
+        raise StoreError("native CQL codec not built: run `python -m nexus_supervisor_amd._build`") from _IMPORT_ERROR
+    return N
+
+
+if N is not None:
+    N.set_timestamp_factory(_ms_to_dt)
+
+OP_ERROR, OP_READY, OP_AUTHENTICATE, OP_SUPPORTED, OP_RESULT, OP_AUTH_SUCCESS = 0x00, 0x02, 0x03, 0x06, 0x08, 0x10
+OP_EVENT, OP_AUTH_CHALLENGE = 0x0C, 0x0E
+
+CONSISTENCY = {"ANY": 0, "ONE": 1, "TWO": 2, "THREE": 3, "QUORUM": 4, "ALL": 5, "LOCAL_QUORUM": 6, "EACH_QUORUM": 7,
+               "SERIAL": 8, "LOCAL_SERIAL": 9, "LOCAL_ONE": 10}
+T_VARCHAR, T_TIMESTAMP, T_BOOLEAN = 0x0D, 0x0B, 0x04
+_TYPE_IDS = {"text": T_VARCHAR, "timestamp": T_TIMESTAMP}
+
+ERR_OVERLOADED, ERR_UNAVAILABLE, ERR_IS_BOOTSTRAPPING = 0x1001, 0x1000, 0x1002
+ERR_WRITE_TIMEOUT, ERR_READ_TIMEOUT, ERR_UNPREPARED, ERR_SERVER = 0x1100, 0x1200, 0x2500, 0x0000
+RETRYABLE = {ERR_OVERLOADED, ERR_UNAVAILABLE, ERR_IS_BOOTSTRAPPING, ERR_WRITE_TIMEOUT, ERR_READ_TIMEOUT, ERR_SERVER}
+
+
+class CqlError(StoreError):
+    def __init__(self, code: int, message: str, extra: Optional[Dict[str, Any]] = None):
+        super().__init__(f"CQL error 0x{code:04x}: {message}")
+        self.code = code
+        self.message = message
+        self.extra = extra or {}
+
+
+class ConnectionClosed(StoreError):
+    pass
+
+
+class RequestTimeout(StoreError):
+    pass
+
+
+# ---------------------------------------------------------------------------- connection
+class _Protocol(asyncio.Protocol):
+    def __init__(self, conn: "CqlConnection"):
+        self.conn = conn
+
+    def connection_made(self, transport):
+        self.conn._transport = transport
+
+    def data_received(self, data: bytes):
+        self.conn._on_data(data)
+
+    def connection_lost(self, exc):
+        self.conn._on_lost(exc)
+
+
+class CqlConnection:
+    """One multiplexed CQL connection."""
+
+    MAX_STREAMS = 32768
+
+    def __init__(self, host: str, port: int, *, user: str = "", password: str = "", ssl_ctx: Optional[ssl.SSLContext] = None,
+                 server_hostname: Optional[str] = None, request_timeout: float = 5.0, connect_timeout: float = 5.0):
+        self.host, self.port = host, port
+        self.user, self.password = user, password
+        self.ssl_ctx, self.server_hostname = ssl_ctx, server_hostname
+        self.request_timeout, self.connect_timeout = request_timeout, connect_timeout
+        self._transport: Optional[asyncio.Transport] = None
+        self._reader = _native().FrameReader()
+        self._pending: Dict[int, asyncio.Future] = {}
+        self._free: List[int] = list(range(self.MAX_STREAMS - 1, 0, -1))  # stream 0 unused, -1.. events
+        self._out: List[bytes] = []
+        self._flush_scheduled = False
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self.closed = True
+        self.keyspace: Optional[str] = None
+        self.prepared_here: set = set()
+        self.requests = 0
+
+    @property
+    def address(self) -> Tuple[str, int]:
+        return (self.host, self.port)
+
+    async def connect(self, keyspace: Optional[str] = None) -> None:
+        self._loop = asyncio.get_running_loop()
+        kw: Dict[str, Any] = {}
+        if self.ssl_ctx is not None:
+            kw["ssl"] = self.ssl_ctx
+            kw["server_hostname"] = self.server_hostname or self.host
+        await asyncio.wait_for(self._loop.create_connection(lambda: _Protocol(self), self.host, self.port, **kw),
+                               self.connect_timeout)
+        self.closed = False
+        sock = self._transport.get_extra_info("socket")
+        if sock is not None:
+            import socket as _s
+
+            try:
+                sock.setsockopt(_s.IPPROTO_TCP, _s.TCP_NODELAY, 1)
+            except OSError:
+                pass
+        resp = await self.request(lambda s: N.encode_startup(s, {"CQL_VERSION": "3.0.0"}))
+        if resp[0] == "authenticate":
+            token = b"\x00" + self.user.encode() + b"\x00" + self.password.encode()
+            resp = await self.request(lambda s: N.encode_auth_response(s, token))
+            if resp[0] == "error":
+                raise CqlError(resp[1], resp[2], resp[3])
+        elif resp[0] != "ready":
+            raise StoreError(f"unexpected STARTUP response {resp!r}")
+        if keyspace:
+            await self.use(keyspace)
+
+    async def use(self, keyspace: str) -> None:
+        r = await self.request(lambda s: N.encode_query(s, f'USE "{keyspace}"', None, None, CONSISTENCY["ONE"]))
+        if r[0] == "error":
+            raise CqlError(r[1], r[2], r[3])
+        self.keyspace = keyspace
+
+    # -------------------------------------------------------------- I/O
+    def _on_data(self, data: bytes) -> None:
+        try:
+            frames = self._reader.feed(data)
+        except ValueError as exc:
+            log.error("protocol error from %s:%s: %s", self.host, self.port, exc)
+            self.close()
+            return
+        pending = self._pending
+        for stream, _op, dec in frames:
+            fut = pending.pop(stream, None)
+            if fut is None:
+                continue  # server push (EVENT) or a timed-out request
+            self._free.append(stream)
+            if not fut.done():
+                fut.set_result(dec)
+
+    def _on_lost(self, exc) -> None:
+        self.closed = True
+        err = ConnectionClosed(f"connection to {self.host}:{self.port} lost: {exc}")
+        pending, self._pending = self._pending, {}
+        for fut in pending.values():
+            if not fut.done():
+                fut.set_exception(err)
+        self._free = list(range(self.MAX_STREAMS - 1, 0, -1))
+
+    def _flush(self) -> None:
+        self._flush_scheduled = False
+        if self._out and self._transport is not None and not self.closed:
+            data = b"".join(self._out) if len(self._out) > 1 else self._out[0]
+            self._out = []
+            self._transport.write(data)
+        else:
+            self._out = []
+
+    def request_nowait(self, build, hint=None) -> asyncio.Future:
+        """Send one request frame built by ``build(stream)``; returns the response future."""
+        if self.closed:
+            raise ConnectionClosed(f"connection to {self.host}:{self.port} is closed")
+        if not self._free:
+            raise StoreError("no free stream ids")
+        stream = self._free.pop()
+        fut = self._loop.create_future()
+        self._pending[stream] = fut
+        if hint is not None:
+            self._reader.expect(stream, hint)
+        self._out.append(build(stream))
+        self.requests += 1
+        if not self._flush_scheduled:
+            self._flush_scheduled = True
+            self._loop.call_soon(self._flush)
+        return fut
+
+    async def request(self, build, hint=None, timeout: Optional[float] = None):
+        fut = self.request_nowait(build, hint)
+        try:
+            return await asyncio.wait_for(fut, timeout or self.request_timeout)
+        except asyncio.TimeoutError:
+            raise RequestTimeout(f"request to {self.host}:{self.port} timed out") from None
+
+    @property
+    def in_flight(self) -> int:
+        return len(self._pending)
+
+    def close(self) -> None:
+        if self._transport is not None:
+            self._transport.close()
+        self.closed = True
+
+
+# ---------------------------------------------------------------------------- session
+@dataclass
+class PreparedStatement:
+    query: str
+    query_id: bytes
+    bind_types: List[Any]
+    pk_indexes: List[int]
+    result_names: Optional[Tuple[str, ...]]
+    result_types: Optional[List[Any]]
+    keyspace: str = ""
+
+
+@dataclass
+class Host:
+    address: Tuple[str, int]
+    dc: str = ""
+    rack: str = ""
+    host_id: str = ""
+    tokens: List[int] = field(default_factory=list)
+    conns: List[CqlConnection] = field(default_factory=list)
+    up: bool = False
+    failures: int = 0
+    next_retry: float = 0.0
+    rr: int = 0
+
+    def pick(self) -> Optional[CqlConnection]:
+        live = [c for c in self.conns if not c.closed]
+        if not live:
+            return None
+        # least in-flight of two random choices
+        if len(live) == 1:
+            return live[0]
+        a, b = random.sample(live, 2)
+        return a if a.in_flight <= b.in_flight else b
+
+
+@dataclass
+class Rows:
+    names: Tuple[str, ...]
+    rows: List[tuple]
+    paging_state: Optional[bytes] = None
+
+    def dicts(self) -> List[Dict[str, Any]]:
+        return [dict(zip(self.names, r)) for r in self.rows]
+
+    def __iter__(self):
+        return iter(self.rows)
+
+    def __len__(self):
+        return len(self.rows)
+
+
+class CqlSession:
+    def __init__(self, contact_points: Sequence[Tuple[str, int]], *, keyspace: Optional[str] = None, user: str = "",
+                 password: str = "", local_dc: str = "", connections_per_host: int = 2, request_timeout: float = 5.0,
+                 connect_timeout: float = 5.0, token_aware: bool = True, consistency: str = "LOCAL_QUORUM",
+                 ssl_ctx: Optional[ssl.SSLContext] = None, sni_proxy: Optional[Tuple[str, int]] = None,
+                 max_retries: int = 3, discover: bool = True):
+        if not contact_points:
+            raise StoreError("no CQL contact points configured")
+        self.contact_points = list(contact_points)
+        self.keyspace = keyspace
+        self.user, self.password = user, password
+        self.local_dc = local_dc
+        self.per_host = max(1, connections_per_host)
+        self.request_timeout, self.connect_timeout = request_timeout, connect_timeout
+        self.token_aware = token_aware
+        self.consistency = CONSISTENCY[consistency.upper()]
+        self.ssl_ctx = ssl_ctx
+        self.sni_proxy = sni_proxy
+        self.max_retries = max_retries
+        self.discover = discover
+        self.hosts: Dict[Tuple[str, int], Host] = {}
+        self._ring: List[int] = []
+        self._ring_hosts: List[Host] = []
+        self._prepared: Dict[str, PreparedStatement] = {}
+        self._preparing: Dict[str, asyncio.Future] = {}
+        self._reconnector: Optional[asyncio.Task] = None
+        self._rr = 0
+        self.stats = {"requests": 0, "retries": 0, "reprepares": 0, "token_routed": 0}
+
+    # -------------------------------------------------------------- lifecycle
+    def _new_conn(self, h: Host) -> CqlConnection:
+        host, port = h.address
+        server_hostname = None
+        if self.sni_proxy is not None:
+            server_hostname = h.host_id or host
+            host, port = self.sni_proxy
+        return CqlConnection(host, port, user=self.user, password=self.password, ssl_ctx=self.ssl_ctx,
+                             server_hostname=server_hostname, request_timeout=self.request_timeout,
+                             connect_timeout=self.connect_timeout)
+
+    async def _open_host(self, h: Host) -> None:
+        conns = [self._new_conn(h) for _ in range(self.per_host)]
+        await asyncio.gather(*(c.connect(self.keyspace) for c in conns))
+        for c in h.conns:
+            c.close()
+        h.conns = conns
+        h.up = True
+        h.failures = 0
+
+    async def connect(self) -> None:
+        last: Optional[BaseException] = None
+        for addr in self.contact_points:
+            h = Host(address=addr, host_id=addr[0] if self.sni_proxy is None else "")
+            if self.sni_proxy is not None:
+                h.host_id = addr[0]
+            try:
+                await self._open_host(h)
+            except (OSError, asyncio.TimeoutError, StoreError) as exc:
+                last = exc
+                log.warning("CQL contact point %s:%s unavailable: %s", addr[0], addr[1], exc)
+                continue
+            self.hosts[addr] = h
+            break
+        if not self.hosts:
+            raise StoreError(f"could not connect to any CQL contact point: {last}")
+        if self.discover:
+            try:
+                await self._discover()
+            except StoreError as exc:  # e.g. a server without system tables
+                log.warning("CQL topology discovery failed: %s (routing round-robin)", exc)
+        others = [h for h in self.hosts.values() if not h.up]
+        if others:
+            await asyncio.gather(*(self._try_open(h) for h in others))
+        self._reconnector = asyncio.create_task(self._reconnect_loop(), name="cql-reconnect")
+
+    async def _try_open(self, h: Host) -> None:
+        try:
+            await self._open_host(h)
+        except (OSError, asyncio.TimeoutError, StoreError) as exc:
+            self._mark_down(h, exc)
+
+    async def _discover(self) -> None:
+        first = next(iter(self.hosts.values()))
+        local = await self._query_on(first, "SELECT data_center, rack, host_id, tokens, native_port FROM system.local")
+        peers_rows: List[Dict[str, Any]] = []
+        try:
+            peers = await self._query_on(first, "SELECT peer, rpc_address, data_center, rack, host_id, tokens, native_port FROM system.peers")
+            peers_rows = peers.dicts()
+        except CqlError:  # real Scylla has no native_port column in peers; fall back
+            peers = await self._query_on(first, "SELECT peer, rpc_address, data_center, rack, host_id, tokens FROM system.peers")
+            peers_rows = peers.dicts()
+        lrow = local.dicts()[0] if local.rows else {}
+        first.dc = lrow.get("data_center") or ""
+        first.rack = lrow.get("rack") or ""
+        if self.sni_proxy is None:
+            first.host_id = str(lrow.get("host_id") or "")
+        first.tokens = [int(t) for t in (lrow.get("tokens") or [])]
+        for p in peers_rows:
+            addr = p.get("rpc_address") or p.get("peer")
+            if not addr or addr == "0.0.0.0":
+                addr = p.get("peer")
+            port = int(p.get("native_port") or first.address[1])
+            key = (addr, port)
+            h = self.hosts.get(key) or Host(address=key)
+            h.dc, h.rack = p.get("data_center") or "", p.get("rack") or ""
+            h.host_id = str(p.get("host_id") or "")
+            h.tokens = [int(t) for t in (p.get("tokens") or [])]
+            self.hosts[key] = h
+        self._build_ring()
+
+    def _build_ring(self) -> None:
+        pairs = []
+        for h in self.hosts.values():
+            if self.local_dc and h.dc and h.dc != self.local_dc:
+                continue
+            for t in h.tokens:
+                pairs.append((t, h))
+        pairs.sort(key=lambda p: p[0])
+        self._ring = [p[0] for p in pairs]
+        self._ring_hosts = [p[1] for p in pairs]
+
+    def owner(self, token: int) -> Optional[Host]:
+        """Replica owning ``token``: the first ring token >= it (wrapping)."""
+        if not self._ring:
+            return None
+        i = bisect.bisect_left(self._ring, token)
+        return self._ring_hosts[i % len(self._ring)]
+
+    def _mark_down(self, h: Host, exc: BaseException) -> None:
+        if h.up:
+            log.warning("CQL host %s:%s down: %s", h.address[0], h.address[1], exc)
+        h.up = False
+        h.failures += 1
+        h.next_retry = time.monotonic() + min(30.0, 0.1 * (2 ** min(h.failures, 9))) * (0.8 + 0.4 * random.random())
+
+    async def _reconnect_loop(self) -> None:
+        while True:
+            await asyncio.sleep(0.05)
+            now = time.monotonic()
+            for h in list(self.hosts.values()):
+                if h.up and all(c.closed for c in h.conns):
+                    self._mark_down(h, ConnectionClosed("all connections closed"))
+                if not h.up and now >= h.next_retry:
+                    await self._try_open(h)
+                    if h.up:
+                        log.info("CQL host %s:%s back up", *h.address)
+
+    async def close(self) -> None:
+        if self._reconnector is not None:
+            self._reconnector.cancel()
+            try:
+                await self._reconnector
+            except (asyncio.CancelledError, Exception):
+                pass
+        for h in self.hosts.values():
+            for c in h.conns:
+                c.close()
+        await asyncio.sleep(0)
+
+    # -------------------------------------------------------------- routing
+    def _candidates(self, routing_token: Optional[int]) -> List[Host]:
+        up = [h for h in self.hosts.values() if h.up and (not self.local_dc or not h.dc or h.dc == self.local_dc)]
+        if not up:
+            up = [h for h in self.hosts.values() if h.up]
+        if routing_token is not None and self.token_aware:
+            o = self.owner(routing_token)
+            if o is not None and o.up:
+                self.stats["token_routed"] += 1
+                return [o] + [h for h in up if h is not o]
+        if len(up) > 1:
+            self._rr = (self._rr + 1) % len(up)
+            up = up[self._rr:] + up[: self._rr]
+        return up
+
+    async def _query_on(self, h: Host, cql: str, values=None) -> Rows:
+        conn = h.pick()
+        if conn is None:
+            raise ConnectionClosed("host has no live connection")
+        r = await conn.request(lambda s: N.encode_query(s, cql, values, None, CONSISTENCY["ONE"]))
+        return self._result(r)
+
+    @staticmethod
+    def _result(r):
+        kind = r[0]
+        if kind == "rows":
+            return Rows(tuple(r[1]), r[2], r[3])
+        if kind == "error":
+            raise CqlError(r[1], r[2], r[3])
+        return r
+
+    # -------------------------------------------------------------- statements
+    async def prepare(self, query: str) -> PreparedStatement:
+        ps = self._prepared.get(query)
+        if ps is not None:
+            return ps
+        fut = self._preparing.get(query)
+        if fut is not None:
+            return await fut
+        fut = asyncio.get_running_loop().create_future()
+        self._preparing[query] = fut
+        try:
+            last: Optional[BaseException] = None
+            for h in self._candidates(None):
+                conn = h.pick()
+                if conn is None:
+                    continue
+                try:
+                    r = await conn.request(lambda s: N.encode_prepare(s, query))
+                except (ConnectionClosed, RequestTimeout, OSError) as exc:
+                    last = exc
+                    continue
+                if r[0] == "error":
+                    raise CqlError(r[1], r[2], r[3])
+                _, qid, bind, pk, result = r
+                ps = PreparedStatement(query, qid, [b[3] for b in bind], list(pk),
+                                       tuple(n for n, _ in result) if result is not None else None,
+                                       [t for _, t in result] if result is not None else None)
+                conn.prepared_here.add(qid)
+                self._prepared[query] = ps
+                fut.set_result(ps)
+                return ps
+            raise StoreError(f"prepare failed on every host: {last}")
+        except BaseException as exc:
+            if not fut.done():
+                fut.set_exception(exc)
+                fut.exception()  # consumed
+            raise
+        finally:
+            self._preparing.pop(query, None)
+
+    def routing_token(self, ps: PreparedStatement, values: Sequence[Any]) -> Optional[int]:
+        if not ps.pk_indexes or not self._ring:
+            return None
+        parts = []
+        for i in ps.pk_indexes:
+            v = values[i]
+            if v is None:
+                return None
+            parts.append(N.serialize(v, ps.bind_types[i]))
+        return N.token_for(parts)
+
+    async def execute(self, ps_or_query, values: Sequence[Any] = (), *, consistency: Optional[int] = None,
+                      serial: Optional[int] = None, idempotent: bool = True, timeout: Optional[float] = None):
+        ps = ps_or_query if isinstance(ps_or_query, PreparedStatement) else await self.prepare(ps_or_query)
+        cl = self.consistency if consistency is None else consistency
+        token = self.routing_token(ps, values) if self.token_aware else None
+        vals = list(values)
+        hint = ps.result_types
+        skip = hint is not None
+        attempts = 0
+        last: Optional[BaseException] = None
+        tried: set = set()
+        while attempts <= self.max_retries:
+            cands = [h for h in self._candidates(token) if h.address not in tried] or self._candidates(token)
+            if not cands:
+                raise StoreError(f"no CQL host available: {last}")
+            h = cands[0]
+            conn = h.pick()
+            if conn is None:
+                self._mark_down(h, ConnectionClosed("no live connection"))
+                tried.add(h.address)
+                attempts += 1
+                continue
+            self.stats["requests"] += 1
+            try:
+                qid = ps.query_id
+                r = await conn.request(lambda s: N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None),
+                                       hint if skip else None, timeout)
+            except (ConnectionClosed, OSError) as exc:
+                last = exc
+                self._mark_down(h, exc)
+                tried.add(h.address)
+                attempts += 1
+                self.stats["retries"] += 1
+                continue
+            except RequestTimeout as exc:
+                last = exc
+                if not idempotent:
+                    raise
+                tried.add(h.address)
+                attempts += 1
+                self.stats["retries"] += 1
+                continue
+            kind = r[0]
+            if kind == "error":
+                code = r[1]
+                if code == ERR_UNPREPARED:
+                    self.stats["reprepares"] += 1
+                    rr = await conn.request(lambda s: N.encode_prepare(s, ps.query))
+                    if rr[0] == "error":
+                        raise CqlError(rr[1], rr[2], rr[3])
+                    if rr[1] != ps.query_id:
+                        ps.query_id = rr[1]
+                    attempts += 1
+                    continue
+                if code in RETRYABLE and idempotent and attempts < self.max_retries:
+                    last = CqlError(code, r[2], r[3])
+                    attempts += 1
+                    self.stats["retries"] += 1
+                    await asyncio.sleep(min(0.2, 0.01 * (2 ** attempts)))
+                    continue
+                raise CqlError(code, r[2], r[3])
+            if kind == "rows":
+                names = ps.result_names if skip else tuple(r[1])
+                return Rows(names, r[2], r[3])
+            return r
+        raise StoreError(f"CQL request failed after {attempts} attempts: {last}")
+
+    async def query(self, cql: str, values: Optional[Sequence[Any]] = None, consistency: Optional[int] = None):
+        """Unprepared statement (schema, admin)."""
+        cl = self.consistency if consistency is None else consistency
+        last: Optional[BaseException] = None
+        for h in self._candidates(None):
+            conn = h.pick()
+            if conn is None:
+                continue
+            try:
+                r = await conn.request(lambda s: N.encode_query(s, cql, list(values) if values else None, None, cl))
+            except (ConnectionClosed, RequestTimeout, OSError) as exc:
+                last = exc
+                self._mark_down(h, exc)
+                continue
+            return self._result(r)
+        raise StoreError(f"no CQL host could run the query: {last}")
+
+
+# ---------------------------------------------------------------------------- Astra secure connect bundle
+@dataclass
+class SecureBundle:
+    host: str
+    port: int
+    cql_port: int
+    keyspace: str
+    local_dc: str
+    ssl_ctx: ssl.SSLContext
+    raw_config: Dict[str, Any]
+
+
+def load_secure_bundle(b64: str) -> SecureBundle:
+    """Parse an Astra Secure Connect Bundle (base64 zip) into a mutual-TLS context."""
+    import os
+    import tempfile
+
+    data = base64.b64decode(b64)
+    with zipfile.ZipFile(io.BytesIO(data)) as z:
+        names = set(z.namelist())
+        cfg = json.loads(z.read("config.json"))
+        files = {n: z.read(n) for n in ("ca.crt", "cert", "key") if n in names}
+    if "ca.crt" not in files:
+        raise StoreError("secure connect bundle has no ca.crt")
+    ctx = ssl.create_default_context(ssl.Purpose.SERVER_AUTH, cadata=files["ca.crt"].decode())
+    ctx.check_hostname = False  # Astra SNI routes by host id; the proxy certificate names the proxy
+    if "cert" in files and "key" in files:
+        with tempfile.TemporaryDirectory() as d:
+            cp, kp = os.path.join(d, "cert"), os.path.join(d, "key")
+            with open(cp, "wb") as f:
+                f.write(files["cert"])
+            with open(kp, "wb") as f:
+                f.write(files["key"])
+            ctx.load_cert_chain(cp, kp)
+    return SecureBundle(host=cfg.get("host", ""), port=int(cfg.get("port", 29080)), cql_port=int(cfg.get("cql_port", 29042)),
+                        keyspace=cfg.get("keyspace", ""), local_dc=cfg.get("localDC", ""), ssl_ctx=ctx, raw_config=cfg)
+
+
+async def astra_contact_info(bundle: SecureBundle, timeout: float = 10.0) -> Dict[str, Any]:
+    """Metadata service (``https://host:port/metadata``): SNI proxy address, host ids, local DC."""
+    import aiohttp
+
+    url = f"https://{bundle.host}:{bundle.port}/metadata"
+    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=timeout)) as s:
+        async with s.get(url, ssl=bundle.ssl_ctx) as r:
+            r.raise_for_status()
+            doc = await r.json(content_type=None)
+    return doc.get("contact_info", doc)
+
+
+# ---------------------------------------------------------------------------- checkpoint store
+def _q(name: str) -> str:
+    return name
+
+
+class CqlCheckpointStore(CheckpointStore):
+    """``nexus.checkpoints`` over CQL (schema: ``models.checkpoint``; reference schema
+    ``/root/reference/test-resources/checkpoints.cql:1-29``)."""
+
+    def __init__(self, session: CqlSession, keyspace: str = KEYSPACE, table: str = TABLE,
+                 consistency: str = "LOCAL_QUORUM", serial_consistency: str = "LOCAL_SERIAL"):
+        self.session = session
+        self.keyspace, self.table = keyspace, table
+        self.cl = CONSISTENCY[consistency.upper()]
+        self.serial = CONSISTENCY[serial_consistency.upper()]
+        ft = f"{keyspace}.{table}"
+        cols = ", ".join(COLUMN_NAMES)
+        self.q_read = f"SELECT {cols} FROM {ft} WHERE algorithm = ? AND id = ?"
+        self.q_insert = f"INSERT INTO {ft} ({cols}) VALUES ({', '.join('?' for _ in COLUMN_NAMES)})"
+        self.q_update_failure = (f"UPDATE {ft} SET lifecycle_stage = ?, algorithm_failure_cause = ?, "
+                                 f"algorithm_failure_details = ?, last_modified = ? WHERE algorithm = ? AND id = ?")
+        self.q_update_stage = f"UPDATE {ft} SET lifecycle_stage = ?, last_modified = ? WHERE algorithm = ? AND id = ?"
+        self.reads = self.writes = 0
+
+    @classmethod
+    def from_config(cls, cfg) -> "CqlCheckpointStore":
+        """Build from ``SupervisorConfig`` (``cql-store-type`` scylla | astra)."""
+        from ..config.schema import CQL_STORE_ASTRA
+
+        if cfg.cql_store_type == CQL_STORE_ASTRA:
+            a = cfg.astra_cql_store
+            if not a.secure_connection_bundle_base64:
+                raise StoreError("astra-cql-store.secure-connection-bundle-base64 is empty")
+            bundle = load_secure_bundle(a.secure_connection_bundle_base64)
+            store = cls(CqlSession([(bundle.host, bundle.cql_port)], user=a.gateway_user, password=a.gateway_password,
+                                   ssl_ctx=bundle.ssl_ctx, local_dc=bundle.local_dc, request_timeout=a.request_timeout,
+                                   consistency=a.consistency),
+                        keyspace=a.keyspace or bundle.keyspace or KEYSPACE, table=a.table, consistency=a.consistency)
+            store._bundle = bundle
+            return store
+        s = cfg.scylla_cql_store
+        hosts = []
+        for h in s.hosts:
+            host, _, port = h.partition(":")
+            hosts.append((host, int(port) if port else s.port))
+        sess = CqlSession(hosts, user=s.user, password=s.password, local_dc=s.local_dc,
+                          connections_per_host=s.connections_per_host, request_timeout=s.request_timeout,
+                          connect_timeout=s.connect_timeout, token_aware=s.token_aware, consistency=s.consistency)
+        return cls(sess, keyspace=s.keyspace, table=s.table, consistency=s.consistency)
+
+    async def connect(self) -> None:
+        bundle = getattr(self, "_bundle", None)
+        if bundle is not None:
+            info = await astra_contact_info(bundle)
+            proxy = info.get("sni_proxy_address", "")
+            ph, _, pp = proxy.rpartition(":")
+            self.session.sni_proxy = (ph, int(pp))
+            self.session.local_dc = info.get("local_dc", self.session.local_dc)
+            self.session.contact_points = [(hid, 0) for hid in info.get("contact_points", [])] or self.session.contact_points
+        await self.session.connect()
+        await asyncio.gather(*(self.session.prepare(q) for q in (self.q_read, self.q_insert, self.q_update_failure,
+                                                                  self.q_update_stage)))
+
+    async def close(self) -> None:
+        await self.session.close()
+
+    async def read_checkpoint(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
+        self.reads += 1
+        rows = await self.session.execute(self.q_read, (algorithm, request_id), consistency=self.cl)
+        if not rows.rows:
+            return None
+        return CheckpointedRequest(*rows.rows[0])
+
+    async def upsert_checkpoint(self, checkpoint: CheckpointedRequest) -> None:
+        self.writes += 1
+        await self.session.execute(self.q_insert, checkpoint.as_row(), consistency=self.cl)
+
+    async def update_status(self, algorithm, request_id, lifecycle_stage, failure_cause, failure_details, last_modified,
+                            only_if_stages=None, set_failure=True) -> bool:
+        self.writes += 1
+        if set_failure:
+            q = self.q_update_failure
+            vals: List[Any] = [lifecycle_stage, failure_cause, failure_details, last_modified, algorithm, request_id]
+        else:
+            q = self.q_update_stage
+            vals = [lifecycle_stage, last_modified, algorithm, request_id]
+        if only_if_stages is None:
+            await self.session.execute(q, vals, consistency=self.cl)
+            return True
+        stages = tuple(only_if_stages)
+        cq = q + " IF lifecycle_stage IN (" + ", ".join("?" for _ in stages) + ")"
+        rows = await self.session.execute(cq, vals + list(stages), consistency=self.cl, serial=self.serial)
+        return bool(rows.rows and rows.rows[0][0])
+
+    async def create_schema(self, replication: str = "{'class': 'SimpleStrategy', 'replication_factor': 1}") -> None:
+        """Keyspace + table + indexes (what ``prepare-scylla.sh`` applies in the reference)."""
+        from ..models.checkpoint import create_index_cql, create_table_cql
+
+        await self.session.query(f"CREATE KEYSPACE IF NOT EXISTS {self.keyspace} WITH replication = {replication}")
+        ddl = create_table_cql(self.keyspace, self.table).replace("create table", "CREATE TABLE IF NOT EXISTS", 1)
+        await self.session.query(ddl)
+        for stmt in create_index_cql(self.keyspace, self.table):
+            await self.session.query(stmt.replace("create index", "CREATE INDEX IF NOT EXISTS", 1).rstrip(";"))
