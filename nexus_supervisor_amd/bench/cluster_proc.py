@@ -56,17 +56,30 @@ async def amain(args) -> None:
         state["wl"] = wl
         return web.json_response({"objects": len(objs), "rows": len(rows), "rv": api.rv})
 
+    async def prepare(events: int):
+        # generate the next step's traffic and insert its replacement runs' rows ahead of
+        # time (overlapped with the supervisor working on the current step)
+        wl = state["wl"]
+        failed, traffic, rows = wl.step(events)
+        await write_rows(rows)
+        return failed, traffic
+
     async def h_step(req):
         p = await req.json()
+        events = int(p["events"])
         wl = state["wl"]
-        failed, traffic, rows = wl.step(int(p["events"]))
-        await write_rows(rows)
+        nxt = state.get("next")
+        if nxt is not None and nxt[0] == events:
+            failed, traffic = await nxt[1]
+        else:
+            failed, traffic = await prepare(events)
         t_push = time.monotonic()
         for etype, obj in traffic:
             if etype == "ADDED":
-                api.create(obj)
+                api.create(obj, copy_obj=False)
             else:
-                api.update(obj)
+                api.update(obj, copy_obj=False)
+        state["next"] = (events, asyncio.ensure_future(prepare(events)))
         return web.json_response({"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}})
 
     async def h_stats(req):

@@ -51,6 +51,7 @@ MSG_GPU_FAULT = "Algorithm hit a GPU fault."
 IMAGE_PULL_WAITING = ("ErrImagePull", "ImagePullBackOff", "InvalidImageName", "ErrImageNeverPull")
 CONFIG_WAITING = ("CreateContainerConfigError", "CreateContainerError", "RunContainerError")
 EVICTION_EVENT_REASONS = ("Evicted", "Preempted", "Preempting", "TaintManagerEviction")
+NO_GPU_CLASSES = (F.IMAGE_PULL, F.CONFIG, F.SCHEDULING)
 JOB_FAILED_CONDITION_REASONS = ("DeadlineExceeded", "BackoffLimitExceeded", "PodFailurePolicy",
                                 "MaxFailedIndexesExceeded", "FailedIndexes")
 
@@ -106,6 +107,7 @@ class Classifier:
         # Live GPU evidence for pods without an agent annotation (supervisor co-located
         # with the GPUs, or a node agent in-process): pod -> evidence record or None.
         self.evidence_provider: Optional[Callable[[Dict[str, Any]], Optional[Dict[str, Any]]]] = None
+        self._ctx_cache: Dict[Tuple[str, str, bool], Tuple[Dict[str, Any], Optional[Dict[str, Any]]]] = {}
 
     # ------------------------------------------------------------ helpers
     def is_nexus(self, obj: Optional[Dict[str, Any]]) -> bool:
@@ -312,9 +314,23 @@ class Classifier:
             return None
         return ev if isinstance(ev, dict) else None
 
-    def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
+    def _pod_ctx(self, pod, want_gpu: bool = True):
+        """(topology, gpu evidence) for a pod version, memoised: the OOM verdict and the
+        enrichment of one decision read the same pod, and evidence snapshots are not free."""
+        key = (kube.uid_of(pod) or kube.name_of(pod), kube.resource_version(pod), want_gpu)
+        hit = self._ctx_cache.get(key)
+        if hit is not None:
+            return hit
         topo = topology_from_pod(pod, self.gpu.gpu_resource_name)
-        return oom_mod.analyze(texts, terms, self._gpu_evidence(pod), topo.get("expected_gpu"),
+        gev = self._gpu_evidence(pod) if want_gpu else None
+        if len(self._ctx_cache) > 4096:
+            self._ctx_cache.clear()
+        self._ctx_cache[key] = (topo, gev)
+        return topo, gev
+
+    def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
+        topo, gev = self._pod_ctx(pod)
+        return oom_mod.analyze(texts, terms, gev, topo.get("expected_gpu"),
                                self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
 
     def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
@@ -324,8 +340,9 @@ class Classifier:
         key = res.key
         if pods:
             pod = pods[-1]
-            topo = topology_from_pod(pod, self.gpu.gpu_resource_name)
-            gev = self._gpu_evidence(pod)
+            # a container that never started (image pull / config / scheduling) never touched a GPU
+            want_gpu = res.failure_class not in NO_GPU_CLASSES
+            topo, gev = self._pod_ctx(pod, want_gpu)
             topo = merge_process_ranks(topo, gev)
             if topo:
                 res.evidence["topology"] = topo

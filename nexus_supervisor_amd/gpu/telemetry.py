@@ -275,6 +275,9 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
     from ..models import kube
     from .topology import topology_from_pod
 
+    cache = {"t": -1.0, "snap": None}
+    ttl = max(0.005, telemetry.interval / 2)  # the native sampler cannot have anything newer
+
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         topo = topology_from_pod(pod, gpu_resource)
         gpus = []
@@ -283,7 +286,11 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
             gpus.append(int(exp))
         elif topo.get("visible_devices"):
             gpus.extend(int(d) for d in topo["visible_devices"] if str(d).isdigit())
+        now = time.monotonic()
+        if cache["snap"] is None or now - cache["t"] > ttl:
+            cache["snap"] = telemetry.snapshot(True)
+            cache["t"] = now
         return evidence_for(telemetry, pod_uid=kube.uid_of(pod), gpu_indices=gpus, lookback=lookback,
-                            node=node or (pod.get("spec") or {}).get("nodeName", ""))
+                            node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=cache["snap"])
 
     return provider

@@ -353,6 +353,8 @@ class CqlSession:
             try:
                 await self._open_host(h)
             except (OSError, asyncio.TimeoutError, StoreError) as exc:
+                if isinstance(exc, CqlError) and exc.code in (0x0100, 0x2100):
+                    raise  # bad credentials / unauthorized: no point trying other hosts
                 last = exc
                 log.warning("CQL contact point %s:%s unavailable: %s", addr[0], addr[1], exc)
                 continue

@@ -157,8 +157,8 @@ class FakeApiServer:
             if (not w.ns or w.ns == ns) and _matches(labels, w.sel):
                 w.queue.put_nowait(line)
 
-    def create(self, obj: Dict[str, Any]) -> Dict[str, Any]:
-        obj = copy.deepcopy(obj)
+    def create(self, obj: Dict[str, Any], copy_obj: bool = True) -> Dict[str, Any]:
+        obj = copy.deepcopy(obj) if copy_obj else obj
         kind = obj["kind"]
         obj.setdefault("apiVersion", _API_VERSION.get(kind, "v1"))
         meta = obj.setdefault("metadata", {})
@@ -192,8 +192,8 @@ class FakeApiServer:
                 if not s:
                     del self._pods_by_job[k]
 
-    def update(self, obj: Dict[str, Any], check_rv: bool = False) -> Dict[str, Any]:
-        obj = copy.deepcopy(obj)
+    def update(self, obj: Dict[str, Any], check_rv: bool = False, copy_obj: bool = True) -> Dict[str, Any]:
+        obj = copy.deepcopy(obj) if copy_obj else obj
         kind = obj["kind"]
         meta = obj["metadata"]
         key = (meta.get("namespace", ""), meta["name"])
@@ -221,8 +221,8 @@ class FakeApiServer:
         if obj is None:
             return None
         self._index(kind, obj, False)
-        obj = copy.deepcopy(obj)
-        obj["metadata"]["resourceVersion"] = self._next_rv()
+        obj = dict(obj)
+        obj["metadata"] = dict(obj["metadata"], resourceVersion=self._next_rv())
         self._record(kind, "DELETED", obj)
         self.deleted.append((kind, ns, name, propagation))
         if kind == "Job" and self.gc_pods and propagation in ("Background", "Foreground"):
