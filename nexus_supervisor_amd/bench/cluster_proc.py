@@ -94,7 +94,7 @@ async def amain(args) -> None:
     ctl.router.add_get("/bench/stats", h_stats)
     runner = web.AppRunner(ctl, access_log=None)
     await runner.setup()
-    site = web.TCPSite(runner, args.host, 0)
+    site = web.TCPSite(runner, args.host, 0, backlog=1024)
     await site.start()
     ctl_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
     tmp = args.ready_file + ".tmp"
@@ -107,7 +107,16 @@ async def amain(args) -> None:
 
     for sig in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(sig, stop.set)
+    sampler = None
+    if os.environ.get("NEXUS_CLUSTER_PPROF"):
+        from ..obs.pprof import Sampler
+
+        sampler = Sampler(hz=199).start()
     await stop.wait()
+    if sampler is not None:
+        prof = sampler.stop()
+        with open(os.environ["NEXUS_CLUSTER_PPROF"], "w") as f:
+            f.write(prof.top(40))
     await runner.cleanup()
     await api.stop()
     await store.close()

@@ -36,6 +36,7 @@ class BenchConfig:
     step_timeout: float = 300.0
     cql_latency_us: int = 0
     pprof_out: str = ""
+    kube_connections: int = 256
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:

@@ -48,6 +48,8 @@ class WireHarness:
     async def start(self) -> None:
         self.cql = CqlServer(exec_statements=schema_statements(), latency_us=self.cfg.cql_latency_us).start()
         ready = os.path.join(self.workdir, "cluster.ready")
+        if os.path.exists(ready):
+            os.unlink(ready)
         env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
         self._log = open(os.path.join(self.workdir, "cluster.log"), "ab")
         self.proc = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd.bench.cluster_proc", "--cql",
@@ -72,7 +74,7 @@ class WireHarness:
         sc.cql_store_type = "scylla"
         sc.scylla_cql_store.hosts = [f"127.0.0.1:{self.cql.port}"]
         sc.scylla_cql_store.consistency = "LOCAL_QUORUM"
-        kube = KubeClient(KubeConfig(info["api"]), max_connections=64)
+        kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)
         store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql.port)],
                                               connections_per_host=sc.scylla_cql_store.connections_per_host))
         self.app = Application(sc, kube=kube, store=store)

@@ -155,8 +155,11 @@ class KubeConfig:
 
 class KubeClient:
     def __init__(self, config: KubeConfig, *, request_timeout: float = 30.0, max_connections: int = 32,
-                 user_agent: str = "nexus-supervisor-amd/0.1"):
+                 user_agent: str = "nexus-supervisor-amd/0.1", pipelined_writes: bool = True, write_connections: int = 4):
         self.config = config
+        self.pipelined_writes = pipelined_writes
+        self.write_connections = write_connections
+        self._fast = None
         self.request_timeout = request_timeout
         self.max_connections = max_connections
         self.user_agent = user_agent
@@ -188,6 +191,18 @@ class KubeClient:
         if self._session is not None:
             await self._session.close()
             self._session = None
+        if self._fast is not None:
+            await self._fast.close()
+            self._fast = None
+
+    def _fast_client(self):
+        if self._fast is None:
+            from .fasthttp import PipelinedHttp
+
+            self._fast = PipelinedHttp(self.config.server, connections=self.write_connections,
+                                       ssl_ctx=self.config.ssl_context(), timeout=self.request_timeout,
+                                       default_headers={"User-Agent": self.user_agent, "Accept": "application/json"})
+        return self._fast
 
     async def request(self, method: str, path: str, *, params: Optional[Dict[str, Any]] = None, body: Any = None,
                       content_type: str = "application/json", timeout: Optional[float] = None) -> Dict[str, Any]:
@@ -290,7 +305,19 @@ class KubeClient:
 
     async def delete(self, kind: str, namespace: Optional[str], name: str, propagation_policy: str = "Background") -> Dict[str, Any]:
         body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
-        return await self.request("DELETE", resource_path(kind, namespace, name), body=body)
+        path = resource_path(kind, namespace, name)
+        if not self.pipelined_writes:
+            return await self.request("DELETE", path, body=body)
+        self.requests += 1
+        status, raw = await self._fast_client().request(
+            "DELETE", path, json.dumps(body).encode(), self._headers({"Content-Type": "application/json"}))
+        try:
+            doc = json.loads(raw) if raw else {}
+        except ValueError:
+            doc = {"message": raw[:500].decode("utf-8", "replace")}
+        if status >= 400:
+            raise from_status(status, doc)
+        return doc
 
     # JobClient protocol (Supervisor actuator)
     async def delete_job(self, namespace: str, name: str, propagation_policy: str = "Background") -> None:

@@ -1,0 +1,227 @@
+"""Pipelined HTTP/1.1 client for the supervisor's Kubernetes write path.
+
+Every failing decision issues one ``DELETE …/jobs/{name}`` (the reference:
+``/root/reference/services/supervisor.go:262-291``).  Through a general-purpose
+client each request costs a connection checkout, header objects and at least
+one ``send``/``recv`` pair; at thousands of decisions per second that overhead
+dominates the actuator.  This client keeps a few persistent connections,
+*pipelines* requests on them (HTTP/1.1 §6.3.2 — Go's ``net/http`` and aiohttp
+servers both process pipelined requests in order), coalesces every request
+issued in one loop tick into a single ``send``, and parses responses
+incrementally in arrival order.
+
+Only idempotent methods should be pipelined (a connection dropped mid-flight
+fails every request queued on it; DELETE retried after a lost response sees
+``404``, which the actuator treats as success).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import ssl as _ssl
+from typing import Deque, Dict, List, Optional, Tuple
+from urllib.parse import urlsplit
+
+
+class HttpError(Exception):
+    pass
+
+
+class _Conn(asyncio.Protocol):
+    def __init__(self, pool: "PipelinedHttp"):
+        self.pool = pool
+        self.transport: Optional[asyncio.Transport] = None
+        self.waiting: Deque[asyncio.Future] = collections.deque()
+        self.buf = bytearray()
+        self.out: List[bytes] = []
+        self.flush_scheduled = False
+        self.closed = False
+        # parser state for the response at the head of the queue
+        self._status = 0
+        self._headers: Dict[str, str] = {}
+        self._need = -1       # body bytes still needed (content-length mode)
+        self._chunked = False
+        self._body = bytearray()
+        self._in_body = False
+
+    # ----------------------------------------------------------- asyncio.Protocol
+    def connection_made(self, transport):
+        self.transport = transport
+
+    def connection_lost(self, exc):
+        self.closed = True
+        err = HttpError(f"connection lost: {exc}")
+        while self.waiting:
+            f = self.waiting.popleft()
+            if not f.done():
+                f.set_exception(err)
+        self.pool._drop(self)
+
+    def data_received(self, data: bytes):
+        self.buf += data
+        try:
+            while self.waiting and self._parse():
+                pass
+        except HttpError as exc:
+            self._fail(exc)
+
+    # ----------------------------------------------------------- parsing
+    def _parse(self) -> bool:
+        buf = self.buf
+        if not self._in_body:
+            end = buf.find(b"\r\n\r\n")
+            if end < 0:
+                return False
+            head = bytes(buf[:end]).decode("latin-1").split("\r\n")
+            del buf[: end + 4]
+            parts = head[0].split(" ", 2)
+            if len(parts) < 2 or not parts[0].startswith("HTTP/1."):
+                raise HttpError(f"bad status line {head[0]!r}")
+            self._status = int(parts[1])
+            hdrs = {}
+            for line in head[1:]:
+                k, _, v = line.partition(":")
+                hdrs[k.strip().lower()] = v.strip()
+            self._headers = hdrs
+            self._chunked = "chunked" in hdrs.get("transfer-encoding", "").lower()
+            self._need = int(hdrs.get("content-length", "0")) if not self._chunked else -1
+            self._body = bytearray()
+            self._in_body = True
+        if self._chunked:
+            while True:
+                end = buf.find(b"\r\n")
+                if end < 0:
+                    return False
+                size = int(bytes(buf[:end]).split(b";", 1)[0], 16)
+                if len(buf) < end + 2 + size + 2:
+                    return False
+                if size == 0:
+                    # no trailers expected from the apiserver
+                    del buf[: end + 4]
+                    break
+                self._body += buf[end + 2: end + 2 + size]
+                del buf[: end + 2 + size + 2]
+        else:
+            if len(buf) < self._need:
+                return False
+            self._body = bytearray(buf[: self._need])
+            del buf[: self._need]
+        self._in_body = False
+        fut = self.waiting.popleft()
+        if not fut.done():
+            fut.set_result((self._status, bytes(self._body)))
+        if self._headers.get("connection", "").lower() == "close":
+            self.transport.close()
+        return True
+
+    def _fail(self, exc: Exception) -> None:
+        while self.waiting:
+            f = self.waiting.popleft()
+            if not f.done():
+                f.set_exception(exc)
+        if self.transport is not None:
+            self.transport.close()
+
+    # ----------------------------------------------------------- sending
+    def send(self, data: bytes, fut: asyncio.Future) -> None:
+        self.waiting.append(fut)
+        self.out.append(data)
+        if not self.flush_scheduled:
+            self.flush_scheduled = True
+            asyncio.get_running_loop().call_soon(self._flush)
+
+    def _flush(self) -> None:
+        self.flush_scheduled = False
+        if self.out and not self.closed and self.transport is not None:
+            self.transport.write(b"".join(self.out))
+        self.out = []
+
+
+class PipelinedHttp:
+    def __init__(self, base_url: str, *, connections: int = 4, max_depth: int = 128,
+                 ssl_ctx: Optional[_ssl.SSLContext] = None, default_headers: Optional[Dict[str, str]] = None,
+                 timeout: float = 30.0):
+        u = urlsplit(base_url)
+        self.host = u.hostname or "127.0.0.1"
+        self.port = u.port or (443 if u.scheme == "https" else 80)
+        self.https = u.scheme == "https"
+        self.ssl_ctx = ssl_ctx if self.https else None
+        self.hostport = f"{self.host}:{self.port}" if u.port else self.host
+        self.n = max(1, connections)
+        self.max_depth = max_depth
+        self.default_headers = dict(default_headers or {})
+        self.timeout = timeout
+        self._conns: List[_Conn] = []
+        self._connecting: Optional[asyncio.Future] = None
+        self.requests = 0
+
+    def _drop(self, c: _Conn) -> None:
+        if c in self._conns:
+            self._conns.remove(c)
+
+    async def _open(self) -> _Conn:
+        loop = asyncio.get_running_loop()
+        kw = {"ssl": self.ssl_ctx, "server_hostname": self.host} if self.https else {}
+        _, proto = await loop.create_connection(lambda: _Conn(self), self.host, self.port, **kw)
+        sock = proto.transport.get_extra_info("socket")
+        if sock is not None:
+            import socket
+
+            try:
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+        self._conns.append(proto)
+        return proto
+
+    async def _fill(self) -> None:
+        missing = self.n - len([c for c in self._conns if not c.closed])
+        if missing > 0:
+            await asyncio.gather(*(self._open() for _ in range(missing)))
+
+    async def _pick(self) -> _Conn:
+        live = [c for c in self._conns if not c.closed]
+        if len(live) < self.n:
+            # (re)open the pool once; concurrent callers wait on the same attempt
+            if self._connecting is None or self._connecting.done():
+                self._connecting = asyncio.ensure_future(self._fill())
+            if not live:
+                await asyncio.shield(self._connecting)
+                live = [c for c in self._conns if not c.closed]
+                if not live:
+                    raise HttpError(f"cannot connect to {self.hostport}")
+        best = min(live, key=lambda c: len(c.waiting))
+        if len(best.waiting) >= self.max_depth:
+            # all connections saturated: wait for the shortest queue to drain a bit
+            while len(best.waiting) >= self.max_depth and not best.closed:
+                await asyncio.sleep(0.001)
+        return best
+
+    def _encode(self, method: str, path: str, body: Optional[bytes], headers: Optional[Dict[str, str]]) -> bytes:
+        h = dict(self.default_headers)
+        if headers:
+            h.update(headers)
+        lines = [f"{method} {path} HTTP/1.1", f"Host: {self.hostport}"]
+        lines += [f"{k}: {v}" for k, v in h.items()]
+        lines.append(f"Content-Length: {len(body) if body else 0}")
+        return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1") + (body or b"")
+
+    async def request(self, method: str, path: str, body: Optional[bytes] = None,
+                      headers: Optional[Dict[str, str]] = None) -> Tuple[int, bytes]:
+        conn = await self._pick()
+        fut = asyncio.get_running_loop().create_future()
+        conn.send(self._encode(method, path, body, headers), fut)
+        self.requests += 1
+        try:
+            return await asyncio.wait_for(fut, self.timeout)
+        except asyncio.TimeoutError:
+            # the response order on this connection is now unknown: reset it
+            conn._fail(HttpError("request timed out"))
+            raise HttpError(f"{method} {path} timed out") from None
+
+    async def close(self) -> None:
+        for c in list(self._conns):
+            if c.transport is not None:
+                c.transport.close()
+        self._conns.clear()
+        await asyncio.sleep(0)

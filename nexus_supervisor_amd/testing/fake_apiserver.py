@@ -126,7 +126,7 @@ class FakeApiServer:
             app.router.add_route("GET", f"{prefix}/{plural}", self._h_collection)
         self._runner = web.AppRunner(app, access_log=None)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, host, port)
+        site = web.TCPSite(self._runner, host, port, backlog=4096)
         await site.start()
         sock = site._server.sockets[0]  # noqa: SLF001
         self.url = f"http://{host}:{sock.getsockname()[1]}"
