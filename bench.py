@@ -52,6 +52,8 @@ def parse_args(argv=None):
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
     ap.add_argument("--workers", type=int, default=256)
+    ap.add_argument("--inflight", type=int, default=2, help="steps pushed ahead of acknowledgement")
+    ap.add_argument("--kube-connections", type=int, default=256)
     ap.add_argument("--no-real-oom", action="store_true", help="skip the real HBM-OOM on the rank's GPU")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default="")
@@ -123,7 +125,8 @@ def main(argv=None) -> int:
     cfg = BenchConfig(rank=rank, world=world, local_rank=local_rank, jobs=args.jobs, events=args.events,
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
-                      workdir=workdir, cql_latency_us=args.cql_latency_us,
+                      workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
+                      kube_connections=args.kube_connections,
                       pprof_out=args.pprof_out if rank == 0 else "")
     res = asyncio.run(run_rank(cfg, barrier_sync))
 
@@ -180,6 +183,7 @@ def main(argv=None) -> int:
                 "profile": args.profile,
                 "store": res.get("store"),
                 "workers": res.get("workers"),
+                "inflight_steps": args.inflight,
                 "rate_limit_eps": res.get("eps"),
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),

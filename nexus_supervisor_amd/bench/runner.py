@@ -37,6 +37,7 @@ class BenchConfig:
     cql_latency_us: int = 0
     pprof_out: str = ""
     kube_connections: int = 256
+    inflight: int = 2
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -57,47 +58,65 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
 
 
 class Tracker:
-    """Decision hook: checkpoint-ack time per run; latency = ack − pod-fail push."""
+    """Decision hook: checkpoint-ack time per run; latency = ack − pod-fail push.
+
+    Several steps may be in flight at once (the generator runs ahead of the
+    supervisor, as a live cluster would); each step completes when every run it
+    failed has been acknowledged by the store."""
 
     def __init__(self):
         self.acks: Dict[str, Tuple[float, str]] = {}
-        self.waiting: set = set()
-        self.t_push = 0.0
+        self.owner: Dict[str, "StepState"] = {}
         self.latencies: List[float] = []
         self.errors = 0
-        self.done = asyncio.Event()
         self.record = False
-        self.stage_sums: Dict[str, float] = {}
 
     def __call__(self, d: Decision):
         rid = d.result.request_id
         t = time.monotonic()
-        self.acks[rid] = (t, d.outcome)
-        if rid in self.waiting:
-            self._settle(rid, t, d.outcome)
+        st = self.owner.pop(rid, None)
+        if st is None:
+            self.acks[rid] = (t, d.outcome)  # ack raced ahead of the step response
+            return
+        st.settle(self, rid, t, d.outcome)
 
-    def _settle(self, rid: str, t: float, outcome: str) -> None:
+    def arm(self, rids: List[str], t_push: float) -> "StepState":
+        st = StepState(set(rids), t_push, self.record)
+        for rid in rids:
+            a = self.acks.pop(rid, None)
+            if a is not None:
+                st.settle(self, rid, *a)
+            else:
+                self.owner[rid] = st
+        if not st.waiting:
+            st.done.set()
+        return st
+
+    def abandon(self, st: "StepState") -> None:
+        self.errors += len(st.waiting)
+        for rid in st.waiting:
+            self.owner.pop(rid, None)
+        st.waiting.clear()
+        st.done.set()
+
+
+class StepState:
+    __slots__ = ("waiting", "t_push", "record", "done")
+
+    def __init__(self, waiting, t_push, record):
+        self.waiting = waiting
+        self.t_push = t_push
+        self.record = record
+        self.done = asyncio.Event()
+
+    def settle(self, tr: Tracker, rid: str, t: float, outcome: str) -> None:
         self.waiting.discard(rid)
         if outcome != "applied":
-            self.errors += 1
+            tr.errors += 1
         elif self.record:
-            self.latencies.append((t - self.t_push) * 1000.0)
+            tr.latencies.append((t - self.t_push) * 1000.0)
         if not self.waiting:
             self.done.set()
-
-    def arm(self, rids: List[str], t_push: float) -> None:
-        self.t_push = t_push
-        self.waiting = set(rids)
-        self.done.clear()
-        for rid in rids:
-            a = self.acks.get(rid)
-            if a is not None:
-                self._settle(rid, *a)
-        if not self.waiting:
-            self.done.set()
-
-    def reset_step(self) -> None:
-        self.acks.clear()
 
 
 class InProcHarness:
@@ -150,18 +169,25 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         sup.classifier.evidence_provider = pod_evidence_provider(telemetry)
         sup.decision_hooks.append(tracker)
 
-        async def one_step() -> None:
-            tracker.reset_step()
-            failed, t_push = await harness.step(cfg.events)
-            tracker.arm(failed, t_push)
-            try:
-                await asyncio.wait_for(tracker.done.wait(), cfg.step_timeout)
-            except asyncio.TimeoutError:
-                tracker.errors += len(tracker.waiting)
-                tracker.waiting.clear()
+        async def run_steps(n: int) -> None:
+            """Push ``n`` steps with at most ``cfg.inflight`` unacknowledged at a time."""
+            pending: List[StepState] = []
 
-        for _ in range(cfg.warmup):
-            await one_step()
+            async def finish(st: StepState) -> None:
+                try:
+                    await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
+                except asyncio.TimeoutError:
+                    tracker.abandon(st)
+
+            for _ in range(n):
+                while len(pending) >= cfg.inflight:
+                    await finish(pending.pop(0))
+                failed, t_push = await harness.step(cfg.events)
+                pending.append(tracker.arm(failed, t_push))
+            for st in pending:
+                await finish(st)
+
+        await run_steps(cfg.warmup)
         gc.collect()
         tracker.errors = 0
         tracker.record = True
@@ -171,8 +197,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             sampler = Sampler(hz=199).start()
         barrier_sync()
         t0 = time.perf_counter()
-        for _ in range(cfg.steps):
-            await one_step()
+        await run_steps(cfg.steps)
         barrier_sync()
         elapsed = time.perf_counter() - t0
         if sampler is not None:

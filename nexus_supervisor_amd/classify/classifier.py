@@ -107,6 +107,7 @@ class Classifier:
         # Live GPU evidence for pods without an agent annotation (supervisor co-located
         # with the GPUs, or a node agent in-process): pod -> evidence record or None.
         self.evidence_provider: Optional[Callable[[Dict[str, Any]], Optional[Dict[str, Any]]]] = None
+        self.deferred = False
         self._ctx_cache: Dict[Tuple[str, str, bool], Tuple[Dict[str, Any], Optional[Dict[str, Any]]]] = {}
 
     # ------------------------------------------------------------ helpers
@@ -183,7 +184,15 @@ class Classifier:
         return NOOP, []
 
     # ------------------------------------------------------------ R-POD
-    def classify_pod(self, pod: Dict[str, Any], old: Optional[Dict[str, Any]] = None) -> List[RunStatusAnalysisResult]:
+    def has_gpu_evidence(self, pod: Dict[str, Any]) -> bool:
+        return self.evidence_provider is not None or bool(kube.annotations_of(pod).get(self.gpu.evidence_annotation))
+
+    def classify_pod(self, pod: Dict[str, Any], old: Optional[Dict[str, Any]] = None,
+                     allow_wait: bool = False) -> List[RunStatusAnalysisResult]:
+        """Pod-status rules.  With ``allow_wait`` a failed GPU pod whose node agent has not
+        annotated it yet is *deferred* (``self.deferred`` set, no result) so the caller can
+        give the evidence ``gpu.evidence-wait`` to arrive."""
+        self.deferred = False
         if not self.rules.pod_status_rules or not self.is_nexus(pod):
             return []
         if old is not None and kube.resource_version(old) == kube.resource_version(pod) and kube.resource_version(pod):
@@ -199,6 +208,9 @@ class Classifier:
         # 1. OOM (host cgroup OOMKilled or HIP OOM signature on a terminated container)
         failed_terms = [t for t in current_terms if t.get("exitCode", 0) != 0 or t.get("reason") == "OOMKilled"]
         if failed_terms:
+            if allow_wait and not self.has_gpu_evidence(pod) and kube.gpu_request(pod, self.gpu.gpu_resource_name) > 0:
+                self.deferred = True
+                return []
             verdict = self._oom(pod, [t.get("message", "") for t in failed_terms], failed_terms)
             if verdict.kind:
                 hbm = verdict.kind == "hbm"
@@ -206,6 +218,13 @@ class Classifier:
                 res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_HBM_OOM if hbm else MSG_HOST_OOM,
                                    t0.get("message") or t0.get("reason") or "", inv, request_id, algorithm,
                                    t0.get("reason") or "Error", F.HBM_OOM if hbm else F.HOST_OOM, "pod-status")
+                self._enrich(res, pods=[pod], verdict=verdict)
+                return [res]
+            faults = self._gpu_faults(pod)
+            if faults:
+                t0 = failed_terms[0]
+                res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_GPU_FAULT, t0.get("message") or t0.get("reason") or "", inv,
+                                   request_id, algorithm, "GpuFault:" + ",".join(faults), F.GPU_FAULT, "pod-status")
                 self._enrich(res, pods=[pod], verdict=verdict)
                 return [res]
             for t in failed_terms:
@@ -327,6 +346,18 @@ class Classifier:
             self._ctx_cache.clear()
         self._ctx_cache[key] = (topo, gev)
         return topo, gev
+
+    def _gpu_faults(self, pod) -> List[str]:
+        """GPU fault events (VM fault, reset) inside the pod's evidence window."""
+        _topo, gev = self._pod_ctx(pod)
+        if not gev:
+            return []
+        kinds = set()
+        for g in gev.get("gpus", []):
+            for e in g.get("events", []):
+                if e.get("type") in ("VMFAULT", "GPU_PRE_RESET", "GPU_POST_RESET"):
+                    kinds.add(e["type"])
+        return sorted(kinds)
 
     def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
         topo, gev = self._pod_ctx(pod)

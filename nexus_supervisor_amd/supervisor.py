@@ -119,6 +119,7 @@ class Supervisor:
         self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
         self._applied_cap = 200_000
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
+        self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
         self._sweeper: Optional[asyncio.Task] = None
         self.decision_hooks: List[Callable[[Decision], None]] = []
         self.active = not cfg.leader_election.enabled  # leader gating flips this
@@ -238,12 +239,33 @@ class Supervisor:
         self._unpark("Pod", kube.name_of(pod))
         self._on_pod_update(None, pod)
 
-    def _on_pod_update(self, old, pod):
+    def _on_pod_update(self, old, pod, waited: bool = False):
         if not self.active or old is pod:
             return
         recv = self.wall()
-        for r in self.classifier.classify_pod(pod, old):
+        wait = self.cfg.gpu.evidence_wait
+        results = self.classifier.classify_pod(pod, old, allow_wait=wait > 0 and not waited)
+        key = kube.object_key(pod)
+        if self.classifier.deferred:
+            # failed GPU pod without node-agent evidence yet: give the annotation time to land
+            if key not in self._gpu_wait:
+                self._gpu_wait[key] = time.monotonic() + wait
+                self.metrics.inc("decisions_deferred_for_gpu_evidence")
+            return
+        self._gpu_wait.pop(key, None)
+        for r in results:
             self._submit(r, recv, recv)
+
+    def _expire_gpu_waits(self) -> None:
+        now = time.monotonic()
+        for key, deadline in list(self._gpu_wait.items()):
+            if deadline > now:
+                continue
+            del self._gpu_wait[key]
+            pod = self.pod_informer.indexer.get(key)
+            if pod is not None:
+                self.metrics.inc("gpu_evidence_wait_expired")
+                self._on_pod_update(None, pod, waited=True)
 
     def _on_job_add(self, job):
         self._unpark("Job", kube.name_of(job))
@@ -279,8 +301,12 @@ class Supervisor:
                 self._on_event_add(ev)
 
     async def _sweep_parked(self):
+        tick = max(0.02, min(1.0, self.cfg.rules.stale_event_grace / 4 or 1.0,
+                             self.cfg.gpu.evidence_wait / 4 if self.cfg.gpu.evidence_wait > 0 else 1.0))
         while True:
-            await asyncio.sleep(max(0.05, min(1.0, self.cfg.rules.stale_event_grace / 4 or 1.0)))
+            await asyncio.sleep(tick)
+            if self._gpu_wait:
+                self._expire_gpu_waits()
             now = time.monotonic()
             for key in list(self._parked):
                 lst = [p for p in self._parked[key] if p[0] > now]

@@ -70,6 +70,26 @@ def _matches(labels: Dict[str, str], sel) -> bool:
     return True
 
 
+_FIELD_PATHS = ("metadata.name", "metadata.namespace", "spec.nodeName", "status.phase", "involvedObject.kind",
+                "involvedObject.name", "reason", "type")
+
+
+def _selectable(obj: Dict[str, Any]) -> Dict[str, str]:
+    """Labels plus the supported field-selector paths (prefixed ``\0f:``) of an object."""
+    out = dict(obj.get("metadata", {}).get("labels") or {})
+    for path in _FIELD_PATHS:
+        cur: Any = obj
+        for part in path.split("."):
+            cur = cur.get(part) if isinstance(cur, dict) else None
+        if isinstance(cur, str):
+            out["\0f:" + path] = cur
+    return out
+
+
+def _parse_fields(sel: str):
+    return [("\0f:" + k, op, v) for k, op, v in _parse_selector(sel)]
+
+
 def _merge(dst: Dict[str, Any], patch: Dict[str, Any]) -> Dict[str, Any]:
     for k, v in patch.items():
         if v is None:
@@ -146,7 +166,7 @@ class FakeApiServer:
     def _record(self, kind: str, etype: str, obj: Dict[str, Any]) -> None:
         rv = int(obj["metadata"]["resourceVersion"])
         line = json.dumps({"type": etype, "object": obj}, separators=(",", ":")).encode() + b"\n"
-        labels = obj["metadata"].get("labels") or {}
+        labels = _selectable(obj)
         ns = obj["metadata"].get("namespace", "")
         h = self.history[kind]
         h.append((rv, ns, line, labels))
@@ -288,9 +308,9 @@ class FakeApiServer:
             return bad
         kind = self._kind(req)
         ns = req.match_info.get("ns", "")
-        sel = _parse_selector(req.query.get("labelSelector", ""))
+        sel = _parse_selector(req.query.get("labelSelector", "")) + _parse_fields(req.query.get("fieldSelector", ""))
         items = [o for (ons, _), o in self.objects[kind].items()
-                 if (not ns or ons == ns) and _matches(o["metadata"].get("labels") or {}, sel)]
+                 if (not ns or ons == ns) and _matches(_selectable(o), sel)]
         items.sort(key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
         limit = int(req.query.get("limit", "0") or 0)
         start = int(req.query.get("continue", "0") or 0)
@@ -310,7 +330,7 @@ class FakeApiServer:
         self.watch_requests += 1
         kind = self._kind(req)
         ns = req.match_info.get("ns", "")
-        sel = _parse_selector(req.query.get("labelSelector", ""))
+        sel = _parse_selector(req.query.get("labelSelector", "")) + _parse_fields(req.query.get("fieldSelector", ""))
         rv_s = req.query.get("resourceVersion", "")
         timeout = float(req.query.get("timeoutSeconds", "0") or 0) or 1800.0
         bookmarks = req.query.get("allowWatchBookmarks") in ("true", "1")

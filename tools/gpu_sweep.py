@@ -1,0 +1,27 @@
+"""Bench configuration sweep on the GPU box (one process per config, sequential)."""
+import json
+import subprocess
+import sys
+
+CONFIGS = [
+    ["--transport", "inproc"],
+    ["--inflight", "1"],
+    ["--inflight", "2"],
+    ["--inflight", "3"],
+    ["--inflight", "2", "--workers", "1024"],
+    ["--inflight", "2", "--events", "2000"],
+]
+out = []
+for extra in CONFIGS:
+    cmd = [sys.executable, "bench.py", "--steps", "6", "--warmup", "1", "--no-real-oom"] + extra + sys.argv[1:]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    line = p.stdout.strip().splitlines()[-1] if p.stdout.strip() else ""
+    try:
+        d = json.loads(line)
+        rec = {"args": extra, "value": d["value"], "p50_ms": d["p50_ms"], "p99_ms": d["p99_ms"], "errors": d["errors"]}
+    except Exception:
+        rec = {"args": extra, "error": p.stderr[-800:]}
+    print(json.dumps(rec), flush=True)
+    out.append(rec)
+with open("gpurun_out/sweep.json", "w") as f:
+    json.dump(out, f, indent=1)
