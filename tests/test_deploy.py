@@ -1,0 +1,96 @@
+"""Helm chart render tests (no helm binary offline: ``deploy/render.py`` renders the
+Go-template subset the chart uses).  Parity target: the reference chart maps the
+same values to the same ``NEXUS__*`` env names
+(``/root/reference/.helm/templates/deployment.yaml:48-67``)."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deploy"))
+
+from render import render_docs  # noqa: E402
+
+from nexus_supervisor_amd.config import iter_keys, load_config  # noqa: E402
+
+CHART = os.path.join(ROOT, "deploy", "helm", "nexus-supervisor-amd")
+
+
+def _by_kind(docs):
+    out = {}
+    for d in docs:
+        out.setdefault(d["kind"], []).append(d)
+    return out
+
+
+def _env(container):
+    return {e["name"]: e.get("value") for e in container.get("env", [])}
+
+
+def test_default_render_objects():
+    k = _by_kind(render_docs(CHART))
+    assert {"Deployment", "DaemonSet", "Role", "RoleBinding", "ServiceAccount", "Service", "PodDisruptionBudget"} <= set(k)
+    dep = k["Deployment"][0]
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    assert c["args"] == ["supervisor"]
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz" and c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert dep["spec"]["replicas"] == 2
+
+
+def test_env_names_are_config_keys_and_load_back():
+    dep = _by_kind(render_docs(CHART))["Deployment"][0]
+    env = _env(dep["spec"]["template"]["spec"]["containers"][0])
+    known = {name for _p, name, _d, _f in iter_keys()}
+    nexus = {k: v for k, v in env.items() if k.startswith("NEXUS__")}
+    assert set(nexus) <= known, set(nexus) - known
+    # the reference's env names (deployment.yaml:48-67) are all present
+    for name in ("NEXUS__RESOURCE_NAMESPACE", "NEXUS__CQL_STORE_TYPE", "NEXUS__LOG_LEVEL", "NEXUS__FAILURE_RATE_BASE_DELAY",
+                 "NEXUS__FAILURE_RATE_MAX_DELAY", "NEXUS__RATE_LIMIT_ELEMENTS_PER_SECOND",
+                 "NEXUS__RATE_LIMIT_ELEMENTS_BURST", "NEXUS__WORKERS", "NEXUS__KUBE_CONFIG_PATH"):
+        assert name in nexus, name
+    cfg = load_config(path=None, env=nexus)
+    assert cfg.workers == 2 and cfg.rate_limit_elements_per_second == 10 and cfg.rate_limit_elements_burst == 100
+    assert cfg.failure_rate_base_delay == pytest.approx(0.1) and cfg.failure_rate_max_delay == pytest.approx(1.0)
+    assert cfg.cql_store_type == "astra" and cfg.resource_namespace == "nexus"
+    assert cfg.leader_election.enabled and cfg.leader_election.lease_duration == 15.0
+    assert cfg.gpu.evidence_wait == pytest.approx(2.0) and cfg.observability.http_port == 9100
+
+
+def test_rbac_namespaced_and_cluster_scoped():
+    k = _by_kind(render_docs(CHART))
+    sup_role = [r for r in k["Role"] if not r["metadata"]["name"].endswith("gpu-agent")][0]
+    rules = {(tuple(r["apiGroups"]), tuple(r["resources"])): set(r["verbs"]) for r in sup_role["rules"]}
+    assert rules[(("",), ("events", "pods"))] == {"get", "list", "watch"}
+    assert "delete" in rules[(("batch",), ("jobs",))]
+    assert {"get", "create", "update"} <= rules[(("coordination.k8s.io",), ("leases",))]
+    k2 = _by_kind(render_docs(CHART, sets=["rbac.clusterScoped=true"]))
+    assert "ClusterRole" in k2 and "ClusterRoleBinding" in k2
+    assert k2["ClusterRoleBinding"][0]["roleRef"]["kind"] == "ClusterRole"
+
+
+def test_agent_daemonset_gpu_access():
+    ds = _by_kind(render_docs(CHART))["DaemonSet"][0]
+    spec = ds["spec"]["template"]["spec"]
+    assert spec["hostPID"] is True
+    mounts = {m["mountPath"] for m in spec["containers"][0]["volumeMounts"]}
+    assert {"/dev/kfd", "/dev/dri", "/var/lib/kubelet/pod-resources"} <= mounts
+    env = {e["name"]: e for e in spec["containers"][0]["env"]}
+    assert env["NODE_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"
+    assert spec["nodeSelector"] == {"amd.com/gpu.product-name": "AMD_Instinct_MI355X_OAM"}
+    assert "DaemonSet" not in _by_kind(render_docs(CHART, sets=["agent.enabled=false"]))
+
+
+def test_scylla_and_datadog_values():
+    docs = render_docs(CHART, values={"supervisor": {"config": {"cqlStore": {"type": "scylla", "scylla": {
+        "hosts": ["scylla-0.scylla", "scylla-1.scylla"], "localDc": "dc1"}}}}, "datadog": {"enabled": True}})
+    dep = _by_kind(docs)["Deployment"][0]
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    env = _env(c)
+    assert env["NEXUS__SCYLLA_CQL_STORE__HOSTS"] == "scylla-0.scylla,scylla-1.scylla"
+    cfg = load_config(path=None, env={k: v for k, v in env.items() if k.startswith("NEXUS__") and v is not None})
+    assert cfg.scylla_cql_store.hosts == ["scylla-0.scylla", "scylla-1.scylla"] and cfg.scylla_cql_store.local_dc == "dc1"
+    assert env["DD_DOGSTATSD_URL"] == "unix:///var/run/datadog/dsd.socket"
+    assert any(v["name"] == "dsdsocket" for v in dep["spec"]["template"]["spec"]["volumes"])
+    # the secretRef is rendered whenever secretRefEnabled (reference quirk fixed)
+    assert c["envFrom"][0]["secretRef"]["name"].endswith("-cql")
