@@ -53,6 +53,13 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
             "deps": [proto],
             "cmd": lambda out, srcs: [_cxx(), *common, "-shared", "-fPIC", *_pybind_includes(), *srcs, "-o", out],
         },
+        "kube_native": {
+            "out": os.path.join(PKG, "_kube_native" + EXT),
+            "srcs": [os.path.join(CSRC, "kube", "watch_decoder.cpp")],
+            "deps": [],
+            "cmd": lambda out, srcs: [_cxx(), *common, "-O3", "-shared", "-fPIC", f"-I{sysconfig.get_paths()['include']}",
+                                      *srcs, "-o", out],
+        },
         "amdsmi_monitor": {
             "out": os.path.join(PKG, "_amdsmi_monitor" + EXT),
             "srcs": [os.path.join(CSRC, "amdsmi", "gpu_monitor.cpp")],

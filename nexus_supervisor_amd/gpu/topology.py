@@ -93,6 +93,17 @@ def expected_gpu(topo: Dict[str, Any]) -> Optional[str]:
 
 
 def topology_from_pod(pod: Dict[str, Any], gpu_resource: str = "amd.com/gpu") -> Dict[str, Any]:
+    """Topology of one pod version, memoised on the (immutable, per-version) object."""
+    rv = kube.resource_version(pod)
+    cache = pod.get("_topo")
+    if cache is not None and cache[0] == gpu_resource and cache[1] == rv and rv:
+        return cache[2]
+    topo = _topology_from_pod(pod, gpu_resource)
+    pod["_topo"] = (gpu_resource, rv, topo)
+    return topo
+
+
+def _topology_from_pod(pod: Dict[str, Any], gpu_resource: str) -> Dict[str, Any]:
     env = kube.pod_env(pod)
     ann = kube.annotations_of(pod)
     idx = ann.get("batch.kubernetes.io/job-completion-index")

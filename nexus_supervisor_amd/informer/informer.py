@@ -62,7 +62,10 @@ class SharedInformer:
         self.lw = lw
         self.resync_period = resync_period
         self.indexer = Indexer(indexers)
-        self.transform = transform if transform is not None else kube.SLIMMERS.get(kind)
+        if transform is None:
+            # a ListWatch that already projects objects (native decode) supplies its own finisher
+            transform = getattr(lw, "transform", kube.SLIMMERS.get(kind)) if hasattr(lw, "transform") else kube.SLIMMERS.get(kind)
+        self.transform = transform
         self.handlers: List[Handler] = []
         self._synced = asyncio.Event() if _has_loop() else None
         self._rv = ""

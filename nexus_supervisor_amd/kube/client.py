@@ -31,7 +31,24 @@ from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 import aiohttp
 
 from ..informer.informer import ListWatch
+from ..models.kube import FINISHERS, PROJECTIONS, list_projection, watch_projection
 from .errors import ApiError, from_status
+
+
+def _native_decoder_available() -> bool:
+    try:
+        from .. import _kube_native  # noqa: F401
+
+        return True
+    except ImportError:
+        log.warning("native watch decoder (_kube_native) not built; using json + Python slimming")
+        return False
+
+
+def _decoder(projection):
+    from .. import _kube_native
+
+    return _kube_native.ProjectedDecoder(projection)
 
 log = logging.getLogger("nexus_supervisor_amd.kube")
 
@@ -51,6 +68,17 @@ def resource_path(kind: str, namespace: Optional[str], name: Optional[str] = Non
     prefix, plural = RESOURCES[kind]
     p = f"{prefix}/namespaces/{namespace}/{plural}" if namespace else f"{prefix}/{plural}"
     return f"{p}/{name}" if name else p
+
+
+_DELETE_BODIES: Dict[str, bytes] = {}
+
+
+def _delete_body(policy: str) -> bytes:
+    b = _DELETE_BODIES.get(policy)
+    if b is None:
+        b = _DELETE_BODIES[policy] = json.dumps(
+            {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": policy}).encode()
+    return b
 
 
 class KubeConfig:
@@ -205,7 +233,8 @@ class KubeClient:
         return self._fast
 
     async def request(self, method: str, path: str, *, params: Optional[Dict[str, Any]] = None, body: Any = None,
-                      content_type: str = "application/json", timeout: Optional[float] = None) -> Dict[str, Any]:
+                      content_type: str = "application/json", timeout: Optional[float] = None,
+                      decoder=None) -> Dict[str, Any]:
         s = await self._s()
         self.requests += 1
         data = json.dumps(body) if body is not None else None
@@ -214,7 +243,10 @@ class KubeClient:
                              timeout=aiohttp.ClientTimeout(total=timeout or self.request_timeout)) as r:
             raw = await r.read()
             try:
-                doc = json.loads(raw) if raw else {}
+                if decoder is not None and r.status < 400 and raw:
+                    doc = decoder.decode(raw)
+                else:
+                    doc = json.loads(raw) if raw else {}
             except ValueError:
                 doc = {"message": raw[:500].decode("utf-8", "replace")}
             if r.status >= 400:
@@ -223,7 +255,8 @@ class KubeClient:
 
     # ------------------------------------------------------------------ typed helpers
     async def list(self, kind: str, namespace: Optional[str], *, label_selector: str = "", field_selector: str = "",
-                   limit: int = 500) -> Tuple[List[Dict[str, Any]], str]:
+                   limit: int = 500, projected: bool = False) -> Tuple[List[Dict[str, Any]], str]:
+        decoder = _decoder(list_projection(kind)) if projected else None
         items: List[Dict[str, Any]] = []
         cont = ""
         rv = ""
@@ -235,7 +268,7 @@ class KubeClient:
                 params["fieldSelector"] = field_selector
             if cont:
                 params["continue"] = cont
-            doc = await self.request("GET", resource_path(kind, namespace), params=params)
+            doc = await self.request("GET", resource_path(kind, namespace), params=params, decoder=decoder)
             api_version, k = doc.get("apiVersion", ""), kind
             for it in doc.get("items") or []:
                 it.setdefault("kind", k)
@@ -249,7 +282,8 @@ class KubeClient:
                 return items, rv
 
     async def watch(self, kind: str, namespace: Optional[str], resource_version: str, *, label_selector: str = "",
-                    field_selector: str = "", timeout_seconds: int = 300) -> AsyncIterator[Tuple[str, Dict[str, Any]]]:
+                    field_selector: str = "", timeout_seconds: int = 300,
+                    projected: bool = False) -> AsyncIterator[Tuple[str, Dict[str, Any]]]:
         s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "allowWatchBookmarks": "true",
                   "timeoutSeconds": str(timeout_seconds)}
@@ -270,6 +304,19 @@ class KubeClient:
                     yield "ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": doc.get("message", "")}
                     return
                 raise from_status(r.status, doc)
+            decoder = _decoder(watch_projection(kind)) if projected else None
+            if decoder is not None:
+                n = 0
+                async for chunk in r.content.iter_any():
+                    for ev in decoder.feed(chunk):
+                        obj = ev.get("object") or {}
+                        if obj.get("kind") is None:
+                            obj["kind"] = kind
+                        yield ev.get("type", ""), obj
+                        n += 1
+                        if n % 64 == 0:
+                            await asyncio.sleep(0)  # let workers interleave with a large chunk
+                return
             loads = json.loads
             buf = b""
             async for chunk in r.content.iter_any():
@@ -304,13 +351,13 @@ class KubeClient:
                                   content_type="application/merge-patch+json")
 
     async def delete(self, kind: str, namespace: Optional[str], name: str, propagation_policy: str = "Background") -> Dict[str, Any]:
-        body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
         path = resource_path(kind, namespace, name)
         if not self.pipelined_writes:
+            body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
             return await self.request("DELETE", path, body=body)
         self.requests += 1
         status, raw = await self._fast_client().request(
-            "DELETE", path, json.dumps(body).encode(), self._headers({"Content-Type": "application/json"}))
+            "DELETE", path, _delete_body(propagation_policy), self._headers({"Content-Type": "application/json"}))
         try:
             doc = json.loads(raw) if raw else {}
         except ValueError:
@@ -328,7 +375,7 @@ class KubeListWatch(ListWatch):
     """Informer transport over :class:`KubeClient` (one kind, one namespace)."""
 
     def __init__(self, client: KubeClient, kind: str, namespace: Optional[str], *, label_selector: str = "",
-                 field_selector: str = "", watch_timeout: int = 300, page_size: int = 500):
+                 field_selector: str = "", watch_timeout: int = 300, page_size: int = 500, projected: bool = True):
         self.client = client
         self.kind = kind
         self.namespace = namespace
@@ -336,11 +383,17 @@ class KubeListWatch(ListWatch):
         self.field_selector = field_selector
         self.watch_timeout = watch_timeout
         self.page_size = page_size
+        # native projected decoding when available: objects arrive already slimmed, the
+        # informer then only runs the cheap finisher instead of the Python slimmer
+        self.projected = projected and _native_decoder_available() and kind in PROJECTIONS
+        if self.projected:
+            self.transform = FINISHERS.get(kind)
 
     async def list(self):
         return await self.client.list(self.kind, self.namespace, label_selector=self.label_selector,
-                                      field_selector=self.field_selector, limit=self.page_size)
+                                      field_selector=self.field_selector, limit=self.page_size, projected=self.projected)
 
     def watch(self, resource_version: str):
         return self.client.watch(self.kind, self.namespace, resource_version, label_selector=self.label_selector,
-                                 field_selector=self.field_selector, timeout_seconds=self.watch_timeout)
+                                 field_selector=self.field_selector, timeout_seconds=self.watch_timeout,
+                                 projected=self.projected)

@@ -101,6 +101,8 @@ def slim_pod(pod: Dict[str, Any]) -> Dict[str, Any]:
         s["nodeName"] = spec["nodeName"]
     if spec.get("containers"):
         s["containers"] = [_slim_container(c) for c in spec["containers"]]
+        # derived once per pod version: every classification of this version reuses it
+        s["_env"] = pod_env(out | {"spec": s})
     out["spec"] = s
     st: Dict[str, Any] = {}
     for k in ("phase", "reason", "message", "hostIP", "podIP", "startTime"):
@@ -158,8 +160,12 @@ def waiting_states(pod) -> Iterable[Dict[str, Any]]:
 
 def pod_env(pod) -> Dict[str, str]:
     """Merged literal env of all containers (first definition wins)."""
+    spec = pod.get("spec") or {}
+    cached = spec.get("_env")
+    if cached is not None:
+        return cached
     out: Dict[str, str] = {}
-    for c in (pod.get("spec") or {}).get("containers") or []:
+    for c in spec.get("containers") or []:
         for e in c.get("env") or []:
             n = e.get("name")
             if n and n not in out and e.get("value") is not None:
@@ -185,3 +191,52 @@ def condition(obj, ctype: str) -> Optional[Dict[str, Any]]:
         if c.get("type") == ctype:
             return c
     return None
+
+
+# ----------------------------------------------------------------- projections (native decode)
+# Field projections applied *while* decoding watch/list JSON (csrc/kube/watch_decoder.cpp):
+# the same fields the slimmers above keep.  The top level of every kind also keeps the
+# Status fields (kind/code/reason/message) so an ERROR event's Status survives.
+_STATUS_FIELDS = {"kind": True, "apiVersion": True, "code": True, "reason": True, "message": True}
+_META = {"name": True, "namespace": True, "uid": True, "resourceVersion": True, "creationTimestamp": True,
+         "deletionTimestamp": True, "labels": True, "annotations": ["prefix", *_KEEP_ANNOTATIONS_PREFIXES],
+         "ownerReferences": ["list", {"kind": True, "name": True, "uid": True}]}
+_CONDITIONS = ["list", {"type": True, "status": True, "reason": True, "message": True}]
+_CSTATUS = ["list", {"name": True, "state": True, "lastState": True, "restartCount": True, "ready": True, "started": True}]
+
+PROJECTIONS: Dict[str, Any] = {
+    "Pod": dict(_STATUS_FIELDS, metadata=_META, spec={
+        "nodeName": True,
+        "containers": ["list", {"name": True, "env": ["list", {"name": True, "value": True}], "resources": True}]},
+        status={"phase": True, "reason": True, "message": True, "hostIP": True, "podIP": True, "startTime": True,
+                "containerStatuses": _CSTATUS, "initContainerStatuses": _CSTATUS, "conditions": _CONDITIONS}),
+    "Job": dict(_STATUS_FIELDS, metadata=_META, spec={
+        "backoffLimit": True, "activeDeadlineSeconds": True, "completions": True, "parallelism": True, "completionMode": True},
+        status={"active": True, "failed": True, "succeeded": True, "startTime": True, "completionTime": True,
+                "conditions": _CONDITIONS}),
+    "Event": dict(_STATUS_FIELDS, metadata={k: v for k, v in _META.items() if k != "labels"}, involvedObject=True,
+                  type=True, count=True, firstTimestamp=True, lastTimestamp=True, eventTime=True, series=True,
+                  reportingComponent=True, source=True),
+}
+
+
+def finish_pod(pod: Dict[str, Any]) -> Dict[str, Any]:
+    """Post-projection step for pods: derive the merged env once per version."""
+    spec = pod.get("spec")
+    if isinstance(spec, dict) and spec.get("containers") and "_env" not in spec:
+        spec["_env"] = pod_env(pod)
+    return pod
+
+
+# transform after native projection (projection already slimmed the object)
+FINISHERS: Dict[str, Any] = {"Pod": finish_pod, "Job": None, "Event": None, "Lease": None}
+
+
+def watch_projection(kind: str) -> Any:
+    p = PROJECTIONS.get(kind)
+    return True if p is None else {"type": True, "object": p}
+
+
+def list_projection(kind: str) -> Any:
+    p = PROJECTIONS.get(kind)
+    return True if p is None else {"kind": True, "apiVersion": True, "metadata": True, "items": ["list", p]}

@@ -127,6 +127,12 @@ class CqlConnection:
         self._reader = _native().FrameReader()
         self._pending: Dict[int, asyncio.Future] = {}
         self._free: List[int] = list(range(self.MAX_STREAMS - 1, 0, -1))  # stream 0 unused, -1.. events
+        # request deadlines, checked by one sweeper per connection instead of a timer per
+        # request; a timed-out stream id stays reserved ("orphaned") until its late
+        # response arrives, so it can never resolve a newer request
+        self._deadline: Dict[int, float] = {}
+        self._orphans: set = set()
+        self._sweeper: Optional[asyncio.Task] = None
         self._out: List[bytes] = []
         self._flush_scheduled = False
         self._loop: Optional[asyncio.AbstractEventLoop] = None
@@ -148,6 +154,7 @@ class CqlConnection:
         await asyncio.wait_for(self._loop.create_connection(lambda: _Protocol(self), self.host, self.port, **kw),
                                self.connect_timeout)
         self.closed = False
+        self._sweeper = self._loop.create_task(self._sweep_deadlines())
         sock = self._transport.get_extra_info("socket")
         if sock is not None:
             import socket as _s
@@ -182,10 +189,15 @@ class CqlConnection:
             self.close()
             return
         pending = self._pending
+        deadline = self._deadline
         for stream, _op, dec in frames:
             fut = pending.pop(stream, None)
             if fut is None:
-                continue  # server push (EVENT) or a timed-out request
+                if stream in self._orphans:  # late answer to a timed-out request
+                    self._orphans.discard(stream)
+                    self._free.append(stream)
+                continue  # or a server push (EVENT)
+            deadline.pop(stream, None)
             self._free.append(stream)
             if not fut.done():
                 fut.set_result(dec)
@@ -198,6 +210,10 @@ class CqlConnection:
             if not fut.done():
                 fut.set_exception(err)
         self._free = list(range(self.MAX_STREAMS - 1, 0, -1))
+        self._deadline.clear()
+        self._orphans.clear()
+        if self._sweeper is not None:
+            self._sweeper.cancel()
 
     def _flush(self) -> None:
         self._flush_scheduled = False
@@ -208,7 +224,7 @@ class CqlConnection:
         else:
             self._out = []
 
-    def request_nowait(self, build, hint=None) -> asyncio.Future:
+    def request_nowait(self, build, hint=None, timeout: Optional[float] = None) -> asyncio.Future:
         """Send one request frame built by ``build(stream)``; returns the response future."""
         if self.closed:
             raise ConnectionClosed(f"connection to {self.host}:{self.port} is closed")
@@ -217,6 +233,7 @@ class CqlConnection:
         stream = self._free.pop()
         fut = self._loop.create_future()
         self._pending[stream] = fut
+        self._deadline[stream] = self._loop.time() + (timeout or self.request_timeout)
         if hint is not None:
             self._reader.expect(stream, hint)
         self._out.append(build(stream))
@@ -227,11 +244,22 @@ class CqlConnection:
         return fut
 
     async def request(self, build, hint=None, timeout: Optional[float] = None):
-        fut = self.request_nowait(build, hint)
-        try:
-            return await asyncio.wait_for(fut, timeout or self.request_timeout)
-        except asyncio.TimeoutError:
-            raise RequestTimeout(f"request to {self.host}:{self.port} timed out") from None
+        return await self.request_nowait(build, hint, timeout)
+
+    async def _sweep_deadlines(self) -> None:
+        while not self.closed:
+            await asyncio.sleep(min(0.1, self.request_timeout / 4))
+            now = self._loop.time()
+            expired = [s for s, d in self._deadline.items() if d <= now]
+            for stream in expired:
+                del self._deadline[stream]
+                fut = self._pending.pop(stream, None)
+                self._reader.forget(stream)
+                self._orphans.add(stream)
+                if fut is not None and not fut.done():
+                    fut.set_exception(RequestTimeout(f"request to {self.host}:{self.port} timed out"))
+            if len(self._orphans) > 1024:  # the server stopped answering: start over
+                self.close()
 
     @property
     def in_flight(self) -> int:
@@ -241,6 +269,8 @@ class CqlConnection:
         if self._transport is not None:
             self._transport.close()
         self.closed = True
+        if self._sweeper is not None:
+            self._sweeper.cancel()
 
 
 # ---------------------------------------------------------------------------- session
