@@ -73,7 +73,8 @@ class Tracker:
 
     def __call__(self, d: Decision):
         rid = d.result.request_id
-        t = time.monotonic()
+        # the metric is pod-fail → checkpoint *write ack* (the Job DELETE follows the write)
+        t = d.result.stamps.get("ack_mono") or time.monotonic()
         st = self.owner.pop(rid, None)
         if st is None:
             self.acks[rid] = (t, d.outcome)  # ack raced ahead of the step response

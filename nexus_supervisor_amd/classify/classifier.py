@@ -390,11 +390,40 @@ class Classifier:
             if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.CRASH_LOOP):
                 res.failure_class = F.HBM_OOM if verdict.kind == "hbm" else F.HOST_OOM
         if res.action != A.TO_RUNNING:
-            prior = self.evidence.get(key)
-            if prior:
-                res.evidence["history"] = prior
-                if res.failure_class == F.BACKOFF_LIMIT and any(p.get("kind") == "evicted" for p in prior):
-                    res.failure_class = F.EVICTED
+            self._apply_history(res)
+
+    def _apply_history(self, res: RunStatusAnalysisResult) -> None:
+        prior = self.evidence.get(res.key)
+        if prior:
+            res.evidence["history"] = prior
+            if res.failure_class == F.BACKOFF_LIMIT and any(p.get("kind") == "evicted" for p in prior):
+                res.failure_class = F.EVICTED
+
+    def late_enrich(self, res: RunStatusAnalysisResult, lookup: ObjectLookup) -> None:
+        """Re-enrich a Job-level decision just before it is written.
+
+        Pods and Jobs arrive on separate watch streams, so a Job's failure can be
+        classified before its pods' last updates (eviction, OOM termination) are seen.
+        By actuation time (after queueing and the checkpoint read) they usually have
+        been; this costs no extra latency."""
+        if not self.gpu.attribution_enabled or res.action == A.TO_RUNNING or res.object_kind != "Job":
+            return
+        if res.failure_class in (F.BACKOFF_LIMIT, F.FATAL, F.NONE):
+            pods = lookup.pods_of_job(res.request_id)
+            for pod in pods:
+                st = pod.get("status") or {}
+                if st.get("reason") == "Evicted" or self._disruption(pod):
+                    self.evidence.add(res.key, {"kind": "evicted", "message": st.get("message", ""), "pod": kube.name_of(pod)})
+            if pods and "oom" not in res.evidence:
+                terms = [t for p in pods for t in kube.terminated_states(p)]
+                if terms:
+                    topo, gev = self._pod_ctx(pods[-1])
+                    v = oom_mod.analyze([t.get("message", "") for t in terms], terms, gev, topo.get("expected_gpu"),
+                                        self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+                    if v.kind:
+                        res.evidence["oom"] = v.as_dict()
+                        res.failure_class = F.HBM_OOM if v.kind == "hbm" else F.HOST_OOM
+        self._apply_history(res)
 
 
 def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:

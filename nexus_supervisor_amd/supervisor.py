@@ -50,6 +50,10 @@ STAGE_FOR_ACTION = {
 }
 
 
+def _FAILED_STAGES():
+    return (LifecycleStage.FAILED, LifecycleStage.SCHEDULING_FAILED, LifecycleStage.DEADLINE_EXCEEDED)
+
+
 class JobClient:
     """What the actuator needs from the K8s API."""
 
@@ -386,7 +390,10 @@ class Supervisor:
         if cp.is_finished():
             self.log.info("algorithm run completed, skipping action", algorithm=r.algorithm, requestId=r.request_id)
             deleted = False
-            if r.pending_delete:
+            # a failing decision on a run already in a failed stage: the Job may have survived
+            # a crash between write and delete (or a failed delete) — finish the delete
+            if r.pending_delete or (failing and cp.lifecycle_stage in _FAILED_STAGES()
+                                    and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is not None):
                 deleted = await self._delete_job(r.request_id)
                 r.pending_delete = False
             self._remember(key, cp.lifecycle_stage)
@@ -400,31 +407,35 @@ class Supervisor:
                 return Decision(r, "skipped-already-running", stage, False)
             await self._write(cp, stage, None, None, now_dt, set_failure=False)
             stamps["ack"] = wall()
+            stamps["ack_mono"] = time.monotonic()
             self._observe(r)
             self._remember(key, stage)
             return Decision(r, "applied", stage, False)
         cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
+        self.classifier.late_enrich(r, self.lookup)
         details = render_trace(r, self.cfg.rules.trace_format)
-        # The reference deletes, then upserts (2 sequential RTTs after the read). Both are
-        # idempotent, so they are issued concurrently; a failed delete is remembered on the
-        # item so the retry still deletes after it sees the (now finished) row.
-        del_res, write_res = await asyncio.gather(
-            self._delete_job(r.request_id),
-            self._write(cp, stage, cause, details, now_dt, set_failure=True),
-            return_exceptions=True,
-        )
-        if isinstance(del_res, BaseException):
-            self.log.error(del_res, "failed to delete an algorithm submission", requestId=r.request_id, algorithm=r.algorithm)
-            r.pending_delete = True
-            raise del_res
-        if isinstance(write_res, BaseException):
-            self.log.error(write_res, "failed to update algorithm submission status", requestId=r.request_id, algorithm=r.algorithm)
-            raise write_res
+        # The reference deletes the Job, then upserts the row (supervisor.go:289-301).  This
+        # build writes first: deleting first (or concurrently) lets a crash between the two
+        # lose the decision for good — the Job's pods are garbage-collected, so the replay
+        # after failover has nothing to re-decide from.  Written-then-crashed instead leaves
+        # a failed row whose Job still exists, which the replay finishes (finished path).
+        try:
+            await self._write(cp, stage, cause, details, now_dt, set_failure=True)
+        except Exception as exc:
+            self.log.error(exc, "failed to update algorithm submission status", requestId=r.request_id, algorithm=r.algorithm)
+            raise
         stamps["ack"] = wall()
+        stamps["ack_mono"] = time.monotonic()
         self._observe(r)
         self._remember(key, stage)
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
-        return Decision(r, "applied", stage, bool(del_res))
+        try:
+            deleted = await self._delete_job(r.request_id)
+        except Exception as exc:
+            self.log.error(exc, "failed to delete an algorithm submission", requestId=r.request_id, algorithm=r.algorithm)
+            r.pending_delete = True  # the retry sees the finished row and only deletes
+            raise
+        return Decision(r, "applied", stage, deleted)
 
     async def _write(self, cp, stage, cause, details, now_dt, set_failure):
         compat = self.cfg.compat

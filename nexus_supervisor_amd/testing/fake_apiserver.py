@@ -126,6 +126,7 @@ class FakeApiServer:
         self.deleted: List[Tuple[str, str, str, str]] = []  # (kind, ns, name, propagation)
         self._pods_by_job: Dict[Tuple[str, str], Set[str]] = {}  # (ns, job-name label) -> pod names (GC index)
         self.fail_next: Dict[Tuple[str, str], int] = {}  # (method, kind) -> count of 500s to inject
+        self._snapshots: Dict[str, Tuple[int, List[Dict[str, Any]]]] = {}  # paginated LIST snapshots
         self.latency = 0.0
         self.requests = 0
         self.watch_requests = 0
@@ -308,15 +309,32 @@ class FakeApiServer:
             return bad
         kind = self._kind(req)
         ns = req.match_info.get("ns", "")
-        sel = _parse_selector(req.query.get("labelSelector", "")) + _parse_fields(req.query.get("fieldSelector", ""))
-        items = [o for (ons, _), o in self.objects[kind].items()
-                 if (not ns or ons == ns) and _matches(_selectable(o), sel)]
-        items.sort(key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
         limit = int(req.query.get("limit", "0") or 0)
-        start = int(req.query.get("continue", "0") or 0)
-        meta: Dict[str, Any] = {"resourceVersion": str(self.rv)}
+        token = req.query.get("continue", "")
+        if token:
+            # every page of a paginated LIST comes from the snapshot taken by the first
+            # page, at that page's resourceVersion (apiserver semantics)
+            snap = self._snapshots.get(token.split(":", 1)[0])
+            if snap is None:
+                return self._status(410, "Expired", "the provided continue parameter is too old")
+            snap_rv, items = snap
+            start = int(token.split(":", 1)[1])
+        else:
+            sel = _parse_selector(req.query.get("labelSelector", "")) + _parse_fields(req.query.get("fieldSelector", ""))
+            items = [o for (ons, _), o in self.objects[kind].items()
+                     if (not ns or ons == ns) and _matches(_selectable(o), sel)]
+            items.sort(key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
+            snap_rv, start = self.rv, 0
+        meta: Dict[str, Any] = {"resourceVersion": str(snap_rv)}
         if limit and start + limit < len(items):
-            meta["continue"] = str(start + limit)
+            if not token:
+                sid = uuid.uuid4().hex[:12]
+                self._snapshots[sid] = (snap_rv, items)
+                while len(self._snapshots) > 64:
+                    self._snapshots.pop(next(iter(self._snapshots)))
+            else:
+                sid = token.split(":", 1)[0]
+            meta["continue"] = f"{sid}:{start + limit}"
             page = items[start:start + limit]
         else:
             page = items[start:]
