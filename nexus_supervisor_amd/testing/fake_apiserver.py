@@ -26,7 +26,7 @@ import time
 import uuid
 from typing import Any, Deque, Dict, List, Optional, Set, Tuple
 
-from aiohttp import web
+from . import miniweb as web
 
 from ..kube.client import RESOURCES
 
@@ -128,36 +128,35 @@ class FakeApiServer:
         self.fail_next: Dict[Tuple[str, str], int] = {}  # (method, kind) -> count of 500s to inject
         self._snapshots: Dict[str, Tuple[int, List[Dict[str, Any]]]] = {}  # paginated LIST snapshots
         self.latency = 0.0
+        self.coalesce = 0.0005  # watch write coalescing window (seconds)
         self.requests = 0
         self.watch_requests = 0
-        self._runner: Optional[web.AppRunner] = None
+        self._server: Optional[web.Server] = None
         self.url = ""
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, host: str = "127.0.0.1", port: int = 0) -> str:
-        app = web.Application(client_max_size=64 << 20)
+        srv = web.Server()
         for kind, (prefix, plural) in RESOURCES.items():
             base = f"{prefix}/namespaces/{{ns}}/{plural}"
-            app.router.add_route("GET", base, self._h_collection)
-            app.router.add_route("POST", base, self._h_create)
-            app.router.add_route("GET", base + "/{name}", self._h_get)
-            app.router.add_route("PUT", base + "/{name}", self._h_replace)
-            app.router.add_route("PATCH", base + "/{name}", self._h_patch)
-            app.router.add_route("DELETE", base + "/{name}", self._h_delete)
-            app.router.add_route("GET", f"{prefix}/{plural}", self._h_collection)
-        self._runner = web.AppRunner(app, access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, host, port, backlog=4096)
-        await site.start()
-        sock = site._server.sockets[0]  # noqa: SLF001
-        self.url = f"http://{host}:{sock.getsockname()[1]}"
+            srv.add_route("GET", base, self._h_collection)
+            srv.add_route("POST", base, self._h_create)
+            srv.add_route("GET", base + "/{name}", self._h_get)
+            srv.add_route("PUT", base + "/{name}", self._h_replace)
+            srv.add_route("PATCH", base + "/{name}", self._h_patch)
+            srv.add_route("DELETE", base + "/{name}", self._h_delete)
+            srv.add_route("GET", f"{prefix}/{plural}", self._h_collection)
+        port = await srv.start(host, port)
+        self._server = srv
+        self.url = f"http://{host}:{port}"
         return self.url
 
     async def stop(self) -> None:
         self.close_watches()
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        await asyncio.sleep(0)
+        if self._server is not None:
+            await self._server.stop()
+            self._server = None
 
     # ------------------------------------------------------------------ programmatic API (loop thread)
     def _next_rv(self) -> str:
@@ -339,7 +338,7 @@ class FakeApiServer:
         else:
             page = items[start:]
         body = {"kind": f"{kind}List", "apiVersion": _API_VERSION.get(kind, "v1"), "metadata": meta, "items": page}
-        return web.Response(body=json.dumps(body, separators=(",", ":")).encode(), content_type="application/json")
+        return web.Response(body=json.dumps(body, separators=(",", ":")).encode())
 
     async def _watch(self, req: web.Request):
         bad = self._auth(req)
@@ -391,6 +390,10 @@ class FakeApiServer:
                     continue
                 if line is None:
                     break
+                if w.queue.empty() and self.coalesce > 0:
+                    # like the apiserver's buffered watch writer: let a burst accumulate
+                    # briefly and send it as one chunk instead of one write per event
+                    await asyncio.sleep(self.coalesce)
                 chunk = [line]
                 while not w.queue.empty():
                     nxt = w.queue.get_nowait()
