@@ -85,6 +85,51 @@ std::unique_ptr<Proj> compile(PyObject* spec) {
   return nullptr;
 }
 
+// Interned Python key strings, looked up by bytes without allocating (open addressing).
+class KeyCache {
+ public:
+  KeyCache() : slots_(kCap) {}
+  ~KeyCache() {
+    for (auto& sl : slots_) Py_XDECREF(sl.obj);
+  }
+  // New reference to the Python str for `k`.
+  PyObject* get(std::string_view k) {
+    uint64_t h = 1469598103934665603ULL;
+    for (unsigned char c : k) h = (h ^ c) * 1099511628211ULL;
+    size_t i = h & (kCap - 1);
+    for (size_t probe = 0; probe < 16; ++probe, i = (i + 1) & (kCap - 1)) {
+      Slot& sl = slots_[i];
+      if (!sl.obj) {
+        PyObject* o = PyUnicode_DecodeUTF8(k.data(), static_cast<Py_ssize_t>(k.size()), "replace");
+        if (!o) return nullptr;
+        if (used_ < kCap / 2) {
+          sl.hash = h;
+          sl.key.assign(k.data(), k.size());
+          sl.obj = o;
+          Py_INCREF(o);
+          ++used_;
+        }
+        return o;
+      }
+      if (sl.hash == h && sl.key.size() == k.size() && memcmp(sl.key.data(), k.data(), k.size()) == 0) {
+        Py_INCREF(sl.obj);
+        return sl.obj;
+      }
+    }
+    return PyUnicode_DecodeUTF8(k.data(), static_cast<Py_ssize_t>(k.size()), "replace");
+  }
+
+ private:
+  static constexpr size_t kCap = 8192;
+  struct Slot {
+    uint64_t hash = 0;
+    std::string key;
+    PyObject* obj = nullptr;
+  };
+  std::vector<Slot> slots_;
+  size_t used_ = 0;
+};
+
 struct ParseError {
   const char* msg;
   size_t at;
@@ -92,7 +137,7 @@ struct ParseError {
 
 class Parser {
  public:
-  Parser(const char* s, size_t n, std::unordered_map<std::string, PyObject*>* keys) : s_(s), n_(n), keys_(keys) {}
+  Parser(const char* s, size_t n, KeyCache* keys) : s_(s), n_(n), keys_(keys) {}
 
   size_t pos() const { return i_; }
   void set_pos(size_t p) { i_ = p; }
@@ -298,34 +343,27 @@ class Parser {
     return PyUnicode_DecodeUTF8(u.data(), static_cast<Py_ssize_t>(u.size()), "replace");
   }
 
-  // Key string: returns the (possibly unescaped) key text; interned Python key on demand.
-  std::string key_text() {
+  // Key text as a view into the buffer (or into scratch_ when it had escapes).
+  std::string_view key_text() {
     ws();
     if (i_ >= n_ || s_[i_] != '"') throw ParseError{"expected key", i_};
     size_t a, b;
     bool esc;
     string_span(a, b, esc);
-    std::string k = esc ? unescape(a, b) : std::string(s_ + a, b - a);
+    std::string_view k;
+    if (esc) {
+      scratch_ = unescape(a, b);
+      k = scratch_;
+    } else {
+      k = std::string_view(s_ + a, b - a);
+    }
     ws();
     if (i_ >= n_ || s_[i_] != ':') throw ParseError{"expected ':'", i_};
     ++i_;
     return k;
   }
 
-  PyObject* key_obj(const std::string& k) {
-    auto it = keys_->find(k);
-    if (it != keys_->end()) {
-      Py_INCREF(it->second);
-      return it->second;
-    }
-    PyObject* o = PyUnicode_DecodeUTF8(k.data(), static_cast<Py_ssize_t>(k.size()), "replace");
-    if (!o) return nullptr;
-    if (keys_->size() < 4096) {
-      Py_INCREF(o);
-      (*keys_)[k] = o;
-    }
-    return o;
-  }
+  PyObject* key_obj(std::string_view k) { return keys_->get(k); }
 
   template <typename F>
   PyObject* object_loop(F&& on_member) {
@@ -339,7 +377,12 @@ class Parser {
         return d;
       }
       while (true) {
-        std::string k = key_text();
+        std::string_view k = key_text();
+        std::string owned;
+        if (k.data() == scratch_.data()) {  // nested keys reuse scratch_: keep our own copy
+          owned.assign(k.data(), k.size());
+          k = owned;
+        }
         if (!on_member(d, k)) {
           Py_DECREF(d);
           return nullptr;
@@ -362,7 +405,7 @@ class Parser {
     }
   }
 
-  bool set_item(PyObject* d, const std::string& k, PyObject* v) {
+  bool set_item(PyObject* d, std::string_view k, PyObject* v) {
     if (!v) return false;
     PyObject* ko = key_obj(k);
     if (!ko) {
@@ -376,11 +419,11 @@ class Parser {
   }
 
   PyObject* object_full() {
-    return object_loop([&](PyObject* d, const std::string& k) { return set_item(d, k, value(nullptr)); });
+    return object_loop([&](PyObject* d, std::string_view k) { return set_item(d, k, value(nullptr)); });
   }
 
   PyObject* object_proj(const Proj* p) {
-    return object_loop([&](PyObject* d, const std::string& k) {
+    return object_loop([&](PyObject* d, std::string_view k) {
       const Proj* sub = p->field(k);
       if (!sub) {
         skip();
@@ -391,16 +434,16 @@ class Parser {
   }
 
   PyObject* object_prefix(const Proj* p) {
-    return object_loop([&](PyObject* d, const std::string& k) {
+    return object_loop([&](PyObject* d, std::string_view k) {
       for (auto& pre : p->prefixes)
-        if (k.compare(0, pre.size(), pre) == 0) return set_item(d, k, value(nullptr));
+        if (k.substr(0, pre.size()) == pre) return set_item(d, k, value(nullptr));
       skip();
       return true;
     });
   }
 
   PyObject* object_map(const Proj* elem) {
-    return object_loop([&](PyObject* d, const std::string& k) {
+    return object_loop([&](PyObject* d, std::string_view k) {
       return set_item(d, k, value(elem && elem->kind != Proj::KEEP ? elem : nullptr));
     });
   }
@@ -444,7 +487,8 @@ class Parser {
   const char* s_;
   size_t n_;
   size_t i_ = 0;
-  std::unordered_map<std::string, PyObject*>* keys_;
+  KeyCache* keys_;
+  std::string scratch_;
 };
 
 // ------------------------------------------------------------------ Python type
@@ -452,7 +496,7 @@ typedef struct {
   PyObject_HEAD
   Proj* proj;        // projection of the whole document (watch envelope or list body)
   std::string* buf;  // pending partial line (watch streams)
-  std::unordered_map<std::string, PyObject*>* keys;
+  KeyCache* keys;
   unsigned long long docs;
   unsigned long long bytes;
 } Decoder;
@@ -460,10 +504,7 @@ typedef struct {
 void Decoder_dealloc(Decoder* self) {
   delete self->proj;
   delete self->buf;
-  if (self->keys) {
-    for (auto& kv : *self->keys) Py_DECREF(kv.second);
-    delete self->keys;
-  }
+  delete self->keys;
   Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
 }
 
@@ -476,7 +517,7 @@ int Decoder_init(Decoder* self, PyObject* args, PyObject* kw) {
   delete self->proj;
   self->proj = p.release();
   if (!self->buf) self->buf = new std::string();
-  if (!self->keys) self->keys = new std::unordered_map<std::string, PyObject*>();
+  if (!self->keys) self->keys = new KeyCache();
   return 0;
 }
 

@@ -197,6 +197,10 @@ class Classifier:
             return []
         if old is not None and kube.resource_version(old) == kube.resource_version(pod) and kube.resource_version(pod):
             return []  # resync replay of an unchanged object
+        status = pod.get("status") or {}
+        if (not status.get("containerStatuses") and not status.get("initContainerStatuses")
+                and not status.get("conditions") and status.get("reason") != "Evicted"):
+            return []  # freshly created / not yet scheduled: nothing any rule can match
         request_id = self._pod_request_id(pod)
         if not request_id:
             return []
