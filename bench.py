@@ -189,6 +189,7 @@ def main(argv=None) -> int:
                 "real_hbm_oom": bool(hip_msg),
                 "cql_latency_us": args.cql_latency_us,
                 "stages_ms": res.get("stages"),
+                "cpu_util_rank0": res.get("cpu"),
                 "baseline": "reference derived ceiling 10 decisions/s (Helm defaults; BASELINE.md)",
             },
         }

@@ -74,11 +74,13 @@ async def amain(args) -> None:
         else:
             failed, traffic = await prepare(events)
         t_push = time.monotonic()
-        for etype, obj in traffic:
+        for i, (etype, obj) in enumerate(traffic):
             if etype == "ADDED":
                 api.create(obj, copy_obj=False)
             else:
                 api.update(obj, copy_obj=False)
+            if i % 256 == 255:
+                await asyncio.sleep(0)  # keep serving DELETEs / watch writes during a burst
         state["next"] = (events, asyncio.ensure_future(prepare(events)))
         return web.json_response({"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}})
 

@@ -149,6 +149,9 @@ class InProcHarness:
     async def stop(self):
         await self.cluster.stop()
 
+    def external_cpu(self):
+        return {}
+
 
 async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[str, Any]:
     from ..gpu.telemetry import FakeTelemetry, make_telemetry, pod_evidence_provider
@@ -198,9 +201,15 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             sampler = Sampler(hz=199).start()
         barrier_sync()
         t0 = time.perf_counter()
+        c0 = time.process_time()
+        x0 = harness.external_cpu()
         await run_steps(cfg.steps)
         barrier_sync()
         elapsed = time.perf_counter() - t0
+        cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3)}
+        x1 = harness.external_cpu()
+        for k in x1:
+            cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
         if sampler is not None:
             prof = sampler.stop()
             sampler = None
@@ -216,7 +225,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         telemetry.stop()
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
-            "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages}
+            "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu}
 
 
 def _stage_breakdown(sup) -> Dict[str, Any]:

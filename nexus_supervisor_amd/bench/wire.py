@@ -93,6 +93,18 @@ class WireHarness:
             doc = await r.json()
         return doc["rids"], doc["t_push"]
 
+    def external_cpu(self):
+        """CPU seconds used so far by the harness processes (utilisation diagnostics)."""
+        out = {}
+        for name, proc in (("cluster", self.proc), ("cqlsrv", self.cql.proc if self.cql else None)):
+            try:
+                with open(f"/proc/{proc.pid}/stat") as f:
+                    parts = f.read().rsplit(")", 1)[1].split()
+                out[name] = (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
+            except (OSError, AttributeError, IndexError):
+                pass
+        return out
+
     async def stop(self) -> None:
         try:
             if self.app is not None:

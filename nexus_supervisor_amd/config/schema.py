@@ -126,8 +126,6 @@ class GpuConfig:
     # hold a failed GPU pod's decision this long for the node agent's evidence annotation
     # (0 = decide immediately on whatever is there)
     evidence_wait: float = field(default=0.0, metadata=_k("evidence-wait", "duration"))
-    # node agent: how often to publish evidence, and whether to annotate failed pods
-    agent_publish: bool = field(default=True, metadata=_k("agent-publish"))
 
 
 @dataclass
@@ -178,6 +176,9 @@ class SupervisorConfig:
     informer_label_selector: bool = field(default=True, metadata=_k("informer-label-selector"))
     watch_timeout: float = field(default=300.0, metadata=_k("watch-timeout", "duration"))
     max_retries: int = field(default=16, metadata=_k("max-retries"))  # 0 = retry forever
+    # issue the Job DELETE after the checkpoint write without holding a worker (retried
+    # in the background with the failure backoff); false = delete inside the worker
+    async_job_delete: bool = field(default=True, metadata=_k("async-job-delete"))
     compat: CompatConfig = field(default_factory=CompatConfig, metadata=_k("compat"))
     labels: LabelConfig = field(default_factory=LabelConfig, metadata=_k("labels"))
     rules: RulesConfig = field(default_factory=RulesConfig, metadata=_k("rules"))

@@ -124,6 +124,7 @@ class Supervisor:
         self._applied_cap = 200_000
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
+        self._deletes: set = set()  # in-flight asynchronous Job DELETEs
         self._sweeper: Optional[asyncio.Task] = None
         self.decision_hooks: List[Callable[[Decision], None]] = []
         self.active = not cfg.leader_election.enabled  # leader gating flips this
@@ -182,6 +183,13 @@ class Supervisor:
         await self.factory.stop()
         if self.pipeline is not None:
             await self.pipeline.stop(drain=drain, timeout=timeout)
+        if self._deletes:
+            pending = list(self._deletes)
+            if drain:
+                await asyncio.wait(pending, timeout=timeout)
+            for t in pending:
+                t.cancel()
+            await asyncio.gather(*pending, return_exceptions=True)
 
     def set_active(self, active: bool) -> None:
         """Leader gating: on gaining leadership replay the caches (idempotent) so nothing
@@ -429,6 +437,11 @@ class Supervisor:
         self._observe(r)
         self._remember(key, stage)
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
+        if self.cfg.async_job_delete:
+            # the decision is durable; the Job DELETE must not hold a worker (and with it
+            # every later decision) hostage to API-server latency
+            self._spawn_delete(r)
+            return Decision(r, "applied", stage, False)
         try:
             deleted = await self._delete_job(r.request_id)
         except Exception as exc:
@@ -436,6 +449,32 @@ class Supervisor:
             r.pending_delete = True  # the retry sees the finished row and only deletes
             raise
         return Decision(r, "applied", stage, deleted)
+
+    def _spawn_delete(self, r: RunStatusAnalysisResult) -> None:
+        t = asyncio.ensure_future(self._delete_with_retry(r))
+        self._deletes.add(t)
+        t.add_done_callback(self._deletes.discard)
+
+    async def _delete_with_retry(self, r: RunStatusAnalysisResult) -> None:
+        c = self.cfg
+        delay = c.failure_rate_base_delay
+        attempt = 0
+        while True:
+            attempt += 1
+            try:
+                await self._delete_job(r.request_id)
+                return
+            except asyncio.CancelledError:
+                raise
+            except Exception as exc:  # noqa: BLE001 - retried with backoff
+                if c.max_retries and attempt >= c.max_retries:
+                    self.metrics.inc("job_deletes_failed")
+                    self.log.error(exc, "giving up deleting an algorithm submission", requestId=r.request_id,
+                                   algorithm=r.algorithm)
+                    return
+                self.metrics.inc("job_delete_retries")
+                await asyncio.sleep(delay)
+                delay = min(delay * 2, c.failure_rate_max_delay)
 
     async def _write(self, cp, stage, cause, details, now_dt, set_failure):
         compat = self.cfg.compat

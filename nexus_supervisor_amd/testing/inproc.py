@@ -66,6 +66,8 @@ class InProcCluster:
             ok = await self.supervisor.pipeline.join(timeout)
             if not ok:
                 return False
+            if self.supervisor._deletes:  # background Job DELETEs issued after the writes
+                await asyncio.wait(list(self.supervisor._deletes), timeout=timeout)
         return True
 
     async def stop(self):

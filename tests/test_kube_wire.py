@@ -164,6 +164,8 @@ async def _settle(app, decisions, n, timeout=10.0):
     while len(decisions) < n and asyncio.get_running_loop().time() - t < timeout:
         await asyncio.sleep(0.02)
     await app.supervisor.pipeline.join(timeout)
+    if app.supervisor._deletes:  # background Job DELETEs
+        await asyncio.wait(list(app.supervisor._deletes), timeout=timeout)
 
 
 def test_reference_parity_over_http_and_cql(arun):
