@@ -25,6 +25,11 @@ GPUS_PER_NODE = 8
 XGMI_LINKS_PER_GPU = 7
 
 
+_INT_VARS = (("RANK", "rank"), ("WORLD_SIZE", "world_size"), ("LOCAL_RANK", "local_rank"),
+             ("LOCAL_WORLD_SIZE", "local_world_size"), ("GROUP_RANK", "group_rank"), ("NODE_RANK", "node_rank"),
+             ("NNODES", "nnodes"), ("JOB_COMPLETION_INDEX", "completion_index"), ("MASTER_PORT", "master_port"))
+
+
 def _int(v) -> Optional[int]:
     try:
         return int(str(v).strip())
@@ -42,13 +47,12 @@ def parse_visible_devices(value: Optional[str]) -> List[str]:
 def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = "") -> Dict[str, Any]:
     """Fold torchrun / RCCL env into a topology record (only non-empty keys)."""
     topo: Dict[str, Any] = {}
-    ints = {"RANK": "rank", "WORLD_SIZE": "world_size", "LOCAL_RANK": "local_rank",
-            "LOCAL_WORLD_SIZE": "local_world_size", "GROUP_RANK": "group_rank", "NODE_RANK": "node_rank",
-            "NNODES": "nnodes", "JOB_COMPLETION_INDEX": "completion_index", "MASTER_PORT": "master_port"}
-    for var, key in ints.items():
-        v = _int(env.get(var))
-        if v is not None:
-            topo[key] = v
+    for var, key in _INT_VARS:
+        raw = env.get(var)
+        if raw is not None:
+            v = _int(raw)
+            if v is not None:
+                topo[key] = v
     if env.get("MASTER_ADDR"):
         topo["master_addr"] = env["MASTER_ADDR"]
     if "rank" not in topo and "completion_index" in topo:

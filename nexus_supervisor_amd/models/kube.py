@@ -101,8 +101,6 @@ def slim_pod(pod: Dict[str, Any]) -> Dict[str, Any]:
         s["nodeName"] = spec["nodeName"]
     if spec.get("containers"):
         s["containers"] = [_slim_container(c) for c in spec["containers"]]
-        # derived once per pod version: every classification of this version reuses it
-        s["_env"] = pod_env(out | {"spec": s})
     out["spec"] = s
     st: Dict[str, Any] = {}
     for k in ("phase", "reason", "message", "hostIP", "podIP", "startTime"):
@@ -160,11 +158,15 @@ def waiting_states(pod) -> Iterable[Dict[str, Any]]:
 
 def pod_env(pod) -> Dict[str, str]:
     """Merged literal env of all containers (first definition wins)."""
-    spec = pod.get("spec") or {}
+    spec = pod.get("spec")
+    if not spec:
+        return {}
     cached = spec.get("_env")
     if cached is not None:
         return cached
     out: Dict[str, str] = {}
+    # memoised on the (per-version) spec: computed only for pods a rule actually inspects
+    spec["_env"] = out
     for c in spec.get("containers") or []:
         for e in c.get("env") or []:
             n = e.get("name")
@@ -229,7 +231,7 @@ def finish_pod(pod: Dict[str, Any]) -> Dict[str, Any]:
 
 
 # transform after native projection (projection already slimmed the object)
-FINISHERS: Dict[str, Any] = {"Pod": finish_pod, "Job": None, "Event": None, "Lease": None}
+FINISHERS: Dict[str, Any] = {"Pod": None, "Job": None, "Event": None, "Lease": None}  # env is derived lazily
 
 
 def watch_projection(kind: str) -> Any:

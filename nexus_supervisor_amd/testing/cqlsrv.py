@@ -21,7 +21,8 @@ class CqlServer:
                  dc: str = "datacenter1", host: str = "127.0.0.1", port: int = 0, extra_args: Sequence[str] = ()):
         from .._build import binary
 
-        self.exe = binary("nexus-cqlsrv")
+        # NEXUS_CQLSRV_BINARY selects e.g. a sanitizer build (bin/nexus-cqlsrv-address)
+        self.exe = os.environ.get("NEXUS_CQLSRV_BINARY") or binary("nexus-cqlsrv")
         self.dir = tempfile.mkdtemp(prefix="nexus-cqlsrv-")
         self.host = host
         self.port = port

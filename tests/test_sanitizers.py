@@ -1,0 +1,137 @@
+"""Sanitizer and fuzz coverage for the native code (host code only — GPU sanitizers are
+not available on the pool).  The reference has no race/sanitizer testing at all
+(CI runs `go test` without `-race`).
+
+* ``nexus-cqlsrv`` built with ``-fsanitize=address`` / ``undefined`` and driven through the
+  real client (schema, seed, prepared reads/writes, LWT, WAL restart, malformed frames);
+  the test fails on any sanitizer report in the server's stderr.
+* random / truncated inputs into the in-process decoders (``_cql_native.FrameReader``,
+  ``_kube_native.ProjectedDecoder``) must raise ``ValueError`` — never crash.
+"""
+import asyncio
+import json
+import os
+import random
+import socket
+import struct
+
+import pytest
+
+from nexus_supervisor_amd import _build
+from nexus_supervisor_amd import _cql_native as N
+from nexus_supervisor_amd import _kube_native as K
+from nexus_supervisor_amd.models import kube
+from nexus_supervisor_amd.testing.seed import ALGORITHM, seed_cql_statements, seed_rows
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture(scope="module", params=["address", "undefined"])
+def sanitized_server(request):
+    try:
+        _build.build(sanitize=request.param)
+    except RuntimeError as exc:  # pragma: no cover - toolchain without the runtime
+        pytest.skip(f"sanitizer build unavailable: {exc}")
+    exe = os.path.join(_build.BIN, f"nexus-cqlsrv-{request.param}")
+    os.environ["NEXUS_CQLSRV_BINARY"] = exe
+    yield request.param
+    os.environ.pop("NEXUS_CQLSRV_BINARY", None)
+
+
+def _garbage_frames(port: int, seed: int = 0) -> None:
+    rng = random.Random(seed)
+    for i in range(60):
+        s = socket.create_connection(("127.0.0.1", port), timeout=2)
+        try:
+            kind = i % 4
+            if kind == 0:  # random bytes
+                s.sendall(bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 200))))
+            elif kind == 1:  # valid header, lying length, truncated body
+                body = bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 40)))
+                s.sendall(struct.pack(">BBhBI", 4, 0, 1, rng.choice([1, 5, 7, 9, 10, 13, 15]), len(body) + 100) + body)
+            elif kind == 2:  # valid frame, garbage body
+                body = bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 60)))
+                s.sendall(struct.pack(">BBhBI", 4, 0, 1, rng.choice([7, 9, 10, 13]), len(body)) + body)
+            else:  # STARTUP then a QUERY with random CQL text
+                s.sendall(N.encode_startup(1, {"CQL_VERSION": "3.0.0"}))
+                q = "".join(rng.choice("SELECT *FROM nexus.checkpoints WHERE id='x' AND (?,) ;\"") for _ in range(60))
+                s.sendall(N.encode_query(2, q, None, None, 1))
+            s.settimeout(0.05)
+            try:
+                s.recv(65536)
+            except OSError:
+                pass
+        finally:
+            s.close()
+
+
+def test_cqlsrv_under_sanitizer(sanitized_server, arun):
+    from nexus_supervisor_amd.store.cql import CqlCheckpointStore, CqlError, CqlSession
+    from nexus_supervisor_amd.testing.cqlsrv import CqlServer
+    import datetime as dt
+
+    srv = CqlServer(persist=True, exec_statements=seed_cql_statements(), user="u", password="p").start(timeout=30)
+    try:
+        async def go():
+            st = CqlCheckpointStore(CqlSession([srv.address], user="u", password="p", request_timeout=3.0))
+            await st.connect()
+            for row in seed_rows():
+                assert await st.read_checkpoint(ALGORITHM, row.id) == row
+            now = dt.datetime.now(dt.timezone.utc)
+            assert await st.update_status(ALGORITHM, seed_rows()[0].id, "FAILED", "c" * 5000, "d☃", now)
+            assert not await st.update_status(ALGORITHM, seed_rows()[0].id, "RUNNING", None, None, now,
+                                              only_if_stages=["BUFFERED"])
+            with pytest.raises(CqlError):
+                await st.session.query("SELECT FROM WHERE")
+            await st.close()
+
+        arun(go())
+        _garbage_frames(srv.port)
+        srv.restart(timeout=30)  # WAL replay under the sanitizer
+        _garbage_frames(srv.port, seed=1)
+    finally:
+        srv.stop()
+    log = srv.log()
+    assert "AddressSanitizer" not in log and "runtime error" not in log and "LeakSanitizer" not in log, log[-3000:]
+
+
+def test_frame_reader_fuzz():
+    rng = random.Random(42)
+    ok = bad = 0
+    for _ in range(3000):
+        r = N.FrameReader()
+        n = rng.randint(0, 64)
+        data = bytes([0x84, 0, 0, 1, rng.choice([0, 2, 3, 6, 8, 0x0C, 0x10, 0x55])]) + struct.pack(">I", n)
+        data += bytes(rng.getrandbits(8) for _ in range(n))
+        try:
+            r.feed(data)
+            ok += 1
+        except ValueError:
+            bad += 1
+    assert ok + bad == 3000 and bad > 0
+
+
+def test_projected_decoder_fuzz():
+    rng = random.Random(7)
+    d = K.ProjectedDecoder(kube.watch_projection("Pod"))
+    base = json.dumps({"type": "ADDED", "object": {"metadata": {"name": "x☃", "labels": {"a": "b"}},
+                                                   "status": {"phase": "Running", "containerStatuses": [{"name": "c"}]}}}).encode()
+    ok = bad = 0
+    for _ in range(5000):
+        b = bytearray(base)
+        for _ in range(rng.randint(1, 6)):
+            op = rng.random()
+            i = rng.randrange(len(b))
+            if op < 0.4:
+                b[i] = rng.getrandbits(8)
+            elif op < 0.7:
+                del b[i]
+            else:
+                b.insert(i, rng.choice(b'{}[]",:\\u0'))
+        d.reset()
+        try:
+            d.feed(bytes(b).replace(b"\n", b" ") + b"\n")
+            ok += 1
+        except ValueError:
+            bad += 1
+    assert ok + bad == 5000 and bad > 0 and ok > 0
