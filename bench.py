@@ -54,6 +54,9 @@ def parse_args(argv=None):
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--inflight", type=int, default=2, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--kube-connections", type=int, default=256)
+    ap.add_argument("--probe-events", type=int, default=60,
+                    help="after the timed steps: open-loop latency probe with this many single failures (0 = off)")
+    ap.add_argument("--probe-rate", type=float, default=1000.0, help="probe rate, pod failures per minute (BASELINE config 4)")
     ap.add_argument("--no-real-oom", action="store_true", help="skip the real HBM-OOM on the rank's GPU")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default="")
@@ -126,7 +129,8 @@ def main(argv=None) -> int:
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
-                      kube_connections=args.kube_connections,
+                      kube_connections=args.kube_connections, probe_events=args.probe_events,
+                      probe_rate_per_min=args.probe_rate,
                       pprof_out=args.pprof_out if rank == 0 else "")
     res = asyncio.run(run_rank(cfg, barrier_sync))
 
@@ -169,8 +173,11 @@ def main(argv=None) -> int:
             "vs_baseline": round(eps / REFERENCE_EPS, 2),
             "dtype": "n/a (control plane, no GPU compute)",
             "data": "synthetic pod-failure events, random job ids (no cluster / dataset)",
+            # latency of the timed (saturating) steps: 1000-failure bursts queue behind each other
             "p50_ms": round(q[0], 3) if q[0] is not None else None,
             "p99_ms": round(q[1], 3) if q[1] is not None else None,
+            # open-loop latency at the north-star churn rate (1000 pod-fail events/min), rank 0
+            "latency_at_rate": res.get("probe"),
             "errors": int(total_errors),
             "config": {
                 "model": "nexus-supervisor (informer→classify→CQL write), 1 replica-shard per GPU-job slot",

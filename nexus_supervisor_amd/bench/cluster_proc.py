@@ -68,10 +68,17 @@ async def amain(args) -> None:
         p = await req.json()
         events = int(p["events"])
         wl = state["wl"]
-        nxt = state.get("next")
+        nxt = state.pop("next", None)
         if nxt is not None and nxt[0] == events:
             failed, traffic = await nxt[1]
         else:
+            if nxt is not None:
+                # a prefetched step of another size is dropped: its replacement runs are
+                # already live in the workload, so they must exist in the cluster too
+                _f, stale = await nxt[1]
+                for etype, obj in stale:
+                    if etype == "ADDED" and obj.get("kind") in ("Pod", "Job"):
+                        api.create(obj, copy_obj=False)
             failed, traffic = await prepare(events)
         t_push = time.monotonic()
         for i, (etype, obj) in enumerate(traffic):

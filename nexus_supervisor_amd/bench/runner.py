@@ -38,6 +38,8 @@ class BenchConfig:
     pprof_out: str = ""
     kube_connections: int = 256
     inflight: int = 2
+    probe_events: int = 60
+    probe_rate_per_min: float = 1000.0
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -218,6 +220,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             with open(cfg.pprof_out + ".top.txt", "w") as f:
                 f.write(prof.top(40))
         stages = _stage_breakdown(sup)
+        probe = None
+        if cfg.probe_events > 0:
+            probe = await _latency_probe(harness, tracker, cfg)
     finally:
         if sampler is not None:
             sampler.stop()
@@ -225,7 +230,37 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         telemetry.stop()
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
-            "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu}
+            "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
+            "probe": probe}
+
+
+async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dict[str, Any]:
+    """Open-loop latency at a fixed pod-failure rate (BASELINE config 4: 1000 pod-fail
+    events/min): single failures pushed on a fixed schedule, each timed from push to
+    checkpoint ack — the latency a run sees when the supervisor is not saturated."""
+    saved, tracker.latencies = tracker.latencies, []
+    interval = 60.0 / cfg.probe_rate_per_min
+    loop = asyncio.get_running_loop()
+    start = loop.time()
+    states = []
+    for i in range(cfg.probe_events):
+        delay = start + i * interval - loop.time()
+        if delay > 0:
+            await asyncio.sleep(delay)
+        failed, t_push = await harness.step(1)
+        states.append(tracker.arm(failed, t_push))
+    for st in states:
+        try:
+            await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
+        except asyncio.TimeoutError:
+            tracker.abandon(st)
+    lat = sorted(tracker.latencies)
+    tracker.latencies = saved
+    if not lat:
+        return {"events": 0}
+    q = lambda p: lat[min(len(lat) - 1, int(round(p * (len(lat) - 1))))]  # noqa: E731
+    return {"rate_per_min": cfg.probe_rate_per_min, "events": len(lat), "p50_ms": round(q(0.5), 3),
+            "p99_ms": round(q(0.99), 3), "max_ms": round(lat[-1], 3)}
 
 
 def _stage_breakdown(sup) -> Dict[str, Any]:
