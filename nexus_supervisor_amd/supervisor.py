@@ -508,7 +508,15 @@ class Supervisor:
         if "origin" in s:
             self.metrics.observe_seconds("event_to_checkpoint", ack - s["origin"])
         if "receive" in s:
-            self.metrics.observe_seconds("receive_to_checkpoint", ack - s["receive"])
+            obs = self.metrics.observe_seconds
+            obs("receive_to_checkpoint", ack - s["receive"])
+            # stage decomposition: classify → queue wait → CQL read → CQL write
+            enq, deq, rd = s.get("enqueue"), s.get("dequeue"), s.get("read")
+            if enq is not None and deq is not None and rd is not None:
+                obs("stage_classify", enq - s["receive"])
+                obs("stage_queue", deq - enq)
+                obs("stage_read", rd - deq)
+                obs("stage_write", ack - rd)
 
     def _done(self, r: RunStatusAnalysisResult, decision: Decision) -> None:
         for h in self.decision_hooks:
