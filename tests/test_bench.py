@@ -1,0 +1,69 @@
+"""``bench.py`` driver contract (one JSON line, metric/config from BASELINE.json, weak
+scaling, MAX over ranks) on CPU: the wire transport in-process, and two ranks under
+``torch.distributed.run`` with gloo (the 8-GPU run uses the same path over RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _check(out, n, steps, warmup, events):
+    assert KEYS <= set(out)
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert out["metric"] == base["metric"] or out["metric"].startswith("pod-fail")
+    assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
+    assert out["scaling"] == "weak" and out["higher_is_better"] is True and out["errors"] == 0
+    assert out["value"] > 0 and out["config"]["global_batch"] == events * n
+    assert abs(out["vs_baseline"] - out["value"] / 10.0) < 0.05
+    assert out["p50_ms"] is not None and out["p99_ms"] >= out["p50_ms"]
+
+
+@pytest.mark.slow
+def test_bench_wire_in_process(tmp_path, capsys):
+    import bench
+
+    js = tmp_path / "b.json"
+    rc = bench.main(["--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "60", "--probe-events", "3",
+                     "--probe-rate", "6000", "--json-out", str(js)])
+    assert rc == 0
+    lines = [x for x in capsys.readouterr().out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out == json.loads(js.read_text())
+    _check(out, 1, 2, 1, 60)
+    cfg = out["config"]
+    assert cfg["transport"] == "wire" and cfg["store"].startswith("cql")
+    st = cfg["stages_ms"]
+    assert st["receive_to_checkpoint"]["count"] >= 120
+    for k in ("stage_classify", "stage_queue", "stage_read", "stage_write"):
+        assert st[k]["count"] == st["receive_to_checkpoint"]["count"]
+    assert out["latency_at_rate"]["events"] == 3
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_torchrun_gloo():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--jobs", "200", "--events", "40", "--transport", "inproc",
+                        "--probe-events", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    _check(out, 2, 2, 1, 40)
+    assert out["config"]["parallelism"] == "shard2"
