@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import gc
 import json
 import os
 import sys
@@ -54,6 +55,11 @@ async def amain(args) -> None:
         for o in objs:
             api.create(o)
         state["wl"] = wl
+        # the simulated cluster holds the same 10k-run heap as the supervisor: keep it out
+        # of full collections so the generator never paces the measured process
+        gc.collect()
+        gc.freeze()
+        gc.set_threshold(20000, 20, 20)
         return web.json_response({"objects": len(objs), "rows": len(rows), "rv": api.rv})
 
     async def prepare(events: int):

@@ -147,6 +147,19 @@ class ShardingConfig:
 
 
 @dataclass
+class RuntimeConfig:
+    """Python runtime tuning for a large, long-lived informer cache (see ``utils/gctune.py``)."""
+
+    # after the initial cache sync: collect once, then move every surviving object to the
+    # permanent generation so full collections stop re-traversing 10k cached runs
+    gc_freeze: bool = field(default=True, metadata=_k("gc-freeze"))
+    gc_threshold0: int = field(default=20000, metadata=_k("gc-threshold0"))  # CPython default 700
+    gc_threshold1: int = field(default=20, metadata=_k("gc-threshold1"))
+    gc_threshold2: int = field(default=20, metadata=_k("gc-threshold2"))
+    gc_refreeze_interval: float = field(default=600.0, metadata=_k("gc-refreeze-interval", "duration"))  # 0 = never
+
+
+@dataclass
 class ObservabilityConfig:
     statsd_name: str = field(default="nexus_supervisor", metadata=_k("statsd-name"))
     http_port: int = field(default=0, metadata=_k("http-port"))  # /metrics /healthz /readyz /debug/pprof; 0 = off
@@ -186,6 +199,7 @@ class SupervisorConfig:
     leader_election: LeaderElectionConfig = field(default_factory=LeaderElectionConfig, metadata=_k("leader-election"))
     sharding: ShardingConfig = field(default_factory=ShardingConfig, metadata=_k("sharding"))
     observability: ObservabilityConfig = field(default_factory=ObservabilityConfig, metadata=_k("observability"))
+    runtime: RuntimeConfig = field(default_factory=RuntimeConfig, metadata=_k("runtime"))
 
 
 class ConfigError(ValueError):

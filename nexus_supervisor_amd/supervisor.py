@@ -41,6 +41,7 @@ from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
 from .store.base import CheckpointStore
+from .utils.gctune import GcTuner
 
 STAGE_FOR_ACTION = {
     A.TO_FAIL_STUCK_IN_PENDING: lambda: LifecycleStage.SCHEDULING_FAILED,
@@ -129,6 +130,7 @@ class Supervisor:
         self.decision_hooks: List[Callable[[Decision], None]] = []
         self.active = not cfg.leader_election.enabled  # leader gating flips this
         self._unfinished_cache: Optional[Tuple[str, ...]] = None
+        self.gc_tuner = GcTuner.from_config(cfg.runtime, self.metrics)
         m = self.metrics
         m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
@@ -169,11 +171,13 @@ class Supervisor:
             if not ok:
                 raise RuntimeError("failed to wait for pod informer caches to sync")
             self.log.info("resource informers synced")
+            self.gc_tuner.after_sync()
 
         await self.pipeline.start(post_start)
         self._sweeper = asyncio.create_task(self._sweep_parked(), name="stale-event-sweeper")
 
     async def stop(self, drain: bool = True, timeout: float = 10.0) -> None:
+        self.gc_tuner.stop()
         if self._sweeper:
             self._sweeper.cancel()
             try:

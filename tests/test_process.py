@@ -206,3 +206,29 @@ def test_supervisor_process_end_to_end(arun, tmp_path):
         arun(go(), timeout=120)
     finally:
         srv.stop()
+
+
+def test_gc_tuner_freezes_after_sync_and_restores(arun):
+    import gc
+
+    from nexus_supervisor_amd.obs.metrics import Metrics
+    from nexus_supervisor_amd.utils.gctune import GcTuner
+
+    saved = gc.get_threshold()
+    cache = [{"metadata": {"name": f"r{i}"}} for i in range(1000)]  # long-lived, acyclic
+
+    async def go():
+        m = Metrics("t")
+        t = GcTuner(thresholds=(12345, 11, 7), refreeze_interval=0.01, metrics=m)
+        t.after_sync()
+        assert gc.get_threshold() == (12345, 11, 7) and gc.get_freeze_count() >= len(cache)
+        await asyncio.sleep(0.05)
+        assert t.freezes >= 2 and m.gauge("gc_frozen_objects") > 0
+        t.stop()
+        assert gc.get_freeze_count() == 0 and gc.get_threshold() == saved
+
+    arun(go())
+    cfg = load_config(path=None, env={"NEXUS__RUNTIME__GC_THRESHOLD0": "5000", "NEXUS__RUNTIME__GC_FREEZE": "false"})
+    t = GcTuner.from_config(cfg.runtime)
+    assert t.thresholds[0] == 5000 and not t.freeze_enabled
+    del cache
