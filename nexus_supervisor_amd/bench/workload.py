@@ -162,8 +162,10 @@ class Workload:
         self.expected[rid] = self._stage[kind]
         return out
 
-    def step(self, events: int) -> Tuple[List[str], List[Tuple[str, Dict[str, Any]]], List[CheckpointedRequest]]:
-        """Fail ``events`` random live runs; returns (failed ids, watch traffic, new rows)."""
+    def step(self, events: int, kinds: Optional[List[str]] = None
+             ) -> Tuple[List[str], List[Tuple[str, Dict[str, Any]]], List[CheckpointedRequest]]:
+        """Fail ``events`` random live runs; returns (failed ids, watch traffic, new rows).
+        ``kinds`` restricts the failure mix (uniform over the given kinds)."""
         traffic: List[Tuple[str, Dict[str, Any]]] = []
         failed: List[str] = []
         rows: List[CheckpointedRequest] = []
@@ -172,8 +174,11 @@ class Workload:
         picked = [self.live[i] for i in idx]
         dead = set(picked)
         self.live = [r for r in self.live if r not in dead]
-        kinds = self.rng.choices(self._kinds, self._weights, k=n)
-        for rid, kind in zip(picked, kinds):
+        if kinds:
+            chosen = self.rng.choices(list(kinds), k=n)
+        else:
+            chosen = self.rng.choices(self._kinds, self._weights, k=n)
+        for rid, kind in zip(picked, chosen):
             traffic += self._fail(rid, kind)
             failed.append(rid)
             _, job, pod, row = self.new_run()

@@ -88,8 +88,9 @@ class PipelineStage:
         self._pending: Dict[Hashable, Deque[_Entry]] = {}
         self._ready: Deque[Hashable] = collections.deque()
         self._active: set = set()       # keys held by a worker or waiting out a backoff
-        self._cond: Optional[asyncio.Condition] = None
-        self._wake: Optional[asyncio.Event] = None
+        # idle workers park on their own future; a signal wakes exactly one (a shared
+        # Event would wake every idle worker per item: 256 wakeups for one decision)
+        self._waiters: Deque[asyncio.Future] = collections.deque()
         self._tasks = []
         self._timers = set()
         self._closed = False
@@ -124,8 +125,12 @@ class PipelineStage:
         self._loop.call_soon_threadsafe(self.receive, item)
 
     def _signal(self):
-        if self._wake is not None:
-            self._wake.set()
+        waiters = self._waiters
+        while waiters:
+            w = waiters.popleft()
+            if not w.done():
+                w.set_result(None)
+                return
 
     # ---------------------------------------------------------------- workers
     async def _next_key(self) -> Optional[Hashable]:
@@ -134,9 +139,15 @@ class PipelineStage:
                 return self._ready.popleft()
             if self._closed and not self._pending and not self._active:
                 return None
-            self._wake.clear()
             self._check_idle()
-            await self._wake.wait()
+            fut = self._loop.create_future()
+            self._waiters.append(fut)
+            try:
+                await fut
+            except asyncio.CancelledError:
+                if fut.done() and not fut.cancelled():
+                    self._signal()  # woken, then cancelled: hand the wakeup on
+                raise
 
     def _check_idle(self):
         if self._idle is not None and not self._pending and not self._active and not self._ready:
@@ -221,7 +232,6 @@ class PipelineStage:
         """Spawn workers, then run ``post_start`` (e.g. start informers + wait for sync;
         ``/root/reference/services/supervisor.go:377-387``)."""
         self._loop = asyncio.get_running_loop()
-        self._wake = asyncio.Event()
         self._idle = asyncio.Event()
         self._tasks = [asyncio.create_task(self._worker(i), name=f"{self.name}-w{i}") for i in range(self.n_workers)]
         if self._ready:

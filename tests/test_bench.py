@@ -67,3 +67,21 @@ def test_bench_two_ranks_torchrun_gloo():
     out = json.loads(lines[0])
     _check(out, 2, 2, 1, 40)
     assert out["config"]["parallelism"] == "shard2"
+
+
+@pytest.mark.slow
+def test_baseline_scenarios_small(arun):
+    """BASELINE configs 1, 2, 4, 5 (scaled down): every run reaches its expected stage,
+    the leader crash fails over, latencies are reported."""
+    from nexus_supervisor_amd.bench import scenarios as sc
+
+    r1 = arun(sc.cfg1_single("uncapped", n=5), timeout=60)
+    assert r1["acked"] == 5 and r1["wrong_stage"] == 0 and r1["p50_ms"] < 1000
+    r2 = arun(sc.cfg2_burst("reference", n=40), timeout=60)
+    assert r2["acked"] == 40 and r2["wrong_stage"] == 0
+    r4 = arun(sc.cfg4_rate("uncapped", seconds=2.0, rate=1200, jobs=300), timeout=60)
+    assert r4["drained"] and r4["wrong_stage"] == 0 and r4["acked"] == r4["events"] == 40
+    r5 = arun(sc.cfg5_chaos("uncapped", seconds=4.0, rate=1200, jobs=300), timeout=120)
+    assert r5["drained"] and r5["wrong_stage"] == 0
+    assert {"cql_restart", "storm", "leader_crash", "failover_s"} <= set(r5["chaos"])
+    assert r5["chaos"]["failover_s"] < 10

@@ -71,12 +71,7 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
         expected = {}
 
         async def push(n, kinds=None):
-            if kinds:
-                wl._kinds, saved = kinds, wl._kinds
-                wl._weights, saved_w = [1.0] * len(kinds), wl._weights
-            failed, traffic, new_rows = wl.step(n)
-            if kinds:
-                wl._kinds, wl._weights = saved, saved_w
+            failed, traffic, new_rows = wl.step(n, kinds)
             for r in new_rows:
                 for _ in range(50):
                     try:

@@ -135,3 +135,19 @@ def test_hold_workload_visible_as_process(telemetry, stress_exe):
     finally:
         out, err = p.communicate(timeout=60)
     assert p.returncode == 0, err
+
+
+def test_cfg3_stress_pods_with_real_hbm_oom(arun):
+    """BASELINE config 3 on the box's one MI355X: 7 pods hold 30 GiB each, an 8th is
+    driven to a real HIP OOM; the checkpoint row must say hbm-oom on GPU 0 with the
+    VRAM peak near the 288 GB capacity."""
+    from nexus_supervisor_amd.bench.scenarios import cfg3_gpu
+
+    r = arun(cfg3_gpu("uncapped", holders=7, hold_gib=30.0), timeout=300)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/cfg3.json", "w") as f:
+        json.dump(r, f, indent=1)
+    assert r["oom_rc"] == 1 and r["stage"] == "FAILED", r
+    assert r["trace_class"] == "hbm-oom" and r["gpu_index"] == 0, r
+    assert r["vram_peak_mb"] >= 0.9 * r["vram_total_mb"], r
+    assert r["acked"] == 1 and r["p50_ms"] < 1000, r
