@@ -15,6 +15,7 @@
 //     queue evictions, GPU pre/post reset, KFD process start/end.
 //
 // Python reads snapshots under a mutex; neither thread ever takes the GIL.
+#include <algorithm>
 #include <amd_smi/amdsmi.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -121,6 +122,10 @@ struct GpuRec {
   uint32_t vram_total_mb = 0, vram_used_mb = 0, vram_peak_mb = 0;
   uint64_t ecc_correctable = 0, ecc_uncorrectable = 0;
   bool events_ok = false;
+  // xGMI fabric health (RCCL's transport between the node's GPUs); -1 = not reported
+  int xgmi_links_total = -1, xgmi_links_up = -1, xgmi_links_down = -1;
+  int xgmi_error = -1;  // amdsmi_xgmi_status_t
+  bool health_seen = false;
 };
 
 struct EventRec {
@@ -223,6 +228,12 @@ class GpuMonitor {
       d["vram_peak_mb"] = g.vram_peak_mb;
       d["ecc_correctable"] = g.ecc_correctable;
       d["ecc_uncorrectable"] = g.ecc_uncorrectable;
+      if (g.xgmi_links_total >= 0) {
+        d["xgmi_links_total"] = g.xgmi_links_total;
+        d["xgmi_links_up"] = g.xgmi_links_up;
+        d["xgmi_links_down"] = g.xgmi_links_down;
+      }
+      if (g.xgmi_error >= 0) d["xgmi_error"] = g.xgmi_error;
       py::list procs;
       for (auto& kv : procs_) {
         const ProcRec& p = kv.second;
@@ -393,7 +404,18 @@ class GpuMonitor {
     std::vector<amdsmi_error_count_t> ecc(gs.size());
     std::vector<bool> vram_ok(gs.size()), ecc_ok(gs.size());
     std::vector<amdsmi_proc_info_t> buf(64);
+    // link / fabric health changes slowly: poll it every 10th sample
+    const bool health = (samples_.load() % 10) == 0;
+    std::vector<amdsmi_xgmi_link_status_t> links(gs.size());
+    std::vector<bool> links_ok(gs.size(), false);
+    std::vector<int> xerr(gs.size(), -1);
     for (size_t i = 0; i < gs.size(); ++i) {
+      if (health) {
+        memset(&links[i], 0, sizeof links[i]);
+        links_ok[i] = amdsmi_get_gpu_xgmi_link_status(gs[i].h, &links[i]) == AMDSMI_STATUS_SUCCESS;
+        amdsmi_xgmi_status_t xs;
+        if (amdsmi_gpu_xgmi_error_status(gs[i].h, &xs) == AMDSMI_STATUS_SUCCESS) xerr[i] = static_cast<int>(xs);
+      }
       memset(&vram[i], 0, sizeof vram[i]);
       vram_ok[i] = amdsmi_get_gpu_vram_usage(gs[i].h, &vram[i]) == AMDSMI_STATUS_SUCCESS;
       memset(&ecc[i], 0, sizeof ecc[i]);
@@ -459,8 +481,34 @@ class GpuMonitor {
         while (hist_[i].size() > hist_cap) hist_[i].pop_front();
       }
       if (ecc_ok[i]) {
+        if (g.health_seen && ecc[i].uncorrectable_count > g.ecc_uncorrectable)
+          record_event_locked(EventRec{g.index, "ECC_UNCORRECTABLE",
+                                       std::to_string(ecc[i].uncorrectable_count - g.ecc_uncorrectable) +
+                                           " new uncorrectable ECC error(s)", t});
         g.ecc_correctable = ecc[i].correctable_count;
         g.ecc_uncorrectable = ecc[i].uncorrectable_count;
+      }
+      if (health) {
+        if (links_ok[i]) {
+          uint32_t n = std::min<uint32_t>(links[i].total_links, AMDSMI_MAX_NUM_XGMI_LINKS);
+          int up = 0, down = 0;
+          for (uint32_t k = 0; k < n; ++k) {
+            if (links[i].status[k] == AMDSMI_XGMI_LINK_UP) ++up;
+            else if (links[i].status[k] == AMDSMI_XGMI_LINK_DOWN) ++down;
+          }
+          if (g.health_seen && g.xgmi_links_down >= 0 && down > g.xgmi_links_down)
+            record_event_locked(EventRec{g.index, "XGMI_LINK_DOWN",
+                                         std::to_string(down) + "/" + std::to_string(n) + " xGMI links down", t});
+          g.xgmi_links_total = static_cast<int>(n);
+          g.xgmi_links_up = up;
+          g.xgmi_links_down = down;
+        }
+        if (xerr[i] >= 0) {
+          if (g.health_seen && xerr[i] > 0 && g.xgmi_error == 0)
+            record_event_locked(EventRec{g.index, "XGMI_ERROR", "xGMI error status " + std::to_string(xerr[i]), t});
+          g.xgmi_error = xerr[i];
+        }
+        g.health_seen = true;
       }
     }
     samples_.fetch_add(1);

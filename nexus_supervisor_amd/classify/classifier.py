@@ -26,6 +26,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..config.schema import GpuConfig, LabelConfig, RulesConfig
 from ..gpu import oom as oom_mod
+from ..gpu.telemetry import FAULT_EVENTS
 from ..gpu.topology import merge_process_ranks, topology_from_pod
 from ..models import kube
 from ..models.decisions import DecisionAction as A
@@ -359,7 +360,7 @@ class Classifier:
         kinds = set()
         for g in gev.get("gpus", []):
             for e in g.get("events", []):
-                if e.get("type") in ("VMFAULT", "GPU_PRE_RESET", "GPU_POST_RESET"):
+                if e.get("type") in FAULT_EVENTS:
                     kinds.add(e["type"])
         return sorted(kinds)
 

@@ -26,12 +26,11 @@ from typing import Any, Dict, List, Optional, Set, Tuple
 from ..informer import InformerFactory
 from ..models import kube
 from .podresources import PodResourcesClient, gpu_allocations, normalize_bdf
-from .telemetry import ATTRIBUTION_EVENTS, GpuTelemetry, evidence_for
+from .telemetry import ATTRIBUTION_EVENTS, FAULT_EVENTS, GpuTelemetry, evidence_for
 from .topology import topology_from_pod
 
 log = logging.getLogger("nexus_supervisor_amd.agent")
 
-FAULT_EVENTS = ("VMFAULT", "GPU_PRE_RESET", "GPU_POST_RESET")
 
 
 def pod_failed(pod: Dict[str, Any]) -> bool:

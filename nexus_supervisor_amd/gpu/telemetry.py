@@ -24,7 +24,10 @@ from typing import Any, Dict, Iterable, List, Optional
 
 from .topology import _int
 
-ATTRIBUTION_EVENTS = ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET", "GPU_POST_RESET", "THERMAL_THROTTLE")
+ATTRIBUTION_EVENTS = ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET", "GPU_POST_RESET", "THERMAL_THROTTLE",
+                      "ECC_UNCORRECTABLE", "XGMI_LINK_DOWN", "XGMI_ERROR")
+# events that by themselves explain a job failure (hardware / driver faults)
+FAULT_EVENTS = ("VMFAULT", "GPU_PRE_RESET", "GPU_POST_RESET", "ECC_UNCORRECTABLE", "XGMI_LINK_DOWN", "XGMI_ERROR")
 
 
 class TelemetryUnavailable(RuntimeError):
@@ -164,6 +167,25 @@ class FakeTelemetry(GpuTelemetry):
             p["last_seen"] = self.clock()
         self.inject_event(gpu, "PROCESS_END", f"pid {pid}")
 
+    def set_xgmi(self, gpu: int, total: int = 7, down: int = 0, error: int = 0) -> None:
+        """Link / fabric health as the native monitor reports it (events on degradation)."""
+        with self._lock:
+            g = self._gpus[gpu]
+            prev_down, prev_err = g.get("xgmi_links_down", 0), g.get("xgmi_error", 0)
+            g.update(xgmi_links_total=total, xgmi_links_up=total - down, xgmi_links_down=down, xgmi_error=error)
+        if down > prev_down:
+            self.inject_event(gpu, "XGMI_LINK_DOWN", f"{down}/{total} xGMI links down")
+        if error and not prev_err:
+            self.inject_event(gpu, "XGMI_ERROR", f"xGMI error status {error}")
+
+    def set_ecc(self, gpu: int, uncorrectable: int, correctable: int = 0) -> None:
+        with self._lock:
+            g = self._gpus[gpu]
+            prev = g["ecc_uncorrectable"]
+            g["ecc_uncorrectable"], g["ecc_correctable"] = uncorrectable, correctable
+        if uncorrectable > prev:
+            self.inject_event(gpu, "ECC_UNCORRECTABLE", f"{uncorrectable - prev} new uncorrectable ECC error(s)")
+
     def inject_event(self, gpu: int, etype: str, message: str = "") -> None:
         e = {"gpu": gpu, "type": etype, "message": message, "t": self.clock()}
         with self._lock:
@@ -249,6 +271,11 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
                                "window": [round(t0, 3), round(t1, 3)]}
         if g.get("ecc_uncorrectable"):
             rec["ecc_uncorrectable"] = g["ecc_uncorrectable"]
+        if g.get("xgmi_links_down"):
+            rec["xgmi_links_down"] = g["xgmi_links_down"]
+            rec["xgmi_links_total"] = g.get("xgmi_links_total")
+        if g.get("xgmi_error"):
+            rec["xgmi_error"] = g["xgmi_error"]
         rec["procs"] = [dict({"pid": p["pid"], "vram_bytes": p.get("vram_bytes", 0),
                               "peak_vram_bytes": p.get("peak_vram_bytes", 0), "alive": p.get("alive", False)},
                              **_rank_fields(p.get("env") or {})) for p in procs]

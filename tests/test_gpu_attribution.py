@@ -78,3 +78,36 @@ def test_merge_process_ranks_and_environ():
     assert [e["gpu"] for e in t["rank_map"]] == [1, 2]
     env = rank_env_from_environ(["RANK=3", "PATH=/bin", "LOCAL_RANK=1", "HIP_VISIBLE_DEVICES=1"])
     assert env == {"RANK": "3", "LOCAL_RANK": "1", "HIP_VISIBLE_DEVICES": "1"}
+
+
+def test_xgmi_link_down_and_ecc_are_gpu_faults():
+    """A rank whose GPU lost xGMI links (RCCL transport) or took an uncorrectable ECC error
+    fails as a GPU fault, not a plain error; the trace carries the link state."""
+    from nexus_supervisor_amd.classify import Classifier, render_trace
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry, pod_evidence_provider
+    from nexus_supervisor_amd.models.decisions import FailureClass
+    from nexus_supervisor_amd.testing.seed import make_pod
+
+    labels = LabelConfig()
+    for gpu, inject, expect in ((5, lambda t: t.set_xgmi(5, total=7, down=2), "XGMI_LINK_DOWN"),
+                                (2, lambda t: t.set_ecc(2, uncorrectable=3), "ECC_UNCORRECTABLE")):
+        tel = FakeTelemetry(n_gpus=8)
+        inject(tel)
+        tel.set_xgmi(0, total=7, down=0)  # healthy GPU: no event
+        c = Classifier(labels)
+        c.evidence_provider = pod_evidence_provider(tel)
+        env = {"LOCAL_RANK": str(gpu), "RANK": str(gpu), "WORLD_SIZE": "8", "HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}
+        pod = make_pod(f"run-{gpu}", labels, env=env, gpus=1, rv="2", status={
+            "phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {"terminated": {
+                "reason": "Error", "exitCode": 1,
+                "message": "RuntimeError: NCCL Error 6: remote process exited or there was a network error"}}}]})
+        res = c.classify_pod(pod)
+        assert len(res) == 1 and res[0].failure_class == FailureClass.GPU_FAULT, res
+        assert expect in res[0].run_status_trace or expect in (res[0].reason or "")
+        trace = json.loads(render_trace(res[0]))
+        g = trace["gpu"]["gpus"][0]
+        assert g["index"] == gpu and any(e["type"] == expect for e in g["events"])
+        if expect == "XGMI_LINK_DOWN":
+            assert g["xgmi_links_down"] == 2 and g["xgmi_links_total"] == 7
+        assert not [e for e in tel.snapshot()[0]["events"]]
