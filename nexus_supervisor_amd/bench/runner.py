@@ -266,7 +266,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
 def _stage_breakdown(sup) -> Dict[str, Any]:
     m = sup.metrics
     out = {}
-    for name in ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_write"):
+    for name in ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_write", "stage_delete"):
         h = m.histogram(name)
         if h is not None:
             out[name] = {k: (int(v) if k == "count" else round(v / 1000.0, 3)) for k, v in h.summary().items()}

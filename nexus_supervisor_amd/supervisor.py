@@ -134,6 +134,11 @@ class Supervisor:
         m = self.metrics
         m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
+        m.describe("stage_classify", "Watch receive to pipeline enqueue (classification)")
+        m.describe("stage_queue", "Pipeline enqueue to worker dequeue (rate limit + queueing)")
+        m.describe("stage_read", "Checkpoint read round trip")
+        m.describe("stage_write", "Checkpoint write round trip")
+        m.describe("stage_delete", "Checkpoint ack to Job DELETE accepted")
 
     # ------------------------------------------------------------------ Init
     def init(self) -> None:
@@ -467,6 +472,9 @@ class Supervisor:
             attempt += 1
             try:
                 await self._delete_job(r.request_id)
+                ack = r.stamps.get("ack") if r.stamps else None
+                if ack is not None:
+                    self.metrics.observe_seconds("stage_delete", self.wall() - ack)
                 return
             except asyncio.CancelledError:
                 raise
