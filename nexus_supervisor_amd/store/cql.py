@@ -285,6 +285,9 @@ class PreparedStatement:
     keyspace: str = ""
 
 
+_HOST_EPOCH = [0]  # bumped on every host up/down flip: invalidates routing caches
+
+
 @dataclass
 class Host:
     address: Tuple[str, int]
@@ -293,20 +296,35 @@ class Host:
     host_id: str = ""
     tokens: List[int] = field(default_factory=list)
     conns: List[CqlConnection] = field(default_factory=list)
-    up: bool = False
+    _up: bool = False
     failures: int = 0
     next_retry: float = 0.0
     rr: int = 0
 
+    @property
+    def up(self) -> bool:
+        return self._up
+
+    @up.setter
+    def up(self, v: bool) -> None:
+        if v != self._up:
+            self._up = v
+            _HOST_EPOCH[0] += 1
+
     def pick(self) -> Optional[CqlConnection]:
-        live = [c for c in self.conns if not c.closed]
-        if not live:
-            return None
-        # least in-flight of two random choices
-        if len(live) == 1:
-            return live[0]
-        a, b = random.sample(live, 2)
-        return a if a.in_flight <= b.in_flight else b
+        """Least in-flight live connection, scanning from a rotating start (ties spread)."""
+        conns = self.conns
+        n = len(conns)
+        if n == 1:
+            c = conns[0]
+            return None if c.closed else c
+        self.rr += 1
+        best = None
+        for k in range(n):
+            c = conns[(self.rr + k) % n]
+            if not c.closed and (best is None or c.in_flight < best.in_flight):
+                best = c
+        return best
 
 
 @dataclass
@@ -352,6 +370,9 @@ class CqlSession:
         self._preparing: Dict[str, asyncio.Future] = {}
         self._reconnector: Optional[asyncio.Task] = None
         self._rr = 0
+        self._plan_key: Optional[Tuple[int, int]] = None
+        self._plan_up: List[Host] = []
+        self._plan_owner: Dict[int, List[Host]] = {}
         self.stats = {"requests": 0, "retries": 0, "reprepares": 0, "token_routed": 0}
 
     # -------------------------------------------------------------- lifecycle
@@ -488,17 +509,28 @@ class CqlSession:
 
     # -------------------------------------------------------------- routing
     def _candidates(self, routing_token: Optional[int]) -> List[Host]:
-        up = [h for h in self.hosts.values() if h.up and (not self.local_dc or not h.dc or h.dc == self.local_dc)]
-        if not up:
-            up = [h for h in self.hosts.values() if h.up]
+        """Query plan: the token owner first (token-aware), then the other live local-DC
+        hosts round-robin.  Plans are cached until a host flips up/down or joins."""
+        key = (_HOST_EPOCH[0], len(self.hosts))
+        if self._plan_key != key:
+            up = [h for h in self.hosts.values() if h.up and (not self.local_dc or not h.dc or h.dc == self.local_dc)]
+            if not up:
+                up = [h for h in self.hosts.values() if h.up]
+            self._plan_up = up
+            self._plan_owner = {}
+            self._plan_key = key
+        up = self._plan_up
         if routing_token is not None and self.token_aware:
             o = self.owner(routing_token)
             if o is not None and o.up:
                 self.stats["token_routed"] += 1
-                return [o] + [h for h in up if h is not o]
+                plan = self._plan_owner.get(id(o))
+                if plan is None:
+                    plan = self._plan_owner[id(o)] = [o] + [h for h in up if h is not o]
+                return plan
         if len(up) > 1:
             self._rr = (self._rr + 1) % len(up)
-            up = up[self._rr:] + up[: self._rr]
+            return up[self._rr:] + up[: self._rr]
         return up
 
     async def _query_on(self, h: Host, cql: str, values=None) -> Rows:
@@ -580,7 +612,9 @@ class CqlSession:
         last: Optional[BaseException] = None
         tried: set = set()
         while attempts <= self.max_retries:
-            cands = [h for h in self._candidates(token) if h.address not in tried] or self._candidates(token)
+            cands = self._candidates(token)
+            if tried:
+                cands = [h for h in cands if h.address not in tried] or cands
             if not cands:
                 raise StoreError(f"no CQL host available: {last}")
             h = cands[0]
