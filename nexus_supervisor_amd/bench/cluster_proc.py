@@ -122,16 +122,30 @@ async def amain(args) -> None:
 
     for sig in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(sig, stop.set)
-    sampler = None
+    sampler = cprof = None
     if os.environ.get("NEXUS_CLUSTER_PPROF"):
         from ..obs.pprof import Sampler
 
         sampler = Sampler(hz=199).start()
+    if os.environ.get("NEXUS_CLUSTER_CPROFILE"):
+        import cProfile
+
+        cprof = cProfile.Profile()
+        cprof.enable()
     await stop.wait()
     if sampler is not None:
         prof = sampler.stop()
         with open(os.environ["NEXUS_CLUSTER_PPROF"], "w") as f:
             f.write(prof.top(40))
+    if cprof is not None:
+        import io
+        import pstats
+
+        cprof.disable()
+        buf = io.StringIO()
+        pstats.Stats(cprof, stream=buf).sort_stats("tottime").print_stats(40)
+        with open(os.environ["NEXUS_CLUSTER_CPROFILE"], "w") as f:
+            f.write(buf.getvalue())
     await runner.cleanup()
     await api.stop()
     await store.close()

@@ -74,15 +74,20 @@ _FIELD_PATHS = ("metadata.name", "metadata.namespace", "spec.nodeName", "status.
                 "involvedObject.name", "reason", "type")
 
 
+_FIELD_KEYS = tuple(("\0f:" + p, tuple(p.split("."))) for p in _FIELD_PATHS)
+
+
 def _selectable(obj: Dict[str, Any]) -> Dict[str, str]:
     """Labels plus the supported field-selector paths (prefixed ``\0f:``) of an object."""
-    out = dict(obj.get("metadata", {}).get("labels") or {})
-    for path in _FIELD_PATHS:
+    out = dict((obj.get("metadata") or {}).get("labels") or {})
+    for key, parts in _FIELD_KEYS:
         cur: Any = obj
-        for part in path.split("."):
-            cur = cur.get(part) if isinstance(cur, dict) else None
-        if isinstance(cur, str):
-            out["\0f:" + path] = cur
+        for part in parts:
+            cur = cur.get(part) if type(cur) is dict else None
+            if cur is None:
+                break
+        if type(cur) is str:
+            out[key] = cur
     return out
 
 
@@ -102,13 +107,43 @@ def _merge(dst: Dict[str, Any], patch: Dict[str, Any]) -> Dict[str, Any]:
 
 
 class _Watcher:
-    __slots__ = ("ns", "sel", "queue", "closed")
+    """One watch stream: committed lines buffer here until the stream's writer drains
+    them (a list + one wakeup future: no per-event queue/task machinery)."""
+
+    __slots__ = ("ns", "sel", "buf", "closed", "wake")
 
     def __init__(self, ns, sel):
         self.ns = ns
         self.sel = sel
-        self.queue: "asyncio.Queue[Optional[bytes]]" = asyncio.Queue()
+        self.buf: List[bytes] = []
         self.closed = False
+        self.wake: Optional[asyncio.Future] = None
+
+    def push(self, line: bytes) -> None:
+        if self.closed:
+            return  # committed after the stream was cut: the client resumes (or gets 410)
+        self.buf.append(line)
+        w = self.wake
+        if w is not None and not w.done():
+            w.set_result(None)
+
+    def close(self) -> None:
+        self.closed = True
+        w = self.wake
+        if w is not None and not w.done():
+            w.set_result(None)
+
+    async def wait(self, timeout: float) -> None:
+        if self.buf or self.closed:
+            return
+        loop = asyncio.get_running_loop()
+        fut = self.wake = loop.create_future()
+        h = loop.call_later(timeout, lambda: fut.done() or fut.set_result(None))
+        try:
+            await fut
+        finally:
+            h.cancel()
+            self.wake = None
 
 
 class FakeApiServer:
@@ -175,7 +210,7 @@ class FakeApiServer:
             self.compacted[kind] = old[0]
         for w in list(self.watchers[kind]):
             if (not w.ns or w.ns == ns) and _matches(labels, w.sel):
-                w.queue.put_nowait(line)
+                w.push(line)
 
     def create(self, obj: Dict[str, Any], copy_obj: bool = True) -> Dict[str, Any]:
         obj = copy.deepcopy(obj) if copy_obj else obj
@@ -264,8 +299,7 @@ class FakeApiServer:
     def close_watches(self, kind: Optional[str] = None) -> None:
         for k in ([kind] if kind else list(RESOURCES)):
             for w in list(self.watchers[k]):
-                w.closed = True
-                w.queue.put_nowait(None)
+                w.close()
 
     # ------------------------------------------------------------------ HTTP
     def _auth(self, req: web.Request) -> Optional[web.Response]:
@@ -380,27 +414,20 @@ class FakeApiServer:
                 remaining = deadline - time.monotonic()
                 if remaining <= 0:
                     break
-                try:
-                    line = await asyncio.wait_for(w.queue.get(), min(remaining, self.bookmark_interval))
-                except asyncio.TimeoutError:
+                await w.wait(min(remaining, self.bookmark_interval))
+                if not w.buf:
+                    if w.closed:
+                        break
                     if bookmarks:
                         bm = {"type": "BOOKMARK", "object": {"kind": kind, "apiVersion": _API_VERSION.get(kind, "v1"),
                                                              "metadata": {"resourceVersion": str(self.rv)}}}
                         await resp.write(json.dumps(bm).encode() + b"\n")
                     continue
-                if line is None:
-                    break
-                if w.queue.empty() and self.coalesce > 0:
+                if len(w.buf) == 1 and self.coalesce > 0 and not w.closed:
                     # like the apiserver's buffered watch writer: let a burst accumulate
                     # briefly and send it as one chunk instead of one write per event
                     await asyncio.sleep(self.coalesce)
-                chunk = [line]
-                while not w.queue.empty():
-                    nxt = w.queue.get_nowait()
-                    if nxt is None:
-                        w.closed = True
-                        break
-                    chunk.append(nxt)
+                chunk, w.buf = w.buf, []
                 if skip_upto:
                     chunk = [c for c in chunk if _line_rv(c) > skip_upto]
                     if chunk:
