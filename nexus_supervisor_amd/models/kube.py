@@ -18,38 +18,43 @@ from typing import Any, Dict, Iterable, List, Optional
 _KEEP_ANNOTATIONS_PREFIXES = ("nexus.amd.com/", "batch.kubernetes.io/job-completion-index")
 
 
+_EMPTY: Dict[str, Any] = {}
+
+
+# (hot path: called several times per watch event — kept to one dict lookup chain each)
 def meta(obj: Dict[str, Any]) -> Dict[str, Any]:
-    return obj.get("metadata") or {}
+    return obj.get("metadata") or _EMPTY
 
 
 def name_of(obj) -> str:
-    return meta(obj).get("name", "")
+    return (obj.get("metadata") or _EMPTY).get("name", "")
 
 
 def namespace_of(obj) -> str:
-    return meta(obj).get("namespace", "")
+    return (obj.get("metadata") or _EMPTY).get("namespace", "")
 
 
 def uid_of(obj) -> str:
-    return meta(obj).get("uid", "")
+    return (obj.get("metadata") or _EMPTY).get("uid", "")
 
 
 def labels_of(obj) -> Dict[str, str]:
-    return meta(obj).get("labels") or {}
+    return (obj.get("metadata") or _EMPTY).get("labels") or _EMPTY
 
 
 def annotations_of(obj) -> Dict[str, str]:
-    return meta(obj).get("annotations") or {}
+    return (obj.get("metadata") or _EMPTY).get("annotations") or _EMPTY
 
 
 def resource_version(obj) -> str:
-    return meta(obj).get("resourceVersion", "")
+    return (obj.get("metadata") or _EMPTY).get("resourceVersion", "")
 
 
 def object_key(obj) -> str:
     """``namespace/name`` (client-go ``cache.MetaNamespaceKeyFunc``)."""
-    ns = namespace_of(obj)
-    return f"{ns}/{name_of(obj)}" if ns else name_of(obj)
+    m = obj.get("metadata") or _EMPTY
+    ns = m.get("namespace")
+    return f"{ns}/{m.get('name', '')}" if ns else m.get("name", "")
 
 
 def _slim_meta(m: Dict[str, Any], keep_labels=True) -> Dict[str, Any]:
