@@ -36,13 +36,19 @@ from .errors import ApiError, from_status
 
 
 def _native_decoder_available() -> bool:
+    """The projected watch decoder is native (``csrc/kube/watch_decoder.cpp``).  A missing
+    build is an error — ``python -m nexus_supervisor_amd build`` — unless the plain
+    ``json`` path is asked for explicitly with ``NEXUS_PY_WATCH_DECODER=1``."""
     try:
         from .. import _kube_native  # noqa: F401
 
         return True
-    except ImportError:
-        log.warning("native watch decoder (_kube_native) not built; using json + Python slimming")
-        return False
+    except ImportError as exc:
+        if os.environ.get("NEXUS_PY_WATCH_DECODER") == "1":
+            log.warning("native watch decoder (_kube_native) not built; using json (NEXUS_PY_WATCH_DECODER=1)")
+            return False
+        raise ImportError("native watch decoder _kube_native is not built: run `python -m nexus_supervisor_amd build` "
+                          "(or set NEXUS_PY_WATCH_DECODER=1 to use the slower json path)") from exc
 
 
 def _decoder(projection):
