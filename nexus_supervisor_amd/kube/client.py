@@ -121,6 +121,7 @@ class KubeConfig:
     def from_file(cls, path: str, context: Optional[str] = None) -> "KubeConfig":
         import yaml
 
+        path = os.path.expanduser(path)
         with open(path) as f:
             doc = yaml.safe_load(f) or {}
         base = os.path.dirname(os.path.abspath(path))

@@ -4,6 +4,7 @@ same values to the same ``NEXUS__*`` env names
 (``/root/reference/.helm/templates/deployment.yaml:48-67``)."""
 import os
 import sys
+import time
 
 import pytest
 
@@ -94,3 +95,60 @@ def test_scylla_and_datadog_values():
     assert any(v["name"] == "dsdsocket" for v in dep["spec"]["template"]["spec"]["volumes"])
     # the secretRef is rendered whenever secretRefEnabled (reference quirk fixed)
     assert c["envFrom"][0]["secretRef"]["name"].endswith("-cql")
+
+
+def test_local_harness_files():
+    """docker-compose (reference docker-compose.yaml), schema/seed file generated from the
+    model, and the local config overlay."""
+    import yaml
+
+    sys_path_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(sys_path_root, "tools"))
+    import gen_test_resources
+
+    with open(gen_test_resources.OUT) as f:
+        assert f.read() == gen_test_resources.render(), "run tools/gen_test_resources.py"
+    with open(os.path.join(sys_path_root, "deploy", "docker-compose.yaml")) as f:
+        dc = yaml.safe_load(f)
+    assert {"scylla", "prepare_scylla", "cqlsrv"} <= set(dc["services"])
+    from nexus_supervisor_amd.config import load_config
+
+    c = load_config(path=os.path.join(sys_path_root, "deploy", "appconfig.yaml"), env={"APPLICATION_ENVIRONMENT": "local"})
+    assert c.cql_store_type == "scylla" and c.scylla_cql_store.hosts == ["127.0.0.1"] and c.observability.http_port == 8080
+
+
+def test_kindload_manifests_seed_and_wait(arun):
+    """BASELINE config 2 tooling: real failing Job manifests + row seeding + stage wait."""
+    from nexus_supervisor_amd.bench import kindload as kl
+    from nexus_supervisor_amd.bench.wire import schema_statements
+    from nexus_supervisor_amd.testing.cqlsrv import CqlServer
+
+    docs = kl.manifests(10, seed=3)
+    assert len(docs) == 10 and len({d["metadata"]["name"] for d in docs}) == 10
+    assert [d["metadata"]["name"] for d in docs] == [r for r, _ in kl.runs(10, seed=3)]
+    oom = docs[0]["spec"]["template"]["spec"]["containers"][0]
+    assert oom["resources"]["limits"]["memory"] == "24Mi" and "tail /dev/zero" in oom["command"][-1]
+    assert docs[0]["spec"]["podFailurePolicy"]["rules"][0]["onExitCodes"]["values"] == [137, 255]
+    assert ".invalid/" in docs[1]["spec"]["template"]["spec"]["containers"][0]["image"]
+    labels = docs[0]["spec"]["template"]["metadata"]["labels"]
+    assert labels["science.sneaksanddata.com/nexus-component"] == "algorithm-run"
+    assert kl.to_yaml(docs).count("---\n") == 10
+    srv = CqlServer(exec_statements=schema_statements()).start()
+    try:
+        addr = f"127.0.0.1:{srv.port}"
+
+        async def go():
+            assert await kl.seed_rows(addr, 10, seed=3) == 10
+            st = await kl._store(addr)
+            import datetime as dt
+
+            for rid, stage in kl.expected(10, seed=3).items():
+                await st.update_status(kl.ALGORITHM, rid, stage, "cause", "details", dt.datetime.now(dt.timezone.utc))
+            await st.close()
+            return await kl.wait_rows(addr, 10, seed=3, timeout=10, t_apply=time.time() - 1)
+
+        res = arun(go())
+        assert res["in_expected_stage"] == 10 and not res["wrong_stage"] and res["missing"] == 0
+        assert res["apply_to_checkpoint_p50_ms"] > 0
+    finally:
+        srv.stop()
