@@ -19,7 +19,9 @@ using namespace nxcql;
 
 namespace {
 
-py::object g_ts_factory;  // ms -> Python timestamp object (None: keep int ms)
+// ms -> Python timestamp object (None: keep int ms).  Heap-held and never destroyed: a
+// static py::object would be DECREF'd by the C++ runtime after interpreter finalisation.
+py::object& g_ts_factory = *new py::object();
 
 // ---------------------------------------------------------------- types <-> Python
 Type type_from_py(const py::handle& h) {

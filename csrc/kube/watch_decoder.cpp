@@ -618,8 +618,20 @@ PyGetSetDef Decoder_getset[] = {{"stats", reinterpret_cast<getter>(Decoder_stats
 
 PyTypeObject DecoderType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
+}  // namespace
+
+extern "C" PyObject* nexus_json_dumps(PyObject*, PyObject* args, PyObject* kw);  // json_encode.cpp
+
+namespace {
+
+PyMethodDef module_methods[] = {
+    {"dumps", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(nexus_json_dumps)),
+     METH_VARARGS | METH_KEYWORDS, "dumps(obj, sort_keys=False, default=None, newline=False) -> bytes (compact UTF-8 JSON)"},
+    {nullptr, nullptr, 0, nullptr}};
+
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_kube_native",
-                      "Projected JSON decoding of Kubernetes watch streams and LIST bodies", -1, nullptr};
+                      "Projected JSON decoding of Kubernetes watch streams and LIST bodies; fast JSON encoding", -1,
+                      module_methods};
 
 }  // namespace
 

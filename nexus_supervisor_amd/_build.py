@@ -55,7 +55,7 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
         },
         "kube_native": {
             "out": os.path.join(PKG, "_kube_native" + EXT),
-            "srcs": [os.path.join(CSRC, "kube", "watch_decoder.cpp")],
+            "srcs": [os.path.join(CSRC, "kube", "watch_decoder.cpp"), os.path.join(CSRC, "kube", "json_encode.cpp")],
             "deps": [],
             "cmd": lambda out, srcs: [_cxx(), *common, "-O3", "-shared", "-fPIC", f"-I{sysconfig.get_paths()['include']}",
                                       *srcs, "-o", out],

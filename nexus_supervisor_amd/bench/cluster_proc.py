@@ -37,13 +37,9 @@ async def amain(args) -> None:
     state = {"wl": None}
 
     async def write_rows(rows):
-        sem = asyncio.Semaphore(512)
-
-        async def one(r):
-            async with sem:
-                await store.upsert_checkpoint(r)
-
-        await asyncio.gather(*(one(r) for r in rows))
+        # windows of 512 concurrent upserts (no per-row semaphore wakeups)
+        for i in range(0, len(rows), 512):
+            await asyncio.gather(*(store.upsert_checkpoint(r) for r in rows[i:i + 512]))
 
     async def h_init(req):
         p = await req.json()
@@ -71,6 +67,9 @@ async def amain(args) -> None:
         return failed, traffic
 
     async def h_step(req):
+        cp = state.pop("cprof", None)
+        if cp is not None:
+            cp.enable()
         p = await req.json()
         events = int(p["events"])
         wl = state["wl"]
@@ -130,8 +129,7 @@ async def amain(args) -> None:
     if os.environ.get("NEXUS_CLUSTER_CPROFILE"):
         import cProfile
 
-        cprof = cProfile.Profile()
-        cprof.enable()
+        cprof = state["cprof"] = cProfile.Profile()  # enabled by the first step (init excluded)
     await stop.wait()
     if sampler is not None:
         prof = sampler.stop()

@@ -444,4 +444,12 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
     doc = {"message": res.run_status_trace, "reason": res.reason, "class": res.failure_class,
            "source": res.evidence.get("source", "")}
     doc.update(extra)
-    return json.dumps(doc, sort_keys=True, separators=(",", ":"), default=str)
+    if _native_dumps is not None:
+        return _native_dumps(doc, sort_keys=True, default=str).decode()
+    return json.dumps(doc, sort_keys=True, separators=(",", ":"), default=str, ensure_ascii=False)
+
+
+try:  # compact UTF-8 JSON (csrc/kube/json_encode.cpp); same document as the json fallback
+    from .._kube_native import dumps as _native_dumps
+except ImportError:  # pragma: no cover - CPU hosts without the native build
+    _native_dumps = None
