@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import asyncio
 import gc
+import resource
 import time
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -208,7 +209,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         await run_steps(cfg.steps)
         barrier_sync()
         elapsed = time.perf_counter() - t0
-        cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3)}
+        cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3),
+               "supervisor_max_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1)}
         x1 = harness.external_cpu()
         for k in x1:
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)

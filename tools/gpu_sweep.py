@@ -8,8 +8,11 @@ CONFIGS = [
     ["--inflight", "1"],
     ["--inflight", "2"],
     ["--inflight", "3"],
-    ["--inflight", "2", "--workers", "1024"],
+    ["--inflight", "4"],
+    ["--inflight", "2", "--workers", "128"],
+    ["--inflight", "2", "--workers", "512"],
     ["--inflight", "2", "--events", "2000"],
+    ["--inflight", "2", "--kube-connections", "64"],
 ]
 out = []
 for extra in CONFIGS:
