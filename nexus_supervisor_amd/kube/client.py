@@ -90,7 +90,8 @@ def _delete_body(policy: str) -> bytes:
 class KubeConfig:
     def __init__(self, server: str, token: str = "", token_file: str = "", ca_data: Optional[bytes] = None,
                  ca_file: str = "", cert_data: Optional[bytes] = None, key_data: Optional[bytes] = None,
-                 insecure: bool = False, username: str = "", password: str = "", namespace: str = ""):
+                 insecure: bool = False, username: str = "", password: str = "", namespace: str = "",
+                 exec_config: Optional[Dict[str, Any]] = None):
         self.server = server.rstrip("/")
         self.token = token
         self.token_file = token_file
@@ -100,6 +101,9 @@ class KubeConfig:
         self.username, self.password = username, password
         self.namespace = namespace
         self._token_read = 0.0
+        # client.authentication.k8s.io exec credential plugin (kubeconfig users[].user.exec)
+        self.exec_config = exec_config
+        self._exec_expiry = 0.0
 
     @classmethod
     def in_cluster(cls) -> "KubeConfig":
@@ -148,7 +152,8 @@ class KubeConfig:
         return cls(cl.get("server", ""), token=token, token_file=token_file, ca_data=data(cl, "certificate-authority"),
                    cert_data=data(us, "client-certificate"), key_data=data(us, "client-key"),
                    insecure=bool(cl.get("insecure-skip-tls-verify")), username=us.get("username", ""),
-                   password=us.get("password", ""), namespace=ctx.get("namespace", ""))
+                   password=us.get("password", ""), namespace=ctx.get("namespace", ""),
+                   exec_config=us.get("exec") or None)
 
     @classmethod
     def load(cls, kube_config_path: str = "") -> "KubeConfig":
@@ -156,7 +161,40 @@ class KubeConfig:
         (``/root/reference/app/app_dependencies.go:39``)."""
         return cls.from_file(kube_config_path) if kube_config_path else cls.in_cluster()
 
+    def _run_exec_plugin(self) -> None:
+        """Run the kubeconfig ``exec`` credential plugin (client-go semantics: ExecCredential
+        JSON on stdout, ``status.token`` + optional ``expirationTimestamp``; cached until
+        shortly before expiry)."""
+        import subprocess
+
+        ex = self.exec_config or {}
+        cmd = [ex.get("command", "")] + list(ex.get("args") or [])
+        env = dict(os.environ)
+        for e in ex.get("env") or []:
+            env[e["name"]] = e.get("value", "")
+        api = ex.get("apiVersion", "client.authentication.k8s.io/v1")
+        env["KUBERNETES_EXEC_INFO"] = json.dumps({"apiVersion": api, "kind": "ExecCredential",
+                                                  "spec": {"interactive": False}})
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=60)
+        if p.returncode != 0:
+            raise ApiError(401, "Unauthorized", f"exec credential plugin {cmd[0]!r} failed: {p.stderr.strip()[-300:]}")
+        status = (json.loads(p.stdout or "{}").get("status") or {})
+        if not status.get("token"):
+            raise ApiError(401, "Unauthorized", f"exec credential plugin {cmd[0]!r} returned no token")
+        self.token = status["token"]
+        exp = status.get("expirationTimestamp")
+        if exp:
+            import datetime as _dt
+
+            t = _dt.datetime.fromisoformat(exp.replace("Z", "+00:00")).timestamp()
+            self._exec_expiry = time.monotonic() + max(0.0, t - time.time() - 30.0)
+        else:
+            self._exec_expiry = float("inf")
+
     def bearer(self) -> str:
+        if self.exec_config and (not self.token or time.monotonic() >= self._exec_expiry):
+            self._run_exec_plugin()
+            return self.token
         if self.token_file and (not self.token or time.monotonic() - self._token_read > 60):
             try:
                 with open(self.token_file) as f:
@@ -357,7 +395,8 @@ class KubeClient:
         return await self.request("PATCH", resource_path(kind, namespace, name), body=patch,
                                   content_type="application/merge-patch+json")
 
-    async def delete(self, kind: str, namespace: Optional[str], name: str, propagation_policy: str = "Background") -> Dict[str, Any]:
+    async def delete(self, kind: str, namespace: Optional[str], name: str, propagation_policy: str = "Background",
+                     want_body: bool = True) -> Dict[str, Any]:
         path = resource_path(kind, namespace, name)
         if not self.pipelined_writes:
             body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
@@ -365,6 +404,8 @@ class KubeClient:
         self.requests += 1
         status, raw = await self._fast_client().request(
             "DELETE", path, _delete_body(propagation_policy), self._headers({"Content-Type": "application/json"}))
+        if status < 400 and not want_body:
+            return {}  # the deleted object is not needed: skip decoding it
         try:
             doc = json.loads(raw) if raw else {}
         except ValueError:
@@ -375,7 +416,7 @@ class KubeClient:
 
     # JobClient protocol (Supervisor actuator)
     async def delete_job(self, namespace: str, name: str, propagation_policy: str = "Background") -> None:
-        await self.delete("Job", namespace, name, propagation_policy)
+        await self.delete("Job", namespace, name, propagation_policy, want_body=False)
 
 
 class KubeListWatch(ListWatch):

@@ -23,6 +23,15 @@ from typing import Deque, Dict, List, Optional, Tuple
 from urllib.parse import urlsplit
 
 
+class _Expired(Exception):
+    pass
+
+
+def _expire(fut: asyncio.Future) -> None:
+    if not fut.done():
+        fut.set_exception(_Expired())
+
+
 class HttpError(Exception):
     pass
 
@@ -209,15 +218,20 @@ class PipelinedHttp:
     async def request(self, method: str, path: str, body: Optional[bytes] = None,
                       headers: Optional[Dict[str, str]] = None) -> Tuple[int, bytes]:
         conn = await self._pick()
-        fut = asyncio.get_running_loop().create_future()
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
         conn.send(self._encode(method, path, body, headers), fut)
         self.requests += 1
+        # deadline as a timer on the future (asyncio.wait_for would cost a Task per request)
+        timer = loop.call_later(self.timeout, _expire, fut)
         try:
-            return await asyncio.wait_for(fut, self.timeout)
-        except asyncio.TimeoutError:
+            return await fut
+        except _Expired:
             # the response order on this connection is now unknown: reset it
             conn._fail(HttpError("request timed out"))
             raise HttpError(f"{method} {path} timed out") from None
+        finally:
+            timer.cancel()
 
     async def close(self) -> None:
         for c in list(self._conns):

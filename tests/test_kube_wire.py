@@ -250,3 +250,50 @@ def test_late_event_then_object_is_not_lost(arun):
             await api.stop()
 
     arun(go(), timeout=60)
+
+
+def test_kubeconfig_exec_credential_plugin(arun, tmp_path):
+    """users[].user.exec (EKS/GKE style): the plugin's ExecCredential token authenticates,
+    and is re-run once it expires."""
+    import sys
+
+    plugin = tmp_path / "cred.py"
+    count = tmp_path / "count"
+    plugin.write_text(
+        "import json, os, sys\n"
+        f"p = {str(count)!r}\n"
+        "n = int(open(p).read()) + 1 if os.path.exists(p) else 1\n"
+        "open(p, 'w').write(str(n))\n"
+        "assert json.loads(os.environ['KUBERNETES_EXEC_INFO'])['kind'] == 'ExecCredential'\n"
+        "print(json.dumps({'apiVersion': 'client.authentication.k8s.io/v1', 'kind': 'ExecCredential',\n"
+        "                  'status': {'token': os.environ['TOK'], 'expirationTimestamp': '2000-01-01T00:00:00Z'}}))\n")
+    kc = tmp_path / "config"
+
+    async def go():
+        api = FakeApiServer(token="s3cret")
+        url = await api.start()
+        kc.write_text(f"""apiVersion: v1
+kind: Config
+current-context: c
+clusters: [{{name: k, cluster: {{server: "{url}"}}}}]
+contexts: [{{name: c, context: {{cluster: k, user: u}}}}]
+users:
+- name: u
+  user:
+    exec:
+      apiVersion: client.authentication.k8s.io/v1
+      command: {sys.executable}
+      args: ["{plugin}"]
+      env: [{{name: TOK, value: s3cret}}]
+""")
+        cfg = KubeConfig.load(str(kc))
+        c = KubeClient(cfg)
+        api.create(make_pod("r1", _cfg().labels))
+        items, _ = await c.list("Pod", "nexus")
+        assert len(items) == 1
+        await c.list("Pod", "nexus")  # already-expired credential: plugin runs again
+        assert int(count.read_text()) >= 2
+        await c.close()
+        await api.stop()
+
+    arun(go())
