@@ -418,6 +418,29 @@ class KubeClient:
     async def delete_job(self, namespace: str, name: str, propagation_policy: str = "Background") -> None:
         await self.delete("Job", namespace, name, propagation_policy, want_body=False)
 
+    def delete_job_nowait(self, namespace: str, name: str, propagation_policy: str = "Background"):
+        """Fire the Job DELETE on an already-open pipelined connection; returns a future of
+        ``(status, body)`` for :meth:`check_delete`, or ``None`` (use :meth:`delete_job`)."""
+        if not self.pipelined_writes or self._fast is None:
+            return None
+        fut = self._fast.request_nowait("DELETE", resource_path("Job", namespace, name), _delete_body(propagation_policy),
+                                        self._headers({"Content-Type": "application/json"}))
+        if fut is not None:
+            self.requests += 1
+        return fut
+
+    @staticmethod
+    def check_delete(result) -> None:
+        """Raise the API error of a :meth:`delete_job_nowait` response (2xx: nothing)."""
+        status, raw = result
+        if status < 400:
+            return
+        try:
+            doc = json.loads(raw) if raw else {}
+        except ValueError:
+            doc = {"message": raw[:500].decode("utf-8", "replace")}
+        raise from_status(status, doc)
+
 
 class KubeListWatch(ListWatch):
     """Informer transport over :class:`KubeClient` (one kind, one namespace)."""

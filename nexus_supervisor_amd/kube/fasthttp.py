@@ -36,6 +36,12 @@ class HttpError(Exception):
     pass
 
 
+def _expire_and_reset(fut: asyncio.Future, conn: "_Conn", what: str) -> None:
+    if not fut.done():
+        fut.set_exception(HttpError(f"{what} timed out"))
+        conn._fail(HttpError("request timed out"))  # response order on this connection unknown
+
+
 class _Conn(asyncio.Protocol):
     def __init__(self, pool: "PipelinedHttp"):
         self.pool = pool
@@ -205,6 +211,26 @@ class PipelinedHttp:
             while len(best.waiting) >= self.max_depth and not best.closed:
                 await asyncio.sleep(0.001)
         return best
+
+    def request_nowait(self, method: str, path: str, body: Optional[bytes] = None,
+                       headers: Optional[Dict[str, str]] = None) -> Optional[asyncio.Future]:
+        """Send on an open connection with room in its pipeline and return the response
+        future (``(status, body)``; fails with :class:`HttpError` on timeout / connection
+        loss) — no coroutine, no Task.  ``None`` when no connection can take it right now
+        (the caller falls back to :meth:`request`)."""
+        best = None
+        for c in self._conns:
+            if not c.closed and len(c.waiting) < self.max_depth and (best is None or len(c.waiting) < len(best.waiting)):
+                best = c
+        if best is None or len(self._conns) < self.n:
+            return None
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        best.send(self._encode(method, path, body, headers), fut)
+        self.requests += 1
+        timer = loop.call_later(self.timeout, _expire_and_reset, fut, best, f"{method} {path}")
+        fut.add_done_callback(lambda _f, t=timer: t.cancel())
+        return fut
 
     def _encode(self, method: str, path: str, body: Optional[bytes], headers: Optional[Dict[str, str]]) -> bytes:
         h = dict(self.default_headers)

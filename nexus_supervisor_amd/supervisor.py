@@ -460,14 +460,53 @@ class Supervisor:
         return Decision(r, "applied", stage, deleted)
 
     def _spawn_delete(self, r: RunStatusAnalysisResult) -> None:
+        nowait = getattr(self.jobs, "delete_job_nowait", None)
+        if nowait is not None:
+            # fast path: the request goes straight onto an open pipelined connection and a
+            # callback settles it (no coroutine / Task per decision); failures fall back to
+            # the retrying coroutine below
+            fut = nowait(self.namespace, r.request_id, "Background")
+            if fut is not None:
+                self._deletes.add(fut)
+                fut.add_done_callback(lambda f, r=r: self._delete_settled(r, f))
+                return
         t = asyncio.ensure_future(self._delete_with_retry(r))
         self._deletes.add(t)
         t.add_done_callback(self._deletes.discard)
 
-    async def _delete_with_retry(self, r: RunStatusAnalysisResult) -> None:
+    def _delete_settled(self, r: RunStatusAnalysisResult, fut) -> None:
+        self._deletes.discard(fut)
+        if fut.cancelled():
+            return
+        exc = fut.exception()
+        if exc is None:
+            try:
+                self.jobs.check_delete(fut.result())
+            except NotFound as e:
+                if self.cfg.compat.delete_not_found_ok:
+                    return  # already gone (reference retried this forever: SURVEY §2.9.2)
+                exc = e
+            except Exception as e:  # noqa: BLE001 - API error: retried below
+                exc = e
+        if exc is None:
+            self.metrics.inc("jobs_deleted")
+            ack = r.stamps.get("ack") if r.stamps else None
+            if ack is not None:
+                self.metrics.observe_seconds("stage_delete", self.wall() - ack)
+            return
+        self.metrics.inc("job_delete_retries")
+        t = asyncio.ensure_future(self._delete_with_retry(r, first_delay=self.cfg.failure_rate_base_delay))
+        self._deletes.add(t)
+        t.add_done_callback(self._deletes.discard)
+
+    async def _delete_with_retry(self, r: RunStatusAnalysisResult, first_delay: float = 0.0) -> None:
         c = self.cfg
         delay = c.failure_rate_base_delay
         attempt = 0
+        if first_delay > 0:
+            attempt = 1
+            await asyncio.sleep(first_delay)
+            delay = min(delay * 2, c.failure_rate_max_delay)
         while True:
             attempt += 1
             try:

@@ -297,3 +297,42 @@ users:
         await api.stop()
 
     arun(go())
+
+
+def test_background_job_delete_retries_on_api_errors(arun):
+    """The Job DELETE after a durable write goes out on the pipelined connection without a
+    task; a 500 from the API server falls back to the retrying path until it succeeds."""
+    rows = [r for r in seed_rows() if r.lifecycle_stage in ("RUNNING", "BUFFERED")][:2]
+    labels = _cfg().labels
+    objs = []
+    for r in rows:
+        objs += [make_job(r.id, labels), make_pod(r.id, labels)]
+
+    async def go():
+        api, srv, app, store, decisions = await _wire_cluster(objs)
+        try:
+            def fail(rid, rv):
+                p = make_pod(rid, labels, rv=rv)
+                p["status"] = {"phase": "Failed", "containerStatuses": [
+                    {"name": "algorithm", "state": {"terminated": {"reason": "OOMKilled", "exitCode": 137}}}]}
+                api.update(p)
+
+            fail(rows[0].id, "50")  # opens the pipelined write connections
+            await _settle(app, decisions, 1)
+            assert api.get("Job", "nexus", rows[0].id) is None
+            api.fail_next[("DELETE", "Job")] = 2
+            fail(rows[1].id, "51")
+            await _settle(app, decisions, 2)
+            for _ in range(100):
+                if api.get("Job", "nexus", rows[1].id) is None:
+                    break
+                await asyncio.sleep(0.05)
+            assert api.get("Job", "nexus", rows[1].id) is None
+            m = app.supervisor.metrics
+            assert m.counter("job_delete_retries") >= 1 and m.counter("jobs_deleted") >= 2
+        finally:
+            await app.stop()
+            await api.stop()
+            srv.stop()
+
+    arun(go())
