@@ -151,3 +151,67 @@ def test_cfg3_stress_pods_with_real_hbm_oom(arun):
     assert r["trace_class"] == "hbm-oom" and r["gpu_index"] == 0, r
     assert r["vram_peak_mb"] >= 0.9 * r["vram_total_mb"], r
     assert r["acked"] == 1 and r["p50_ms"] < 1000, r
+
+
+def test_node_agent_annotates_real_hbm_oom(stress_exe, tmp_path, arun):
+    """The per-node agent on a real MI355X: the pod's GPU comes from the kubelet
+    pod-resources allocation (the device's real PCI BDF from amd-smi); after a real HIP
+    OOM the failed pod is annotated with that GPU's evidence (VRAM peak ≈ 288 GB)."""
+    from nexus_supervisor_amd.config import load_config
+    from nexus_supervisor_amd.gpu.agent import NodeAgent
+    from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig
+    from nexus_supervisor_amd.testing.fake_apiserver import FakeApiServer
+    from nexus_supervisor_amd.gpu.telemetry import AmdSmiTelemetry
+    from nexus_supervisor_amd.testing.seed import make_pod
+
+    telemetry = AmdSmiTelemetry(interval=0.1)  # the agent owns (and stops) its monitor
+    telemetry.start()
+    dev0 = telemetry.devices()[0]
+    assert dev0.get("bdf"), dev0
+
+    class PodRes:
+        def list(self):
+            return [{"name": "oom-run-w0", "namespace": "nexus", "containers": [
+                {"name": "algorithm", "devices": [{"resource_name": "amd.com/gpu", "device_ids": [dev0["bdf"]]}]}]}]
+
+        def close(self):
+            pass
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        labels = load_config(path=None, env={}).labels
+        api.create(make_pod("oom-run", labels, suffix="w0", gpus=1, node="mi355x-box", status={"phase": "Running"}))
+        kc = KubeClient(KubeConfig(url))
+        agent = NodeAgent(kc, telemetry, "mi355x-box", "nexus", pod_resources=PodRes())
+        await agent.start()
+        assert await agent.factory.wait_for_cache_sync(10)
+        loop = asyncio.get_running_loop()
+        pid, rc, msg, out, err, t0, t1 = await loop.run_in_executor(None, _run_oom, stress_exe, tmp_path,
+                                                                     {"HIP_VISIBLE_DEVICES": "0"})
+        assert rc == 1, (rc, err[-400:])
+        p = api.get("Pod", "nexus", "oom-run-w0")
+        p = dict(p, status={"phase": "Failed", "containerStatuses": [{"name": "algorithm", "state": {
+            "terminated": {"reason": "Error", "exitCode": 1, "message": msg}}}]})
+        api.update(p)
+        ann = None
+        for _ in range(200):
+            ann = (api.get("Pod", "nexus", "oom-run-w0")["metadata"].get("annotations") or {}).get(
+                "nexus.amd.com/gpu-evidence")
+            if ann:
+                break
+            await asyncio.sleep(0.05)
+        await agent.stop()
+        await kc.close()
+        await api.stop()
+        return ann
+
+    import asyncio
+
+    ann = arun(go(), timeout=240)
+    assert ann, "agent never annotated the failed pod"
+    ev = json.loads(ann)
+    g = ev["gpus"][0]
+    assert g["index"] == 0 and g["bdf"].lower().endswith(dev0["bdf"].lower()[-7:])
+    assert g["vram_peak_mb"] >= 0.9 * g["vram_total_mb"], g
+    assert ev["source"] == "amdsmi" and ev["reason"] == "pod-failed"
