@@ -11,6 +11,7 @@ directly.  The protobuf is hand-encoded (no generated code needed).
 from __future__ import annotations
 
 import gzip
+import signal
 import sys
 import threading
 import time
@@ -139,9 +140,17 @@ def _fmt(fr: Frame) -> str:
 
 
 class Sampler:
-    """Samples one thread's stack at ``hz`` into a :class:`Profile`."""
+    """Samples one thread's stack at ``hz`` into a :class:`Profile`.
 
-    def __init__(self, hz: int = 97, thread_id: Optional[int] = None, max_depth: int = 64):
+    ``mode="signal"`` (the default when started on the main thread for the main thread):
+    ``ITIMER_PROF`` delivers SIGPROF every 1/hz s of *process CPU time* and the handler
+    records the interrupted frame — an unbiased CPU profile of the event loop.
+    ``mode="thread"``: a sampler thread reads ``sys._current_frames()`` on a wall clock;
+    it only gets the GIL when the target releases it, so it over-samples frames that sit
+    in syscalls (socket writes, epoll) — use it for non-main threads only.
+    """
+
+    def __init__(self, hz: int = 97, thread_id: Optional[int] = None, max_depth: int = 64, mode: str = "auto"):
         self.hz = max(1, hz)
         self.thread_id = thread_id if thread_id is not None else threading.main_thread().ident
         self.max_depth = max_depth
@@ -149,19 +158,48 @@ class Sampler:
         self._stop = threading.Event()
         self._t: Optional[threading.Thread] = None
         self._t0 = 0.0
+        on_main = threading.current_thread() is threading.main_thread()
+        target_main = self.thread_id == threading.main_thread().ident
+        if mode == "auto":
+            mode = "signal" if (on_main and target_main and hasattr(signal, "setitimer")) else "thread"
+        self.mode = mode
+        self._prev_handler = None
 
     def start(self) -> "Sampler":
         self._t0 = time.monotonic()
+        if self.mode == "signal":
+            self._prev_handler = signal.signal(signal.SIGPROF, self._on_signal)
+            period = 1.0 / self.hz
+            signal.setitimer(signal.ITIMER_PROF, period, period)
+            return self
         self._t = threading.Thread(target=self._loop, name="pprof-sampler", daemon=True)
         self._t.start()
         return self
 
     def stop(self) -> Profile:
+        if self.mode == "signal":
+            signal.setitimer(signal.ITIMER_PROF, 0, 0)
+            if self._prev_handler is not None:
+                signal.signal(signal.SIGPROF, self._prev_handler)
+                self._prev_handler = None
         self._stop.set()
         if self._t is not None:
             self._t.join()
         self.profile.duration_ns = int((time.monotonic() - self._t0) * 1e9)
         return self.profile
+
+    def _record(self, frame) -> None:
+        stack = []
+        f = frame
+        while f is not None and len(stack) < self.max_depth:
+            co = f.f_code
+            stack.append((co.co_filename, co.co_name, co.co_firstlineno, f.f_lineno or 0))
+            f = f.f_back
+        if stack:
+            self.profile.add(tuple(stack))
+
+    def _on_signal(self, signum, frame) -> None:
+        self._record(frame)
 
     def _loop(self) -> None:
         period = 1.0 / self.hz
@@ -170,13 +208,7 @@ class Sampler:
         while not self._stop.is_set():
             frame = sys._current_frames().get(tid)  # noqa: SLF001
             if frame is not None:
-                stack = []
-                f = frame
-                while f is not None and len(stack) < self.max_depth:
-                    co = f.f_code
-                    stack.append((co.co_filename, co.co_name, co.co_firstlineno, f.f_lineno or 0))
-                    f = f.f_back
-                self.profile.add(tuple(stack))
+                self._record(frame)
             del frame
             nxt += period
             delay = nxt - time.monotonic()

@@ -153,9 +153,17 @@ def test_http_endpoints(arun):
             async with s.get(base + "/metrics") as r:
                 text = await r.text()
                 assert "nexus_supervisor_queue_depth" in text and 'kind="Pod"' in text
-            async with s.get(base + "/debug/pprof/profile?seconds=0.2&hz=200") as r:
-                d = decode_profile(await r.read())
-                assert d["samples"] >= 1
+            async def fetch():
+                async with s.get(base + "/debug/pprof/profile?seconds=0.3&hz=200") as r:
+                    return await r.read()
+
+            t = asyncio.ensure_future(fetch())
+            await asyncio.sleep(0.05)
+            t_end = time.monotonic() + 0.15  # CPU on the loop thread while the profile runs
+            while time.monotonic() < t_end:
+                pass
+            d = decode_profile(await t)
+            assert d["samples"] >= 1
             async with s.get(base + "/debug/vars") as r:
                 doc = json.loads(await r.text())
                 assert doc["active"] is True and "pipeline" in doc
@@ -164,3 +172,31 @@ def test_http_endpoints(arun):
         await api.stop()
 
     arun(go())
+
+
+def test_signal_sampler_is_cpu_time_based():
+    """SIGPROF mode (main thread): CPU-bound code is sampled, time blocked in a syscall
+    is not (the thread sampler over-counts such frames)."""
+    def cpu_marker(t_end):
+        x = 0
+        while time.monotonic() < t_end:
+            x += 1
+        return x
+
+    def sleep_marker():
+        time.sleep(0.3)
+
+    s = Sampler(hz=500)
+    assert s.mode == "signal"
+    s.start()
+    cpu_marker(time.monotonic() + 0.3)
+    sleep_marker()
+    prof = s.stop()
+    leaf = {}
+    for st, n in prof.stacks.items():
+        leaf[st[0][1]] = leaf.get(st[0][1], 0) + n
+    assert leaf.get("cpu_marker", 0) >= 20, leaf
+    assert leaf.get("sleep_marker", 0) <= 3, leaf
+    import signal as _signal
+
+    assert _signal.getsignal(_signal.SIGPROF) in (_signal.SIG_DFL, None) or callable(_signal.getsignal(_signal.SIGPROF))
