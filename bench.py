@@ -52,6 +52,8 @@ def parse_args(argv=None):
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
     ap.add_argument("--workers", type=int, default=256)
+    ap.add_argument("--procs", type=int, default=1,
+                    help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport)")
     ap.add_argument("--inflight", type=int, default=2, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--kube-connections", type=int, default=256)
     ap.add_argument("--probe-events", type=int, default=60,
@@ -130,7 +132,7 @@ def main(argv=None) -> int:
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
-                      probe_rate_per_min=args.probe_rate,
+                      probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pprof_out=args.pprof_out if rank == 0 else "")
     res = asyncio.run(run_rank(cfg, barrier_sync))
 
@@ -190,6 +192,7 @@ def main(argv=None) -> int:
                 "profile": args.profile,
                 "store": res.get("store"),
                 "workers": res.get("workers"),
+                "worker_processes": args.procs if args.transport == "wire" else 1,
                 "inflight_steps": args.inflight,
                 "rate_limit_eps": res.get("eps"),
                 "gpu_telemetry": res.get("telemetry"),

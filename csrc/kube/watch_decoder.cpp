@@ -18,9 +18,12 @@
 // Status objects in ERROR events survive any kind's schema).
 #include <Python.h>
 
+#include <time.h>
+
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <string>
 #include <string_view>
@@ -491,6 +494,293 @@ class Parser {
   std::string scratch_;
 };
 
+
+// ------------------------------------------------------------------ shard routing
+// A supervisor replica split into shard-worker processes (parallel/workers.py) has
+// every worker read every watch stream, but each owns only the runs whose Job name
+// hashes to it.  The router decides ownership from the raw line *before* the line
+// is materialised: a scan that skips everything except the few key paths
+// (object.metadata.name, the job-name label, involvedObject.kind/name) costs a
+// fraction of building the projected dict, so a non-owned object costs the worker
+// almost nothing.  Placement is zlib.crc32(job_name, seed) % count (same as the
+// Python WorkerShard); pods map name → owner so Pod Events can be routed too.
+
+uint32_t crc32_update(uint32_t start, const char* p, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = start ^ 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) c = table[(c ^ static_cast<uint8_t>(p[i])) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+double mono_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<double>(ts.tv_sec) + static_cast<double>(ts.tv_nsec) * 1e-9;
+}
+
+// Allocation-free path lookup in one JSON document.  Finds the string at a key path
+// (each step an object key); returns false when absent, not a string, or escaped.
+class Scan {
+ public:
+  Scan(const char* s, size_t n) : s_(s), n_(n) {}
+
+  bool find(const char* const* path, size_t depth, std::string_view& out) {
+    i_ = 0;
+    try {
+      return walk(path, depth, out);
+    } catch (const ParseError&) {
+      return false;
+    }
+  }
+
+ private:
+  const char* s_;
+  size_t n_;
+  size_t i_ = 0;
+
+  void ws() {
+    while (i_ < n_ && (s_[i_] == ' ' || s_[i_] == '\t' || s_[i_] == '\r' || s_[i_] == '\n')) ++i_;
+  }
+  // raw string token at i_ (on the opening quote); escaped = contains a backslash
+  std::string_view str(bool& escaped) {
+    size_t st = ++i_;
+    escaped = false;
+    while (i_ < n_) {
+      char c = s_[i_];
+      if (c == '\\') {
+        escaped = true;
+        i_ += 2;
+        continue;
+      }
+      if (c == '"') {
+        std::string_view v(s_ + st, i_ - st);
+        ++i_;
+        return v;
+      }
+      ++i_;
+    }
+    throw ParseError{"unterminated string", i_};
+  }
+  void skip_value() {
+    ws();
+    if (i_ >= n_) throw ParseError{"unexpected end", i_};
+    char c = s_[i_];
+    if (c == '"') {
+      bool e;
+      str(e);
+      return;
+    }
+    if (c == '{' || c == '[') {
+      int depth = 0;
+      while (i_ < n_) {
+        char d = s_[i_];
+        if (d == '"') {
+          bool e;
+          str(e);
+          continue;
+        }
+        if (d == '{' || d == '[') ++depth;
+        else if ((d == '}' || d == ']') && --depth == 0) {
+          ++i_;
+          return;
+        }
+        ++i_;
+      }
+      throw ParseError{"unterminated container", i_};
+    }
+    while (i_ < n_ && s_[i_] != ',' && s_[i_] != '}' && s_[i_] != ']') ++i_;
+  }
+  bool walk(const char* const* path, size_t depth, std::string_view& out) {
+    ws();
+    if (i_ >= n_ || s_[i_] != '{') return false;
+    ++i_;
+    while (true) {
+      ws();
+      if (i_ >= n_) return false;
+      if (s_[i_] == '}') return false;
+      if (s_[i_] != '"') return false;
+      bool esc;
+      std::string_view k = str(esc);
+      ws();
+      if (i_ >= n_ || s_[i_] != ':') return false;
+      ++i_;
+      if (!esc && k == path[0]) {
+        if (depth == 1) {
+          ws();
+          if (i_ >= n_ || s_[i_] != '"') return false;
+          out = str(esc);
+          return !esc;
+        }
+        return walk(path + 1, depth - 1, out);
+      }
+      skip_value();
+      ws();
+      if (i_ < n_ && s_[i_] == ',') ++i_;
+    }
+  }
+};
+
+struct Owners {
+  std::unordered_map<std::string, int> pod;
+  std::deque<std::pair<double, std::string>> gone;
+};
+
+typedef struct {
+  PyObject_HEAD
+  int index;
+  int count;
+  uint32_t seed;
+  double forget_after;
+  std::string* job_label;
+  Owners* owners;
+  unsigned long long passed;
+  unsigned long long dropped;
+} Router;
+
+enum Role { ROLE_NONE = 0, ROLE_JOB, ROLE_POD, ROLE_EVENT };
+
+int owner_of(const Router* r, std::string_view key) {
+  return static_cast<int>(crc32_update(r->seed, key.data(), key.size()) % static_cast<uint32_t>(r->count));
+}
+
+void expire_owners(Router* r) {
+  auto& g = r->owners->gone;
+  if (g.empty()) return;
+  double now = mono_s();
+  while (!g.empty() && g.front().first <= now) {
+    r->owners->pod.erase(g.front().second);
+    g.pop_front();
+  }
+}
+
+// true = this worker owns (or must see) the watch line
+bool route_line(Router* r, int role, const char* s, size_t n) {
+  static const char* const P_TYPE[] = {"type"};
+  static const char* const P_NAME[] = {"object", "metadata", "name"};
+  static const char* const P_IKIND[] = {"object", "involvedObject", "kind"};
+  static const char* const P_INAME[] = {"object", "involvedObject", "name"};
+  Scan sc(s, n);
+  std::string_view v;
+  if (role == ROLE_JOB) {
+    if (!sc.find(P_NAME, 3, v)) return true;  // BOOKMARK / ERROR / unparsable: keep
+    return owner_of(r, v) == r->index;
+  }
+  if (role == ROLE_POD) {
+    std::string_view name;
+    if (!sc.find(P_NAME, 3, name)) return true;
+    const char* P_JOB[] = {"object", "metadata", "labels", r->job_label->c_str()};
+    int owner = sc.find(P_JOB, 4, v) ? owner_of(r, v) : 0;
+    std::string key(name);
+    r->owners->pod[key] = owner;
+    std::string_view type;
+    if (sc.find(P_TYPE, 1, type) && type == "DELETED") r->owners->gone.emplace_back(mono_s() + r->forget_after, key);
+    expire_owners(r);
+    return owner == r->index;
+  }
+  if (role == ROLE_EVENT) {
+    std::string_view kind;
+    if (!sc.find(P_IKIND, 3, kind)) return true;
+    if (!sc.find(P_INAME, 3, v)) return true;
+    if (kind == "Job") return owner_of(r, v) == r->index;
+    if (kind == "Pod") {
+      auto it = r->owners->pod.find(std::string(v));
+      return it == r->owners->pod.end() || it->second == r->index;  // unknown pod: keep (parked upstream)
+    }
+    return r->index == 0;
+  }
+  return true;
+}
+
+void Router_dealloc(Router* self) {
+  delete self->job_label;
+  delete self->owners;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+PyObject* Router_new(PyTypeObject* type, PyObject*, PyObject*) {
+  Router* self = reinterpret_cast<Router*>(type->tp_alloc(type, 0));
+  if (self) {
+    self->index = 0;
+    self->count = 1;
+    self->seed = 0;
+    self->forget_after = 120.0;
+    self->job_label = new std::string("batch.kubernetes.io/job-name");
+    self->owners = new Owners();
+    self->passed = self->dropped = 0;
+  }
+  return reinterpret_cast<PyObject*>(self);
+}
+
+int Router_init(Router* self, PyObject* args, PyObject* kw) {
+  static const char* kwlist[] = {"index", "count", "seed", "job_label", "forget_after", nullptr};
+  unsigned long seed = 0;
+  const char* label = nullptr;
+  double forget = 120.0;
+  if (!PyArg_ParseTupleAndKeywords(args, kw, "iik|sd", const_cast<char**>(kwlist), &self->index, &self->count, &seed,
+                                   &label, &forget))
+    return -1;
+  if (self->count < 1 || self->index < 0 || self->index >= self->count) {
+    PyErr_SetString(PyExc_ValueError, "index must be in [0, count)");
+    return -1;
+  }
+  self->seed = static_cast<uint32_t>(seed);
+  self->forget_after = forget;
+  if (label) *self->job_label = label;
+  return 0;
+}
+
+PyObject* Router_owner_of(Router* self, PyObject* arg) {
+  Py_ssize_t n;
+  const char* s = PyUnicode_AsUTF8AndSize(arg, &n);
+  if (!s) return nullptr;
+  return PyLong_FromLong(owner_of(self, std::string_view(s, static_cast<size_t>(n))));
+}
+
+PyObject* Router_pod_owner(Router* self, PyObject* arg) {
+  Py_ssize_t n;
+  const char* s = PyUnicode_AsUTF8AndSize(arg, &n);
+  if (!s) return nullptr;
+  auto it = self->owners->pod.find(std::string(s, static_cast<size_t>(n)));
+  if (it == self->owners->pod.end()) Py_RETURN_NONE;
+  return PyLong_FromLong(it->second);
+}
+
+PyObject* Router_note_pod(Router* self, PyObject* args) {
+  const char* name;
+  int owner;
+  int deleted = 0;
+  if (!PyArg_ParseTuple(args, "si|p", &name, &owner, &deleted)) return nullptr;
+  self->owners->pod[name] = owner;
+  if (deleted) self->owners->gone.emplace_back(mono_s() + self->forget_after, name);
+  expire_owners(self);
+  Py_RETURN_NONE;
+}
+
+PyObject* Router_stats(Router* self, void*) {
+  return Py_BuildValue("{s:K,s:K,s:n}", "passed", self->passed, "dropped", self->dropped, "pods",
+                       static_cast<Py_ssize_t>(self->owners->pod.size()));
+}
+
+PyMethodDef Router_methods[] = {
+    {"owner_of", reinterpret_cast<PyCFunction>(Router_owner_of), METH_O, "Owner worker of a job name"},
+    {"pod_owner", reinterpret_cast<PyCFunction>(Router_pod_owner), METH_O, "Owner worker of a pod seen so far (or None)"},
+    {"note_pod", reinterpret_cast<PyCFunction>(Router_note_pod), METH_VARARGS, "Record a pod's owner (name, owner[, deleted])"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef Router_getset[] = {{"stats", reinterpret_cast<getter>(Router_stats), nullptr, nullptr, nullptr},
+                               {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PyTypeObject RouterType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
 // ------------------------------------------------------------------ Python type
 typedef struct {
   PyObject_HEAD
@@ -499,12 +789,15 @@ typedef struct {
   KeyCache* keys;
   unsigned long long docs;
   unsigned long long bytes;
+  Router* router;    // optional shard filter (owned reference)
+  int role;
 } Decoder;
 
 void Decoder_dealloc(Decoder* self) {
   delete self->proj;
   delete self->buf;
   delete self->keys;
+  Py_XDECREF(reinterpret_cast<PyObject*>(self->router));
   Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
 }
 
@@ -528,6 +821,8 @@ PyObject* Decoder_new(PyTypeObject* type, PyObject*, PyObject*) {
     self->buf = nullptr;
     self->keys = nullptr;
     self->docs = self->bytes = 0;
+    self->router = nullptr;
+    self->role = ROLE_NONE;
   }
   return reinterpret_cast<PyObject*>(self);
 }
@@ -581,7 +876,13 @@ PyObject* Decoder_feed(Decoder* self, PyObject* arg) {
     size_t a = start, b = end;
     while (a < b && (buf[a] == ' ' || buf[a] == '\r')) ++a;
     while (b > a && (buf[b - 1] == ' ' || buf[b - 1] == '\r')) --b;
+    if (b > a && self->router && !route_line(self->router, self->role, buf.data() + a, b - a)) {
+      ++self->router->dropped;
+      start = end + 1;
+      continue;
+    }
     if (b > a) {
+      if (self->router) ++self->router->passed;
       PyObject* v = decode_one(self, buf.data() + a, b - a);
       if (!v || PyList_Append(out, v) != 0) {
         Py_XDECREF(v);
@@ -595,6 +896,31 @@ PyObject* Decoder_feed(Decoder* self, PyObject* arg) {
   }
   buf.erase(0, start);
   return out;
+}
+
+// set_router(router, role) — role: "job" | "pod" | "event" | None (clears)
+PyObject* Decoder_set_router(Decoder* self, PyObject* args) {
+  PyObject* r;
+  const char* role = nullptr;
+  if (!PyArg_ParseTuple(args, "O|z", &r, &role)) return nullptr;
+  Py_XDECREF(reinterpret_cast<PyObject*>(self->router));
+  self->router = nullptr;
+  self->role = ROLE_NONE;
+  if (r == Py_None) Py_RETURN_NONE;
+  if (!PyObject_TypeCheck(r, &RouterType)) {
+    PyErr_SetString(PyExc_TypeError, "router must be a ShardRouter");
+    return nullptr;
+  }
+  int rl = role == nullptr ? ROLE_NONE : !strcmp(role, "job") ? ROLE_JOB : !strcmp(role, "pod") ? ROLE_POD
+                                                               : !strcmp(role, "event") ? ROLE_EVENT : -1;
+  if (rl < 0) {
+    PyErr_SetString(PyExc_ValueError, "role must be job, pod or event");
+    return nullptr;
+  }
+  Py_INCREF(r);
+  self->router = reinterpret_cast<Router*>(r);
+  self->role = rl;
+  Py_RETURN_NONE;
 }
 
 PyObject* Decoder_reset(Decoder* self, PyObject*) {
@@ -611,6 +937,8 @@ PyMethodDef Decoder_methods[] = {
     {"decode", reinterpret_cast<PyCFunction>(Decoder_decode), METH_O, "Decode one JSON document with projection"},
     {"feed", reinterpret_cast<PyCFunction>(Decoder_feed), METH_O, "Feed stream bytes; decode complete lines"},
     {"reset", reinterpret_cast<PyCFunction>(Decoder_reset), METH_NOARGS, "Drop a partial line"},
+    {"set_router", reinterpret_cast<PyCFunction>(Decoder_set_router), METH_VARARGS,
+     "Drop watch lines another shard worker owns (router, role)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef Decoder_getset[] = {{"stats", reinterpret_cast<getter>(Decoder_stats), nullptr, nullptr, nullptr},
@@ -646,9 +974,21 @@ PyMODINIT_FUNC PyInit__kube_native(void) {
   DecoderType.tp_getset = Decoder_getset;
   DecoderType.tp_doc = "ProjectedDecoder(projection=True)";
   if (PyType_Ready(&DecoderType) < 0) return nullptr;
+  RouterType.tp_name = "_kube_native.ShardRouter";
+  RouterType.tp_basicsize = sizeof(Router);
+  RouterType.tp_flags = Py_TPFLAGS_DEFAULT;
+  RouterType.tp_new = Router_new;
+  RouterType.tp_init = reinterpret_cast<initproc>(Router_init);
+  RouterType.tp_dealloc = reinterpret_cast<destructor>(Router_dealloc);
+  RouterType.tp_methods = Router_methods;
+  RouterType.tp_getset = Router_getset;
+  RouterType.tp_doc = "ShardRouter(index, count, seed, job_label='batch.kubernetes.io/job-name', forget_after=120.0)";
+  if (PyType_Ready(&RouterType) < 0) return nullptr;
   PyObject* m = PyModule_Create(&moddef);
   if (!m) return nullptr;
   Py_INCREF(&DecoderType);
   PyModule_AddObject(m, "ProjectedDecoder", reinterpret_cast<PyObject*>(&DecoderType));
+  Py_INCREF(&RouterType);
+  PyModule_AddObject(m, "ShardRouter", reinterpret_cast<PyObject*>(&RouterType));
   return m;
 }

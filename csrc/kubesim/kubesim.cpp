@@ -1,0 +1,1081 @@
+// nexus-kubesim — a native kube-apiserver simulator for benchmarks and tests.
+//
+// The reference runs client-go informers against a real API server (LIST+WATCH of
+// Events, Pods and Jobs in one namespace, Job DELETE with Background propagation:
+// /root/reference/services/supervisor.go:70-75,262-270).  The benchmark needs an API
+// server that is never the bottleneck while 10k live runs churn at thousands of
+// failures per second and every supervisor shard-worker process holds its own three
+// watch streams.  The Python fake (nexus_supervisor_amd/testing/fake_apiserver.py)
+// keeps the fault-injection surface for tests; this server implements the same REST
+// + watch wire protocol on one epoll thread:
+//
+//   GET    …/{plural}                 LIST (labelSelector / fieldSelector, limit+continue
+//                                      over a consistent snapshot)
+//   GET    …/{plural}?watch=1         WATCH from resourceVersion: history replay, 410 Gone
+//                                      below the compaction point, BOOKMARKs, timeoutSeconds;
+//                                      chunked JSON lines, one chunk per burst per stream
+//   GET    …/{plural}/{name}          GET
+//   POST   …/{plural}                 create (generateName, uid, creationTimestamp, RV)
+//   PUT    …/{plural}/{name}          replace (409 on a stale resourceVersion)
+//   PATCH  …/{plural}/{name}          JSON merge patch
+//   DELETE …/{plural}/{name}          delete; Background/Foreground propagation deletes the
+//                                      Job's pods (batch.kubernetes.io/job-name) like the GC
+//   POST   /sim/apply[?expire=1]      bulk NDJSON {"type": ADDED|MODIFIED|DELETED, "object": …}
+//                                      (the benchmark's cluster generator); answers the
+//                                      CLOCK_MONOTONIC commit time of the batch; expire=1
+//                                      then compacts past undelivered lines (watchers get 410)
+//   POST   /sim/expire[?kind=Pod]     compact history (resuming watches get 410) + cut streams
+//   POST   /sim/close-watches         cut every watch stream
+//   GET    /sim/stats                 counters
+//
+// Paths: /api/v1/namespaces/{ns}/{plural}[/{name}], /apis/{group}/{version}/namespaces/…,
+// and the cluster-wide /api/v1/{plural}.  Optional bearer token (--token).
+//
+// nexus-kubesim [--host 127.0.0.1] [--port 0] [--ready-file F] [--history N]
+//               [--bookmark-ms 1000] [--token T]
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <map>
+#include <memory>
+#include <random>
+#include <set>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "json.hpp"
+
+using kjson::Value;
+
+namespace {
+
+// ============================================================ options / clock
+struct Options {
+  std::string host = "127.0.0.1";
+  int port = 0;
+  std::string ready_file;
+  size_t history = 400000;
+  int64_t bookmark_ms = 1000;
+  std::string token;
+} g_opt;
+
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+int64_t mono_ms() { return mono_ns() / 1000000; }
+
+std::string now_rfc3339() {
+  static time_t cached_t = 0;
+  static std::string cached;
+  time_t t = time(nullptr);
+  if (t != cached_t) {
+    char buf[32];
+    tm g;
+    gmtime_r(&t, &g);
+    strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%SZ", &g);
+    cached = buf;
+    cached_t = t;
+  }
+  return cached;
+}
+
+std::mt19937_64 g_rng(0x6b756265u ^ static_cast<uint64_t>(mono_ns()));
+
+std::string random_suffix(int n) {
+  static const char* al = "bcdfghjklmnpqrstvwxz2456789";
+  std::string s;
+  for (int i = 0; i < n; ++i) s += al[g_rng() % 27];
+  return s;
+}
+
+std::string uuid4() {
+  uint64_t a = g_rng(), b = g_rng();
+  a = (a & 0xFFFFFFFFFFFF0FFFULL) | 0x0000000000004000ULL;
+  b = (b & 0x3FFFFFFFFFFFFFFFULL) | 0x8000000000000000ULL;
+  char buf[40];
+  snprintf(buf, sizeof buf, "%08x-%04x-%04x-%04x-%012llx", static_cast<unsigned>(a >> 32),
+           static_cast<unsigned>((a >> 16) & 0xFFFF), static_cast<unsigned>(a & 0xFFFF), static_cast<unsigned>(b >> 48),
+           static_cast<unsigned long long>(b & 0xFFFFFFFFFFFFULL));
+  return buf;
+}
+
+// ============================================================ kinds
+struct KindInfo {
+  const char* kind;
+  const char* api_version;
+  const char* plural;
+};
+const KindInfo KINDS[] = {{"Event", "v1", "events"},
+                          {"Pod", "v1", "pods"},
+                          {"Job", "batch/v1", "jobs"},
+                          {"Lease", "coordination.k8s.io/v1", "leases"},
+                          {"Node", "v1", "nodes"}};
+constexpr int NKINDS = sizeof(KINDS) / sizeof(KINDS[0]);
+constexpr int K_POD = 1, K_JOB = 2;
+
+int kind_by_plural(std::string_view p) {
+  for (int i = 0; i < NKINDS; ++i)
+    if (p == KINDS[i].plural) return i;
+  return -1;
+}
+int kind_by_name(std::string_view k) {
+  for (int i = 0; i < NKINDS; ++i)
+    if (k == KINDS[i].kind) return i;
+  return -1;
+}
+
+// ============================================================ selectors
+// Selectable attributes of an object: its labels plus a fixed set of field paths
+// (prefixed "\x01f:" so they never collide with a label key).
+using Attrs = std::vector<std::pair<std::string, std::string>>;
+const char* const FIELD_PATHS[][3] = {{"metadata", "name", nullptr},        {"metadata", "namespace", nullptr},
+                                      {"spec", "nodeName", nullptr},        {"status", "phase", nullptr},
+                                      {"involvedObject", "kind", nullptr}, {"involvedObject", "name", nullptr},
+                                      {"reason", nullptr, nullptr},         {"type", nullptr, nullptr}};
+
+std::shared_ptr<const Attrs> attrs_of(const Value& obj) {
+  auto a = std::make_shared<Attrs>();
+  const Value* md = obj.get("metadata");
+  const Value* labels = md ? md->get("labels") : nullptr;
+  if (labels && labels->t == Value::OBJ)
+    for (auto& kv : labels->o)
+      if (kv.second.t == Value::STR) a->emplace_back(kv.first, kv.second.s);
+  for (auto& fp : FIELD_PATHS) {
+    const Value* cur = &obj;
+    std::string key = "\x01" "f:";
+    for (int i = 0; i < 3 && fp[i]; ++i) {
+      cur = cur->get(fp[i]);
+      if (!cur) break;
+      if (i) key += '.';
+      key += fp[i];
+    }
+    if (cur && cur->t == Value::STR) a->emplace_back(key, cur->s);
+  }
+  return a;
+}
+
+struct Req {
+  std::string key;
+  char op;  // '=', '!', 'e' (exists), 'n' (not exists)
+  std::string val;
+};
+using Selector = std::vector<Req>;
+
+std::string trim(std::string_view s) {
+  size_t b = 0, e = s.size();
+  while (b < e && isspace(static_cast<unsigned char>(s[b]))) ++b;
+  while (e > b && isspace(static_cast<unsigned char>(s[e - 1]))) --e;
+  return std::string(s.substr(b, e - b));
+}
+
+void parse_selector(std::string_view sel, bool fields, Selector& out) {
+  size_t pos = 0;
+  while (pos <= sel.size()) {
+    size_t comma = sel.find(',', pos);
+    if (comma == std::string_view::npos) comma = sel.size();
+    std::string part = trim(sel.substr(pos, comma - pos));
+    pos = comma + 1;
+    if (part.empty()) {
+      if (comma >= sel.size()) break;
+      continue;
+    }
+    Req r;
+    size_t i;
+    if ((i = part.find("!=")) != std::string::npos) {
+      r = {trim(part.substr(0, i)), '!', trim(part.substr(i + 2))};
+    } else if ((i = part.find("==")) != std::string::npos) {
+      r = {trim(part.substr(0, i)), '=', trim(part.substr(i + 2))};
+    } else if ((i = part.find('=')) != std::string::npos) {
+      r = {trim(part.substr(0, i)), '=', trim(part.substr(i + 1))};
+    } else if (part[0] == '!') {
+      r = {trim(part.substr(1)), 'n', ""};
+    } else {
+      r = {part, 'e', ""};
+    }
+    if (fields) r.key = "\x01" "f:" + r.key;
+    out.push_back(std::move(r));
+    if (comma >= sel.size()) break;
+  }
+}
+
+bool matches(const Attrs& a, const Selector& sel) {
+  for (auto& r : sel) {
+    const std::string* v = nullptr;
+    for (auto& kv : a)
+      if (kv.first == r.key) {
+        v = &kv.second;
+        break;
+      }
+    switch (r.op) {
+      case '=': if (!v || *v != r.val) return false; break;
+      case '!': if (v && *v == r.val) return false; break;
+      case 'e': if (!v) return false; break;
+      case 'n': if (v) return false; break;
+    }
+  }
+  return true;
+}
+
+// ============================================================ store
+struct Obj {
+  std::shared_ptr<const std::string> json;
+  std::shared_ptr<const Attrs> attrs;
+  std::string ns, name, job;  // job: batch.kubernetes.io/job-name label (pods)
+  int64_t rv = 0;
+};
+
+struct Hist {
+  int64_t rv;
+  std::string ns;
+  std::shared_ptr<const std::string> line;
+  std::shared_ptr<const Attrs> attrs;
+};
+
+struct Conn;
+
+struct Watch {
+  int fd;
+  int kind;
+  std::string ns;
+  Selector sel;
+  bool bookmarks;
+  int64_t deadline_ms;
+  int64_t last_ms;
+  std::string pending;  // lines committed this loop iteration, sent as one chunk
+};
+
+struct KindStore {
+  std::map<std::string, Obj> objs;  // ns \x01 name → object (sorted: LIST order)
+  std::deque<Hist> history;
+  int64_t compacted = 0;
+  std::vector<Watch*> watchers;
+};
+
+KindStore g_store[NKINDS];
+std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x01 job → pod names
+int64_t g_rv = 1000;
+struct Stats {
+  uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0;
+} g_stats;
+
+struct Snapshot {
+  int64_t rv;
+  std::vector<std::shared_ptr<const std::string>> items;
+};
+std::map<std::string, Snapshot> g_snapshots;
+std::deque<std::string> g_snapshot_order;
+
+std::string okey(std::string_view ns, std::string_view name) {
+  std::string k(ns);
+  k += '\x01';
+  k += name;
+  return k;
+}
+
+void watch_push(Watch* w, const std::string& line);
+
+void record(int kind, const char* etype, const Obj& o) {
+  std::string line;
+  line.reserve(o.json->size() + 32);
+  line += "{\"type\":\"";
+  line += etype;
+  line += "\",\"object\":";
+  line += *o.json;
+  line += "}\n";
+  auto lp = std::make_shared<const std::string>(std::move(line));
+  KindStore& ks = g_store[kind];
+  ks.history.push_back(Hist{o.rv, o.ns, lp, o.attrs});
+  while (ks.history.size() > g_opt.history) {
+    ks.compacted = ks.history.front().rv;
+    ks.history.pop_front();
+  }
+  for (Watch* w : ks.watchers)
+    if ((w->ns.empty() || w->ns == o.ns) && matches(*o.attrs, w->sel)) watch_push(w, *lp);
+}
+
+// Fills metadata defaults, assigns the next resourceVersion, serialises and indexes.
+Obj finish(int kind, Value& doc, const Obj* prev) {
+  if (!doc.get("kind")) doc.at("kind") = Value::str(KINDS[kind].kind);
+  if (!doc.get("apiVersion")) doc.at("apiVersion") = Value::str(KINDS[kind].api_version);
+  Value& md = doc.at("metadata");
+  if (md.path({"name"}).empty()) {
+    std::string gen(md.path({"generateName"}));
+    md.at("name") = Value::str(gen + random_suffix(5));
+  }
+  const Value* uid = md.get("uid");
+  if (!uid || uid->t != Value::STR || uid->s.empty()) {
+    std::string u;
+    if (prev) {
+      Value pv = kjson::parse(*prev->json);
+      u = std::string(pv.path({"metadata", "uid"}));
+      std::string ct(pv.path({"metadata", "creationTimestamp"}));
+      if (!ct.empty() && !md.get("creationTimestamp")) md.at("creationTimestamp") = Value::str(ct);
+    }
+    md.at("uid") = Value::str(u.empty() ? uuid4() : u);
+  }
+  if (!md.get("creationTimestamp")) md.at("creationTimestamp") = Value::str(now_rfc3339());
+  Obj o;
+  o.rv = ++g_rv;
+  md.at("resourceVersion") = Value::str(std::to_string(o.rv));
+  o.ns = std::string(md.path({"namespace"}));
+  o.name = std::string(md.path({"name"}));
+  if (kind == K_POD) {
+    const Value* labels = md.get("labels");
+    const Value* j = labels ? labels->get("batch.kubernetes.io/job-name") : nullptr;
+    if (j && j->t == Value::STR) o.job = j->s;
+  }
+  o.attrs = attrs_of(doc);
+  o.json = std::make_shared<const std::string>(kjson::dump(doc));
+  return o;
+}
+
+void index_pod(const Obj& o, bool add) {
+  if (o.job.empty()) return;
+  std::string k = okey(o.ns, o.job);
+  if (add) {
+    g_pods_by_job[k].insert(o.name);
+  } else {
+    auto it = g_pods_by_job.find(k);
+    if (it != g_pods_by_job.end()) {
+      it->second.erase(o.name);
+      if (it->second.empty()) g_pods_by_job.erase(it);
+    }
+  }
+}
+
+// returns false when the object exists already
+bool create(int kind, Value& doc, std::string* out_json) {
+  Value& md = doc.at("metadata");
+  if (md.path({"name"}).empty() && md.path({"generateName"}).empty()) throw kjson::ParseError("metadata.name required");
+  if (!md.path({"name"}).empty()) {
+    if (g_store[kind].objs.count(okey(md.path({"namespace"}), md.path({"name"})))) return false;
+  }
+  Obj o = finish(kind, doc, nullptr);
+  while (g_store[kind].objs.count(okey(o.ns, o.name))) {  // generateName collision
+    md.at("name") = Value::str(std::string(md.path({"generateName"})) + random_suffix(5));
+    o = finish(kind, doc, nullptr);
+  }
+  if (kind == K_POD) index_pod(o, true);
+  record(kind, "ADDED", o);
+  if (out_json) *out_json = *o.json;
+  g_store[kind].objs[okey(o.ns, o.name)] = std::move(o);
+  return true;
+}
+
+// 0 ok, 1 not found, 2 conflict
+int update(int kind, Value& doc, bool check_rv, std::string* out_json) {
+  Value& md = doc.at("metadata");
+  std::string k = okey(md.path({"namespace"}), md.path({"name"}));
+  auto it = g_store[kind].objs.find(k);
+  if (it == g_store[kind].objs.end()) return 1;
+  std::string want(md.path({"resourceVersion"}));
+  if (check_rv && !want.empty() && want != std::to_string(it->second.rv)) return 2;
+  md.erase("resourceVersion");
+  Obj o = finish(kind, doc, &it->second);
+  if (kind == K_POD) {
+    index_pod(it->second, false);
+    index_pod(o, true);
+  }
+  record(kind, "MODIFIED", o);
+  if (out_json) *out_json = *o.json;
+  it->second = std::move(o);
+  return 0;
+}
+
+bool remove(int kind, const std::string& ns, const std::string& name, const std::string& propagation) {
+  auto it = g_store[kind].objs.find(okey(ns, name));
+  if (it == g_store[kind].objs.end()) return false;
+  Obj o = std::move(it->second);
+  g_store[kind].objs.erase(it);
+  if (kind == K_POD) index_pod(o, false);
+  Value doc = kjson::parse(*o.json);
+  o.rv = ++g_rv;
+  doc.at("metadata").at("resourceVersion") = Value::str(std::to_string(o.rv));
+  o.json = std::make_shared<const std::string>(kjson::dump(doc));
+  record(kind, "DELETED", o);
+  ++g_stats.deleted;
+  if (kind == K_JOB && (propagation == "Background" || propagation == "Foreground")) {
+    auto pit = g_pods_by_job.find(okey(ns, name));
+    if (pit != g_pods_by_job.end()) {
+      std::vector<std::string> pods(pit->second.begin(), pit->second.end());
+      for (auto& p : pods) remove(K_POD, ns, p, propagation);
+    }
+  }
+  return true;
+}
+
+// ============================================================ connections
+struct Conn {
+  int fd;
+  std::string in;
+  std::string out;
+  Watch* watch = nullptr;
+  bool close_after = false;
+};
+
+int g_ep = -1;
+std::unordered_map<int, std::unique_ptr<Conn>> g_conns;
+std::set<Conn*> g_dirty;  // connections with queued output
+
+void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
+
+void interest(Conn& c) {
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0u : static_cast<uint32_t>(EPOLLOUT));
+  ev.data.fd = c.fd;
+  epoll_ctl(g_ep, EPOLL_CTL_MOD, c.fd, &ev);
+}
+
+void end_watch(Conn& c, bool terminate_chunked) {
+  Watch* w = c.watch;
+  if (!w) return;
+  auto& ws = g_store[w->kind].watchers;
+  for (size_t i = 0; i < ws.size(); ++i)
+    if (ws[i] == w) {
+      ws.erase(ws.begin() + static_cast<long>(i));
+      break;
+    }
+  if (terminate_chunked) {
+    if (!w->pending.empty()) {
+      char hdr[24];
+      snprintf(hdr, sizeof hdr, "%zx\r\n", w->pending.size());
+      c.out += hdr;
+      c.out += w->pending;
+      c.out += "\r\n";
+    }
+    c.out += "0\r\n\r\n";
+    g_dirty.insert(&c);
+  }
+  delete w;
+  c.watch = nullptr;
+}
+
+void close_conn(int fd) {
+  auto it = g_conns.find(fd);
+  if (it == g_conns.end()) return;
+  Conn* c = it->second.get();
+  end_watch(*c, false);
+  g_dirty.erase(c);
+  epoll_ctl(g_ep, EPOLL_CTL_DEL, fd, nullptr);
+  close(fd);
+  g_conns.erase(it);
+}
+
+void watch_push(Watch* w, const std::string& line) {
+  w->pending += line;
+  auto it = g_conns.find(w->fd);
+  if (it != g_conns.end()) g_dirty.insert(it->second.get());
+}
+
+// move each watch's pending lines into its connection as one chunk; write out
+bool flush(Conn& c) {
+  if (c.watch && !c.watch->pending.empty()) {
+    char hdr[24];
+    snprintf(hdr, sizeof hdr, "%zx\r\n", c.watch->pending.size());
+    c.out += hdr;
+    c.out += c.watch->pending;
+    c.out += "\r\n";
+    c.watch->pending.clear();
+    c.watch->last_ms = mono_ms();
+  }
+  size_t off = 0;
+  while (off < c.out.size()) {
+    ssize_t n = send(c.fd, c.out.data() + off, c.out.size() - off, MSG_NOSIGNAL);
+    if (n > 0) {
+      off += static_cast<size_t>(n);
+      continue;
+    }
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    if (n < 0 && errno == EINTR) continue;
+    return false;
+  }
+  c.out.erase(0, off);
+  if (c.out.empty() && c.close_after) return false;
+  interest(c);
+  return true;
+}
+
+// ============================================================ HTTP
+std::string status_text(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 410: return "Gone";
+    case 411: return "Length Required";
+    case 500: return "Internal Server Error";
+  }
+  return "Unknown";
+}
+
+void respond(Conn& c, int code, const std::string& body) {
+  char hdr[160];
+  snprintf(hdr, sizeof hdr, "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s\r\n", code,
+           status_text(code).c_str(), body.size(), c.close_after ? "Connection: close\r\n" : "");
+  c.out += hdr;
+  c.out += body;
+  g_dirty.insert(&c);
+}
+
+std::string status_body(int code, const std::string& reason, const std::string& message) {
+  std::string s = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Failure\",\"message\":";
+  kjson::escape(s, message);
+  s += ",\"reason\":";
+  kjson::escape(s, reason);
+  s += ",\"code\":" + std::to_string(code) + "}";
+  return s;
+}
+
+std::string pct_decode(std::string_view s) {
+  auto hv = [](char ch) -> int {
+    if (ch >= '0' && ch <= '9') return ch - '0';
+    if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+    if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+    return -1;
+  };
+  std::string out;
+  out.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '+') {
+      out += ' ';
+    } else if (s[i] == '%' && i + 2 < s.size() && hv(s[i + 1]) >= 0 && hv(s[i + 2]) >= 0) {
+      out += static_cast<char>(hv(s[i + 1]) * 16 + hv(s[i + 2]));
+      i += 2;
+    } else {
+      out += s[i];
+    }
+  }
+  return out;
+}
+
+struct Request {
+  std::string method, path;
+  std::map<std::string, std::string> query;
+  std::string auth;
+  std::string body;
+  bool close = false;
+};
+
+std::string q(const Request& r, const char* k, const char* dflt = "") {
+  auto it = r.query.find(k);
+  return it == r.query.end() ? std::string(dflt) : it->second;
+}
+
+// splits /api/v1/namespaces/{ns}/{plural}[/{name}] (and /apis/{g}/{v}/..., cluster-wide)
+bool route(const std::string& path, int& kind, std::string& ns, std::string& name) {
+  std::vector<std::string_view> seg;
+  std::string_view p(path);
+  size_t i = 0;
+  while (i < p.size()) {
+    while (i < p.size() && p[i] == '/') ++i;
+    size_t j = p.find('/', i);
+    if (j == std::string_view::npos) j = p.size();
+    if (j > i) seg.push_back(p.substr(i, j - i));
+    i = j;
+  }
+  size_t k;
+  if (seg.size() >= 2 && seg[0] == "api") k = 2;
+  else if (seg.size() >= 3 && seg[0] == "apis") k = 3;
+  else return false;
+  ns.clear();
+  name.clear();
+  if (seg.size() > k + 1 && seg[k] == "namespaces" && kind_by_plural(seg[k]) < 0) {
+    ns = std::string(seg[k + 1]);
+    k += 2;
+  }
+  if (seg.size() <= k) return false;
+  kind = kind_by_plural(seg[k]);
+  if (kind < 0) return false;
+  if (seg.size() == k + 2) name = std::string(seg[k + 1]);
+  else if (seg.size() > k + 2) return false;
+  return true;
+}
+
+void h_list(Conn& c, const Request& r, int kind, const std::string& ns) {
+  std::string cont = q(r, "continue");
+  long limit = atol(q(r, "limit", "0").c_str());
+  const Snapshot* snap = nullptr;
+  Snapshot fresh;
+  std::string sid;
+  size_t start = 0;
+  if (!cont.empty()) {
+    size_t colon = cont.find(':');
+    sid = cont.substr(0, colon);
+    auto it = g_snapshots.find(sid);
+    if (it == g_snapshots.end() || colon == std::string::npos) {
+      respond(c, 410, status_body(410, "Expired", "the provided continue parameter is too old"));
+      return;
+    }
+    snap = &it->second;
+    start = static_cast<size_t>(atol(cont.c_str() + colon + 1));
+  } else {
+    Selector sel;
+    parse_selector(q(r, "labelSelector"), false, sel);
+    parse_selector(q(r, "fieldSelector"), true, sel);
+    fresh.rv = g_rv;
+    for (auto& kv : g_store[kind].objs)
+      if ((ns.empty() || kv.second.ns == ns) && matches(*kv.second.attrs, sel)) fresh.items.push_back(kv.second.json);
+    snap = &fresh;
+  }
+  size_t end = snap->items.size();
+  std::string next;
+  if (limit > 0 && start + static_cast<size_t>(limit) < snap->items.size()) {
+    end = start + static_cast<size_t>(limit);
+    if (cont.empty()) {
+      sid = uuid4().substr(0, 12);
+      g_snapshots[sid] = std::move(fresh);
+      snap = &g_snapshots[sid];
+      g_snapshot_order.push_back(sid);
+      while (g_snapshot_order.size() > 64) {
+        g_snapshots.erase(g_snapshot_order.front());
+        g_snapshot_order.pop_front();
+      }
+    }
+    next = sid + ":" + std::to_string(end);
+  }
+  std::string body = "{\"kind\":\"";
+  body += KINDS[kind].kind;
+  body += "List\",\"apiVersion\":\"";
+  body += KINDS[kind].api_version;
+  body += "\",\"metadata\":{\"resourceVersion\":\"" + std::to_string(snap->rv) + "\"";
+  if (!next.empty()) body += ",\"continue\":\"" + next + "\"";
+  body += "},\"items\":[";
+  for (size_t i = start; i < end && i < snap->items.size(); ++i) {
+    if (i > start) body += ',';
+    body += *snap->items[i];
+  }
+  body += "]}";
+  respond(c, 200, body);
+}
+
+void h_watch(Conn& c, const Request& r, int kind, const std::string& ns) {
+  ++g_stats.watch_requests;
+  auto* w = new Watch{c.fd, kind, ns, {}, q(r, "allowWatchBookmarks") == "true" || q(r, "allowWatchBookmarks") == "1", 0, 0, {}};
+  parse_selector(q(r, "labelSelector"), false, w->sel);
+  parse_selector(q(r, "fieldSelector"), true, w->sel);
+  long timeout = atol(q(r, "timeoutSeconds", "0").c_str());
+  w->deadline_ms = mono_ms() + (timeout > 0 ? timeout : 1800) * 1000;
+  w->last_ms = mono_ms();
+  c.out += "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n";
+  c.watch = w;
+  KindStore& ks = g_store[kind];
+  std::string rv_s = q(r, "resourceVersion");
+  if (!rv_s.empty() && rv_s != "0") {
+    int64_t rv = atoll(rv_s.c_str());
+    if (rv < ks.compacted) {
+      std::string msg = "too old resource version: " + rv_s + " (" + std::to_string(ks.compacted) + ")";
+      w->pending = "{\"type\":\"ERROR\",\"object\":" + status_body(410, "Expired", msg) + "}\n";
+      ks.watchers.push_back(w);
+      end_watch(c, true);
+      return;
+    }
+    // history is in RV order: binary-search the first entry after rv
+    size_t lo = 0, hi = ks.history.size();
+    while (lo < hi) {
+      size_t mid = (lo + hi) / 2;
+      if (ks.history[mid].rv <= rv) lo = mid + 1;
+      else hi = mid;
+    }
+    for (size_t i = lo; i < ks.history.size(); ++i) {
+      const Hist& h = ks.history[i];
+      if ((ns.empty() || h.ns == ns) && matches(*h.attrs, w->sel)) w->pending += *h.line;
+    }
+  }
+  ks.watchers.push_back(w);
+  g_dirty.insert(&c);
+}
+
+void expire_kind(int kind) {
+  KindStore& ks = g_store[kind];
+  if (!ks.history.empty()) ks.compacted = ks.history.back().rv;
+  ks.history.clear();
+}
+
+void close_watches(int only_kind) {
+  std::vector<Conn*> cs;
+  for (auto& kv : g_conns)
+    if (kv.second->watch && (only_kind < 0 || kv.second->watch->kind == only_kind)) cs.push_back(kv.second.get());
+  for (Conn* c : cs) end_watch(*c, true);
+}
+
+void h_apply(Conn& c, const Request& r) {
+  int64_t t0 = mono_ns();
+  size_t pos = 0, n = 0;
+  const std::string& b = r.body;
+  while (pos < b.size()) {
+    size_t nl = b.find('\n', pos);
+    if (nl == std::string::npos) nl = b.size();
+    std::string_view line(b.data() + pos, nl - pos);
+    pos = nl + 1;
+    if (line.find_first_not_of(" \t\r") == std::string_view::npos) continue;
+    Value ev = kjson::parse(line);
+    std::string type(ev.path({"type"}));
+    Value* obj = ev.get("object");
+    if (!obj || obj->t != Value::OBJ) throw kjson::ParseError("event without object");
+    int kind = kind_by_name(obj->path({"kind"}));
+    if (kind < 0) throw kjson::ParseError("unknown kind");
+    if (type == "DELETED") {
+      remove(kind, std::string(obj->path({"metadata", "namespace"})), std::string(obj->path({"metadata", "name"})),
+             "Background");
+    } else if (type == "MODIFIED") {
+      if (update(kind, *obj, false, nullptr) == 1) create(kind, *obj, nullptr);
+    } else {
+      if (!create(kind, *obj, nullptr)) update(kind, *obj, false, nullptr);
+    }
+    ++n;
+  }
+  g_stats.applied += n;
+  if (q(r, "expire") == "1") {
+    // compaction that overtakes the watchers: undelivered lines are lost, resuming
+    // streams get 410 Gone and must re-list (exercises the informer's relist diff)
+    for (auto& kv : g_conns)
+      if (kv.second->watch) kv.second->watch->pending.clear();
+    for (int k = 0; k < NKINDS; ++k) expire_kind(k);
+    close_watches(-1);
+  }
+  char buf[160];
+  snprintf(buf, sizeof buf, "{\"applied\":%zu,\"rv\":%lld,\"t_push\":%.9f}", n, static_cast<long long>(g_rv),
+           static_cast<double>(t0) / 1e9);
+  respond(c, 200, buf);
+}
+
+void handle(Conn& c, Request& r) {
+  ++g_stats.requests;
+  c.close_after = r.close;
+  if (r.path.rfind("/sim/", 0) == 0) {
+    if (r.path == "/sim/apply" && r.method == "POST") return h_apply(c, r);
+    if (r.path == "/sim/stats") {
+      std::string s = "{\"requests\":" + std::to_string(g_stats.requests) +
+                      ",\"watch_requests\":" + std::to_string(g_stats.watch_requests) + ",\"rv\":" + std::to_string(g_rv) +
+                      ",\"deleted\":" + std::to_string(g_stats.deleted) + ",\"applied\":" + std::to_string(g_stats.applied) +
+                      ",\"objects\":{";
+      for (int k = 0; k < NKINDS; ++k) {
+        if (k) s += ',';
+        s += "\"" + std::string(KINDS[k].kind) + "\":" + std::to_string(g_store[k].objs.size());
+      }
+      s += "}}";
+      return respond(c, 200, s);
+    }
+    if (r.path == "/sim/expire" || r.path == "/sim/close-watches") {
+      std::string k = q(r, "kind");
+      int kind = k.empty() ? -1 : kind_by_name(k);
+      if (r.path == "/sim/expire")
+        for (int i = 0; i < NKINDS; ++i)
+          if (kind < 0 || kind == i) expire_kind(i);
+      close_watches(kind);
+      return respond(c, 200, "{}");
+    }
+    return respond(c, 404, status_body(404, "NotFound", "no such simulator endpoint"));
+  }
+  if (!g_opt.token.empty() && r.auth != "Bearer " + g_opt.token)
+    return respond(c, 401, status_body(401, "Unauthorized", "Unauthorized"));
+  int kind;
+  std::string ns, name;
+  if (!route(r.path, kind, ns, name)) return respond(c, 404, status_body(404, "NotFound", "the server could not find the requested resource"));
+  const char* kn = KINDS[kind].kind;
+  std::string lower(kn);
+  for (auto& ch : lower) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
+  if (r.method == "GET" && name.empty()) {
+    std::string wq = q(r, "watch");
+    if (wq == "1" || wq == "true") return h_watch(c, r, kind, ns);
+    return h_list(c, r, kind, ns);
+  }
+  if (r.method == "GET") {
+    auto it = g_store[kind].objs.find(okey(ns, name));
+    if (it == g_store[kind].objs.end()) return respond(c, 404, status_body(404, "NotFound", lower + "s \"" + name + "\" not found"));
+    return respond(c, 200, *it->second.json);
+  }
+  if (r.method == "DELETE" && !name.empty()) {
+    std::string prop = "Background";
+    if (!r.body.empty()) {
+      Value b = kjson::parse(r.body);
+      std::string p(b.path({"propagationPolicy"}));
+      if (!p.empty()) prop = p;
+    }
+    std::string qp = q(r, "propagationPolicy");
+    if (!qp.empty()) prop = qp;
+    if (!remove(kind, ns, name, prop))
+      return respond(c, 404, status_body(404, "NotFound", lower + "s" + (kind == K_JOB ? ".batch" : "") + " \"" + name + "\" not found"));
+    std::string s = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Success\",\"details\":{\"name\":";
+    kjson::escape(s, name);
+    s += ",\"kind\":\"" + lower + "s\"}}";
+    return respond(c, 200, s);
+  }
+  if (r.method == "POST" && name.empty()) {
+    Value doc = kjson::parse(r.body);
+    doc.at("kind") = Value::str(kn);
+    doc.at("metadata").at("namespace") = Value::str(ns);
+    std::string out;
+    if (!create(kind, doc, &out))
+      return respond(c, 409, status_body(409, "AlreadyExists", lower + "s \"" + std::string(doc.path({"metadata", "name"})) + "\" already exists"));
+    return respond(c, 201, out);
+  }
+  if (r.method == "PUT" && !name.empty()) {
+    Value doc = kjson::parse(r.body);
+    doc.at("kind") = Value::str(kn);
+    Value& md = doc.at("metadata");
+    md.at("namespace") = Value::str(ns);
+    md.at("name") = Value::str(name);
+    std::string out;
+    int rc = update(kind, doc, true, &out);
+    if (rc == 1) return respond(c, 404, status_body(404, "NotFound", "not found"));
+    if (rc == 2) return respond(c, 409, status_body(409, "Conflict", "the object has been modified; please apply your changes to the latest version"));
+    return respond(c, 200, out);
+  }
+  if (r.method == "PATCH" && !name.empty()) {
+    auto it = g_store[kind].objs.find(okey(ns, name));
+    if (it == g_store[kind].objs.end()) return respond(c, 404, status_body(404, "NotFound", "not found"));
+    Value cur = kjson::parse(*it->second.json);
+    kjson::merge_patch(cur, kjson::parse(r.body));
+    cur.at("metadata").erase("resourceVersion");
+    std::string out;
+    update(kind, cur, false, &out);
+    return respond(c, 200, out);
+  }
+  respond(c, 405, status_body(405, "MethodNotAllowed", "method not allowed"));
+}
+
+// parses as many complete requests as the buffer holds; false = protocol error (close)
+bool on_input(Conn& c) {
+  while (!c.watch) {
+    size_t he = c.in.find("\r\n\r\n");
+    if (he == std::string::npos) return c.in.size() < (1u << 20);
+    Request r;
+    std::string_view head(c.in.data(), he);
+    size_t le = head.find("\r\n");
+    std::string_view rl = head.substr(0, le);
+    size_t s1 = rl.find(' '), s2 = rl.rfind(' ');
+    if (s1 == std::string_view::npos || s2 <= s1) return false;
+    r.method = std::string(rl.substr(0, s1));
+    std::string_view target = rl.substr(s1 + 1, s2 - s1 - 1);
+    std::string_view version = rl.substr(s2 + 1);
+    size_t qm = target.find('?');
+    r.path = pct_decode(target.substr(0, qm));
+    if (qm != std::string_view::npos) {
+      std::string_view qs = target.substr(qm + 1);
+      size_t p = 0;
+      while (p <= qs.size()) {
+        size_t amp = qs.find('&', p);
+        if (amp == std::string_view::npos) amp = qs.size();
+        std::string_view kv = qs.substr(p, amp - p);
+        size_t eq = kv.find('=');
+        if (!kv.empty()) r.query[pct_decode(kv.substr(0, eq))] = eq == std::string_view::npos ? "" : pct_decode(kv.substr(eq + 1));
+        p = amp + 1;
+      }
+    }
+    size_t clen = 0;
+    bool chunked = false;
+    r.close = version == "HTTP/1.0";
+    size_t pos = le == std::string_view::npos ? head.size() : le + 2;
+    while (pos < head.size()) {
+      size_t e = head.find("\r\n", pos);
+      if (e == std::string_view::npos) e = head.size();
+      std::string_view line = head.substr(pos, e - pos);
+      pos = e + 2;
+      size_t colon = line.find(':');
+      if (colon == std::string_view::npos) continue;
+      std::string name(line.substr(0, colon));
+      for (auto& ch : name) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
+      std::string val = trim(line.substr(colon + 1));
+      if (name == "content-length") clen = static_cast<size_t>(atol(val.c_str()));
+      else if (name == "authorization") r.auth = val;
+      else if (name == "transfer-encoding" && val.find("chunked") != std::string::npos) chunked = true;
+      else if (name == "connection") {
+        std::string v = val;
+        for (auto& ch : v) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
+        if (v == "close") r.close = true;
+        else if (v == "keep-alive") r.close = false;
+      }
+    }
+    if (chunked) {
+      c.close_after = true;
+      respond(c, 411, status_body(411, "LengthRequired", "chunked request bodies are not supported"));
+      c.in.clear();
+      return true;
+    }
+    if (c.in.size() < he + 4 + clen) return true;  // body incomplete
+    r.body = c.in.substr(he + 4, clen);
+    c.in.erase(0, he + 4 + clen);
+    try {
+      handle(c, r);
+    } catch (const std::exception& e) {
+      respond(c, 400, status_body(400, "BadRequest", e.what()));
+    }
+    if (c.close_after) return true;
+  }
+  return true;
+}
+
+volatile sig_atomic_t g_stop = 0;
+void on_signal(int) { g_stop = 1; }
+
+void usage() {
+  fprintf(stderr,
+          "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        usage();
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--host") g_opt.host = next();
+    else if (a == "--port") g_opt.port = atoi(next().c_str());
+    else if (a == "--ready-file") g_opt.ready_file = next();
+    else if (a == "--history") g_opt.history = static_cast<size_t>(atol(next().c_str()));
+    else if (a == "--bookmark-ms") g_opt.bookmark_ms = atol(next().c_str());
+    else if (a == "--token") g_opt.token = next();
+    else {
+      usage();
+      return 2;
+    }
+  }
+  signal(SIGPIPE, SIG_IGN);
+  signal(SIGTERM, on_signal);
+  signal(SIGINT, on_signal);
+
+  int lfd = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(static_cast<uint16_t>(g_opt.port));
+  if (inet_pton(AF_INET, g_opt.host.c_str(), &addr.sin_addr) != 1) {
+    fprintf(stderr, "bad --host %s\n", g_opt.host.c_str());
+    return 2;
+  }
+  if (bind(lfd, reinterpret_cast<sockaddr*>(&addr), sizeof addr) < 0 || listen(lfd, 1024) < 0) {
+    perror("bind/listen");
+    return 1;
+  }
+  socklen_t alen = sizeof addr;
+  getsockname(lfd, reinterpret_cast<sockaddr*>(&addr), &alen);
+  int port = ntohs(addr.sin_port);
+  set_nonblock(lfd);
+  g_ep = epoll_create1(0);
+  epoll_event lev{};
+  lev.events = EPOLLIN;
+  lev.data.fd = lfd;
+  epoll_ctl(g_ep, EPOLL_CTL_ADD, lfd, &lev);
+
+  char info[160];
+  snprintf(info, sizeof info, "{\"port\":%d,\"pid\":%d,\"url\":\"http://%s:%d\"}\n", port, getpid(), g_opt.host.c_str(), port);
+  if (!g_opt.ready_file.empty()) {
+    std::string tmp = g_opt.ready_file + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (!f) {
+      perror("ready-file");
+      return 1;
+    }
+    fputs(info, f);
+    fclose(f);
+    rename(tmp.c_str(), g_opt.ready_file.c_str());
+  }
+  fputs(info, stdout);
+  fflush(stdout);
+
+  std::vector<epoll_event> evs(512);
+  int64_t last_tick = mono_ms();
+  char buf[1 << 16];
+  while (!g_stop) {
+    int n = epoll_wait(g_ep, evs.data(), static_cast<int>(evs.size()), 100);
+    if (n < 0 && errno != EINTR) {
+      perror("epoll_wait");
+      break;
+    }
+    for (int i = 0; i < n; ++i) {
+      int fd = evs[i].data.fd;
+      if (fd == lfd) {
+        while (true) {
+          int cfd = accept(lfd, nullptr, nullptr);
+          if (cfd < 0) break;
+          set_nonblock(cfd);
+          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          auto c = std::make_unique<Conn>();
+          c->fd = cfd;
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.fd = cfd;
+          epoll_ctl(g_ep, EPOLL_CTL_ADD, cfd, &ev);
+          g_conns[cfd] = std::move(c);
+        }
+        continue;
+      }
+      auto it = g_conns.find(fd);
+      if (it == g_conns.end()) continue;
+      Conn& c = *it->second;
+      bool dead = false;
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+        while (true) {
+          ssize_t r = recv(fd, buf, sizeof buf, 0);
+          if (r > 0) {
+            c.in.append(buf, static_cast<size_t>(r));
+            continue;
+          }
+          if (r == 0) dead = true;
+          else if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) dead = true;
+          break;
+        }
+        if (!dead && !on_input(c)) dead = true;
+      }
+      if (dead) {
+        close_conn(fd);
+        continue;
+      }
+      if (evs[i].events & EPOLLOUT) g_dirty.insert(&c);
+    }
+    int64_t now = mono_ms();
+    if (now - last_tick >= 50) {
+      last_tick = now;
+      std::vector<Conn*> ended;
+      for (auto& kv : g_conns) {
+        Watch* w = kv.second->watch;
+        if (!w) continue;
+        if (now >= w->deadline_ms) {
+          ended.push_back(kv.second.get());
+        } else if (w->bookmarks && w->pending.empty() && now - w->last_ms >= g_opt.bookmark_ms) {
+          w->pending = std::string("{\"type\":\"BOOKMARK\",\"object\":{\"kind\":\"") + KINDS[w->kind].kind +
+                       "\",\"apiVersion\":\"" + KINDS[w->kind].api_version + "\",\"metadata\":{\"resourceVersion\":\"" +
+                       std::to_string(g_rv) + "\"}}}\n";
+          g_dirty.insert(kv.second.get());
+        }
+      }
+      for (Conn* c : ended) end_watch(*c, true);
+    }
+    if (!g_dirty.empty()) {
+      std::vector<Conn*> dirty(g_dirty.begin(), g_dirty.end());
+      g_dirty.clear();
+      for (Conn* c : dirty)
+        if (!flush(*c)) close_conn(c->fd);
+    }
+  }
+  for (auto& kv : g_conns) close(kv.first);
+  close(lfd);
+  return 0;
+}

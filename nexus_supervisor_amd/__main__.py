@@ -2,6 +2,8 @@
 
 ``supervisor``  the cluster supervisor (default; reference ``main.go``)
 ``agent``       the per-node GPU attribution agent (needs ``NODE_NAME``)
+``worker``      one shard-worker process (spawned by the supervisor when
+                ``runtime.worker-processes`` > 1; not started by hand)
 ``config``      print the effective configuration (secrets masked)
 ``build``       build the native components in-tree
 ``cqlsrv``      run the native in-memory CQL server (tests / local runs)
@@ -22,6 +24,10 @@ def main(argv=None) -> int:
         from .app import main as run
 
         return run(argv)
+    if cmd == "worker":
+        from .parallel.workers import worker_main
+
+        return worker_main()
     if cmd == "agent":
         import asyncio
 

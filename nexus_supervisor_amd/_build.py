@@ -7,6 +7,7 @@ artefact               sources                                 toolchain
 ``_cql_native``        ``csrc/cql/cql_native.cpp`` (+ proto)   g++ + pybind11
 ``_amdsmi_monitor``    ``csrc/amdsmi/gpu_monitor.cpp``         g++ + libamd_smi
 ``bin/nexus-cqlsrv``   ``csrc/cqlsrv/*.cpp`` (+ proto)         g++ (epoll)
+``bin/nexus-kubesim``  ``csrc/kubesim/*.cpp`` (+ json.hpp)     g++ (epoll)
 ``bin/gpu_stress``     ``csrc/stress/gpu_stress.hip``          hipcc gfx950
 =====================  ======================================  ==================
 
@@ -74,6 +75,12 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
             "deps": [proto],
             "cmd": lambda out, srcs: [_cxx(), *common, *san, "-pthread", f"-I{os.path.join(CSRC, 'cql')}", *srcs, "-o", out],
         },
+        "kubesim": {
+            "out": os.path.join(BIN, "nexus-kubesim" + (f"-{sanitize}" if sanitize else "")),
+            "srcs": [os.path.join(CSRC, "kubesim", "kubesim.cpp")],
+            "deps": [os.path.join(CSRC, "kubesim", "json.hpp")],
+            "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, *srcs, "-o", out],
+        },
         "gpu_stress": {
             "out": os.path.join(BIN, "gpu_stress"),
             "srcs": [os.path.join(CSRC, "stress", "gpu_stress.hip")],
@@ -117,7 +124,7 @@ def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optio
     ts = targets(sanitize)
     names = [n for n in ts if not only or n in only]
     if sanitize:
-        names = [n for n in names if n == "cqlsrv"]
+        names = [n for n in names if n in ("cqlsrv", "kubesim")]
     with cf.ThreadPoolExecutor(max_workers=min(4, len(names) or 1)) as ex:
         futs = {ex.submit(build_one, n, ts[n], force, verbose): n for n in names}
         return [f.result() for f in cf.as_completed(futs)]
@@ -126,7 +133,7 @@ def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optio
 def binary(name: str) -> str:
     """Path of a built helper binary, building it on demand."""
     ts = targets()
-    key = {"nexus-cqlsrv": "cqlsrv", "gpu_stress": "gpu_stress"}[name]
+    key = {"nexus-cqlsrv": "cqlsrv", "gpu_stress": "gpu_stress", "nexus-kubesim": "kubesim"}[name]
     t = ts[key]
     if _stale(t):
         build_one(key, t)

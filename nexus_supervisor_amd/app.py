@@ -111,6 +111,9 @@ class Application:
     def ready(self) -> bool:
         return self.factory is not None and all(i.has_synced() for i in self.factory.informers.values())
 
+    async def wait_for_cache_sync(self, timeout: Optional[float] = None) -> bool:
+        return await self.factory.wait_for_cache_sync(timeout)
+
     async def stop(self, drain_timeout: float = 10.0) -> None:
         if self.elector is not None:
             await self.elector.stop(release=True)
@@ -131,6 +134,110 @@ class Application:
         await self.stop()
 
 
+class _SupervisorFacade:
+    """What in-process callers (bench, tests) use of a supervisor, backed by worker processes."""
+
+    def __init__(self, app: "ShardedApplication"):
+        self._app = app
+        self.namespace = app.cfg.resource_namespace
+        self.decision_hooks = app.pool.decision_hooks
+        self.classifier = type("RemoteClassifier", (), {"evidence_provider": None})()
+
+    @property
+    def active(self) -> bool:
+        return self._app.pool.active
+
+    def set_active(self, active: bool) -> None:
+        self._app.pool.set_active(active)
+
+    @property
+    def metrics(self) -> Metrics:
+        return self._app.merged_metrics
+
+
+class ShardedApplication:
+    """A replica of ``runtime.worker-processes`` shard-worker processes
+    (:mod:`.parallel.workers`): this process holds the lease, relays active/standby,
+    serves the merged ``/metrics`` and supervises the workers."""
+
+    def __init__(self, cfg: SupervisorConfig, *, kube=None, logger: Optional[KLogger] = None,
+                 metrics: Optional[Metrics] = None, report_decisions: bool = False, log_dir: str = ""):
+        from .parallel.workers import WorkerPool
+
+        self.cfg = cfg
+        self.log = logger or KLogger()
+        self.metrics = metrics or Metrics(cfg.observability.statsd_name, {"version": __version__})
+        self.kube = kube
+        self.pool = WorkerPool(cfg, report_decisions=report_decisions, log_dir=log_dir)
+        self.supervisor = _SupervisorFacade(self)
+        self.merged_metrics = self.metrics
+        self.store = None
+        self.elector = None
+        self.http = None
+        self._stopped = asyncio.Event()
+
+    async def start(self) -> None:
+        cfg = self.cfg
+        self.log.info("Starting Nexus Supervisor", version=__version__, namespace=cfg.resource_namespace,
+                      store=cfg.cql_store_type, worker_processes=self.pool.count)
+        le = cfg.leader_election
+        await self.pool.start(active=not le.enabled)
+        if cfg.observability.http_port:
+            from .obs.http import ObsServer
+
+            self.http = ObsServer(self)
+            await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
+        if le.enabled:
+            from .ha.leader import LeaderElector, LeaseLock
+
+            if self.kube is None:
+                from .kube.client import KubeClient, KubeConfig
+
+                self.kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+            identity = le.identity or os.environ.get("POD_NAME") or f"{socket.gethostname()}-{os.getpid()}"
+            self.elector = LeaderElector(
+                LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, identity),
+                lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
+                on_started_leading=lambda: self.pool.set_active(True),
+                on_stopped_leading=lambda: self.pool.set_active(False), metrics=self.metrics)
+            self.elector.start()
+
+    def ready(self) -> bool:
+        return self.pool.all_synced()
+
+    async def wait_for_cache_sync(self, timeout: Optional[float] = None) -> bool:
+        return await self.pool.wait_synced(timeout)
+
+    async def refresh_metrics(self) -> Metrics:
+        await self.pool.refresh_metrics()
+        self.merged_metrics = self.pool.merged_metrics(self.metrics)
+        return self.merged_metrics
+
+    async def stop(self, drain_timeout: float = 10.0) -> None:
+        if self.elector is not None:
+            await self.elector.stop(release=True)
+        await self.pool.stop(drain_timeout)
+        self.merged_metrics = self.pool.merged_metrics(self.metrics)
+        if self.http is not None:
+            await self.http.stop()
+        if self.kube is not None:
+            await self.kube.close()
+        self._stopped.set()
+
+    async def run(self, stop: asyncio.Event) -> None:
+        await self.start()
+        await stop.wait()
+        self.log.info("shutting down: draining worker processes")
+        await self.stop()
+
+
+def make_application(cfg: SupervisorConfig, **kw):
+    """``Application`` or, with ``runtime.worker-processes`` > 1, ``ShardedApplication``."""
+    if cfg.runtime.worker_processes > 1:
+        return ShardedApplication(cfg, logger=kw.get("logger"), metrics=kw.get("metrics"), kube=kw.get("kube"))
+    return Application(cfg, **kw)
+
+
 def main(argv=None) -> int:
     """Process entry (``/root/reference/main.go:12-43``)."""
     cfg = load_config()
@@ -145,7 +252,7 @@ def main(argv=None) -> int:
         for sig in (signal.SIGTERM, signal.SIGINT):
             loop.add_signal_handler(sig, stop.set)
         try:
-            app = Application(cfg, logger=log, metrics=metrics)
+            app = make_application(cfg, logger=log, metrics=metrics)
         except Exception as exc:  # noqa: BLE001 - fatal init (klog.FlushAndExit analog)
             log.error(exc, "failed to initialise application services")
             return 1

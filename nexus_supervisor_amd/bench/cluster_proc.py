@@ -1,7 +1,8 @@
 """Synthetic cluster process for the wire-mode benchmark.
 
 Runs, in its own process (so its CPU does not count against the supervisor's
-event loop): the fake kube-apiserver, the :class:`~.workload.Workload`
+event loop): the kube-apiserver (the native ``nexus-kubesim`` child by default,
+``--api python`` for the Python fake), the :class:`~.workload.Workload`
 generator, and the "receiver" role that inserts each new run's checkpoint row
 into the CQL store before the run's pods exist (what nexus's receiver does
 upstream of the supervisor).  A small control API drives it:
@@ -30,7 +31,33 @@ async def amain(args) -> None:
     from ..testing.fake_apiserver import FakeApiServer
     from .workload import DEFAULT_HIP_OOM, Workload
 
-    api = FakeApiServer(history=args.history, bookmark_interval=2.0)
+    sim = simctl = api = None
+    if args.api == "kubesim":
+        # native apiserver simulator: the generator below only produces traffic
+        from ..testing.kubesim import KubeSim, SimControl
+
+        sim = KubeSim(host=args.host, port=args.port, history=args.history, bookmark_ms=2000).start()
+        simctl = SimControl(sim.url)
+    else:
+        api = FakeApiServer(history=args.history, bookmark_interval=2.0)
+
+    async def apply(events):
+        """Commit watch traffic to the API server; returns the commit (push) time."""
+        if simctl is not None:
+            t = None
+            for i in range(0, len(events), 4096):
+                doc = await simctl.apply(events[i:i + 4096])
+                t = doc["t_push"] if t is None else t
+            return t if t is not None else time.monotonic()
+        t = time.monotonic()
+        for i, (etype, obj) in enumerate(events):
+            if etype == "ADDED":
+                api.create(obj, copy_obj=False)
+            else:
+                api.update(obj, copy_obj=False)
+            if i % 256 == 255:
+                await asyncio.sleep(0)  # keep serving DELETEs / watch writes during a burst
+        return t
     host, _, port = args.cql.partition(":")
     store = CqlCheckpointStore(CqlSession([(host, int(port))], connections_per_host=2, consistency="ONE"), consistency="ONE")
     await store.connect()
@@ -48,15 +75,14 @@ async def amain(args) -> None:
                       shard_index=p.get("shard_index", 0))
         objs, rows = wl.initial()
         await write_rows(rows)
-        for o in objs:
-            api.create(o)
+        await apply([("ADDED", o) for o in objs])
         state["wl"] = wl
         # the simulated cluster holds the same 10k-run heap as the supervisor: keep it out
         # of full collections so the generator never paces the measured process
         gc.collect()
         gc.freeze()
         gc.set_threshold(20000, 20, 20)
-        return web.json_response({"objects": len(objs), "rows": len(rows), "rv": api.rv})
+        return web.json_response({"objects": len(objs), "rows": len(rows)})
 
     async def prepare(events: int):
         # generate the next step's traffic and insert its replacement runs' rows ahead of
@@ -81,26 +107,19 @@ async def amain(args) -> None:
                 # a prefetched step of another size is dropped: its replacement runs are
                 # already live in the workload, so they must exist in the cluster too
                 _f, stale = await nxt[1]
-                for etype, obj in stale:
-                    if etype == "ADDED" and obj.get("kind") in ("Pod", "Job"):
-                        api.create(obj, copy_obj=False)
+                await apply([(e, o) for e, o in stale if e == "ADDED" and o.get("kind") in ("Pod", "Job")])
             failed, traffic = await prepare(events)
-        t_push = time.monotonic()
-        for i, (etype, obj) in enumerate(traffic):
-            if etype == "ADDED":
-                api.create(obj, copy_obj=False)
-            else:
-                api.update(obj, copy_obj=False)
-            if i % 256 == 255:
-                await asyncio.sleep(0)  # keep serving DELETEs / watch writes during a burst
+        t_push = await apply(traffic)
         state["next"] = (events, asyncio.ensure_future(prepare(events)))
         return web.json_response({"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}})
 
     async def h_stats(req):
+        if simctl is not None:
+            return web.json_response(await simctl.stats())
         return web.json_response({"requests": api.requests, "watch_requests": api.watch_requests, "rv": api.rv,
                                   "deleted": len(api.deleted)})
 
-    url = await api.start(args.host, args.port)
+    url = sim.url if sim is not None else await api.start(args.host, args.port)
     # control routes live on a second tiny app (the apiserver app is frozen once started)
     ctl = web.Application(client_max_size=64 << 20)
     ctl.router.add_post("/bench/init", h_init)
@@ -113,7 +132,8 @@ async def amain(args) -> None:
     ctl_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
     tmp = args.ready_file + ".tmp"
     with open(tmp, "w") as f:
-        json.dump({"api": url, "ctl": f"http://{args.host}:{ctl_port}", "pid": os.getpid()}, f)
+        json.dump({"api": url, "ctl": f"http://{args.host}:{ctl_port}", "pid": os.getpid(),
+                   "sim_pid": sim.proc.pid if sim is not None else None}, f)
     os.replace(tmp, args.ready_file)
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
@@ -145,7 +165,12 @@ async def amain(args) -> None:
         with open(os.environ["NEXUS_CLUSTER_CPROFILE"], "w") as f:
             f.write(buf.getvalue())
     await runner.cleanup()
-    await api.stop()
+    if api is not None:
+        await api.stop()
+    if simctl is not None:
+        await simctl.close()
+    if sim is not None:
+        sim.stop()
     await store.close()
 
 
@@ -156,6 +181,8 @@ def main(argv=None) -> int:
     ap.add_argument("--cql", required=True)
     ap.add_argument("--ready-file", required=True)
     ap.add_argument("--history", type=int, default=400_000)
+    ap.add_argument("--api", choices=("kubesim", "python"), default="kubesim",
+                    help="native apiserver simulator (default) or the Python fake")
     args = ap.parse_args(argv)
     asyncio.run(amain(args))
     return 0

@@ -41,6 +41,7 @@ class BenchConfig:
     inflight: int = 2
     probe_events: int = 60
     probe_rate_per_min: float = 1000.0
+    procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -214,6 +215,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         x1 = harness.external_cpu()
         for k in x1:
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
+        workers = [v for k, v in cpu.items() if k.startswith("worker")]
+        if workers:
+            cpu["workers_util_sum"] = round(sum(workers), 3)
         if sampler is not None:
             prof = sampler.stop()
             sampler = None
@@ -221,6 +225,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
                 f.write(prof.encode_gz())
             with open(cfg.pprof_out + ".top.txt", "w") as f:
                 f.write(prof.top(40))
+        sync = getattr(harness, "sync_metrics", None)
+        if sync is not None:
+            await sync()
         stages = _stage_breakdown(sup)
         probe = None
         if cfg.probe_events > 0:

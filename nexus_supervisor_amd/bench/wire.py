@@ -19,7 +19,7 @@ from typing import List, Tuple
 
 import aiohttp
 
-from ..app import Application
+from ..app import Application, ShardedApplication
 from ..config.schema import SupervisorConfig
 from ..kube.client import KubeClient, KubeConfig
 from ..models.checkpoint import create_index_cql, create_table_cql
@@ -63,6 +63,7 @@ class WireHarness:
         with open(ready) as f:
             info = json.load(f)
         self.ctl = info["ctl"]
+        self.sim_pid = info.get("sim_pid")
         self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=600))
         async with self.http.post(self.ctl + "/bench/init", json={
                 "jobs": self.cfg.jobs, "seed": self.cfg.seed, "rank": self.cfg.rank, "world": self.cfg.world,
@@ -74,12 +75,26 @@ class WireHarness:
         sc.cql_store_type = "scylla"
         sc.scylla_cql_store.hosts = [f"127.0.0.1:{self.cql.port}"]
         sc.scylla_cql_store.consistency = "LOCAL_QUORUM"
-        kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)
-        store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql.port)],
-                                              connections_per_host=sc.scylla_cql_store.connections_per_host))
-        self.app = Application(sc, kube=kube, store=store)
+        if self.cfg.procs > 1:
+            # process-per-core replica: the workers build their own clients from the config
+            kcfg = os.path.join(self.workdir, "kubeconfig.yaml")
+            with open(kcfg, "w") as f:
+                json.dump({"apiVersion": "v1", "kind": "Config", "current-context": "bench",
+                           "clusters": [{"name": "bench", "cluster": {"server": info["api"]}}],
+                           "contexts": [{"name": "bench", "context": {"cluster": "bench", "user": "bench"}}],
+                           "users": [{"name": "bench", "user": {}}]}, f)
+            sc.kube_config_path = kcfg
+            sc.runtime.worker_processes = self.cfg.procs
+            sc.gpu.local_telemetry = True
+            sc.gpu.backend = self.cfg.telemetry
+            self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir)
+        else:
+            kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)
+            store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql.port)],
+                                                  connections_per_host=sc.scylla_cql_store.connections_per_host))
+            self.app = Application(sc, kube=kube, store=store)
         await self.app.start()
-        ok = await self.app.factory.wait_for_cache_sync(120)
+        ok = await self.app.wait_for_cache_sync(120)
         if not ok:
             raise RuntimeError("informer caches did not sync")
 
@@ -93,10 +108,21 @@ class WireHarness:
             doc = await r.json()
         return doc["rids"], doc["t_push"]
 
+    async def sync_metrics(self) -> None:
+        refresh = getattr(self.app, "refresh_metrics", None)
+        if refresh is not None:
+            await refresh()
+
     def external_cpu(self):
         """CPU seconds used so far by the harness processes (utilisation diagnostics)."""
         out = {}
-        for name, proc in (("cluster", self.proc), ("cqlsrv", self.cql.proc if self.cql else None)):
+        procs = [("cluster", self.proc), ("cqlsrv", self.cql.proc if self.cql else None)]
+        if getattr(self, "sim_pid", None):
+            procs.append(("kubesim", type("P", (), {"pid": self.sim_pid})()))
+        pool = getattr(self.app, "pool", None)
+        if pool is not None:
+            procs += [(f"worker{w.index}", w.proc) for w in pool.workers]
+        for name, proc in procs:
             try:
                 with open(f"/proc/{proc.pid}/stat") as f:
                     parts = f.read().rsplit(")", 1)[1].split()

@@ -165,6 +165,22 @@ def iter_keys(cls=SupervisorConfig, path=()):
             yield fpath, env_name(fpath), sub, f
 
 
+def to_mapping(cfg) -> Dict[str, Any]:
+    """Config as a kebab-keyed dict, secrets included (hand-off to worker processes)."""
+    out: Dict[str, Any] = {}
+    for f in dataclasses.fields(cfg):
+        v = getattr(cfg, f.name)
+        out[f.metadata["key"]] = to_mapping(v) if dataclasses.is_dataclass(v) else (list(v) if isinstance(v, list) else v)
+    return out
+
+
+def from_mapping(data: Mapping[str, Any], do_validate: bool = True) -> SupervisorConfig:
+    """Inverse of :func:`to_mapping` (no files, no environment)."""
+    cfg = SupervisorConfig()
+    _apply(cfg, data, {})
+    return validate(cfg) if do_validate else cfg
+
+
 def redacted(cfg) -> Dict[str, Any]:
     """Config as a kebab-keyed dict with secrets masked (for the startup log line)."""
     out: Dict[str, Any] = {}

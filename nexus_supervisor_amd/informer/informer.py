@@ -75,6 +75,11 @@ class SharedInformer:
         self.relists = 0
         self.watch_events = 0
         self.last_receive = 0.0
+        # ingest filter (shard workers): ``accept(obj, etype)`` false → the object is neither
+        # cached nor dispatched; ``on_reject(obj)`` is told about it instead
+        self.accept: Optional[Callable[[Dict[str, Any], str], bool]] = None
+        self.on_reject: Optional[Callable[[Dict[str, Any]], None]] = None
+        self.rejected = 0
 
     # ------------------------------------------------------------------ API
     def add_event_handler(self, on_add=None, on_update=None, on_delete=None) -> Handler:
@@ -170,6 +175,9 @@ class SharedInformer:
         rv = kube.resource_version(obj)
         if rv:
             self._rv = rv
+        if self.accept is not None and not self.accept(obj, etype):
+            self._reject(obj)
+            return
         if etype == DELETED:
             old = self.indexer.delete(obj)
             self._dispatch_delete(old or obj)
@@ -180,8 +188,24 @@ class SharedInformer:
         else:
             self._dispatch_update(old, obj)
 
+    def _reject(self, obj) -> None:
+        self.rejected += 1
+        if self.on_reject is not None:
+            try:
+                self.on_reject(obj)
+            except Exception:
+                log.exception("%s reject handler failed", self.kind)
+
     def _relist_apply(self, items: List[Dict[str, Any]]) -> None:
         objs = [self.transform(o) if self.transform else o for o in items]
+        if self.accept is not None:
+            kept = []
+            for o in objs:
+                if self.accept(o, ADDED):
+                    kept.append(o)
+                else:
+                    self._reject(o)
+            objs = kept
         old = self.indexer.replace(objs)
         for o in objs:
             k = kube.object_key(o)

@@ -327,8 +327,10 @@ class KubeClient:
                 return items, rv
 
     async def watch(self, kind: str, namespace: Optional[str], resource_version: str, *, label_selector: str = "",
-                    field_selector: str = "", timeout_seconds: int = 300,
-                    projected: bool = False) -> AsyncIterator[Tuple[str, Dict[str, Any]]]:
+                    field_selector: str = "", timeout_seconds: int = 300, projected: bool = False,
+                    router=None) -> AsyncIterator[Tuple[str, Dict[str, Any]]]:
+        """Watch stream as ``(type, object)``.  ``router`` = ``(ShardRouter, role)`` drops
+        lines another shard worker owns before they are decoded (native decoder only)."""
         s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "allowWatchBookmarks": "true",
                   "timeoutSeconds": str(timeout_seconds)}
@@ -350,6 +352,8 @@ class KubeClient:
                     return
                 raise from_status(r.status, doc)
             decoder = _decoder(watch_projection(kind)) if projected else None
+            if decoder is not None and router is not None:
+                decoder.set_router(*router)
             if decoder is not None:
                 n = 0
                 async for chunk in r.content.iter_any():
@@ -459,6 +463,7 @@ class KubeListWatch(ListWatch):
         self.projected = projected and _native_decoder_available() and kind in PROJECTIONS
         if self.projected:
             self.transform = FINISHERS.get(kind)
+        self.shard_router = None  # (native ShardRouter, role) when this replica is split into workers
 
     async def list(self):
         return await self.client.list(self.kind, self.namespace, label_selector=self.label_selector,
@@ -467,4 +472,4 @@ class KubeListWatch(ListWatch):
     def watch(self, resource_version: str):
         return self.client.watch(self.kind, self.namespace, resource_version, label_selector=self.label_selector,
                                  field_selector=self.field_selector, timeout_seconds=self.watch_timeout,
-                                 projected=self.projected)
+                                 projected=self.projected, router=self.shard_router if self.projected else None)

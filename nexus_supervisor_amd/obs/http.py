@@ -26,25 +26,29 @@ class ObsServer:
         self.port = 0
         self._loop_thread = threading.get_ident()
 
-    def _gauges(self) -> None:
-        sup = self.app.supervisor
-        m = self.app.metrics
-        if sup.pipeline is not None:
-            m.set("queue_depth", sup.pipeline.depth())
-            m.set("in_flight", sup.pipeline.in_flight())
-            for k, v in sup.pipeline.stats.as_dict().items():
-                m.set(f"pipeline_{k}", v)
-        for kind, inf in sup.factory.informers.items():
-            m.set("informer_objects", len(inf.indexer), {"kind": kind})
-            m.set("informer_relists", inf.relists, {"kind": kind})
-        m.set("active", 1.0 if sup.active else 0.0)
+    async def _metrics(self):
+        pool = getattr(self.app, "pool", None)
+        if pool is not None:  # process-per-core replica: merge the shard workers' registries
+            await pool.refresh_metrics(2.0)
+            m = pool.merged_metrics(self.app.metrics)
+            m.set("active", 1.0 if pool.active else 0.0)
+            m.set("worker_processes_alive", sum(1 for w in pool.workers if w.proc is not None and w.proc.poll() is None))
+            return m
+        from ..parallel.workers import collect_gauges
+
+        collect_gauges(self.app.supervisor, self.app.metrics)
+        return self.app.metrics
 
     async def h_metrics(self, req):
-        self._gauges()
-        return web.Response(text=self.app.metrics.prometheus_text(), content_type="text/plain", charset="utf-8",
+        m = await self._metrics()
+        return web.Response(text=m.prometheus_text(), content_type="text/plain", charset="utf-8",
                             headers={"X-Content-Type-Options": "nosniff"})
 
     async def h_healthz(self, req):
+        pool = getattr(self.app, "pool", None)
+        if pool is not None:
+            ok = pool.alive()
+            return web.Response(status=200 if ok else 503, text="ok" if ok else "worker process exited")
         sup = self.app.supervisor
         ok = sup.pipeline is not None and any(not t.done() for t in sup.pipeline._tasks)  # noqa: SLF001
         return web.Response(status=200 if ok else 503, text="ok" if ok else "workers stopped")
@@ -72,6 +76,17 @@ class ObsServer:
         return web.Response(text=s.profile.top(int(req.query.get("n", "30"))))
 
     async def h_vars(self, req):
+        pool = getattr(self.app, "pool", None)
+        if pool is not None:
+            m = await self._metrics()
+            doc = {"active": pool.active, "worker_processes": pool.count, "restarts": pool.restarts,
+                   "workers": [{"index": w.index, "pid": w.proc.pid if w.proc else None, "synced": w.synced.is_set(),
+                                "alive": w.proc is not None and w.proc.poll() is None} for w in pool.workers],
+                   "metrics": m.snapshot()}
+            if self.app.elector is not None:
+                doc["leader"] = {"identity": self.app.elector.identity, "leader": self.app.elector.leader,
+                                 "observed_holder": self.app.elector.observed_holder}
+            return web.json_response(doc, dumps=lambda o: __import__("json").dumps(o, default=str))
         sup = self.app.supervisor
         doc = {"active": sup.active, "namespace": sup.namespace,
                "pipeline": sup.pipeline.stats.as_dict() if sup.pipeline else {},

@@ -131,6 +131,13 @@ class Supervisor:
         self.active = not cfg.leader_election.enabled  # leader gating flips this
         self._unfinished_cache: Optional[Tuple[str, ...]] = None
         self.gc_tuner = GcTuner.from_config(cfg.runtime, self.metrics)
+        self.worker_shard = None
+        if cfg.runtime.worker_processes > 1:
+            from .parallel.workers import WorkerShard
+
+            self.worker_shard = WorkerShard(cfg.runtime.worker_index, cfg.runtime.worker_processes,
+                                            cfg.labels.job_name_label)
+            self.worker_shard.install(self)
         m = self.metrics
         m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
@@ -218,6 +225,9 @@ class Supervisor:
 
     # ------------------------------------------------------------------ ownership
     def owns(self, key: Tuple[str, str]) -> bool:
+        ws = self.worker_shard
+        if ws is not None and ws.of(key[1]) != ws.index:
+            return False
         s = self.cfg.sharding
         if s.shards <= 1:
             return True
@@ -321,6 +331,11 @@ class Supervisor:
             for _deadline, ev, _recv in lst:
                 self._on_event_add(ev)
 
+    def drop_parked(self, kind, name):
+        """Another shard worker owns this object: forget events parked waiting for it."""
+        if self._parked:
+            self._parked.pop((kind, name), None)
+
     async def _sweep_parked(self):
         tick = max(0.02, min(1.0, self.cfg.rules.stale_event_grace / 4 or 1.0,
                              self.cfg.gpu.evidence_wait / 4 if self.cfg.gpu.evidence_wait > 0 else 1.0))
@@ -329,9 +344,12 @@ class Supervisor:
             if self._gpu_wait:
                 self._expire_gpu_waits()
             now = time.monotonic()
+            ws = self.worker_shard
             for key in list(self._parked):
                 lst = [p for p in self._parked[key] if p[0] > now]
                 dropped = len(self._parked[key]) - len(lst)
+                if dropped and ws is not None and key[0] == "Pod" and ws.owner_of_pod(key[1]) not in (None, ws.index):
+                    dropped = 0  # another shard worker owns that pod: not stale, just not ours
                 if dropped:
                     self.metrics.inc("events_stale", dropped)
                     self.log.info("Algorithm object not found - stale event", kind=key[0], requestId=key[1])

@@ -1,0 +1,139 @@
+"""Process wrapper for the native kube-apiserver simulator (``csrc/kubesim`` →
+``bin/nexus-kubesim``).
+
+The simulator speaks the same REST + watch protocol as
+:mod:`.fake_apiserver` (the supervisor's :class:`~..kube.client.KubeClient` and
+informers run unchanged against it) but on a native epoll loop, so a benchmark's
+cluster side is never the bottleneck.  State is driven over HTTP: ordinary REST
+calls, or ``POST /sim/apply`` with NDJSON watch events for bulk traffic.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import tempfile
+import time
+from typing import Any, Dict, Iterable, List, Optional, Tuple
+
+try:
+    from .._kube_native import dumps as _dumps
+
+    def _line(etype: str, obj: Dict[str, Any]) -> bytes:
+        return _dumps({"type": etype, "object": obj}, newline=True)
+except ImportError:  # pragma: no cover
+    def _line(etype: str, obj: Dict[str, Any]) -> bytes:
+        return json.dumps({"type": etype, "object": obj}, separators=(",", ":")).encode() + b"\n"
+
+
+def encode_events(events: Iterable[Tuple[str, Dict[str, Any]]]) -> bytes:
+    """NDJSON body for ``/sim/apply``."""
+    return b"".join(_line(t, o) for t, o in events)
+
+
+class KubeSim:
+    def __init__(self, *, host: str = "127.0.0.1", port: int = 0, history: int = 400_000, bookmark_ms: int = 1000,
+                 token: str = ""):
+        from .._build import binary
+
+        self.exe = os.environ.get("NEXUS_KUBESIM_BINARY") or binary("nexus-kubesim")
+        self.dir = tempfile.mkdtemp(prefix="nexus-kubesim-")
+        self.host, self.port = host, port
+        self.history, self.bookmark_ms, self.token = history, bookmark_ms, token
+        self.proc: Optional[subprocess.Popen] = None
+        self.log_path = os.path.join(self.dir, "server.log")
+        self.url = ""
+
+    def start(self, timeout: float = 10.0) -> "KubeSim":
+        ready = os.path.join(self.dir, "ready")
+        if os.path.exists(ready):
+            os.unlink(ready)
+        argv = [self.exe, "--host", self.host, "--port", str(self.port), "--ready-file", ready,
+                "--history", str(self.history), "--bookmark-ms", str(self.bookmark_ms)]
+        if self.token:
+            argv += ["--token", self.token]
+        logf = open(self.log_path, "ab")
+        self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True)
+        logf.close()
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if os.path.exists(ready):
+                with open(ready) as f:
+                    info = json.load(f)
+                self.port = info["port"]
+                self.url = info["url"]
+                return self
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"nexus-kubesim exited rc={self.proc.returncode}: {self.log()}")
+            time.sleep(0.01)
+        self.stop()
+        raise RuntimeError("nexus-kubesim did not become ready")
+
+    def log(self) -> str:
+        try:
+            with open(self.log_path) as f:
+                return f.read()[-4000:]
+        except OSError:
+            return ""
+
+    def stop(self) -> None:
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait(5)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+
+class SimControl:
+    """Async client for the ``/sim/*`` control endpoints (one pooled aiohttp session)."""
+
+    def __init__(self, url: str):
+        self.url = url.rstrip("/")
+        self._s = None
+
+    async def _session(self):
+        if self._s is None:
+            import aiohttp
+
+            self._s = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=600))
+        return self._s
+
+    async def apply(self, events: List[Tuple[str, Dict[str, Any]]], expire: bool = False) -> Dict[str, Any]:
+        """Commit watch events; ``expire`` compacts history past them before any watcher
+        reads them (resuming watches get 410 Gone)."""
+        s = await self._session()
+        async with s.post(self.url + "/sim/apply", data=encode_events(events), params={"expire": "1"} if expire else None,
+                          headers={"Content-Type": "application/x-ndjson"}) as r:
+            doc = await r.json(content_type=None)
+            if r.status != 200:
+                raise RuntimeError(f"/sim/apply: {r.status} {doc}")
+            return doc
+
+    async def _post(self, path: str, kind: str = "") -> None:
+        s = await self._session()
+        async with s.post(self.url + path, params={"kind": kind} if kind else None) as r:
+            r.raise_for_status()
+
+    async def expire(self, kind: str = "") -> None:
+        await self._post("/sim/expire", kind)
+
+    async def close_watches(self, kind: str = "") -> None:
+        await self._post("/sim/close-watches", kind)
+
+    async def stats(self) -> Dict[str, Any]:
+        s = await self._session()
+        async with s.get(self.url + "/sim/stats") as r:
+            return await r.json(content_type=None)
+
+    async def close(self) -> None:
+        if self._s is not None:
+            await self._s.close()
+            self._s = None

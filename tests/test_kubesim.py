@@ -1,0 +1,163 @@
+"""Native kube-apiserver simulator (``csrc/kubesim``): the supervisor's own REST/watch
+client and informers against it, the same contract the Python fake apiserver is
+tested for in ``test_kube_wire.py``, and the reference parity suite over
+kubesim + the native CQL server."""
+import asyncio
+
+import pytest
+
+from nexus_supervisor_amd.app import Application
+from nexus_supervisor_amd.config import load_config
+from nexus_supervisor_amd.informer import InformerFactory
+from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig, KubeListWatch
+from nexus_supervisor_amd.kube.errors import ApiError, Conflict, NotFound
+from nexus_supervisor_amd.store.cql import CqlCheckpointStore, CqlSession
+from nexus_supervisor_amd.testing.cqlsrv import CqlServer
+from nexus_supervisor_amd.testing.kubesim import KubeSim, SimControl
+from nexus_supervisor_amd.testing.seed import ALGORITHM, make_event, make_job, make_pod, reference_scenarios, seed_cql_statements
+
+
+def _cfg(**over):
+    base = {"cql-store-type": "scylla", "workers": 4, "rate-limit-elements-per-second": 0,
+            "rate-limit-elements-burst": 100, "failure-rate-base-delay": "100ms", "failure-rate-max-delay": "1s",
+            "resync-period": "0s"}
+    base.update(over)
+    return load_config(path=None, env={}, overrides=base)
+
+
+def test_rest_semantics(arun):
+    async def go():
+        labels = _cfg().labels
+        with KubeSim(token="t0k") as sim:
+            ctl = SimControl(sim.url)
+            out = await ctl.apply([("ADDED", make_pod(f"r{i}", labels)) for i in range(7)])
+            assert out["applied"] == 7 and out["t_push"] > 0
+            c = KubeClient(KubeConfig(sim.url, token="t0k"))
+            items, rv = await c.list("Pod", "nexus", limit=3)  # 3 pages over one snapshot
+            assert len(items) == 7 and items[0]["kind"] == "Pod" and int(rv) == out["rv"]
+            assert all(i["metadata"]["uid"] and i["metadata"]["creationTimestamp"] for i in items)
+            items, _ = await c.list("Pod", "nexus", label_selector="batch.kubernetes.io/job-name=r3")
+            assert [i["metadata"]["name"] for i in items] == ["r3-acdey"]
+            items, _ = await c.list("Pod", "nexus", label_selector="batch.kubernetes.io/job-name!=r3")
+            assert len(items) == 6
+            items, _ = await c.list("Pod", "nexus", field_selector="metadata.name=r5-acdey")
+            assert [i["metadata"]["name"] for i in items] == ["r5-acdey"]
+            got = await c.get("Pod", "nexus", "r1-acdey")
+            patched = await c.patch_merge("Pod", "nexus", "r1-acdey", {"metadata": {"annotations": {"a": "b"}}})
+            assert patched["metadata"]["annotations"] == {"a": "b"}
+            assert patched["metadata"]["uid"] == got["metadata"]["uid"]
+            with pytest.raises(Conflict):
+                await c.replace("Pod", "nexus", "r1-acdey", got)  # stale resourceVersion
+            fresh = await c.replace("Pod", "nexus", "r1-acdey", patched)
+            assert int(fresh["metadata"]["resourceVersion"]) > int(patched["metadata"]["resourceVersion"])
+            ev = make_event("Job", "r1", "DeadlineExceeded")
+            ev["metadata"] = {"generateName": "r1.", "namespace": "nexus"}
+            created = await c.create("Event", "nexus", ev)
+            assert created["metadata"]["name"].startswith("r1.") and len(created["metadata"]["name"]) == 8
+            await c.create("Job", "nexus", make_job("r1", labels))
+            with pytest.raises(ApiError) as ei:
+                await c.create("Job", "nexus", make_job("r1", labels))
+            assert ei.value.status == 409
+            await c.delete_job("nexus", "r1")  # Background: the Job's pod is garbage-collected
+            with pytest.raises(NotFound):
+                await c.get("Pod", "nexus", "r1-acdey")
+            with pytest.raises(NotFound):
+                await c.delete_job("nexus", "r1")
+            st = await ctl.stats()
+            assert st["objects"]["Pod"] == 6 and st["objects"]["Job"] == 0 and st["deleted"] == 2
+            bad = KubeClient(KubeConfig(sim.url, token="nope"))
+            with pytest.raises(ApiError) as ei:
+                await bad.list("Pod", "nexus")
+            assert ei.value.status == 401
+            await bad.close()
+            await c.close()
+            await ctl.close()
+
+    arun(go())
+
+
+def test_watch_resume_bookmarks_and_410_relist(arun):
+    async def go():
+        labels = _cfg().labels
+        with KubeSim(bookmark_ms=50) as sim:
+            ctl = SimControl(sim.url)
+            await ctl.apply([("ADDED", make_job("a", labels))])
+            c = KubeClient(KubeConfig(sim.url))
+            # raw stream: bookmarks while idle, resume from an RV replays history
+            _, rv0 = await c.list("Job", "nexus")
+            await ctl.apply([("ADDED", make_job("b", labels))])
+            seen = []
+            async for et, o in c.watch("Job", "nexus", rv0, timeout_seconds=1):
+                seen.append(et)
+                if et == "BOOKMARK":
+                    break
+            assert seen[0] == "ADDED" and "BOOKMARK" in seen
+            f = InformerFactory(lambda kind: KubeListWatch(c, kind, "nexus", watch_timeout=5), resync_period=0)
+            inf = f.informer("Job")
+            log = []
+            inf.add_event_handler(on_add=lambda o: log.append(("add", o["metadata"]["name"])),
+                                  on_update=lambda o, n: log.append(("upd", n["metadata"]["name"])),
+                                  on_delete=lambda o: log.append(("del", o["metadata"]["name"])))
+            f.start()
+            assert await f.wait_for_cache_sync(5)
+            j = make_job("a", labels)
+            j["status"] = {"active": 1}
+            await ctl.apply([("MODIFIED", j), ("ADDED", make_job("c", labels))])
+            for _ in range(200):
+                if ("upd", "a") in log and ("add", "c") in log:
+                    break
+                await asyncio.sleep(0.02)
+            assert ("upd", "a") in log and ("add", "c") in log
+            relists = inf.relists
+            # compaction: the stream is cut and the resume gets 410 → re-list emits the diff
+            await ctl.apply([("DELETED", make_job("b", labels)), ("ADDED", make_job("d", labels))], expire=True)
+            for _ in range(300):
+                if ("add", "d") in log and ("del", "b") in log:
+                    break
+                await asyncio.sleep(0.02)
+            assert ("add", "d") in log and ("del", "b") in log
+            assert inf.relists > relists
+            assert sorted(inf.indexer.keys()) == ["nexus/a", "nexus/c", "nexus/d"]
+            await f.stop()
+            await c.close()
+            await ctl.close()
+
+    arun(go(), timeout=60)
+
+
+def test_reference_parity_over_kubesim_and_cql(arun):
+    scenarios = reference_scenarios()
+
+    async def go():
+        with KubeSim(bookmark_ms=200) as sim:
+            ctl = SimControl(sim.url)
+            await ctl.apply([("ADDED", o) for s in scenarios for o in s.objects])
+            srv = CqlServer(exec_statements=seed_cql_statements()).start()
+            cfg = _cfg()
+            kube = KubeClient(KubeConfig(sim.url))
+            store = CqlCheckpointStore(CqlSession([srv.address]))
+            app = Application(cfg, kube=kube, store=store)
+            decisions = []
+            app.supervisor.decision_hooks.append(decisions.append)
+            try:
+                await app.start()
+                assert await app.wait_for_cache_sync(10)
+                for _ in range(500):
+                    if len(decisions) >= 8:
+                        break
+                    await asyncio.sleep(0.02)
+                await app.supervisor.pipeline.join(10)
+                if app.supervisor._deletes:
+                    await asyncio.wait(list(app.supervisor._deletes), timeout=10)
+                for s in scenarios:
+                    for rid, stage in s.expected.items():
+                        row = await store.read_checkpoint(ALGORITHM, rid)
+                        assert row.lifecycle_stage == stage, (s.name, rid, row.lifecycle_stage)
+                st = await ctl.stats()
+                assert st["deleted"] >= 5  # failing decisions deleted their Jobs (+ GC'd pods)
+            finally:
+                await app.stop()
+                srv.stop()
+                await ctl.close()
+
+    arun(go(), timeout=60)

@@ -1,0 +1,231 @@
+"""Process-per-core replica (``parallel/workers.py``): placement, the native pre-decode
+shard router, ingest filtering, metrics hand-off, and a 2-worker replica running the
+reference parity scenarios end to end over kubesim + the native CQL server."""
+import asyncio
+import json
+import random
+import zlib
+
+import aiohttp
+import pytest
+
+from nexus_supervisor_amd import _kube_native
+from nexus_supervisor_amd.app import ShardedApplication, make_application
+from nexus_supervisor_amd.config import from_mapping, load_config, to_mapping
+from nexus_supervisor_amd.config.schema import ConfigError, LabelConfig
+from nexus_supervisor_amd.obs.metrics import Metrics
+from nexus_supervisor_amd.parallel.workers import (_SEED, WorkerPool, WorkerShard, merge_metrics_state, metrics_state,
+                                                   worker_of)
+from nexus_supervisor_amd.store.cql import CqlCheckpointStore, CqlSession
+from nexus_supervisor_amd.testing.cqlsrv import CqlServer
+from nexus_supervisor_amd.testing.kubesim import KubeSim, SimControl
+from nexus_supervisor_amd.testing.seed import ALGORITHM, make_event, make_job, make_pod, reference_scenarios, seed_cql_statements
+
+JOB_LABEL = LabelConfig().job_name_label
+
+
+def _line(etype, obj):
+    return _kube_native.dumps({"type": etype, "object": obj}, newline=True)
+
+
+def test_placement_native_matches_python():
+    rng = random.Random(7)
+    for count in (2, 3, 4, 8):
+        routers = [_kube_native.ShardRouter(i, count, _SEED, JOB_LABEL) for i in range(count)]
+        for _ in range(300):
+            rid = "%032x" % rng.getrandbits(128)
+            w = worker_of(rid, count)
+            assert w == zlib.crc32(rid.encode(), _SEED) % count
+            assert all(r.owner_of(rid) == w for r in routers)
+    assert worker_of("anything", 1) == 0
+
+
+def test_native_router_drops_other_workers_lines():
+    labels = LabelConfig()
+    rids = [f"run-{i}" for i in range(40)]
+    pods = [make_pod(r, labels) for r in rids]
+    jobs = [make_job(r, labels) for r in rids]
+    job_events = [make_event("Job", r, "DeadlineExceeded") for r in rids]
+    pod_events = [make_event("Pod", p["metadata"]["name"], "BackOff") for p in pods]
+    unknown = make_event("Pod", "never-seen-pod", "Failed")
+    got = {}
+    for idx in range(2):
+        router = _kube_native.ShardRouter(idx, 2, _SEED, JOB_LABEL)
+        decs = {}
+        for role in ("job", "pod", "event"):
+            d = _kube_native.ProjectedDecoder(True)
+            d.set_router(router, role)
+            decs[role] = d
+        out_jobs = decs["job"].feed(b"".join(_line("ADDED", j) for j in jobs))
+        out_pods = decs["pod"].feed(b"".join(_line("ADDED", p) for p in pods))
+        out_ev = decs["event"].feed(b"".join(_line("ADDED", e) for e in job_events + pod_events + [unknown])
+                                    + b'{"type":"BOOKMARK","object":{"kind":"Event","metadata":{"resourceVersion":"9"}}}\n')
+        got[idx] = (out_jobs, out_pods, out_ev)
+        owned = {r for r in rids if worker_of(r, 2) == idx}
+        assert {o["object"]["metadata"]["name"] for o in out_jobs} == owned
+        assert {o["object"]["metadata"]["labels"][JOB_LABEL] for o in out_pods} == owned
+        names = [(o["object"].get("involvedObject") or {}).get("name") for o in out_ev]
+        assert names.count("never-seen-pod") == 1 and names[-1] is None  # unknown pod + bookmark pass everywhere
+        ev_runs = {n if n in rids else n.rsplit("-", 1)[0] for n in names if n and n != "never-seen-pod"}
+        assert ev_runs == owned
+        assert router.pod_owner(pods[0]["metadata"]["name"]) == worker_of(rids[0], 2)
+        assert router.stats["dropped"] > 0
+    # the two workers partition the traffic
+    assert len(got[0][0]) + len(got[1][0]) == len(jobs)
+    assert len(got[0][1]) + len(got[1][1]) == len(pods)
+
+
+def test_worker_shard_python_filter_and_pod_expiry():
+    now = [0.0]
+    shards = [WorkerShard(i, 3, JOB_LABEL, forget_after=10.0, clock=lambda: now[0]) for i in range(3)]
+    labels = LabelConfig()
+    pod = make_pod("r-1", labels)
+    owner = worker_of("r-1", 3)
+    assert [s.accept_pod(pod, "ADDED") for s in shards] == [i == owner for i in range(3)]
+    assert [s.accept_job(make_job("r-1", labels), "ADDED") for s in shards] == [i == owner for i in range(3)]
+    ev = make_event("Pod", pod["metadata"]["name"], "BackOff")
+    assert [s.accept_event(ev, "ADDED") for s in shards] == [i == owner for i in range(3)]
+    stray = make_event("Pod", "unknown-pod", "BackOff")
+    assert all(s.accept_event(stray, "ADDED") for s in shards)  # parked everywhere until the pod shows up
+    other = {"involvedObject": {"kind": "Node", "name": "n1"}}
+    assert [s.accept_event(other, "ADDED") for s in shards] == [True, False, False]
+    for s in shards:
+        s.accept_pod(pod, "DELETED")
+    now[0] = 5.0
+    shards[0].accept_pod(make_pod("r-2", labels), "ADDED")
+    assert shards[0].owner_of_pod(pod["metadata"]["name"]) == owner  # still remembered for late events
+    now[0] = 11.0
+    shards[0].accept_pod(make_pod("r-3", labels), "ADDED")
+    assert shards[0].pod_owner.get(pod["metadata"]["name"]) is None
+
+
+def test_metrics_state_merge():
+    a, b = Metrics("ns"), Metrics("ns")
+    a.inc("decisions", 3, {"action": "x"})
+    b.inc("decisions", 4, {"action": "x"})
+    a.observe_seconds("lat", 0.010)
+    b.observe_seconds("lat", 0.030)
+    b.set("queue_depth", 5)
+    m = Metrics("ns")
+    merge_metrics_state(m, json.loads(json.dumps(metrics_state(a))), {"worker": "0"})
+    merge_metrics_state(m, json.loads(json.dumps(metrics_state(b))), {"worker": "1"})
+    assert m.counter("decisions", {"action": "x"}) == 7
+    h = m.histogram("lat")
+    assert h.total == 2 and 9_000 <= h.min <= 10_100 and 29_000 <= h.max <= 30_100
+    assert m.gauge("queue_depth", {"worker": "1"}) == 5
+    assert "ns_lat_seconds_count 2" in m.prometheus_text()
+
+
+def test_config_handoff_and_admission_split():
+    cfg = load_config(path=None, env={}, overrides={"workers": 9, "rate-limit-elements-per-second": 10,
+                                                    "rate-limit-elements-burst": 100, "cql-store-type": "scylla",
+                                                    "scylla-cql-store": {"hosts": "a:1,b:2", "password": "s3cret"},
+                                                    "runtime": {"worker-processes": 4}})
+    m = to_mapping(cfg)
+    assert from_mapping(json.loads(json.dumps(m))) == cfg
+    pool = WorkerPool(cfg)
+    child = from_mapping(pool._child_mapping(3))
+    assert child.runtime.worker_index == 3 and child.workers == 3  # ceil(9 / 4)
+    assert child.rate_limit_elements_per_second == 2.5 and child.rate_limit_elements_burst == 25
+    assert not child.leader_election.enabled and child.observability.http_port == 0
+    assert child.scylla_cql_store.password == "s3cret"
+    assert isinstance(make_application(cfg), ShardedApplication)
+    with pytest.raises(ConfigError):
+        load_config(path=None, env={}, overrides={"runtime": {"worker-processes": 2, "worker-index": 2}})
+
+
+@pytest.mark.slow
+def test_two_worker_replica_reference_parity(arun, tmp_path):
+    scenarios = reference_scenarios()
+
+    async def go():
+        with KubeSim(bookmark_ms=200) as sim:
+            ctl = SimControl(sim.url)
+            await ctl.apply([("ADDED", o) for s in scenarios for o in s.objects])
+            srv = CqlServer(exec_statements=seed_cql_statements()).start()
+            kc = tmp_path / "kubeconfig"
+            kc.write_text(json.dumps({"clusters": [{"name": "c", "cluster": {"server": sim.url}}],
+                                      "contexts": [{"name": "x", "context": {"cluster": "c"}}], "current-context": "x"}))
+            cfg = load_config(path=None, env={}, overrides={
+                "cql-store-type": "scylla", "workers": 8, "rate-limit-elements-per-second": 0, "resync-period": "0s",
+                "kube-config-path": str(kc), "scylla-cql-store": {"hosts": f"127.0.0.1:{srv.port}"},
+                "runtime": {"worker-processes": 2}, "observability": {"http-port": 0}})
+            app = ShardedApplication(cfg, report_decisions=True, log_dir=str(tmp_path))
+            decisions = []
+            app.supervisor.decision_hooks.append(decisions.append)
+            store = CqlCheckpointStore(CqlSession([srv.address]))
+            await store.connect()
+            try:
+                await app.start()
+                assert await app.wait_for_cache_sync(30), [w.proc.poll() for w in app.pool.workers]
+                assert app.ready() and app.pool.alive()
+                for _ in range(500):
+                    if sum(1 for d in decisions if d.outcome == "applied") >= 7:
+                        break
+                    await asyncio.sleep(0.02)
+                for s in scenarios:
+                    for rid, stage in s.expected.items():
+                        row = await store.read_checkpoint(ALGORITHM, rid)
+                        assert row.lifecycle_stage == stage, (s.name, rid, row.lifecycle_stage)
+                applied = [d for d in decisions if d.outcome == "applied"]
+                assert all(d.result.stamps.get("ack_mono") for d in applied)
+                # each run was decided by exactly one worker
+                assert len({d.result.request_id for d in applied}) == len(applied)
+                m = await app.refresh_metrics()
+                assert m.counter("decisions_applied", {"stage": "FAILED", "class": "fatal"}) >= 1 or \
+                    sum(v for k, v in m.counters.get("decisions_applied", {}).items()) >= 7
+                objs = {k: v for k, v in m.gauges.get("informer_objects", {}).items() if ("kind", "Job") in k}
+                assert len(objs) == 2  # one gauge per worker: each caches only its own runs
+                # new failure while running: routed to its owner worker
+                pod = make_pod("df1b6e8d-cc3c-fb5b-a3f6-5d7b9e2c7f2b", cfg.labels)  # CANCELLED seed row
+                await ctl.apply([("ADDED", make_event("Pod", pod["metadata"]["name"], "BackOff"))])
+                await asyncio.sleep(0.3)
+            finally:
+                await app.stop(drain_timeout=5)
+                await store.close()
+                srv.stop()
+                await ctl.close()
+            assert all(w.proc.poll() == 0 for w in app.pool.workers), [w.proc.poll() for w in app.pool.workers]
+
+    arun(go(), timeout=90)
+
+
+@pytest.mark.slow
+def test_sharded_obs_endpoints(arun, tmp_path):
+    async def go():
+        with KubeSim() as sim:
+            kc = tmp_path / "kubeconfig"
+            kc.write_text(json.dumps({"clusters": [{"name": "c", "cluster": {"server": sim.url}}],
+                                      "contexts": [{"name": "x", "context": {"cluster": "c"}}], "current-context": "x"}))
+            cfg = load_config(path=None, env={}, overrides={
+                "cql-store-type": "memory", "resync-period": "0s", "kube-config-path": str(kc),
+                "runtime": {"worker-processes": 2}, "observability": {"http-port": 0}})
+            app = ShardedApplication(cfg)
+            await app.start()
+            from nexus_supervisor_amd.obs.http import ObsServer
+
+            obs = ObsServer(app)
+            port = await obs.start("127.0.0.1", 0)
+            try:
+                assert await app.wait_for_cache_sync(30)
+                async with aiohttp.ClientSession() as s:
+                    async with s.get(f"http://127.0.0.1:{port}/metrics") as r:
+                        text = await r.text()
+                        assert r.status == 200 and 'worker="1"' in text
+                        assert 'nexus_supervisor_worker_processes_alive{version="0.1.0"} 2' in text
+                    async with s.get(f"http://127.0.0.1:{port}/healthz") as r:
+                        assert r.status == 200
+                    async with s.get(f"http://127.0.0.1:{port}/readyz") as r:
+                        assert r.status == 200 and "leader" in await r.text()
+                    async with s.get(f"http://127.0.0.1:{port}/debug/vars") as r:
+                        doc = await r.json()
+                        assert doc["worker_processes"] == 2 and all(w["alive"] for w in doc["workers"])
+                app.supervisor.set_active(False)
+                await app.pool.refresh_metrics()
+                m = app.pool.merged_metrics()
+                assert all(v == 0.0 for v in m.gauges["active"].values())
+            finally:
+                await obs.stop()
+                await app.stop(drain_timeout=5)
+
+    arun(go(), timeout=90)
