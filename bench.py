@@ -6,7 +6,8 @@
                     [--transport wire|inproc] [--profile uncapped|reference]
 
 One process per GPU (``torch.distributed.run`` for N>1).  Each rank runs one
-supervisor replica that owns the shard of runs hashed to it (``sharding``), with
+supervisor replica that owns the shard of runs hashed to it (``sharding``), split
+into ``--procs`` shard-worker processes (``runtime.worker-processes``), with
 its GPU-job slot's telemetry on ``cuda:LOCAL_RANK`` (native amd-smi monitor; the
 HIP OOM message and VRAM peak of a real HBM-OOM on that GPU seed the synthetic
 hbm-oom failures).  Per-rank work is fixed (weak scaling): ``--jobs`` live runs,
@@ -16,7 +17,8 @@ A *step* = ``--events`` pod failures (plus replacement-run churn) pushed through
 the watch → informer → classify → keyed pipeline → checkpoint store path, timed
 until the last of them is acknowledged by the store.  ``--transport wire`` (the
 default) runs the real protocols: a fake kube-apiserver streams the watch over
-HTTP and the native CQL server (``nexus-cqlsrv``) holds ``nexus.checkpoints``;
+HTTP (the native ``nexus-kubesim``) and the native CQL server (``nexus-cqlsrv``)
+holds ``nexus.checkpoints``;
 ``inproc`` feeds informers directly and uses the in-memory store.
 
 Rank 0 prints one JSON line; ``value`` = total events/s over all ranks
@@ -52,7 +54,7 @@ def parse_args(argv=None):
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
     ap.add_argument("--workers", type=int, default=256)
-    ap.add_argument("--procs", type=int, default=1,
+    ap.add_argument("--procs", type=int, default=4,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport)")
     ap.add_argument("--inflight", type=int, default=2, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--kube-connections", type=int, default=256)
@@ -185,7 +187,7 @@ def main(argv=None) -> int:
                 "model": "nexus-supervisor (informer→classify→CQL write), 1 replica-shard per GPU-job slot",
                 "global_batch": args.events * world,
                 "seq_len": None,
-                "parallelism": f"shard{world}",
+                "parallelism": f"shard{world}x{args.procs if args.transport == 'wire' else 1}proc",
                 "concurrent_jobs_per_rank": args.jobs,
                 "events_per_step_per_rank": args.events,
                 "transport": args.transport,

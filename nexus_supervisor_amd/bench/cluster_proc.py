@@ -64,9 +64,9 @@ async def amain(args) -> None:
     state = {"wl": None}
 
     async def write_rows(rows):
-        # windows of 512 concurrent upserts (no per-row semaphore wakeups)
-        for i in range(0, len(rows), 512):
-            await asyncio.gather(*(store.upsert_checkpoint(r) for r in rows[i:i + 512]))
+        # the receiver's inserts as UNLOGGED batches of 64 rows, 8 batches in flight
+        chunk = 64 * 8
+        await asyncio.gather(*(store.upsert_many(rows[i:i + chunk]) for i in range(0, len(rows), chunk)))
 
     async def h_init(req):
         p = await req.json()

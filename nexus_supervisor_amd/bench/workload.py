@@ -34,7 +34,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from ..config.schema import LabelConfig
 from ..models.checkpoint import CheckpointedRequest, LifecycleStage
-from ..testing.seed import make_event, make_job, make_pod
+from ..testing.seed import make_event, make_job, make_pod, run_labels
 
 DEFAULT_HIP_OOM = ("hipErrorOutOfMemory: HIP out of memory. Tried to allocate 4.00 GiB. GPU 0 has a total capacity of "
                    "287.98 GiB; 284.00 GiB already allocated by this process")
@@ -81,10 +81,14 @@ class Workload:
 
     # ------------------------------------------------------------ ids / objects
     def _new_id(self) -> str:
+        bits = self.rng.getrandbits
         while True:
             self._seq += 1
-            rid = str(uuid.UUID(int=self.rng.getrandbits(128), version=4))
-            if shard_of(self.algorithm, rid, self.shards) == self.shard_index:
+            # RFC 4122 v4 layout from 128 random bits (same ids as uuid.UUID(int=..., version=4))
+            n = (bits(128) & ~(0xF000 << 64) | (0x4000 << 64)) & ~(0xC000 << 48) | (0x8000 << 48)
+            h = "%032x" % n
+            rid = f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:]}"
+            if self.shards <= 1 or shard_of(self.algorithm, rid, self.shards) == self.shard_index:
                 return rid
 
     def _next_rv(self) -> str:
@@ -99,12 +103,35 @@ class Workload:
                 "MASTER_PORT": "29500", "HIP_VISIBLE_DEVICES": ",".join(str(i) for i in range(self.gpus_per_node)),
                 "NCCL_IB_DISABLE": "1", "RCCL_MSCCLPP_ENABLE": "1"}
 
+    def _templates(self):
+        """Per-workload constant parts of the Job/Pod objects (built once)."""
+        t = getattr(self, "_tmpl", None)
+        if t is None:
+            env = [{"name": k, "value": v} for k, v in self._run_env("x" * 8).items()]
+            mi = next(i for i, e in enumerate(env) if e["name"] == "MASTER_ADDR")
+            gpu = {"amd.com/gpu": "1"}
+            job_labels = run_labels(self.labels, self.algorithm)
+            t = self._tmpl = (env, mi, gpu, job_labels, f"mi355x-{self.rank // self.gpus_per_node:03d}")
+        return t
+
     def new_run(self) -> Tuple[str, Dict[str, Any], Dict[str, Any], CheckpointedRequest]:
         rid = self._new_id()
-        job = make_job(rid, self.labels, ns=self.ns, algorithm=self.algorithm, rv=self._next_rv(), active=1)
-        pod = make_pod(rid, self.labels, ns=self.ns, algorithm=self.algorithm, suffix="w0", env=self._run_env(rid),
-                       gpus=1, node=f"mi355x-{self.rank // self.gpus_per_node:03d}", rv=self._next_rv(),
-                       status={"phase": "Pending"})
+        env_t, mi, gpu, job_labels, node = self._templates()
+        ns, lab = self.ns, self.labels
+        job = {"apiVersion": "batch/v1", "kind": "Job",
+               "metadata": {"name": rid, "namespace": ns, "uid": f"job-uid-{rid}", "resourceVersion": self._next_rv(),
+                            "labels": dict(job_labels)},
+               "spec": {}, "status": {"active": 1}}
+        env = list(env_t)
+        env[mi] = {"name": "MASTER_ADDR", "value": f"{rid[:8]}-0.nexus-headless"}
+        pod_labels = dict(job_labels)
+        pod_labels[lab.job_name_label] = rid
+        pod = {"apiVersion": "v1", "kind": "Pod",
+               "metadata": {"name": f"{rid}-w0", "namespace": ns, "uid": f"pod-uid-{rid}-w0",
+                            "resourceVersion": self._next_rv(), "labels": pod_labels},
+               "spec": {"containers": [{"name": "algorithm", "image": "algo:latest", "env": env,
+                                        "resources": {"limits": gpu, "requests": gpu}}], "nodeName": node},
+               "status": {"phase": "Pending"}}
         now = _dt.datetime.now(_dt.timezone.utc)
         row = CheckpointedRequest(algorithm=self.algorithm, id=rid, lifecycle_stage=LifecycleStage.RUNNING,
                                   payload_uri=f"s3://nexus/payloads/{rid}", received_by_host="receiver-0", received_at=now,

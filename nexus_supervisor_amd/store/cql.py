@@ -669,6 +669,46 @@ class CqlSession:
             return r
         raise StoreError(f"CQL request failed after {attempts} attempts: {last}")
 
+    async def execute_batch(self, ps: PreparedStatement, rows: Sequence[Sequence[Any]], *,
+                            consistency: Optional[int] = None, logged: bool = False,
+                            timeout: Optional[float] = None) -> None:
+        """One BATCH frame of ``ps`` over many value rows (bulk loads: one round trip and
+        one frame instead of one per row).  UNLOGGED unless ``logged``; retried on
+        another host after a connection failure, re-prepared once on UNPREPARED."""
+        cl = self.consistency if consistency is None else consistency
+        kind = 0 if logged else 1
+        for attempt in range(self.max_retries + 1):
+            cands = self._candidates(None)
+            if not cands:
+                raise StoreError("no CQL host available")
+            h = cands[attempt % len(cands)]
+            conn = h.pick()
+            if conn is None:
+                self._mark_down(h, ConnectionClosed("no live connection"))
+                continue
+            stmts = [(1, ps.query_id, list(r), ps.bind_types) for r in rows]
+            self.stats["requests"] += 1
+            try:
+                r = await conn.request(lambda s: N.encode_batch(s, kind, stmts, cl, None, None), None, timeout)
+            except (ConnectionClosed, OSError) as exc:
+                self._mark_down(h, exc)
+                self.stats["retries"] += 1
+                continue
+            if r[0] == "error":
+                if r[1] == ERR_UNPREPARED:
+                    rr = await conn.request(lambda s: N.encode_prepare(s, ps.query))
+                    if rr[0] == "error":
+                        raise CqlError(rr[1], rr[2], rr[3])
+                    ps.query_id = rr[1]
+                    continue
+                if r[1] in RETRYABLE:
+                    self.stats["retries"] += 1
+                    await asyncio.sleep(min(0.2, 0.01 * (2 ** attempt)))
+                    continue
+                raise CqlError(r[1], r[2], r[3])
+            return
+        raise StoreError("CQL batch failed after retries")
+
     async def query(self, cql: str, values: Optional[Sequence[Any]] = None, consistency: Optional[int] = None):
         """Unprepared statement (schema, admin)."""
         cl = self.consistency if consistency is None else consistency
@@ -813,6 +853,14 @@ class CqlCheckpointStore(CheckpointStore):
     async def upsert_checkpoint(self, checkpoint: CheckpointedRequest) -> None:
         self.writes += 1
         await self.session.execute(self.q_insert, checkpoint.as_row(), consistency=self.cl)
+
+    async def upsert_many(self, checkpoints: Sequence[CheckpointedRequest], chunk: int = 64) -> None:
+        """Bulk full-row upserts as UNLOGGED batches (the receiver's new-run inserts)."""
+        ps = await self.session.prepare(self.q_insert)
+        for i in range(0, len(checkpoints), chunk):
+            part = checkpoints[i:i + chunk]
+            self.writes += len(part)
+            await self.session.execute_batch(ps, [c.as_row() for c in part], consistency=self.cl)
 
     async def update_status(self, algorithm, request_id, lifecycle_stage, failure_cause, failure_details, last_modified,
                             only_if_stages=None, set_failure=True) -> bool:

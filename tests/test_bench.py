@@ -66,7 +66,31 @@ def test_bench_two_ranks_torchrun_gloo():
     assert len(lines) == 1, p.stdout  # rank 0 only
     out = json.loads(lines[0])
     _check(out, 2, 2, 1, 40)
-    assert out["config"]["parallelism"] == "shard2"
+    assert out["config"]["parallelism"] == "shard2x1proc"
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_wire_worker_processes():
+    """The driver's N>1 path on the default (wire) transport: each rank a 2-process replica
+    over its own kubesim + CQL server, MAX-over-ranks timing, one JSON line."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "50", "--procs", "2",
+                        "--probe-events", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    _check(out, 2, 2, 1, 50)
+    cfg = out["config"]
+    assert cfg["parallelism"] == "shard2x2proc" and cfg["worker_processes"] == 2
+    assert cfg["stages_ms"]["receive_to_checkpoint"]["count"] >= 150  # merged from both workers
+    assert {"worker0_util", "worker1_util"} <= set(cfg["cpu_util_rank0"])
 
 
 @pytest.mark.slow

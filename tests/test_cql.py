@@ -262,3 +262,29 @@ def test_server_rejects_bad_cql(seeded, arun):
         await s.close()
 
     arun(go())
+
+
+def test_bulk_upsert_as_unlogged_batches(arun):
+    """Receiver-style bulk load: ``upsert_many`` sends one BATCH frame per 64 rows."""
+    from nexus_supervisor_amd.bench.wire import schema_statements
+    from nexus_supervisor_amd.bench.workload import Workload
+
+    async def go():
+        srv = CqlServer(exec_statements=schema_statements()).start()
+        st = CqlCheckpointStore(CqlSession([srv.address]))
+        try:
+            await st.connect()
+            _, rows = Workload(200).initial()
+            before = st.session.stats["requests"]
+            await st.upsert_many(rows)
+            assert st.session.stats["requests"] - before == 4  # ceil(200 / 64) batches
+            for r in (rows[0], rows[77], rows[-1]):
+                got = await st.read_checkpoint(r.algorithm, r.id)
+                assert got.id == r.id and got.lifecycle_stage == r.lifecycle_stage and got.payload_uri == r.payload_uri
+            cnt = await st.session.query("SELECT COUNT(*) FROM nexus.checkpoints")
+            assert cnt.rows[0][0] == 200
+        finally:
+            await st.close()
+            srv.stop()
+
+    arun(go())

@@ -1,19 +1,17 @@
-"""Bench configuration sweep on the GPU box (one process per config, sequential)."""
+"""Bench configuration sweep on the GPU box (one process per config, sequential).
+
+``python tools/gpu_sweep.py [--legacy] [extra bench args]``
+"""
 import json
 import subprocess
 import sys
 
-CONFIGS = [
-    ["--transport", "inproc"],
-    ["--inflight", "1"],
-    ["--inflight", "2"],
-    ["--inflight", "3"],
-    ["--inflight", "4"],
-    ["--inflight", "2", "--workers", "128"],
-    ["--inflight", "2", "--workers", "512"],
-    ["--inflight", "2", "--events", "2000"],
-    ["--inflight", "2", "--kube-connections", "64"],
-]
+CONFIGS = [["--procs", str(p), "--inflight", str(i)] for p in (1, 4, 6, 8) for i in (2, 3, 4)]
+if len(sys.argv) > 1 and sys.argv[1] == "--legacy":
+    CONFIGS = [["--transport", "inproc"], ["--inflight", "1"], ["--inflight", "2"], ["--inflight", "3"],
+               ["--inflight", "4"], ["--inflight", "2", "--workers", "128"], ["--inflight", "2", "--workers", "512"],
+               ["--inflight", "2", "--events", "2000"], ["--inflight", "2", "--kube-connections", "64"]]
+    sys.argv.pop(1)
 out = []
 for extra in CONFIGS:
     cmd = [sys.executable, "bench.py", "--steps", "6", "--warmup", "1", "--no-real-oom"] + extra + sys.argv[1:]
@@ -21,7 +19,8 @@ for extra in CONFIGS:
     line = p.stdout.strip().splitlines()[-1] if p.stdout.strip() else ""
     try:
         d = json.loads(line)
-        rec = {"args": extra, "value": d["value"], "p50_ms": d["p50_ms"], "p99_ms": d["p99_ms"], "errors": d["errors"]}
+        rec = {"args": extra, "value": d["value"], "p50_ms": d["p50_ms"], "p99_ms": d["p99_ms"], "errors": d["errors"],
+               "cpu": d["config"].get("cpu_util_rank0")}
     except Exception:
         rec = {"args": extra, "error": p.stderr[-800:]}
     print(json.dumps(rec), flush=True)
