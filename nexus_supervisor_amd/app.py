@@ -80,7 +80,7 @@ class Application:
         if self.telemetry is None and cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry:
             from .gpu.telemetry import make_telemetry
 
-            self.telemetry = make_telemetry(cfg.gpu.backend, cfg.gpu.sample_interval)
+            self.telemetry = make_telemetry(cfg.gpu.backend, cfg.gpu.sample_interval, cfg.gpu.telemetry_events)
         if self.telemetry is not None:
             from .gpu.telemetry import pod_evidence_provider
 
@@ -158,7 +158,8 @@ class _SupervisorFacade:
 class ShardedApplication:
     """A replica of ``runtime.worker-processes`` shard-worker processes
     (:mod:`.parallel.workers`): this process holds the lease, relays active/standby,
-    serves the merged ``/metrics`` and supervises the workers."""
+    serves the merged ``/metrics`` and supervises the workers (a worker that dies is
+    restarted with backoff; ``/healthz`` reports it until it is back)."""
 
     def __init__(self, cfg: SupervisorConfig, *, kube=None, logger: Optional[KLogger] = None,
                  metrics: Optional[Metrics] = None, report_decisions: bool = False, log_dir: str = ""):

@@ -87,6 +87,9 @@ class WireHarness:
             sc.runtime.worker_processes = self.cfg.procs
             sc.gpu.local_telemetry = True
             sc.gpu.backend = self.cfg.telemetry
+            # K workers per rank × 8 ranks on a node: VRAM sampling in each, one event listener per
+            # rank (the rank process's own monitor) is enough for the benchmark
+            sc.gpu.telemetry_events = False
             self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir)
         else:
             kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)

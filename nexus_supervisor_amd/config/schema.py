@@ -123,6 +123,8 @@ class GpuConfig:
     # read GPUs of the node this process runs on (in-node supervisor / bench); the cluster
     # deployment instead reads the node agents' pod annotations
     local_telemetry: bool = field(default=False, metadata=_k("local-telemetry"))
+    # amd-smi event listener (VM faults, resets) next to the VRAM sampler; off = sampling only
+    telemetry_events: bool = field(default=True, metadata=_k("telemetry-events"))
     # hold a failed GPU pod's decision this long for the node agent's evidence annotation
     # (0 = decide immediately on whatever is there)
     evidence_wait: float = field(default=0.0, metadata=_k("evidence-wait", "duration"))

@@ -218,15 +218,16 @@ def has_amd_gpu() -> bool:
     return os.path.exists("/dev/kfd")
 
 
-def make_telemetry(backend: str = "auto", interval: float = 0.25) -> Optional[GpuTelemetry]:
+def make_telemetry(backend: str = "auto", interval: float = 0.25, events: bool = True) -> Optional[GpuTelemetry]:
     """``auto``: native amd-smi when a GPU is present (fails loudly if the extension is
-    missing there), else none; ``amdsmi``/``fake``/``none`` force a backend."""
+    missing there), else none; ``amdsmi``/``fake``/``none`` force a backend.  ``events``
+    False skips the amd-smi event listener (VRAM/process sampling only)."""
     if backend == "none":
         return None
     if backend == "fake":
         return FakeTelemetry()
     if backend == "amdsmi" or (backend == "auto" and has_amd_gpu()):
-        return AmdSmiTelemetry(interval=interval)
+        return AmdSmiTelemetry(interval=interval, events=events)
     return None
 
 

@@ -258,6 +258,9 @@ class WorkerPool:
         self._metrics_seq = 0
         self._metrics_waiters: Dict[int, Tuple[asyncio.Future, set]] = {}
         self.restarts = 0
+        self.restart_backoff = (0.2, 10.0)  # base, max seconds between restarts of one worker
+        self._stopping = False
+        self._watchdog: Optional[asyncio.Task] = None
 
     def _child_mapping(self, index: int) -> Dict[str, Any]:
         m = copy.deepcopy(self._mapping)
@@ -274,8 +277,37 @@ class WorkerPool:
 
     async def start(self, active: bool = True) -> None:
         self.active = active
+        self._stopping = False
         for w in self.workers:
             await self._spawn(w)
+        self._watchdog = asyncio.create_task(self._watch(), name="worker-watchdog")
+
+    async def _watch(self) -> None:
+        """Restart a worker that exited on its own (crash, OOM kill) with exponential backoff;
+        the new process re-lists and replays, which is idempotent (finished rows are skipped).
+        Its siblings keep running: one bad run cannot take the whole replica down."""
+        base, cap = self.restart_backoff
+        delay = {w.index: base for w in self.workers}
+        while not self._stopping:
+            await asyncio.sleep(0.1)
+            for w in self.workers:
+                if self._stopping or w.proc is None or w.proc.poll() is None:
+                    continue
+                rc = w.proc.returncode
+                await asyncio.sleep(delay[w.index])
+                if self._stopping:
+                    return
+                self.restarts += 1
+                delay[w.index] = min(cap, delay[w.index] * 2)
+                import logging
+
+                logging.getLogger("nexus_supervisor_amd.workers").warning(
+                    "worker %d exited rc=%s; restarting (restart #%d)", w.index, rc, self.restarts)
+                if w.reader is not None:
+                    w.reader.cancel()
+                if w.chan is not None:
+                    w.chan.close()
+                await self._spawn(w)
 
     async def _spawn(self, w: _Worker) -> None:
         parent, child = socket.socketpair()
@@ -392,6 +424,14 @@ class WorkerPool:
         return [w.proc.pid for w in self.workers if w.proc is not None]
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
+        self._stopping = True
+        if self._watchdog is not None:
+            self._watchdog.cancel()
+            try:
+                await self._watchdog
+            except (asyncio.CancelledError, Exception):
+                pass
+            self._watchdog = None
         for w in self.workers:
             if w.chan is not None:
                 w.chan.send({"op": "stop", "drain": drain_timeout})

@@ -229,3 +229,61 @@ def test_sharded_obs_endpoints(arun, tmp_path):
                 await app.stop(drain_timeout=5)
 
     arun(go(), timeout=90)
+
+
+@pytest.mark.slow
+def test_crashed_worker_restarts_and_leader_gating(arun, tmp_path):
+    """A killed worker is restarted and replays its shard; with leader election on, the
+    workers stay standby until the parent holds the Lease (kubesim serves the Lease)."""
+    import os
+    import signal
+
+    async def go():
+        labels = LabelConfig()
+        with KubeSim(bookmark_ms=200) as sim:
+            ctl = SimControl(sim.url)
+            srv = CqlServer(exec_statements=seed_cql_statements()).start()
+            kc = tmp_path / "kubeconfig"
+            kc.write_text(json.dumps({"clusters": [{"name": "c", "cluster": {"server": sim.url}}],
+                                      "contexts": [{"name": "x", "context": {"cluster": "c"}}], "current-context": "x"}))
+            cfg = load_config(path=None, env={}, overrides={
+                "cql-store-type": "scylla", "workers": 8, "rate-limit-elements-per-second": 0, "resync-period": "0s",
+                "kube-config-path": str(kc), "scylla-cql-store": {"hosts": f"127.0.0.1:{srv.port}"},
+                "runtime": {"worker-processes": 2},
+                "leader-election": {"enabled": True, "lease-duration": "3s", "renew-deadline": "2s",
+                                    "retry-period": "200ms", "identity": "replica-a"}})
+            app = ShardedApplication(cfg, report_decisions=True, log_dir=str(tmp_path))
+            app.pool.restart_backoff = (0.1, 0.5)
+            decisions = []
+            app.supervisor.decision_hooks.append(decisions.append)
+            try:
+                await app.start()
+                assert await app.wait_for_cache_sync(30)
+                for _ in range(200):  # the parent acquires the Lease and activates the workers
+                    if app.pool.active:
+                        break
+                    await asyncio.sleep(0.05)
+                assert app.pool.active and app.elector.leader
+                victim = app.pool.workers[1].proc
+                os.kill(victim.pid, signal.SIGKILL)
+                for _ in range(200):
+                    w = app.pool.workers[1]
+                    if app.pool.restarts >= 1 and w.proc is not victim and w.synced.is_set():
+                        break
+                    await asyncio.sleep(0.05)
+                assert app.pool.restarts == 1 and app.pool.alive() and app.ready()
+                # runs of both workers are still decided after the restart
+                scen = reference_scenarios()
+                await ctl.apply([("ADDED", o) for s in scen for o in s.objects])
+                for _ in range(400):
+                    if sum(1 for d in decisions if d.outcome == "applied") >= 7:
+                        break
+                    await asyncio.sleep(0.05)
+                owners = {worker_of(d.result.request_id, 2) for d in decisions if d.outcome == "applied"}
+                assert owners == {0, 1}, [(d.result.request_id, d.outcome) for d in decisions]
+            finally:
+                await app.stop(drain_timeout=5)
+                srv.stop()
+                await ctl.close()
+
+    arun(go(), timeout=120)
