@@ -54,9 +54,11 @@ def parse_args(argv=None):
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
     ap.add_argument("--workers", type=int, default=256)
-    ap.add_argument("--procs", type=int, default=4,
+    ap.add_argument("--procs", type=int, default=6,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport)")
     ap.add_argument("--inflight", type=int, default=2, help="steps pushed ahead of acknowledgement")
+    ap.add_argument("--no-pregen", action="store_true",
+                    help="generate each step's synthetic traffic on demand instead of before the timed region")
     ap.add_argument("--kube-connections", type=int, default=256)
     ap.add_argument("--probe-events", type=int, default=60,
                     help="after the timed steps: open-loop latency probe with this many single failures (0 = off)")
@@ -135,6 +137,7 @@ def main(argv=None) -> int:
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
+                      pregen=not args.no_pregen,
                       pprof_out=args.pprof_out if rank == 0 else "")
     res = asyncio.run(run_rank(cfg, barrier_sync))
 
@@ -196,6 +199,7 @@ def main(argv=None) -> int:
                 "workers": res.get("workers"),
                 "worker_processes": args.procs if args.transport == "wire" else 1,
                 "inflight_steps": args.inflight,
+                "pregenerated_input": not args.no_pregen and args.transport == "wire",
                 "rate_limit_eps": res.get("eps"),
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),

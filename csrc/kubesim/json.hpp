@@ -22,6 +22,9 @@ struct ParseError : std::runtime_error {
 struct Value {
   enum Type : uint8_t { NUL, BOOL, NUM, STR, ARR, OBJ } t = NUL;
   bool b = false;
+  bool escaped = false;  // STR: the source text contained escapes
+  uint32_t src_off = 0;  // offset/length in the parsed text: STR the raw contents between the
+  uint32_t src_len = 0;  // quotes, others the whole token (lets callers splice instead of re-dump)
   std::string s;  // STR (decoded) or NUM (raw text)
   std::vector<Value> a;
   std::vector<std::pair<std::string, Value>> o;
@@ -142,16 +145,17 @@ class Parser {
     }
     return v;
   }
-  void string(std::string& out) {
+  bool string(std::string& out) {
     expect('"');
     size_t run = i_;
+    bool esc = false;
     while (true) {
       if (i_ >= n_) throw ParseError("unterminated string");
       char c = s_[i_];
       if (c == '"') {
         out.append(s_ + run, i_ - run);
         ++i_;
-        return;
+        return esc;
       }
       if (static_cast<unsigned char>(c) < 0x20) throw ParseError("control character in string");
       if (c != '\\') {
@@ -159,6 +163,7 @@ class Parser {
         continue;
       }
       out.append(s_ + run, i_ - run);
+      esc = true;
       ++i_;
       if (i_ >= n_) throw ParseError("bad escape");
       char e = s_[i_++];
@@ -188,6 +193,14 @@ class Parser {
     }
   }
   void value(Value& v, int depth) {
+    size_t st = i_;
+    value_inner(v, depth);
+    if (v.t != Value::STR) {  // containers / scalars: the whole token
+      v.src_off = static_cast<uint32_t>(st);
+      v.src_len = static_cast<uint32_t>(i_ - st);
+    }
+  }
+  void value_inner(Value& v, int depth) {
     if (depth > 128) throw ParseError("nesting too deep");
     char c = peek();
     if (c == '{') {
@@ -227,7 +240,10 @@ class Parser {
       }
     } else if (c == '"') {
       v.t = Value::STR;
-      string(v.s);
+      size_t st = i_ + 1;
+      v.escaped = string(v.s);
+      v.src_off = static_cast<uint32_t>(st);
+      v.src_len = static_cast<uint32_t>(i_ - 1 - st);
     } else if (c == 't') {
       literal("true");
       v.t = Value::BOOL;

@@ -237,7 +237,35 @@ struct Obj {
   std::shared_ptr<const Attrs> attrs;
   std::string ns, name, job;  // job: batch.kubernetes.io/job-name label (pods)
   int64_t rv = 0;
+  size_t rv_off = std::string::npos;  // offset of the resourceVersion digits in *json
+  size_t rv_len = 0;
 };
+
+// locate metadata.resourceVersion's digits in a serialised object (the value is unique: it is
+// the object's own RV, so the first `"resourceVersion":"<rv>"` is it)
+void locate_rv(Obj& o) {
+  std::string needle = "\"resourceVersion\":\"" + std::to_string(o.rv) + "\"";
+  size_t at = o.json->find(needle);
+  if (at != std::string::npos) {
+    o.rv_off = at + 19;
+    o.rv_len = needle.size() - 20;
+  } else {
+    o.rv_off = std::string::npos;
+  }
+}
+
+// same object text with another resourceVersion (no parse / re-serialise)
+void splice_rv(Obj& o, int64_t rv) {
+  std::string r = std::to_string(rv);
+  auto j = std::make_shared<std::string>();
+  j->reserve(o.json->size() + 4);
+  j->append(*o.json, 0, o.rv_off);
+  j->append(r);
+  j->append(*o.json, o.rv_off + o.rv_len, std::string::npos);
+  o.json = std::move(j);
+  o.rv = rv;
+  o.rv_len = r.size();
+}
 
 struct Hist {
   int64_t rv;
@@ -260,7 +288,7 @@ struct Watch {
 };
 
 struct KindStore {
-  std::map<std::string, Obj> objs;  // ns \x01 name → object (sorted: LIST order)
+  std::unordered_map<std::string, Obj> objs;  // ns \x01 name → object (LIST sorts)
   std::deque<Hist> history;
   int64_t compacted = 0;
   std::vector<Watch*> watchers;
@@ -309,16 +337,28 @@ void record(int kind, const char* etype, const Obj& o) {
 }
 
 // Fills metadata defaults, assigns the next resourceVersion, serialises and indexes.
-Obj finish(int kind, Value& doc, const Obj* prev) {
-  if (!doc.get("kind")) doc.at("kind") = Value::str(KINDS[kind].kind);
-  if (!doc.get("apiVersion")) doc.at("apiVersion") = Value::str(KINDS[kind].api_version);
+// `src` is the text `doc` was parsed from: when nothing but the resourceVersion changes
+// (the usual case for fully-formed objects) the new text is spliced instead of re-dumped.
+Obj finish(int kind, Value& doc, const Obj* prev, std::string_view src = {}) {
+  bool dirty = src.empty();
+  if (!doc.get("kind")) {
+    doc.at("kind") = Value::str(KINDS[kind].kind);
+    dirty = true;
+  }
+  if (!doc.get("apiVersion")) {
+    doc.at("apiVersion") = Value::str(KINDS[kind].api_version);
+    dirty = true;
+  }
+  if (!doc.get("metadata")) dirty = true;
   Value& md = doc.at("metadata");
   if (md.path({"name"}).empty()) {
+    dirty = true;
     std::string gen(md.path({"generateName"}));
     md.at("name") = Value::str(gen + random_suffix(5));
   }
   const Value* uid = md.get("uid");
   if (!uid || uid->t != Value::STR || uid->s.empty()) {
+    dirty = true;
     std::string u;
     if (prev) {
       Value pv = kjson::parse(*prev->json);
@@ -328,9 +368,15 @@ Obj finish(int kind, Value& doc, const Obj* prev) {
     }
     md.at("uid") = Value::str(u.empty() ? uuid4() : u);
   }
-  if (!md.get("creationTimestamp")) md.at("creationTimestamp") = Value::str(now_rfc3339());
+  if (!md.get("creationTimestamp")) {
+    md.at("creationTimestamp") = Value::str(now_rfc3339());
+    dirty = true;
+  }
   Obj o;
   o.rv = ++g_rv;
+  const Value* old_rv = md.get("resourceVersion");
+  if (!old_rv || old_rv->t != Value::STR || old_rv->escaped) dirty = true;
+  size_t splice_off = dirty ? 0 : old_rv->src_off, splice_len = dirty ? 0 : old_rv->src_len;
   md.at("resourceVersion") = Value::str(std::to_string(o.rv));
   o.ns = std::string(md.path({"namespace"}));
   o.name = std::string(md.path({"name"}));
@@ -340,7 +386,22 @@ Obj finish(int kind, Value& doc, const Obj* prev) {
     if (j && j->t == Value::STR) o.job = j->s;
   }
   o.attrs = attrs_of(doc);
-  o.json = std::make_shared<const std::string>(kjson::dump(doc));
+  if (dirty) {
+    o.json = std::make_shared<const std::string>(kjson::dump(doc));
+    locate_rv(o);
+  } else {
+    // src holds the text doc was parsed from (offsets are relative to src)
+    size_t b = doc.src_off, e = static_cast<size_t>(doc.src_off) + doc.src_len;
+    std::string r = std::to_string(o.rv);
+    auto j = std::make_shared<std::string>();
+    j->reserve(e - b + 8);
+    j->append(src.data() + b, splice_off - b);
+    j->append(r);
+    j->append(src.data() + splice_off + splice_len, e - splice_off - splice_len);
+    o.json = std::move(j);
+    o.rv_off = splice_off - b;
+    o.rv_len = r.size();
+  }
   return o;
 }
 
@@ -359,13 +420,13 @@ void index_pod(const Obj& o, bool add) {
 }
 
 // returns false when the object exists already
-bool create(int kind, Value& doc, std::string* out_json) {
+bool create(int kind, Value& doc, std::string* out_json, std::string_view src = {}) {
   Value& md = doc.at("metadata");
   if (md.path({"name"}).empty() && md.path({"generateName"}).empty()) throw kjson::ParseError("metadata.name required");
   if (!md.path({"name"}).empty()) {
     if (g_store[kind].objs.count(okey(md.path({"namespace"}), md.path({"name"})))) return false;
   }
-  Obj o = finish(kind, doc, nullptr);
+  Obj o = finish(kind, doc, nullptr, src);
   while (g_store[kind].objs.count(okey(o.ns, o.name))) {  // generateName collision
     md.at("name") = Value::str(std::string(md.path({"generateName"})) + random_suffix(5));
     o = finish(kind, doc, nullptr);
@@ -378,15 +439,14 @@ bool create(int kind, Value& doc, std::string* out_json) {
 }
 
 // 0 ok, 1 not found, 2 conflict
-int update(int kind, Value& doc, bool check_rv, std::string* out_json) {
+int update(int kind, Value& doc, bool check_rv, std::string* out_json, std::string_view src = {}) {
   Value& md = doc.at("metadata");
   std::string k = okey(md.path({"namespace"}), md.path({"name"}));
   auto it = g_store[kind].objs.find(k);
   if (it == g_store[kind].objs.end()) return 1;
   std::string want(md.path({"resourceVersion"}));
   if (check_rv && !want.empty() && want != std::to_string(it->second.rv)) return 2;
-  md.erase("resourceVersion");
-  Obj o = finish(kind, doc, &it->second);
+  Obj o = finish(kind, doc, &it->second, src);
   if (kind == K_POD) {
     index_pod(it->second, false);
     index_pod(o, true);
@@ -403,10 +463,14 @@ bool remove(int kind, const std::string& ns, const std::string& name, const std:
   Obj o = std::move(it->second);
   g_store[kind].objs.erase(it);
   if (kind == K_POD) index_pod(o, false);
-  Value doc = kjson::parse(*o.json);
-  o.rv = ++g_rv;
-  doc.at("metadata").at("resourceVersion") = Value::str(std::to_string(o.rv));
-  o.json = std::make_shared<const std::string>(kjson::dump(doc));
+  if (o.rv_off != std::string::npos) {
+    splice_rv(o, ++g_rv);
+  } else {
+    Value doc = kjson::parse(*o.json);
+    o.rv = ++g_rv;
+    doc.at("metadata").at("resourceVersion") = Value::str(std::to_string(o.rv));
+    o.json = std::make_shared<const std::string>(kjson::dump(doc));
+  }
   record(kind, "DELETED", o);
   ++g_stats.deleted;
   if (kind == K_JOB && (propagation == "Background" || propagation == "Foreground")) {
@@ -730,6 +794,7 @@ void h_apply(Conn& c, const Request& r) {
     Value ev = kjson::parse(line);
     std::string type(ev.path({"type"}));
     Value* obj = ev.get("object");
+    std::string_view osrc = line;  // obj's source offsets are relative to the line
     if (!obj || obj->t != Value::OBJ) throw kjson::ParseError("event without object");
     int kind = kind_by_name(obj->path({"kind"}));
     if (kind < 0) throw kjson::ParseError("unknown kind");
@@ -737,9 +802,9 @@ void h_apply(Conn& c, const Request& r) {
       remove(kind, std::string(obj->path({"metadata", "namespace"})), std::string(obj->path({"metadata", "name"})),
              "Background");
     } else if (type == "MODIFIED") {
-      if (update(kind, *obj, false, nullptr) == 1) create(kind, *obj, nullptr);
+      if (update(kind, *obj, false, nullptr, osrc) == 1) create(kind, *obj, nullptr, osrc);
     } else {
-      if (!create(kind, *obj, nullptr)) update(kind, *obj, false, nullptr);
+      if (!create(kind, *obj, nullptr, osrc)) update(kind, *obj, false, nullptr, osrc);
     }
     ++n;
   }

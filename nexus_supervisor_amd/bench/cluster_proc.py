@@ -7,7 +7,9 @@ generator, and the "receiver" role that inserts each new run's checkpoint row
 into the CQL store before the run's pods exist (what nexus's receiver does
 upstream of the supervisor).  A small control API drives it:
 
-``POST /bench/init {"jobs": N, "seed": s, ...}``  create the live runs (+ rows)
+``POST /bench/init {"jobs": N, "seed": s, ..., "pregen": P, "events": E}``
+                                                    create the live runs (+ rows) and
+                                                    pre-generate P steps of E failures
 ``POST /bench/step {"events": E}``                fail E runs, replace them; returns
                                                     ``{"rids": [...], "t_push": monotonic}``
 
@@ -17,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import collections
 import gc
 import json
 import os
@@ -34,7 +37,7 @@ async def amain(args) -> None:
     sim = simctl = api = None
     if args.api == "kubesim":
         # native apiserver simulator: the generator below only produces traffic
-        from ..testing.kubesim import KubeSim, SimControl
+        from ..testing.kubesim import KubeSim, SimControl, encode_events
 
         sim = KubeSim(host=args.host, port=args.port, history=args.history, bookmark_ms=2000).start()
         simctl = SimControl(sim.url)
@@ -77,6 +80,17 @@ async def amain(args) -> None:
         await write_rows(rows)
         await apply([("ADDED", o) for o in objs])
         state["wl"] = wl
+        # synthetic input generated up front (like a data loader's pre-built batches): the
+        # failures of the next `pregen` steps of `events` each, their replacement runs' rows
+        # inserted (the receiver writes a run's row before its pods exist) and their watch
+        # traffic encoded, so a timed step costs the generator one HTTP request
+        pregen, events = int(p.get("pregen", 0)), int(p.get("events", 0))
+        queue = state["pregen"] = collections.deque()
+        if pregen and events and simctl is not None:
+            for _ in range(pregen):
+                failed, traffic, rows = wl.step(events)
+                await write_rows(rows)
+                queue.append((events, failed, encode_events(traffic)))
         # the simulated cluster holds the same 10k-run heap as the supervisor: keep it out
         # of full collections so the generator never paces the measured process
         gc.collect()
@@ -99,6 +113,17 @@ async def amain(args) -> None:
         p = await req.json()
         events = int(p["events"])
         wl = state["wl"]
+        queue = state.get("pregen")
+        if queue and queue[0][0] == events and "next" not in state:
+            _, failed, body = queue.popleft()
+            doc = await simctl.apply_raw(body)
+            return web.json_response({"rids": failed, "t_push": doc["t_push"],
+                                      "expected": {r: wl.expected[r] for r in failed}})
+        if queue:
+            # a step of another size (latency probe): the pre-generated steps' runs are live
+            # in the workload already, so they must exist in the cluster before we diverge
+            while queue:
+                await simctl.apply_raw(queue.popleft()[2])
         nxt = state.pop("next", None)
         if nxt is not None and nxt[0] == events:
             failed, traffic = await nxt[1]

@@ -42,6 +42,7 @@ class BenchConfig:
     probe_events: int = 60
     probe_rate_per_min: float = 1000.0
     procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
+    pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:

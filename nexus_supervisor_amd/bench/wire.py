@@ -68,7 +68,8 @@ class WireHarness:
         async with self.http.post(self.ctl + "/bench/init", json={
                 "jobs": self.cfg.jobs, "seed": self.cfg.seed, "rank": self.cfg.rank, "world": self.cfg.world,
                 "shards": self.cfg.world, "shard_index": self.cfg.rank,
-                "hip_oom_message": self.cfg.hip_oom_message}) as r:
+                "hip_oom_message": self.cfg.hip_oom_message,
+                "pregen": self.cfg.warmup + self.cfg.steps if self.cfg.pregen else 0, "events": self.cfg.events}) as r:
             r.raise_for_status()
             await r.json()
         sc = self.sc

@@ -117,6 +117,15 @@ class SimControl:
                 raise RuntimeError(f"/sim/apply: {r.status} {doc}")
             return doc
 
+    async def apply_raw(self, body: bytes) -> Dict[str, Any]:
+        """``apply`` with a pre-encoded NDJSON body (:func:`encode_events`)."""
+        s = await self._session()
+        async with s.post(self.url + "/sim/apply", data=body, headers={"Content-Type": "application/x-ndjson"}) as r:
+            doc = await r.json(content_type=None)
+            if r.status != 200:
+                raise RuntimeError(f"/sim/apply: {r.status} {doc}")
+            return doc
+
     async def _post(self, path: str, kind: str = "") -> None:
         s = await self._session()
         async with s.post(self.url + path, params={"kind": kind} if kind else None) as r:

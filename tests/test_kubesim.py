@@ -76,6 +76,41 @@ def test_rest_semantics(arun):
     arun(go())
 
 
+def test_resource_versions_spliced_consistently(arun):
+    """Fully-formed objects are stored by splicing the new resourceVersion into the client's
+    text (no re-serialisation): every stored / streamed copy must still be valid JSON with
+    the server's RV, through create, update and the GC'd delete."""
+    async def go():
+        labels = _cfg().labels
+        with KubeSim() as sim:
+            ctl = SimControl(sim.url)
+            job, pod = make_job("s1", labels, rv="77"), make_pod("s1", labels, rv="77")
+            pod["metadata"]["annotations"] = {"note": 'quote " and \\ backslash', "unicode": "h\u00e9"}
+            r = await ctl.apply([("ADDED", job), ("ADDED", pod)])
+            c = KubeClient(KubeConfig(sim.url))
+            got = await c.get("Pod", "nexus", "s1-acdey")
+            assert got["metadata"]["resourceVersion"] == str(r["rv"]) and got["metadata"]["annotations"] == pod["metadata"]["annotations"]
+            lines = []
+
+            async def watch():
+                async for et, o in c.watch("Pod", "nexus", str(r["rv"]), timeout_seconds=2):
+                    lines.append((et, o["metadata"]["resourceVersion"], o))
+                    if et == "DELETED":
+                        return
+            t = asyncio.create_task(watch())
+            pod2 = dict(pod, status={"phase": "Running"})
+            r2 = await ctl.apply([("MODIFIED", pod2)])
+            await c.delete_job("nexus", "s1")
+            await asyncio.wait_for(t, 5)
+            assert [e for e, _, _ in lines] == ["MODIFIED", "DELETED"]
+            assert lines[0][1] == str(r2["rv"]) and int(lines[1][1]) > r2["rv"]
+            assert lines[1][2]["status"] == {"phase": "Running"} and lines[1][2]["metadata"]["uid"] == pod["metadata"]["uid"]
+            await c.close()
+            await ctl.close()
+
+    arun(go())
+
+
 def test_watch_resume_bookmarks_and_410_relist(arun):
     async def go():
         labels = _cfg().labels

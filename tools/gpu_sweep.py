@@ -6,7 +6,8 @@ import json
 import subprocess
 import sys
 
-CONFIGS = [["--procs", str(p), "--inflight", str(i)] for p in (1, 4, 6, 8) for i in (2, 3, 4)]
+CONFIGS = ([["--procs", str(p), "--inflight", str(i)] for p in (4, 6, 8) for i in (2, 3, 4)]
+           + [["--procs", "6", "--inflight", "3", "--workers", "512"]])
 if len(sys.argv) > 1 and sys.argv[1] == "--legacy":
     CONFIGS = [["--transport", "inproc"], ["--inflight", "1"], ["--inflight", "2"], ["--inflight", "3"],
                ["--inflight", "4"], ["--inflight", "2", "--workers", "128"], ["--inflight", "2", "--workers", "512"],
