@@ -16,6 +16,7 @@
 //   ["map", sub]                  object: keep all keys, project every value with `sub`
 // A non-object value where an object projection was expected is kept whole (so
 // Status objects in ERROR events survive any kind's schema).
+#define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
 #include <time.h>
@@ -542,6 +543,47 @@ class Scan {
     }
   }
 
+  // LIST body: metadata.resourceVersion and the byte range of every element of "items"
+  bool list_items(std::string_view& rv, std::vector<std::pair<size_t, size_t>>& items) {
+    static const char* const P_RV[] = {"metadata", "resourceVersion"};
+    find(P_RV, 2, rv);
+    i_ = 0;
+    try {
+      ws();
+      if (i_ >= n_ || s_[i_] != '{') return false;
+      ++i_;
+      while (true) {
+        ws();
+        if (i_ >= n_ || s_[i_] != '"') return false;
+        bool esc;
+        std::string_view k = str(esc);
+        ws();
+        if (i_ >= n_ || s_[i_] != ':') return false;
+        ++i_;
+        ws();
+        if (k == "items" && i_ < n_ && s_[i_] == '[') {
+          ++i_;
+          while (true) {
+            ws();
+            if (i_ >= n_) return false;
+            if (s_[i_] == ']') return true;
+            size_t b = i_;
+            skip_value();
+            items.emplace_back(b, i_);
+            ws();
+            if (i_ < n_ && s_[i_] == ',') ++i_;
+          }
+        }
+        skip_value();
+        ws();
+        if (i_ < n_ && s_[i_] == ',') ++i_;
+        else return false;
+      }
+    } catch (const ParseError&) {
+      return false;
+    }
+  }
+
  private:
   const char* s_;
   size_t n_;
@@ -662,42 +704,57 @@ void expire_owners(Router* r) {
   }
 }
 
-// true = this worker owns (or must see) the watch line
-bool route_line(Router* r, int role, const char* s, size_t n) {
+// Owner worker of one object: a watch line ({"type", "object"} envelope) or a bare LIST
+// item.  -1 = every worker must see it (bookmarks, errors, unparsable lines, Events about a
+// Pod not seen yet).  Pod lines also record the pod's owner for Pod-Event routing.
+constexpr int OWNER_ALL = -1;
+
+int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
   static const char* const P_TYPE[] = {"type"};
-  static const char* const P_NAME[] = {"object", "metadata", "name"};
-  static const char* const P_IKIND[] = {"object", "involvedObject", "kind"};
-  static const char* const P_INAME[] = {"object", "involvedObject", "name"};
+  static const char* const E_NAME[] = {"object", "metadata", "name"};
+  static const char* const E_IKIND[] = {"object", "involvedObject", "kind"};
+  static const char* const E_INAME[] = {"object", "involvedObject", "name"};
+  const char* const* P_NAME = envelope ? E_NAME : E_NAME + 1;
+  const char* const* P_IKIND = envelope ? E_IKIND : E_IKIND + 1;
+  const char* const* P_INAME = envelope ? E_INAME : E_INAME + 1;
+  const size_t d = envelope ? 3 : 2;
   Scan sc(s, n);
   std::string_view v;
   if (role == ROLE_JOB) {
-    if (!sc.find(P_NAME, 3, v)) return true;  // BOOKMARK / ERROR / unparsable: keep
-    return owner_of(r, v) == r->index;
+    if (!sc.find(P_NAME, d, v)) return OWNER_ALL;  // BOOKMARK / ERROR / unparsable
+    return owner_of(r, v);
   }
   if (role == ROLE_POD) {
     std::string_view name;
-    if (!sc.find(P_NAME, 3, name)) return true;
-    const char* P_JOB[] = {"object", "metadata", "labels", r->job_label->c_str()};
-    int owner = sc.find(P_JOB, 4, v) ? owner_of(r, v) : 0;
+    if (!sc.find(P_NAME, d, name)) return OWNER_ALL;
+    const char* E_JOB[] = {"object", "metadata", "labels", r->job_label->c_str()};
+    int owner = sc.find(envelope ? E_JOB : E_JOB + 1, d + 1, v) ? owner_of(r, v) : 0;
     std::string key(name);
     r->owners->pod[key] = owner;
     std::string_view type;
-    if (sc.find(P_TYPE, 1, type) && type == "DELETED") r->owners->gone.emplace_back(mono_s() + r->forget_after, key);
+    if (envelope && sc.find(P_TYPE, 1, type) && type == "DELETED")
+      r->owners->gone.emplace_back(mono_s() + r->forget_after, key);
     expire_owners(r);
-    return owner == r->index;
+    return owner;
   }
   if (role == ROLE_EVENT) {
     std::string_view kind;
-    if (!sc.find(P_IKIND, 3, kind)) return true;
-    if (!sc.find(P_INAME, 3, v)) return true;
-    if (kind == "Job") return owner_of(r, v) == r->index;
+    if (!sc.find(P_IKIND, d, kind)) return OWNER_ALL;
+    if (!sc.find(P_INAME, d, v)) return OWNER_ALL;
+    if (kind == "Job") return owner_of(r, v);
     if (kind == "Pod") {
       auto it = r->owners->pod.find(std::string(v));
-      return it == r->owners->pod.end() || it->second == r->index;  // unknown pod: keep (parked upstream)
+      return it == r->owners->pod.end() ? OWNER_ALL : it->second;  // unknown pod: everyone parks it
     }
-    return r->index == 0;
+    return 0;
   }
-  return true;
+  return OWNER_ALL;
+}
+
+// true = this worker owns (or must see) the watch line
+bool route_line(Router* r, int role, const char* s, size_t n) {
+  int owner = route_owner(r, role, s, n, true);
+  return owner == OWNER_ALL || owner == r->index;
 }
 
 void Router_dealloc(Router* self) {
@@ -780,6 +837,184 @@ PyGetSetDef Router_getset[] = {{"stats", reinterpret_cast<getter>(Router_stats),
                                {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 PyTypeObject RouterType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+int role_from(const char* role) {
+  if (!role) return -1;
+  return !strcmp(role, "job") ? ROLE_JOB : !strcmp(role, "pod") ? ROLE_POD : !strcmp(role, "event") ? ROLE_EVENT : -1;
+}
+
+// ------------------------------------------------------------------ watch hub splitter
+// One watch stream per replica, demultiplexed to the shard workers (parallel/watchhub.py):
+// feed(chunk) routes every complete line to its owner's output (bookmarks are consumed
+// here, errors handed back), split_list(body) does the same for a LIST body's items.
+typedef struct {
+  PyObject_HEAD
+  Router* router;
+  int role;
+  std::string* buf;
+  unsigned long long lines;
+} Splitter;
+
+void Splitter_dealloc(Splitter* self) {
+  Py_XDECREF(reinterpret_cast<PyObject*>(self->router));
+  delete self->buf;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+PyObject* Splitter_new(PyTypeObject* type, PyObject*, PyObject*) {
+  Splitter* self = reinterpret_cast<Splitter*>(type->tp_alloc(type, 0));
+  if (self) {
+    self->router = nullptr;
+    self->role = ROLE_NONE;
+    self->buf = new std::string();
+    self->lines = 0;
+  }
+  return reinterpret_cast<PyObject*>(self);
+}
+
+int Splitter_init(Splitter* self, PyObject* args, PyObject*) {
+  PyObject* r;
+  const char* role;
+  if (!PyArg_ParseTuple(args, "Os", &r, &role)) return -1;
+  if (!PyObject_TypeCheck(r, &RouterType)) {
+    PyErr_SetString(PyExc_TypeError, "router must be a ShardRouter");
+    return -1;
+  }
+  int rl = role_from(role);
+  if (rl < 0) {
+    PyErr_SetString(PyExc_ValueError, "role must be job, pod or event");
+    return -1;
+  }
+  Py_INCREF(r);
+  Py_XDECREF(reinterpret_cast<PyObject*>(self->router));
+  self->router = reinterpret_cast<Router*>(r);
+  self->role = rl;
+  return 0;
+}
+
+PyObject* bytes_list(const std::vector<std::string>& outs) {
+  PyObject* l = PyList_New(static_cast<Py_ssize_t>(outs.size()));
+  if (!l) return nullptr;
+  for (size_t w = 0; w < outs.size(); ++w) {
+    PyObject* b = PyBytes_FromStringAndSize(outs[w].data(), static_cast<Py_ssize_t>(outs[w].size()));
+    if (!b) {
+      Py_DECREF(l);
+      return nullptr;
+    }
+    PyList_SET_ITEM(l, static_cast<Py_ssize_t>(w), b);
+  }
+  return l;
+}
+
+// feed(chunk) -> (per-worker NDJSON bytes, last resourceVersion or None, [error lines])
+PyObject* Splitter_feed(Splitter* self, PyObject* arg) {
+  static const char* const P_TYPE[] = {"type"};
+  static const char* const P_RV[] = {"object", "metadata", "resourceVersion"};
+  Py_buffer view;
+  if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) != 0) return nullptr;
+  std::string& buf = *self->buf;
+  buf.append(static_cast<const char*>(view.buf), static_cast<size_t>(view.len));
+  PyBuffer_Release(&view);
+  Router* r = self->router;
+  std::vector<std::string> outs(static_cast<size_t>(r->count));
+  std::string last_rv;
+  PyObject* errors = PyList_New(0);
+  if (!errors) return nullptr;
+  size_t start = 0;
+  while (true) {
+    const void* nl = memchr(buf.data() + start, '\n', buf.size() - start);
+    if (!nl) break;
+    size_t end = static_cast<size_t>(static_cast<const char*>(nl) - buf.data());
+    const char* line = buf.data() + start;
+    size_t n = end - start;
+    start = end + 1;
+    if (n == 0 || (n == 1 && line[0] == '\r')) continue;
+    ++self->lines;
+    Scan sc(line, n);
+    std::string_view type, rv;
+    sc.find(P_TYPE, 1, type);
+    if (sc.find(P_RV, 3, rv)) last_rv.assign(rv.data(), rv.size());
+    if (type == "BOOKMARK") continue;
+    if (type == "ERROR") {
+      PyObject* b = PyBytes_FromStringAndSize(line, static_cast<Py_ssize_t>(n));
+      if (!b || PyList_Append(errors, b) != 0) {
+        Py_XDECREF(b);
+        Py_DECREF(errors);
+        return nullptr;
+      }
+      Py_DECREF(b);
+      continue;
+    }
+    int owner = route_owner(r, self->role, line, n, true);
+    if (owner == OWNER_ALL) {
+      for (auto& o : outs) {
+        o.append(line, n);
+        o += '\n';
+      }
+      ++r->passed;
+    } else {
+      outs[static_cast<size_t>(owner)].append(line, n);
+      outs[static_cast<size_t>(owner)] += '\n';
+      r->dropped += static_cast<unsigned long long>(r->count - 1);
+    }
+  }
+  buf.erase(0, start);
+  PyObject* l = bytes_list(outs);
+  if (!l) {
+    Py_DECREF(errors);
+    return nullptr;
+  }
+  PyObject* rvo = last_rv.empty() ? (Py_INCREF(Py_None), Py_None)
+                                  : PyUnicode_FromStringAndSize(last_rv.data(), static_cast<Py_ssize_t>(last_rv.size()));
+  return Py_BuildValue("(NNN)", l, rvo, errors);
+}
+
+// split_list(body) -> (resourceVersion, per-worker JSON arrays of the LIST's items)
+PyObject* Splitter_split_list(Splitter* self, PyObject* arg) {
+  Py_buffer view;
+  if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) != 0) return nullptr;
+  const char* s = static_cast<const char*>(view.buf);
+  Scan sc(s, static_cast<size_t>(view.len));
+  std::string_view rv;
+  std::vector<std::pair<size_t, size_t>> items;
+  if (!sc.list_items(rv, items)) {
+    PyBuffer_Release(&view);
+    PyErr_SetString(PyExc_ValueError, "not a LIST body with an items array");
+    return nullptr;
+  }
+  Router* r = self->router;
+  std::vector<std::string> outs(static_cast<size_t>(r->count), std::string("["));
+  for (auto& it : items) {
+    int owner = route_owner(r, self->role, s + it.first, it.second - it.first, false);
+    for (int w = 0; w < r->count; ++w) {
+      if (owner != OWNER_ALL && owner != w) continue;
+      std::string& o = outs[static_cast<size_t>(w)];
+      if (o.size() > 1) o += ',';
+      o.append(s + it.first, it.second - it.first);
+    }
+  }
+  for (auto& o : outs) o += ']';
+  std::string rvs(rv);
+  PyBuffer_Release(&view);
+  PyObject* l = bytes_list(outs);
+  if (!l) return nullptr;
+  return Py_BuildValue("(s#N)", rvs.data(), static_cast<Py_ssize_t>(rvs.size()), l);
+}
+
+PyObject* Splitter_reset(Splitter* self, PyObject*) {
+  self->buf->clear();
+  Py_RETURN_NONE;
+}
+
+PyMethodDef Splitter_methods[] = {
+    {"feed", reinterpret_cast<PyCFunction>(Splitter_feed), METH_O,
+     "Route complete watch lines: (per-worker bytes, last resourceVersion, error lines)"},
+    {"split_list", reinterpret_cast<PyCFunction>(Splitter_split_list), METH_O,
+     "Split a LIST body: (resourceVersion, per-worker JSON item arrays)"},
+    {"reset", reinterpret_cast<PyCFunction>(Splitter_reset), METH_NOARGS, "Drop a partial line"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyTypeObject SplitterType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
 // ------------------------------------------------------------------ Python type
 typedef struct {
@@ -911,8 +1146,7 @@ PyObject* Decoder_set_router(Decoder* self, PyObject* args) {
     PyErr_SetString(PyExc_TypeError, "router must be a ShardRouter");
     return nullptr;
   }
-  int rl = role == nullptr ? ROLE_NONE : !strcmp(role, "job") ? ROLE_JOB : !strcmp(role, "pod") ? ROLE_POD
-                                                               : !strcmp(role, "event") ? ROLE_EVENT : -1;
+  int rl = role == nullptr ? ROLE_NONE : role_from(role);
   if (rl < 0) {
     PyErr_SetString(PyExc_ValueError, "role must be job, pod or event");
     return nullptr;
@@ -984,11 +1218,22 @@ PyMODINIT_FUNC PyInit__kube_native(void) {
   RouterType.tp_getset = Router_getset;
   RouterType.tp_doc = "ShardRouter(index, count, seed, job_label='batch.kubernetes.io/job-name', forget_after=120.0)";
   if (PyType_Ready(&RouterType) < 0) return nullptr;
+  SplitterType.tp_name = "_kube_native.WatchSplitter";
+  SplitterType.tp_basicsize = sizeof(Splitter);
+  SplitterType.tp_flags = Py_TPFLAGS_DEFAULT;
+  SplitterType.tp_new = Splitter_new;
+  SplitterType.tp_init = reinterpret_cast<initproc>(Splitter_init);
+  SplitterType.tp_dealloc = reinterpret_cast<destructor>(Splitter_dealloc);
+  SplitterType.tp_methods = Splitter_methods;
+  SplitterType.tp_doc = "WatchSplitter(router, role) — demultiplex one watch stream / LIST body to shard workers";
+  if (PyType_Ready(&SplitterType) < 0) return nullptr;
   PyObject* m = PyModule_Create(&moddef);
   if (!m) return nullptr;
   Py_INCREF(&DecoderType);
   PyModule_AddObject(m, "ProjectedDecoder", reinterpret_cast<PyObject*>(&DecoderType));
   Py_INCREF(&RouterType);
   PyModule_AddObject(m, "ShardRouter", reinterpret_cast<PyObject*>(&RouterType));
+  Py_INCREF(&SplitterType);
+  PyModule_AddObject(m, "WatchSplitter", reinterpret_cast<PyObject*>(&SplitterType));
   return m;
 }

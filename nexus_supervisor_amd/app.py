@@ -175,6 +175,7 @@ class ShardedApplication:
         self.store = None
         self.elector = None
         self.http = None
+        self.hub = None
         self._stopped = asyncio.Event()
 
     async def start(self) -> None:
@@ -183,6 +184,17 @@ class ShardedApplication:
                       store=cfg.cql_store_type, worker_processes=self.pool.count)
         le = cfg.leader_election
         await self.pool.start(active=not le.enabled)
+        if self.pool.hub:
+            from .parallel.watchhub import WatchHub
+
+            if self.kube is None:
+                from .kube.client import KubeClient, KubeConfig
+
+                self.kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+            self.hub = WatchHub(cfg, self.kube, self.pool.count, self.pool.send_data, self.pool.data_buffered,
+                                self.pool.data_drain, metrics=self.metrics)
+            self.pool.on_restart = lambda _index: self.hub.resync()
+            self.hub.start()
         if cfg.observability.http_port:
             from .obs.http import ObsServer
 
@@ -217,6 +229,8 @@ class ShardedApplication:
     async def stop(self, drain_timeout: float = 10.0) -> None:
         if self.elector is not None:
             await self.elector.stop(release=True)
+        if self.hub is not None:
+            await self.hub.stop()
         await self.pool.stop(drain_timeout)
         self.merged_metrics = self.pool.merged_metrics(self.metrics)
         if self.http is not None:

@@ -165,6 +165,9 @@ class RuntimeConfig:
     worker_processes: int = field(default=1, metadata=_k("worker-processes"))
     # set by the coordinator in each worker process (not a user knob)
     worker_index: int = field(default=0, metadata=_k("worker-index"))
+    # with worker processes: the parent holds one LIST+WATCH per kind and routes each object
+    # to its owner worker (parallel/watchhub.py) instead of every worker watching everything
+    watch_hub: bool = field(default=True, metadata=_k("watch-hub"))
 
 
 @dataclass

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import asyncio
 import base64
+import contextlib
 import json
 import logging
 import os
@@ -297,6 +298,24 @@ class KubeClient:
             if r.status >= 400:
                 raise from_status(r.status, doc)
             return doc
+
+    async def get_raw(self, path: str, params: Optional[Dict[str, str]] = None,
+                      timeout: Optional[float] = None) -> Tuple[int, bytes]:
+        """GET returning ``(status, raw body)`` (the watch hub splits LIST bodies natively)."""
+        s = await self._s()
+        self.requests += 1
+        async with s.get(self.config.server + path, params=params, headers=self._headers(),
+                         timeout=aiohttp.ClientTimeout(total=timeout or max(60.0, self.request_timeout))) as r:
+            return r.status, await r.read()
+
+    @contextlib.asynccontextmanager
+    async def stream(self, path: str, params: Optional[Dict[str, str]] = None, timeout: float = 330.0):
+        """Streaming GET (a watch); yields the response, its ``content`` read raw."""
+        s = await self._s()
+        self.requests += 1
+        async with s.get(self.config.server + path, params=params, headers=self._headers(),
+                         timeout=aiohttp.ClientTimeout(total=timeout, sock_read=timeout)) as r:
+            yield r
 
     # ------------------------------------------------------------------ typed helpers
     async def list(self, kind: str, namespace: Optional[str], *, label_selector: str = "", field_selector: str = "",

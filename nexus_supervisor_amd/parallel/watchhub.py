@@ -1,0 +1,265 @@
+"""One watch per replica, demultiplexed to the shard workers.
+
+With ``runtime.worker-processes`` = K and no hub, every worker would hold its own
+Event/Pod/Job LIST+WATCH: the API server serialises and sends every change K times per
+replica, and every worker scans every line.  The reference's single Go process holds
+one watch per kind (``/root/reference/services/supervisor.go:73-75``); so does this
+replica.  The parent process runs the hub:
+
+* per kind, LIST then WATCH from the list's resourceVersion against the API server
+  (same label selectors and timeouts as the informers would use);
+* the native :class:`_kube_native.WatchSplitter` routes each LIST item and each watch
+  line to the worker that owns it (``crc32(job name)``, the same placement as
+  :mod:`.workers`), consuming bookmarks and handing errors back; a chunk costs one C
+  call however many lines it holds;
+* routed bytes go to the worker over a per-worker data socket as length-prefixed
+  frames: ``SNAPSHOT`` (resourceVersion + the worker's items as a JSON array) and
+  ``LINES`` (NDJSON watch lines); the hub pauses reading the API server while any
+  worker's socket buffer is above a high-water mark (back-pressure end to end);
+* on ``410 Gone`` / stream errors the hub re-lists and sends every worker a fresh
+  snapshot; a worker's :class:`HubListWatch` turns that into the informer's 410 →
+  re-list path, so the informer's diff logic is unchanged.  A restarted worker gets a
+  fresh snapshot the same way (:meth:`WatchHub.resync`).
+
+Frame: ``!BBI`` (type, kind index, payload length) + payload.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import struct
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+from ..informer.informer import ListWatch
+from ..models.kube import PROJECTIONS, watch_projection
+
+log = logging.getLogger("nexus_supervisor_amd.watchhub")
+
+KINDS: Tuple[str, ...] = ("Event", "Pod", "Job")
+ROLES = {"Event": "event", "Pod": "pod", "Job": "job"}
+SNAPSHOT, LINES = 1, 2
+HEADER = struct.Struct("!BBI")
+HIGH_WATER = 32 << 20
+
+
+class _Gone(Exception):
+    pass
+
+
+def _is_gone(line: bytes) -> bool:
+    import json
+
+    try:
+        return (json.loads(line).get("object") or {}).get("code") == 410
+    except ValueError:
+        return False
+
+
+class WatchHub:
+    """Parent side: ``send(worker, frame_type, kind_index, payload)`` delivers a frame and
+    ``buffered(worker)`` reports the bytes still queued for it."""
+
+    def __init__(self, cfg, kube, count: int, send: Callable[[int, int, int, bytes], None],
+                 buffered: Callable[[int], int], drain: Callable[[int], Any], metrics=None):
+        from .. import _kube_native
+        from .workers import _SEED
+
+        self.cfg = cfg
+        self.kube = kube
+        self.count = count
+        self.send = send
+        self.buffered = buffered
+        self.drain = drain
+        self.metrics = metrics
+        self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label)
+        self.tasks: Dict[str, asyncio.Task] = {}
+        self.relists = 0
+        self.bytes_routed = 0
+        self.selector = (f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
+                         if cfg.informer_label_selector else "")
+
+    def start(self) -> None:
+        for i, kind in enumerate(KINDS):
+            if kind not in self.tasks:
+                self.tasks[kind] = asyncio.create_task(self._pump(i, kind), name=f"watchhub-{kind}")
+
+    async def stop(self) -> None:
+        tasks = list(self.tasks.values())
+        self.tasks.clear()
+        for t in tasks:
+            t.cancel()
+        for t in tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+
+    async def resync(self) -> None:
+        """Re-list every kind and send every worker a fresh snapshot (a restarted worker
+        has an empty cache; the others apply the relist diff, which is idempotent)."""
+        await self.stop()
+        self.start()
+
+    def _path_params(self, kind: str) -> Tuple[str, Dict[str, str]]:
+        from ..kube.client import resource_path
+
+        params: Dict[str, str] = {}
+        if kind in ("Pod", "Job") and self.selector:
+            params["labelSelector"] = self.selector
+        return resource_path(kind, self.cfg.resource_namespace), params
+
+    async def _route(self, ki: int, outs: List[bytes], ftype: int, prefix: bytes = b"") -> None:
+        for w, b in enumerate(outs):
+            if b or ftype == SNAPSHOT:
+                payload = prefix + b if prefix else b
+                self.send(w, ftype, ki, payload)
+                self.bytes_routed += len(payload)
+        for w in range(self.count):
+            if self.buffered(w) > HIGH_WATER:
+                await self.drain(w)
+
+    async def _pump(self, ki: int, kind: str) -> None:
+        from .. import _kube_native
+
+        splitter = _kube_native.WatchSplitter(self.router, ROLES[kind])
+        path, base = self._path_params(kind)
+        backoff = 0.2
+        rv = ""
+        while True:
+            try:
+                status, body = await self.kube.get_raw(path, base)
+                if status >= 400:
+                    raise RuntimeError(f"LIST {kind}: HTTP {status}")
+                rv, parts = splitter.split_list(body)
+                self.relists += 1
+                if self.metrics is not None:
+                    self.metrics.inc("watchhub_relists", labels={"kind": kind})
+                await self._route(ki, parts, SNAPSHOT, rv.encode() + b"\n")
+                backoff = 0.2
+                while True:
+                    params = dict(base, watch="1", resourceVersion=rv, allowWatchBookmarks="true",
+                                  timeoutSeconds=str(int(self.cfg.watch_timeout)))
+                    splitter.reset()
+                    async with self.kube.stream(path, params, timeout=self.cfg.watch_timeout + 30) as resp:
+                        if resp.status == 410:
+                            raise _Gone()
+                        if resp.status >= 400:
+                            raise RuntimeError(f"WATCH {kind}: HTTP {resp.status}")
+                        async for chunk in resp.content.iter_any():
+                            outs, last, errors = splitter.feed(chunk)
+                            if last:
+                                rv = last
+                            if any(outs):
+                                await self._route(ki, outs, LINES)
+                            if errors:
+                                if any(_is_gone(e) for e in errors):
+                                    raise _Gone()
+                                log.warning("%s watch error: %s", kind, errors[0][:300])
+                                break
+            except asyncio.CancelledError:
+                raise
+            except _Gone:
+                log.info("%s watch expired at rv=%s: re-listing", kind, rv)
+                continue
+            except Exception as exc:  # noqa: BLE001 - connection errors: back off and re-list
+                log.warning("%s hub list/watch failed: %s; retrying in %.1fs", kind, exc, backoff)
+                await asyncio.sleep(backoff)
+                backoff = min(backoff * 2, 30.0)
+
+
+class HubFeed:
+    """Worker side: reads the parent's frames and queues them per kind in arrival order."""
+
+    def __init__(self):
+        self.queues: Dict[int, asyncio.Queue] = {i: asyncio.Queue() for i in range(len(KINDS))}
+        self._task: Optional[asyncio.Task] = None
+        self.frames = 0
+
+    async def start(self, sock) -> None:
+        reader, self._writer = await asyncio.open_connection(sock=sock, limit=1 << 20)
+        self._task = asyncio.create_task(self._read(reader), name="watchhub-feed")
+
+    async def _read(self, reader: asyncio.StreamReader) -> None:
+        hs = HEADER.size
+        try:
+            while True:
+                hdr = await reader.readexactly(hs)
+                ftype, ki, n = HEADER.unpack(hdr)
+                payload = await reader.readexactly(n) if n else b""
+                self.frames += 1
+                q = self.queues.get(ki)
+                if q is not None:
+                    q.put_nowait((ftype, payload))
+        except (asyncio.IncompleteReadError, ConnectionError):
+            for q in self.queues.values():
+                q.put_nowait((0, b""))  # parent gone: informers stop on the closed feed
+
+    def list_watch(self, kind: str) -> "HubListWatch":
+        return HubListWatch(kind, self.queues[KINDS.index(kind)])
+
+    async def close(self) -> None:
+        if self._task is not None:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):
+                pass
+        w = getattr(self, "_writer", None)
+        if w is not None:
+            w.close()
+
+
+class HubListWatch(ListWatch):
+    """Informer transport fed by the parent's hub: ``list()`` returns the next snapshot,
+    ``watch()`` yields routed lines until a newer snapshot arrives (then reports 410 so
+    the informer re-lists, i.e. takes that snapshot)."""
+
+    def __init__(self, kind: str, queue: asyncio.Queue):
+        from .. import _kube_native
+
+        self.kind = kind
+        self.queue = queue
+        proj = PROJECTIONS.get(kind)
+        self._list_decoder = _kube_native.ProjectedDecoder(True if proj is None else ["list", proj])
+        self._watch_proj = watch_projection(kind)
+        self._pending: Optional[bytes] = None
+        self.transform = None
+
+    async def list(self) -> Tuple[List[Dict[str, Any]], str]:
+        while self._pending is None:
+            ftype, payload = await self.queue.get()
+            if ftype == SNAPSHOT:
+                self._pending = payload
+            elif ftype == 0:
+                raise ConnectionError("watch hub closed")
+            # LINES before a snapshot belong to the stream it replaces: dropped
+        payload, self._pending = self._pending, None
+        nl = payload.index(b"\n")
+        rv = payload[:nl].decode()
+        items = self._list_decoder.decode(payload[nl + 1:])
+        for it in items:
+            it.setdefault("kind", self.kind)
+        return items, rv
+
+    async def watch(self, resource_version: str):
+        from .. import _kube_native
+
+        decoder = _kube_native.ProjectedDecoder(self._watch_proj)
+        kind = self.kind
+        n = 0
+        while True:
+            ftype, payload = await self.queue.get()
+            if ftype == SNAPSHOT:
+                self._pending = payload
+                yield "ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": "hub re-listed"}
+                return
+            if ftype == 0:
+                raise ConnectionError("watch hub closed")
+            for ev in decoder.feed(payload):
+                obj = ev.get("object") or {}
+                if obj.get("kind") is None:
+                    obj["kind"] = kind
+                yield ev.get("type", ""), obj
+                n += 1
+                if n % 64 == 0:
+                    await asyncio.sleep(0)

@@ -225,7 +225,7 @@ class Channel:
 
 # ---------------------------------------------------------------------- parent side
 class _Worker:
-    __slots__ = ("index", "proc", "chan", "synced", "state", "reader", "exited", "sock")
+    __slots__ = ("index", "proc", "chan", "synced", "state", "reader", "exited", "sock", "data")
 
     def __init__(self, index: int):
         self.index = index
@@ -236,6 +236,7 @@ class _Worker:
         self.reader: Optional[asyncio.Task] = None
         self.exited = asyncio.Event()
         self.sock: Optional[socket.socket] = None
+        self.data: Optional[asyncio.StreamWriter] = None  # watch-hub frames to this worker
 
 
 class WorkerPool:
@@ -259,6 +260,8 @@ class WorkerPool:
         self._metrics_waiters: Dict[int, Tuple[asyncio.Future, set]] = {}
         self.restarts = 0
         self.restart_backoff = (0.2, 10.0)  # base, max seconds between restarts of one worker
+        self.hub = bool(cfg.runtime.watch_hub)
+        self.on_restart: Optional[Callable[[int], Any]] = None  # async callback (watch hub resync)
         self._stopping = False
         self._watchdog: Optional[asyncio.Task] = None
 
@@ -307,10 +310,17 @@ class WorkerPool:
                     w.reader.cancel()
                 if w.chan is not None:
                     w.chan.close()
+                if w.data is not None:
+                    w.data.close()
                 await self._spawn(w)
+                if self.on_restart is not None:
+                    await self.on_restart(w.index)
 
     async def _spawn(self, w: _Worker) -> None:
         parent, child = socket.socketpair()
+        dparent = dchild = None
+        if self.hub:
+            dparent, dchild = socket.socketpair()
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(self.env if self.env is not None else os.environ)
         env["PYTHONPATH"] = os.pathsep.join(p for p in [pkg_root, env.get("PYTHONPATH", "")] if p)
@@ -318,18 +328,28 @@ class WorkerPool:
         env["NEXUS_WORKER_CTL_FD"] = str(child.fileno())
         env["NEXUS_WORKER_START_ACTIVE"] = "1" if self.active else "0"
         env["NEXUS_WORKER_REPORT"] = "1" if self.report_decisions else "0"
+        fds = [child.fileno()]
+        if dchild is not None:
+            env["NEXUS_WORKER_DATA_FD"] = str(dchild.fileno())
+            fds.append(dchild.fileno())
+        else:
+            env.pop("NEXUS_WORKER_DATA_FD", None)
         out = None
         if self.log_dir:
             out = open(os.path.join(self.log_dir, f"worker-{w.index}.log"), "ab")
         try:
             w.proc = subprocess.Popen([self.python, "-m", "nexus_supervisor_amd", "worker"], env=env,
-                                      pass_fds=(child.fileno(),), stdout=out, stderr=out)
+                                      pass_fds=tuple(fds), stdout=out, stderr=out)
         finally:
             child.close()
+            if dchild is not None:
+                dchild.close()
             if out is not None:
                 out.close()
         w.sock = parent
         w.chan = await Channel.open(parent)
+        if dparent is not None:
+            _r, w.data = await asyncio.open_connection(sock=dparent)
         w.synced.clear()
         w.exited.clear()
         w.reader = asyncio.create_task(self._read(w), name=f"worker-{w.index}-ctl")
@@ -366,6 +386,27 @@ class WorkerPool:
             pending.discard(w.index)
             if not pending and not fut.done():
                 fut.set_result(None)
+
+    # ---- watch-hub data path (parallel/watchhub.py)
+    def send_data(self, index: int, ftype: int, kind: int, payload: bytes) -> None:
+        from .watchhub import HEADER
+
+        d = self.workers[index].data
+        if d is not None and not d.is_closing():
+            d.write(HEADER.pack(ftype, kind, len(payload)))
+            d.write(payload)
+
+    def data_buffered(self, index: int) -> int:
+        d = self.workers[index].data
+        return d.transport.get_write_buffer_size() if d is not None and not d.is_closing() else 0
+
+    async def data_drain(self, index: int) -> None:
+        d = self.workers[index].data
+        if d is not None and not d.is_closing():
+            try:
+                await d.drain()
+            except ConnectionError:
+                pass
 
     def set_active(self, active: bool) -> None:
         self.active = active
@@ -457,6 +498,8 @@ class WorkerPool:
                     pass
             if w.chan is not None:
                 w.chan.close()
+            if w.data is not None:
+                w.data.close()
 
 
 # ---------------------------------------------------------------------- worker side
@@ -471,12 +514,28 @@ def _set_pdeathsig() -> None:
 
 
 async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, report: bool = False,
-                     logger=None, metrics: Optional[Metrics] = None, app_factory=None) -> int:
+                     logger=None, metrics: Optional[Metrics] = None, app_factory=None,
+                     data_sock: Optional[socket.socket] = None) -> int:
     """Body of one shard-worker process (also callable in-process by tests)."""
     from ..app import Application
 
     chan = await Channel.open(sock)
-    app = (app_factory or Application)(cfg, logger=logger, metrics=metrics)
+    feed = None
+    if data_sock is not None:
+        # watch-hub mode: informers are fed by the parent's routed stream; the worker still
+        # talks to the API server itself for Job DELETEs
+        from ..informer import InformerFactory
+        from ..kube.client import KubeClient, KubeConfig
+        from .watchhub import KINDS, HubFeed
+
+        feed = HubFeed()
+        await feed.start(data_sock)
+        kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+        factory = InformerFactory(lambda kind: feed.list_watch(kind) if kind in KINDS else None,
+                                  resync_period=cfg.resync_period)
+        app = (app_factory or Application)(cfg, kube=kube, factory=factory, logger=logger, metrics=metrics)
+    else:
+        app = (app_factory or Application)(cfg, logger=logger, metrics=metrics)
     sup = app.supervisor
     sup.active = start_active
     batch: List[list] = []
@@ -525,6 +584,8 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
     finally:
         sync_task.cancel()
         await app.stop(drain_timeout=drain)
+        if feed is not None:
+            await feed.close()
         flush()
         send_metrics(-1)
         chan.send({"op": "exit"})
@@ -558,8 +619,10 @@ def worker_main() -> int:
         loop = asyncio.get_running_loop()
         for sig in (signal.SIGTERM, signal.SIGINT):
             loop.add_signal_handler(sig, sock.shutdown, socket.SHUT_RD)  # → EOF → drain and exit
+        dfd = os.environ.get("NEXUS_WORKER_DATA_FD")
         return await run_worker(cfg, sock, start_active=os.environ.get("NEXUS_WORKER_START_ACTIVE", "1") == "1",
-                                report=os.environ.get("NEXUS_WORKER_REPORT", "0") == "1", logger=log, metrics=metrics)
+                                report=os.environ.get("NEXUS_WORKER_REPORT", "0") == "1", logger=log, metrics=metrics,
+                                data_sock=socket.socket(fileno=int(dfd)) if dfd else None)
 
     prof_path = os.environ.get("NEXUS_WORKER_CPROFILE")
     if not prof_path:

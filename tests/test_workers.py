@@ -134,8 +134,47 @@ def test_config_handoff_and_admission_split():
         load_config(path=None, env={}, overrides={"runtime": {"worker-processes": 2, "worker-index": 2}})
 
 
+def test_watch_splitter_routes_lines_and_list_items():
+    labels = LabelConfig()
+    router = _kube_native.ShardRouter(0, 3, _SEED, JOB_LABEL)
+    rids = [f"job-{i}" for i in range(30)]
+    pods = [make_pod(r, labels) for r in rids]
+    sp_pod = _kube_native.WatchSplitter(router, "pod")
+    sp_ev = _kube_native.WatchSplitter(router, "event")
+    body = _kube_native.dumps({"kind": "PodList", "apiVersion": "v1", "metadata": {"resourceVersion": "4242"},
+                               "items": pods})
+    rv, parts = sp_pod.split_list(body)
+    assert rv == "4242" and len(parts) == 3
+    for w, part in enumerate(parts):
+        names = {p["metadata"]["labels"][JOB_LABEL] for p in json.loads(part)}
+        assert names == {r for r in rids if worker_of(r, 3) == w}
+    # a chunk boundary in the middle of a line: the tail waits for the next feed
+    stream = b"".join(_line("MODIFIED", p) for p in pods[:10])
+    stream += b'{"type":"BOOKMARK","object":{"kind":"Pod","metadata":{"resourceVersion":"9999"}}}\n'
+    outs1, last1, err1 = sp_pod.feed(stream[:-40])
+    outs2, last2, err2 = sp_pod.feed(stream[-40:])
+    assert last2 == "9999" and not err1 and not err2  # bookmark consumed, its RV reported
+    got = [b"".join(x) for x in zip(outs1, outs2)]
+    for w in range(3):
+        lines = [json.loads(l) for l in got[w].splitlines()]
+        assert {l["object"]["metadata"]["labels"][JOB_LABEL] for l in lines} == \
+            {r for r in rids[:10] if worker_of(r, 3) == w}
+    # Pod events follow their pod's owner; unknown pods go everywhere; errors come back
+    evs = [make_event("Pod", pods[0]["metadata"]["name"], "BackOff"), make_event("Pod", "ghost", "Failed")]
+    outs, last, errs = sp_ev.feed(b"".join(_line("ADDED", e) for e in evs)
+                                  + b'{"type":"ERROR","object":{"kind":"Status","code":410}}\n')
+    owner = worker_of(rids[0], 3)
+    for w in range(3):
+        names = [json.loads(l)["object"]["involvedObject"]["name"] for l in outs[w].splitlines()]
+        assert names == ([pods[0]["metadata"]["name"], "ghost"] if w == owner else ["ghost"])
+    assert len(errs) == 1 and json.loads(errs[0])["object"]["code"] == 410
+    with pytest.raises(ValueError):
+        sp_pod.split_list(b'{"kind":"Status"}')
+
+
 @pytest.mark.slow
-def test_two_worker_replica_reference_parity(arun, tmp_path):
+@pytest.mark.parametrize("hub", [True, False], ids=["watch-hub", "per-worker-watch"])
+def test_two_worker_replica_reference_parity(arun, tmp_path, hub):
     scenarios = reference_scenarios()
 
     async def go():
@@ -149,7 +188,7 @@ def test_two_worker_replica_reference_parity(arun, tmp_path):
             cfg = load_config(path=None, env={}, overrides={
                 "cql-store-type": "scylla", "workers": 8, "rate-limit-elements-per-second": 0, "resync-period": "0s",
                 "kube-config-path": str(kc), "scylla-cql-store": {"hosts": f"127.0.0.1:{srv.port}"},
-                "runtime": {"worker-processes": 2}, "observability": {"http-port": 0}})
+                "runtime": {"worker-processes": 2, "watch-hub": hub}, "observability": {"http-port": 0}})
             app = ShardedApplication(cfg, report_decisions=True, log_dir=str(tmp_path))
             decisions = []
             app.supervisor.decision_hooks.append(decisions.append)
@@ -176,10 +215,22 @@ def test_two_worker_replica_reference_parity(arun, tmp_path):
                     sum(v for k, v in m.counters.get("decisions_applied", {}).items()) >= 7
                 objs = {k: v for k, v in m.gauges.get("informer_objects", {}).items() if ("kind", "Job") in k}
                 assert len(objs) == 2  # one gauge per worker: each caches only its own runs
-                # new failure while running: routed to its owner worker
-                pod = make_pod("df1b6e8d-cc3c-fb5b-a3f6-5d7b9e2c7f2b", cfg.labels)  # CANCELLED seed row
-                await ctl.apply([("ADDED", make_event("Pod", pod["metadata"]["name"], "BackOff"))])
-                await asyncio.sleep(0.3)
+                st = await ctl.stats()
+                assert st["watch_requests"] == (3 if hub else 6)  # one watch per kind per replica with the hub
+                # a compaction that overtakes the streams: 410 → (hub) re-list → fresh snapshots
+                late = [make_job(f"late-{i}", cfg.labels) for i in range(6)]
+                await ctl.apply([("ADDED", j) for j in late], expire=True)
+                live = (await ctl.stats())["objects"]["Job"]
+                for _ in range(300):
+                    m = await app.refresh_metrics()
+                    jobs = sum(v for k, v in m.gauges.get("informer_objects", {}).items() if ("kind", "Job") in k)
+                    if jobs == live and (not hub or app.hub.relists >= 4):
+                        break
+                    await asyncio.sleep(0.05)
+                assert jobs == live  # every live Job cached by exactly one worker after the re-list
+                if hub:
+                    assert app.hub.relists >= 4  # 3 initial LISTs + the Job 410 re-list
+                assert live >= 6
             finally:
                 await app.stop(drain_timeout=5)
                 await store.close()
