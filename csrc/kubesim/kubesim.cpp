@@ -43,6 +43,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -236,6 +237,7 @@ struct Obj {
   std::shared_ptr<const std::string> json;
   std::shared_ptr<const Attrs> attrs;
   std::string ns, name, job;  // job: batch.kubernetes.io/job-name label (pods)
+  std::string uid, created;   // kept so an update that omits them can be completed by splicing
   int64_t rv = 0;
   size_t rv_off = std::string::npos;  // offset of the resourceVersion digits in *json
   size_t rv_len = 0;
@@ -299,6 +301,7 @@ std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x0
 int64_t g_rv = 1000;
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0;
+  uint64_t loops = 0, sends = 0, send_bytes = 0, eagain = 0;
 } g_stats;
 
 struct Snapshot {
@@ -340,6 +343,14 @@ void record(int kind, const char* etype, const Obj& o) {
 // `src` is the text `doc` was parsed from: when nothing but the resourceVersion changes
 // (the usual case for fully-formed objects) the new text is spliced instead of re-dumped.
 Obj finish(int kind, Value& doc, const Obj* prev, std::string_view src = {}) {
+  // Text edits against `src` (offset, bytes removed, text inserted) when the object only
+  // needs server-owned metadata filled in; anything else falls back to a DOM re-dump.
+  struct Edit {
+    size_t off, del;
+    std::string ins;
+    bool rv;
+  };
+  std::vector<Edit> edits;
   bool dirty = src.empty();
   if (!doc.get("kind")) {
     doc.at("kind") = Value::str(KINDS[kind].kind);
@@ -349,37 +360,47 @@ Obj finish(int kind, Value& doc, const Obj* prev, std::string_view src = {}) {
     doc.at("apiVersion") = Value::str(KINDS[kind].api_version);
     dirty = true;
   }
-  if (!doc.get("metadata")) dirty = true;
+  const Value* md0 = doc.get("metadata");
+  if (!md0 || md0->t != Value::OBJ || md0->o.empty()) dirty = true;
   Value& md = doc.at("metadata");
+  const size_t md_open = md.src_off + 1;  // just after the metadata object's '{'
   if (md.path({"name"}).empty()) {
     dirty = true;
     std::string gen(md.path({"generateName"}));
     md.at("name") = Value::str(gen + random_suffix(5));
   }
+  Obj o;
   const Value* uid = md.get("uid");
   if (!uid || uid->t != Value::STR || uid->s.empty()) {
-    dirty = true;
-    std::string u;
-    if (prev) {
-      Value pv = kjson::parse(*prev->json);
-      u = std::string(pv.path({"metadata", "uid"}));
-      std::string ct(pv.path({"metadata", "creationTimestamp"}));
-      if (!ct.empty() && !md.get("creationTimestamp")) md.at("creationTimestamp") = Value::str(ct);
+    std::string u = prev ? prev->uid : std::string();
+    if (prev && !prev->created.empty() && !md.get("creationTimestamp")) {
+      md.at("creationTimestamp") = Value::str(prev->created);
+      edits.push_back({md_open, 0, "\"creationTimestamp\":\"" + prev->created + "\",", false});
     }
-    md.at("uid") = Value::str(u.empty() ? uuid4() : u);
+    if (u.empty()) u = uuid4();
+    md.at("uid") = Value::str(u);
+    edits.push_back({md_open, 0, "\"uid\":\"" + u + "\",", false});
   }
   if (!md.get("creationTimestamp")) {
-    md.at("creationTimestamp") = Value::str(now_rfc3339());
-    dirty = true;
+    std::string ts = now_rfc3339();
+    md.at("creationTimestamp") = Value::str(ts);
+    edits.push_back({md_open, 0, "\"creationTimestamp\":\"" + ts + "\",", false});
   }
-  Obj o;
   o.rv = ++g_rv;
+  std::string rvs = std::to_string(o.rv);
   const Value* old_rv = md.get("resourceVersion");
-  if (!old_rv || old_rv->t != Value::STR || old_rv->escaped) dirty = true;
-  size_t splice_off = dirty ? 0 : old_rv->src_off, splice_len = dirty ? 0 : old_rv->src_len;
-  md.at("resourceVersion") = Value::str(std::to_string(o.rv));
+  if (!old_rv) {
+    edits.push_back({md_open, 0, "\"resourceVersion\":\"" + rvs + "\",", true});
+  } else if (old_rv->t != Value::STR || old_rv->escaped) {
+    dirty = true;
+  } else {
+    edits.push_back({old_rv->src_off, old_rv->src_len, rvs, true});
+  }
+  md.at("resourceVersion") = Value::str(rvs);
   o.ns = std::string(md.path({"namespace"}));
   o.name = std::string(md.path({"name"}));
+  o.uid = std::string(md.path({"uid"}));
+  o.created = std::string(md.path({"creationTimestamp"}));
   if (kind == K_POD) {
     const Value* labels = md.get("labels");
     const Value* j = labels ? labels->get("batch.kubernetes.io/job-name") : nullptr;
@@ -389,20 +410,336 @@ Obj finish(int kind, Value& doc, const Obj* prev, std::string_view src = {}) {
   if (dirty) {
     o.json = std::make_shared<const std::string>(kjson::dump(doc));
     locate_rv(o);
-  } else {
-    // src holds the text doc was parsed from (offsets are relative to src)
-    size_t b = doc.src_off, e = static_cast<size_t>(doc.src_off) + doc.src_len;
-    std::string r = std::to_string(o.rv);
-    auto j = std::make_shared<std::string>();
-    j->reserve(e - b + 8);
-    j->append(src.data() + b, splice_off - b);
-    j->append(r);
-    j->append(src.data() + splice_off + splice_len, e - splice_off - splice_len);
-    o.json = std::move(j);
-    o.rv_off = splice_off - b;
-    o.rv_len = r.size();
+    return o;
   }
+  // src holds the text doc was parsed from (offsets are relative to src)
+  std::stable_sort(edits.begin(), edits.end(), [](const Edit& a, const Edit& b) { return a.off < b.off; });
+  size_t b = doc.src_off, e = static_cast<size_t>(doc.src_off) + doc.src_len, at = b;
+  auto j = std::make_shared<std::string>();
+  j->reserve(e - b + 128);
+  for (auto& ed : edits) {
+    j->append(src.data() + at, ed.off - at);
+    if (ed.rv) {
+      size_t q = ed.ins.find(rvs);  // digits position inside the inserted text
+      o.rv_off = j->size() + (ed.del ? 0 : q);
+      o.rv_len = rvs.size();
+    }
+    j->append(ed.ins);
+    at = ed.off + ed.del;
+  }
+  j->append(src.data() + at, e - at);
+  o.json = std::move(j);
   return o;
+}
+
+void index_pod(const Obj& o, bool add);
+bool remove(int kind, const std::string& ns, const std::string& name, const std::string& propagation);
+
+// ------------------------------------------------------------ raw fast path (bulk apply)
+// The benchmark generator sends fully-formed objects by the thousand.  Building a DOM for
+// each only to read a dozen fields costs more than everything else the simulator does, so
+// /sim/apply scans the raw text once instead: the fields the store needs (kind, name,
+// namespace, labels, the selectable field paths) and the byte positions the server edits
+// (metadata's '{', resourceVersion).  Anything unusual (escapes in a needed field,
+// generateName, a missing kind/metadata) falls back to the DOM path.
+struct Raw {
+  bool ok = true;
+  std::string_view kind, name, ns, uid, created, job;
+  std::string_view node, phase, ikind, iname, reason, type;
+  bool has_kind = false, has_api = false, has_md = false, has_rv = false, has_gen = false;
+  size_t md_open = 0, md_keys = 0, rv_off = 0, rv_len = 0;
+  std::vector<std::pair<std::string_view, std::string_view>> labels;
+};
+
+class RawScan {
+ public:
+  RawScan(const char* s, size_t n) : s_(s), n_(n) {}
+
+  // {"type": "...", "object": {...}} → type + the object's [begin, end) and fields
+  bool envelope(std::string_view& type, size_t& ob, size_t& oe, Raw& r) {
+    try {
+      ws();
+      if (!eat('{')) return false;
+      bool have_obj = false;
+      while (true) {
+        ws();
+        if (peek() == '}') break;
+        bool esc;
+        std::string_view k = str(esc);
+        ws();
+        if (!eat(':')) return false;
+        ws();
+        if (k == "type" && peek() == '"') {
+          type = str(esc);
+          if (esc) return false;
+        } else if (k == "object" && peek() == '{') {
+          ob = i_;
+          object(r);
+          oe = i_;
+          have_obj = true;
+        } else {
+          skip();
+        }
+        ws();
+        if (peek() == ',') ++i_;
+      }
+      return have_obj && r.ok;
+    } catch (const kjson::ParseError&) {
+      return false;
+    }
+  }
+
+ private:
+  const char* s_;
+  size_t n_;
+  size_t i_ = 0;
+
+  void ws() {
+    while (i_ < n_ && (s_[i_] == ' ' || s_[i_] == '\t' || s_[i_] == '\r' || s_[i_] == '\n')) ++i_;
+  }
+  char peek() {
+    if (i_ >= n_) throw kjson::ParseError("unexpected end");
+    return s_[i_];
+  }
+  bool eat(char c) {
+    if (peek() != c) return false;
+    ++i_;
+    return true;
+  }
+  std::string_view str(bool& esc) {
+    if (!eat('"')) throw kjson::ParseError("expected string");
+    size_t st = i_;
+    esc = false;
+    while (i_ < n_) {
+      char c = s_[i_];
+      if (c == '\\') {
+        esc = true;
+        i_ += 2;
+        continue;
+      }
+      if (c == '"') {
+        std::string_view v(s_ + st, i_ - st);
+        ++i_;
+        return v;
+      }
+      ++i_;
+    }
+    throw kjson::ParseError("unterminated string");
+  }
+  void skip() {
+    ws();
+    char c = peek();
+    if (c == '"') {
+      bool e;
+      str(e);
+      return;
+    }
+    if (c == '{' || c == '[') {
+      int depth = 0;
+      while (i_ < n_) {
+        char d = s_[i_];
+        if (d == '"') {
+          bool e;
+          str(e);
+          continue;
+        }
+        if (d == '{' || d == '[') ++depth;
+        else if ((d == '}' || d == ']') && --depth == 0) {
+          ++i_;
+          return;
+        }
+        ++i_;
+      }
+      throw kjson::ParseError("unterminated container");
+    }
+    while (i_ < n_ && s_[i_] != ',' && s_[i_] != '}' && s_[i_] != ']') ++i_;
+  }
+  // string value of a field the store reads: escapes → DOM fallback; non-strings are absent
+  void field(std::string_view& out, Raw& r) {
+    ws();
+    if (peek() != '"') {
+      skip();
+      return;
+    }
+    bool esc;
+    out = str(esc);
+    if (esc) r.ok = false;
+  }
+  // iterate an object's members: fn(key) handles the value at i_ (must consume it)
+  template <class F>
+  void members(F&& fn) {
+    ws();
+    if (!eat('{')) {
+      skip();
+      return;
+    }
+    while (true) {
+      ws();
+      if (peek() == '}') {
+        ++i_;
+        return;
+      }
+      bool esc;
+      std::string_view k = str(esc);
+      ws();
+      if (!eat(':')) throw kjson::ParseError("expected ':'");
+      ws();
+      if (esc) skip();
+      else fn(k);
+      ws();
+      if (peek() == ',') ++i_;
+    }
+  }
+  void object(Raw& r) {
+    members([&](std::string_view k) {
+      if (k == "kind") {
+        r.has_kind = true;
+        field(r.kind, r);
+      } else if (k == "apiVersion") {
+        r.has_api = true;
+        skip();
+      } else if (k == "metadata" && peek() == '{') {
+        r.has_md = true;
+        r.md_open = i_ + 1;
+        members([&](std::string_view m) {
+          ++r.md_keys;
+          if (m == "name") field(r.name, r);
+          else if (m == "namespace") field(r.ns, r);
+          else if (m == "uid") field(r.uid, r);
+          else if (m == "creationTimestamp") field(r.created, r);
+          else if (m == "generateName") {
+            r.has_gen = true;
+            skip();
+          } else if (m == "resourceVersion" && peek() == '"') {
+            bool esc;
+            size_t st = i_ + 1;
+            str(esc);
+            r.has_rv = true;
+            r.rv_off = st;
+            r.rv_len = i_ - 1 - st;
+            if (esc) r.ok = false;
+          } else if (m == "labels" && peek() == '{') {
+            members([&](std::string_view lk) {
+              std::string_view lv;
+              field(lv, r);
+              if (lv.data()) {
+                r.labels.emplace_back(lk, lv);
+                if (lk == "batch.kubernetes.io/job-name") r.job = lv;
+              }
+            });
+          } else {
+            skip();
+          }
+        });
+      } else if (k == "spec" && peek() == '{') {
+        members([&](std::string_view f) { f == "nodeName" ? field(r.node, r) : skip(); });
+      } else if (k == "status" && peek() == '{') {
+        members([&](std::string_view f) { f == "phase" ? field(r.phase, r) : skip(); });
+      } else if (k == "involvedObject" && peek() == '{') {
+        members([&](std::string_view f) {
+          if (f == "kind") field(r.ikind, r);
+          else if (f == "name") field(r.iname, r);
+          else skip();
+        });
+      } else if (k == "reason") {
+        field(r.reason, r);
+      } else if (k == "type") {
+        field(r.type, r);
+      } else {
+        skip();
+      }
+    });
+  }
+};
+
+std::shared_ptr<const Attrs> attrs_raw(const Raw& r) {
+  auto a = std::make_shared<Attrs>();
+  a->reserve(r.labels.size() + 8);
+  for (auto& kv : r.labels) a->emplace_back(std::string(kv.first), std::string(kv.second));
+  const std::pair<const char*, std::string_view> fields[] = {
+      {"\x01" "f:metadata.name", r.name},  {"\x01" "f:metadata.namespace", r.ns},
+      {"\x01" "f:spec.nodeName", r.node},   {"\x01" "f:status.phase", r.phase},
+      {"\x01" "f:involvedObject.kind", r.ikind}, {"\x01" "f:involvedObject.name", r.iname},
+      {"\x01" "f:reason", r.reason},       {"\x01" "f:type", r.type}};
+  for (auto& f : fields)
+    if (f.second.data()) a->emplace_back(f.first, std::string(f.second));
+  return a;
+}
+
+// Store text for a raw-scanned object: server metadata spliced in (src = the line, the
+// object spans [ob, oe)).  Same edits as finish() without the DOM.
+Obj finish_raw(const Raw& r, std::string_view src, size_t ob, size_t oe, const Obj* prev) {
+  Obj o;
+  o.ns = std::string(r.ns);
+  o.name = std::string(r.name);
+  o.job = std::string(r.job);
+  o.rv = ++g_rv;
+  std::string rvs = std::to_string(o.rv);
+  std::string ins;  // inserted right after metadata's '{'
+  if (r.uid.empty()) {
+    o.uid = prev && !prev->uid.empty() ? prev->uid : uuid4();
+    ins += "\"uid\":\"" + o.uid + "\",";
+  } else {
+    o.uid = std::string(r.uid);
+  }
+  if (!r.created.data()) {
+    o.created = prev && !prev->created.empty() ? prev->created : now_rfc3339();
+    ins += "\"creationTimestamp\":\"" + o.created + "\",";
+  } else {
+    o.created = std::string(r.created);
+  }
+  size_t rv_in_ins = std::string::npos;
+  if (!r.has_rv) {
+    rv_in_ins = ins.size() + 19;
+    ins += "\"resourceVersion\":\"" + rvs + "\",";
+  }
+  auto j = std::make_shared<std::string>();
+  j->reserve(oe - ob + ins.size() + 8);
+  j->append(src.data() + ob, r.md_open - ob);
+  size_t ins_at = j->size();
+  j->append(ins);
+  if (r.has_rv) {
+    j->append(src.data() + r.md_open, r.rv_off - r.md_open);
+    o.rv_off = j->size();
+    j->append(rvs);
+    j->append(src.data() + r.rv_off + r.rv_len, oe - r.rv_off - r.rv_len);
+  } else {
+    o.rv_off = ins_at + rv_in_ins;
+    j->append(src.data() + r.md_open, oe - r.md_open);
+  }
+  o.rv_len = rvs.size();
+  o.json = std::move(j);
+  o.attrs = attrs_raw(r);
+  return o;
+}
+
+// true when handled; false → caller takes the DOM path
+bool apply_raw(std::string_view line) {
+  RawScan sc(line.data(), line.size());
+  std::string_view type;
+  size_t ob = 0, oe = 0;
+  Raw r;
+  if (!sc.envelope(type, ob, oe, r)) return false;
+  if (!r.has_kind || !r.has_api || !r.has_md || r.md_keys == 0 || r.name.empty() || r.has_gen) return false;
+  int kind = kind_by_name(r.kind);
+  if (kind < 0) return false;
+  if (type == "DELETED") {
+    remove(kind, std::string(r.ns), std::string(r.name), "Background");
+    return true;
+  }
+  KindStore& ks = g_store[kind];
+  std::string key = okey(r.ns, r.name);
+  auto it = ks.objs.find(key);
+  const Obj* prev = it == ks.objs.end() ? nullptr : &it->second;
+  Obj o = finish_raw(r, line, ob, oe, prev);
+  if (kind == K_POD) {
+    if (prev) index_pod(*prev, false);
+    index_pod(o, true);
+  }
+  record(kind, prev ? "MODIFIED" : "ADDED", o);
+  if (prev) it->second = std::move(o);
+  else ks.objs.emplace(std::move(key), std::move(o));
+  return true;
 }
 
 void index_pod(const Obj& o, bool add) {
@@ -560,11 +897,16 @@ bool flush(Conn& c) {
   size_t off = 0;
   while (off < c.out.size()) {
     ssize_t n = send(c.fd, c.out.data() + off, c.out.size() - off, MSG_NOSIGNAL);
+    ++g_stats.sends;
     if (n > 0) {
       off += static_cast<size_t>(n);
+      g_stats.send_bytes += static_cast<uint64_t>(n);
       continue;
     }
-    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      ++g_stats.eagain;
+      break;
+    }
     if (n < 0 && errno == EINTR) continue;
     return false;
   }
@@ -791,6 +1133,10 @@ void h_apply(Conn& c, const Request& r) {
     std::string_view line(b.data() + pos, nl - pos);
     pos = nl + 1;
     if (line.find_first_not_of(" \t\r") == std::string_view::npos) continue;
+    if (apply_raw(line)) {
+      ++n;
+      continue;
+    }
     Value ev = kjson::parse(line);
     std::string type(ev.path({"type"}));
     Value* obj = ev.get("object");
@@ -832,6 +1178,8 @@ void handle(Conn& c, Request& r) {
       std::string s = "{\"requests\":" + std::to_string(g_stats.requests) +
                       ",\"watch_requests\":" + std::to_string(g_stats.watch_requests) + ",\"rv\":" + std::to_string(g_rv) +
                       ",\"deleted\":" + std::to_string(g_stats.deleted) + ",\"applied\":" + std::to_string(g_stats.applied) +
+                      ",\"loops\":" + std::to_string(g_stats.loops) + ",\"sends\":" + std::to_string(g_stats.sends) +
+                      ",\"send_bytes\":" + std::to_string(g_stats.send_bytes) + ",\"eagain\":" + std::to_string(g_stats.eagain) +
                       ",\"objects\":{";
       for (int k = 0; k < NKINDS; ++k) {
         if (k) s += ',';
@@ -1070,6 +1418,7 @@ int main(int argc, char** argv) {
   char buf[1 << 16];
   while (!g_stop) {
     int n = epoll_wait(g_ep, evs.data(), static_cast<int>(evs.size()), 100);
+    ++g_stats.loops;
     if (n < 0 && errno != EINTR) {
       perror("epoll_wait");
       break;

@@ -105,6 +105,18 @@ def test_resource_versions_spliced_consistently(arun):
             assert [e for e, _, _ in lines] == ["MODIFIED", "DELETED"]
             assert lines[0][1] == str(r2["rv"]) and int(lines[1][1]) > r2["rv"]
             assert lines[1][2]["status"] == {"phase": "Running"} and lines[1][2]["metadata"]["uid"] == pod["metadata"]["uid"]
+            # server-owned metadata missing: inserted into the client's text (uid, timestamp, RV)
+            bare = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "bare", "namespace": "nexus"}}
+            r3 = await ctl.apply([("ADDED", bare)])
+            got = await c.get("Job", "nexus", "bare")
+            md = got["metadata"]
+            assert md["resourceVersion"] == str(r3["rv"]) and len(md["uid"]) == 36 and md["creationTimestamp"].endswith("Z")
+            upd = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "bare", "namespace": "nexus"},
+                   "status": {"active": 1}}
+            await ctl.apply([("MODIFIED", upd)])
+            got2 = await c.get("Job", "nexus", "bare")
+            assert got2["metadata"]["uid"] == md["uid"] and got2["metadata"]["creationTimestamp"] == md["creationTimestamp"]
+            assert got2["status"] == {"active": 1} and int(got2["metadata"]["resourceVersion"]) > r3["rv"]
             await c.close()
             await ctl.close()
 
