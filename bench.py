@@ -56,7 +56,7 @@ def parse_args(argv=None):
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--procs", type=int, default=6,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport)")
-    ap.add_argument("--inflight", type=int, default=2, help="steps pushed ahead of acknowledgement")
+    ap.add_argument("--inflight", type=int, default=3, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--no-pregen", action="store_true",
                     help="generate each step's synthetic traffic on demand instead of before the timed region")
     ap.add_argument("--kube-connections", type=int, default=256)

@@ -125,7 +125,11 @@ class WorkerShard:
             owner = self.native.pod_owner(name)  # pods dropped before decode are only known natively
         return owner
 
-    def install(self, sup) -> None:
+    def install(self, sup, routed_upstream: bool = False) -> None:
+        """Filter this worker's informers.  ``routed_upstream`` (watch hub): the parent
+        already sends only this worker's objects, so no per-object filter is installed."""
+        if routed_upstream:
+            return
         if self.native is not None:
             for inf, role in ((sup.job_informer, "job"), (sup.pod_informer, "pod"), (sup.event_informer, "event")):
                 if hasattr(inf.lw, "shard_router"):

@@ -137,7 +137,9 @@ class Supervisor:
 
             self.worker_shard = WorkerShard(cfg.runtime.worker_index, cfg.runtime.worker_processes,
                                             cfg.labels.job_name_label)
-            self.worker_shard.install(self)
+            hub_fed = all(type(i.lw).__name__ == "HubListWatch"
+                          for i in (self.event_informer, self.pod_informer, self.job_informer))
+            self.worker_shard.install(self, routed_upstream=hub_fed)
         m = self.metrics
         m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
