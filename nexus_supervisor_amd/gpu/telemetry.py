@@ -303,8 +303,18 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
     from ..models import kube
     from .topology import topology_from_pod
 
-    cache = {"t": -1.0, "snap": None}
+    cache: Dict[str, Any] = {"t": -1.0, "snap": None, "by_uid": {}, "by_index": {}}
     ttl = max(0.005, telemetry.interval / 2)  # the native sampler cannot have anything newer
+
+    def refresh(now: float) -> None:
+        snap = telemetry.snapshot(True)
+        by_uid: Dict[str, set] = {}
+        for g in snap:
+            for p in g.get("procs", ()):
+                u = p.get("pod_uid")
+                if u:
+                    by_uid.setdefault(u, set()).add(g["index"])
+        cache.update(t=now, snap=snap, by_uid=by_uid, by_index={g["index"]: g for g in snap})
 
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         topo = topology_from_pod(pod, gpu_resource)
@@ -316,9 +326,13 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
             gpus.extend(int(d) for d in topo["visible_devices"] if str(d).isdigit())
         now = time.monotonic()
         if cache["snap"] is None or now - cache["t"] > ttl:
-            cache["snap"] = telemetry.snapshot(True)
-            cache["t"] = now
-        return evidence_for(telemetry, pod_uid=kube.uid_of(pod), gpu_indices=gpus, lookback=lookback,
-                            node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=cache["snap"])
+            refresh(now)
+        uid = kube.uid_of(pod)
+        # only the GPUs this pod could have used: its expected devices + where its processes ran
+        relevant = set(gpus) | cache["by_uid"].get(uid, set())
+        by_index = cache["by_index"]
+        sub = [by_index[i] for i in sorted(relevant) if i in by_index]
+        return evidence_for(telemetry, pod_uid=uid, gpu_indices=gpus, lookback=lookback,
+                            node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=sub)
 
     return provider
