@@ -283,6 +283,23 @@ class GpuMonitor {
     return peak;
   }
 
+  // VRAM samples of one GPU taken after `since` (seconds, wall clock): [(t, vram_used_mb)].
+  // Lets one process own the amd-smi session and forward history to others (shard workers).
+  py::list history(int gpu_index, double since) {
+    std::vector<std::pair<double, uint32_t>> out;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t i = 0; i < gpus_.size() && i < hist_.size(); ++i) {
+        if (gpus_[i].index != gpu_index) continue;
+        for (auto& smp : hist_[i])
+          if (smp.first > since) out.push_back(smp);
+      }
+    }
+    py::list l;
+    for (auto& smp : out) l.append(py::make_tuple(smp.first, smp.second));
+    return l;
+  }
+
   uint64_t samples() const { return samples_.load(); }
   double last_sample_seconds() const { return last_sample_s_.load(); }
   size_t n_gpus() const { return gpus_.size(); }
@@ -575,6 +592,7 @@ PYBIND11_MODULE(_amdsmi_monitor, m) {
       .def("inject_event", &GpuMonitor::inject_event)
       .def("reset_peaks", &GpuMonitor::reset_peaks)
       .def("peak_between", &GpuMonitor::peak_between)
+      .def("history", &GpuMonitor::history, py::arg("gpu_index"), py::arg("since") = 0.0)
       .def_property_readonly("samples", &GpuMonitor::samples)
       .def_property_readonly("last_sample", &GpuMonitor::last_sample_seconds)
       .def_property_readonly("n_gpus", &GpuMonitor::n_gpus);

@@ -162,7 +162,8 @@ class ShardedApplication:
     restarted with backoff; ``/healthz`` reports it until it is back)."""
 
     def __init__(self, cfg: SupervisorConfig, *, kube=None, logger: Optional[KLogger] = None,
-                 metrics: Optional[Metrics] = None, report_decisions: bool = False, log_dir: str = ""):
+                 metrics: Optional[Metrics] = None, report_decisions: bool = False, log_dir: str = "",
+                 telemetry=None):
         from .parallel.workers import WorkerPool
 
         self.cfg = cfg
@@ -176,7 +177,23 @@ class ShardedApplication:
         self.elector = None
         self.http = None
         self.hub = None
+        self.telemetry = telemetry
+        self._owns_telemetry = telemetry is None
+        self._gpu_task: Optional[asyncio.Task] = None
         self._stopped = asyncio.Event()
+
+    async def _publish_gpu(self) -> None:
+        """Mirror the replica's one GPU monitor into every worker (``RemoteTelemetry``)."""
+        from .gpu.telemetry import telemetry_message
+
+        since: dict = {}
+        interval = max(0.05, self.cfg.gpu.sample_interval)
+        while True:
+            try:
+                self.pool.broadcast(dict(telemetry_message(self.telemetry, since), op="gpu"))
+            except Exception as exc:  # noqa: BLE001 - telemetry must never stop the replica
+                self.log.error(exc, "GPU telemetry publish failed")
+            await asyncio.sleep(interval)
 
     async def start(self) -> None:
         cfg = self.cfg
@@ -184,6 +201,15 @@ class ShardedApplication:
                       store=cfg.cql_store_type, worker_processes=self.pool.count)
         le = cfg.leader_election
         await self.pool.start(active=not le.enabled)
+        if self.pool.remote_gpu:
+            if self.telemetry is None:
+                from .gpu.telemetry import make_telemetry
+
+                self.telemetry = make_telemetry(cfg.gpu.backend, cfg.gpu.sample_interval, cfg.gpu.telemetry_events)
+                if self.telemetry is not None:
+                    self.telemetry.start()
+            if self.telemetry is not None:
+                self._gpu_task = asyncio.create_task(self._publish_gpu(), name="gpu-telemetry-mirror")
         if self.pool.hub:
             from .parallel.watchhub import WatchHub
 
@@ -231,7 +257,15 @@ class ShardedApplication:
             await self.elector.stop(release=True)
         if self.hub is not None:
             await self.hub.stop()
+        if self._gpu_task is not None:
+            self._gpu_task.cancel()
+            try:
+                await self._gpu_task
+            except (asyncio.CancelledError, Exception):
+                pass
         await self.pool.stop(drain_timeout)
+        if self.telemetry is not None and self._owns_telemetry:
+            self.telemetry.stop()
         self.merged_metrics = self.pool.merged_metrics(self.metrics)
         if self.http is not None:
             await self.http.stop()

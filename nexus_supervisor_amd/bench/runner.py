@@ -169,7 +169,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
     else:
         from .wire import WireHarness
 
-        harness = WireHarness(sc, cfg, cfg.workdir)
+        harness = WireHarness(sc, cfg, cfg.workdir, telemetry=telemetry)
     tracker = Tracker()
     sampler = None
     try:

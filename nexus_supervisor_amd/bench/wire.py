@@ -35,8 +35,9 @@ def schema_statements(ks: str = "nexus", table: str = "checkpoints") -> List[str
 class WireHarness:
     store_name = "cql (nexus-cqlsrv over TCP)"
 
-    def __init__(self, sc: SupervisorConfig, cfg, workdir: str):
+    def __init__(self, sc: SupervisorConfig, cfg, workdir: str, telemetry=None):
         self.sc = sc
+        self.telemetry = telemetry
         self.cfg = cfg
         self.workdir = workdir
         self.cql: CqlServer = None
@@ -86,12 +87,10 @@ class WireHarness:
                            "users": [{"name": "bench", "user": {}}]}, f)
             sc.kube_config_path = kcfg
             sc.runtime.worker_processes = self.cfg.procs
+            # the rank's GPU monitor (owned by the runner) is mirrored into every worker
             sc.gpu.local_telemetry = True
             sc.gpu.backend = self.cfg.telemetry
-            # K workers per rank × 8 ranks on a node: VRAM sampling in each, one event listener per
-            # rank (the rank process's own monitor) is enough for the benchmark
-            sc.gpu.telemetry_events = False
-            self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir)
+            self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir, telemetry=self.telemetry)
         else:
             kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)
             store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql.port)],

@@ -104,9 +104,79 @@ class AmdSmiTelemetry(GpuTelemetry):
     def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:
         return int(self._m.peak_between(gpu_index, t0, t1))
 
+    def history(self, gpu_index: int, since: float = 0.0):
+        return self._m.history(gpu_index, since)
+
     @property
     def samples(self) -> int:
         return self._m.samples
+
+
+class RemoteTelemetry(GpuTelemetry):
+    """Telemetry mirrored from another process's monitor (a shard worker's view of the one
+    amd-smi session its replica's parent owns): :meth:`update` applies the parent's
+    periodic message — the latest snapshot plus the VRAM samples taken since the last one —
+    and every query answers from that mirror."""
+
+    name = "remote"
+
+    def __init__(self, interval: float = 0.5, retain: float = 600.0):
+        self.interval = interval
+        self.retain = retain
+        self._snap: List[Dict[str, Any]] = []
+        self._hist: Dict[int, List] = {}
+        self.source = ""
+        self.updates = 0
+
+    def start(self) -> None:
+        return None
+
+    def stop(self) -> None:
+        return None
+
+    def update(self, msg: Dict[str, Any]) -> None:
+        self.updates += 1
+        self.source = msg.get("source", self.source)
+        if msg.get("snap") is not None:
+            self._snap = msg["snap"]
+        horizon = (msg.get("t") or time.time()) - self.retain
+        for gi, samples in (msg.get("hist") or {}).items():
+            h = self._hist.setdefault(int(gi), [])
+            h.extend((float(t), int(mb)) for t, mb in samples)
+            if h and h[0][0] < horizon:
+                self._hist[int(gi)] = [x for x in h if x[0] >= horizon]
+
+    def devices(self):
+        return [{k: g.get(k) for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb")} for g in self._snap]
+
+    def snapshot(self, include_exited: bool = True):
+        if include_exited:
+            return self._snap
+        return [dict(g, procs=[p for p in g.get("procs", []) if p.get("alive")]) for g in self._snap]
+
+    def drain_events(self):
+        return []
+
+    def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:
+        return max((mb for t, mb in self._hist.get(int(gpu_index), ()) if t0 <= t <= t1), default=0)
+
+
+def telemetry_message(tel: GpuTelemetry, since: Dict[int, float]) -> Dict[str, Any]:
+    """What a telemetry owner forwards to its mirrors (:class:`RemoteTelemetry`): the snapshot
+    and each GPU's VRAM samples newer than ``since`` (advanced in place)."""
+    snap = tel.snapshot(True)
+    hist: Dict[str, List] = {}
+    hist_fn = getattr(tel, "history", None)
+    for g in snap:
+        gi = g["index"]
+        if hist_fn is not None:
+            samples = hist_fn(gi, since.get(gi, 0.0))
+        else:  # backends without a history: the current reading as one sample
+            samples = [(time.time(), g.get("vram_used_mb", 0))]
+        if samples:
+            since[gi] = samples[-1][0]
+            hist[str(gi)] = [[t, mb] for t, mb in samples]
+    return {"source": tel.name, "t": time.time(), "snap": snap, "hist": hist}
 
 
 class FakeTelemetry(GpuTelemetry):
@@ -212,6 +282,10 @@ class FakeTelemetry(GpuTelemetry):
     def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:
         with self._lock:
             return max((u for t, u in self._hist[gpu_index] if t0 <= t <= t1), default=0)
+
+    def history(self, gpu_index: int, since: float = 0.0):
+        with self._lock:
+            return [(t, u) for t, u in self._hist[gpu_index] if t > since]
 
 
 def has_amd_gpu() -> bool:

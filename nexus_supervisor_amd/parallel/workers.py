@@ -265,6 +265,9 @@ class WorkerPool:
         self.restarts = 0
         self.restart_backoff = (0.2, 10.0)  # base, max seconds between restarts of one worker
         self.hub = bool(cfg.runtime.watch_hub)
+        # node-local GPU telemetry: the parent owns the one amd-smi session and mirrors it
+        # into every worker (RemoteTelemetry) instead of K monitors per replica
+        self.remote_gpu = bool(cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry)
         self.on_restart: Optional[Callable[[int], Any]] = None  # async callback (watch hub resync)
         self._stopping = False
         self._watchdog: Optional[asyncio.Task] = None
@@ -332,6 +335,7 @@ class WorkerPool:
         env["NEXUS_WORKER_CTL_FD"] = str(child.fileno())
         env["NEXUS_WORKER_START_ACTIVE"] = "1" if self.active else "0"
         env["NEXUS_WORKER_REPORT"] = "1" if self.report_decisions else "0"
+        env["NEXUS_WORKER_REMOTE_GPU"] = "1" if self.remote_gpu else "0"
         fds = [child.fileno()]
         if dchild is not None:
             env["NEXUS_WORKER_DATA_FD"] = str(dchild.fileno())
@@ -411,6 +415,12 @@ class WorkerPool:
                 await d.drain()
             except ConnectionError:
                 pass
+
+    def broadcast(self, msg: Dict[str, Any]) -> None:
+        """Control message to every live worker (e.g. the GPU telemetry mirror)."""
+        for w in self.workers:
+            if w.chan is not None and not w.exited.is_set():
+                w.chan.send(msg)
 
     def set_active(self, active: bool) -> None:
         self.active = active
@@ -519,12 +529,18 @@ def _set_pdeathsig() -> None:
 
 async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, report: bool = False,
                      logger=None, metrics: Optional[Metrics] = None, app_factory=None,
-                     data_sock: Optional[socket.socket] = None) -> int:
+                     data_sock: Optional[socket.socket] = None, remote_gpu: bool = False) -> int:
     """Body of one shard-worker process (also callable in-process by tests)."""
     from ..app import Application
 
     chan = await Channel.open(sock)
     feed = None
+    extra: Dict[str, Any] = {}
+    remote_tel = None
+    if remote_gpu:
+        from ..gpu.telemetry import RemoteTelemetry
+
+        remote_tel = extra["telemetry"] = RemoteTelemetry(cfg.gpu.sample_interval)
     if data_sock is not None:
         # watch-hub mode: informers are fed by the parent's routed stream; the worker still
         # talks to the API server itself for Job DELETEs
@@ -537,9 +553,9 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
         kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
         factory = InformerFactory(lambda kind: feed.list_watch(kind) if kind in KINDS else None,
                                   resync_period=cfg.resync_period)
-        app = (app_factory or Application)(cfg, kube=kube, factory=factory, logger=logger, metrics=metrics)
+        app = (app_factory or Application)(cfg, kube=kube, factory=factory, logger=logger, metrics=metrics, **extra)
     else:
-        app = (app_factory or Application)(cfg, logger=logger, metrics=metrics)
+        app = (app_factory or Application)(cfg, logger=logger, metrics=metrics, **extra)
     sup = app.supervisor
     sup.active = start_active
     batch: List[list] = []
@@ -582,6 +598,8 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
                 sup.set_active(bool(msg.get("v")))
             elif op == "metrics":
                 send_metrics(int(msg.get("seq", 0)))
+            elif op == "gpu" and remote_tel is not None:
+                remote_tel.update(msg)
             elif op == "stop":
                 drain = float(msg.get("drain", drain))
                 break
@@ -626,7 +644,8 @@ def worker_main() -> int:
         dfd = os.environ.get("NEXUS_WORKER_DATA_FD")
         return await run_worker(cfg, sock, start_active=os.environ.get("NEXUS_WORKER_START_ACTIVE", "1") == "1",
                                 report=os.environ.get("NEXUS_WORKER_REPORT", "0") == "1", logger=log, metrics=metrics,
-                                data_sock=socket.socket(fileno=int(dfd)) if dfd else None)
+                                data_sock=socket.socket(fileno=int(dfd)) if dfd else None,
+                                remote_gpu=os.environ.get("NEXUS_WORKER_REMOTE_GPU", "0") == "1")
 
     prof_path = os.environ.get("NEXUS_WORKER_CPROFILE")
     if not prof_path:

@@ -338,3 +338,90 @@ def test_crashed_worker_restarts_and_leader_gating(arun, tmp_path):
                 await ctl.close()
 
     arun(go(), timeout=120)
+
+
+def test_remote_telemetry_mirror_matches_owner():
+    from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry, RemoteTelemetry, telemetry_message
+
+    import time
+
+    owner = FakeTelemetry(n_gpus=2)
+    mirror = RemoteTelemetry()
+    since = {}
+    t = time.time() - 10
+    owner.set_vram(1, 1000, t=t)
+    owner.add_process(7, 1, vram_bytes=5 << 30, pod_uid="pod-a")
+    mirror.update(json.loads(json.dumps(telemetry_message(owner, since))))
+    owner.set_vram(1, 290000, t=t + 1)
+    owner.set_vram(0, 5, t=t + 1.5)
+    mirror.update(json.loads(json.dumps(telemetry_message(owner, since))))  # only the new samples travel
+    assert mirror.peak_between(1, t - 1, t + 2) == owner.peak_between(1, t - 1, t + 2) == 290000
+    assert mirror.peak_between(1, t - 1, t + 0.5) == 1000 and mirror.peak_between(0, t, t + 5) == 5
+    assert [p["pod_uid"] for p in mirror.snapshot()[1]["procs"]] == ["pod-a"]
+    assert len(mirror._hist[1]) == 2 and mirror.updates == 2
+
+
+@pytest.mark.slow
+def test_worker_gpu_evidence_from_parent_monitor(arun, tmp_path):
+    """Node-local attribution with worker processes: one monitor in the parent, mirrored into
+    the workers; an HBM-OOM pod's row carries the GPU and the VRAM peak of its window."""
+    from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry
+    from nexus_supervisor_amd.models.checkpoint import CheckpointedRequest, LifecycleStage
+
+    async def go():
+        labels = LabelConfig()
+        tel = FakeTelemetry(n_gpus=8)
+        tel.set_vram(3, 294000)
+        env = {"LOCAL_RANK": "3", "RANK": "3", "WORLD_SIZE": "8", "HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}
+        rids = [f"hbm-run-{i}" for i in (0, 1, 4, 5)]  # two per worker
+        with KubeSim(bookmark_ms=200) as sim:
+            ctl = SimControl(sim.url)
+            srv = CqlServer(exec_statements=seed_cql_statements()).start()
+            store = CqlCheckpointStore(CqlSession([srv.address]))
+            await store.connect()
+            for rid in rids:
+                await store.upsert_checkpoint(CheckpointedRequest(algorithm=ALGORITHM, id=rid,
+                                                                  lifecycle_stage=LifecycleStage.RUNNING))
+            await ctl.apply([("ADDED", o) for rid in rids for o in (make_job(rid, labels),
+                                                                   make_pod(rid, labels, env=env, gpus=1))])
+            kc = tmp_path / "kubeconfig"
+            kc.write_text(json.dumps({"clusters": [{"name": "c", "cluster": {"server": sim.url}}],
+                                      "contexts": [{"name": "x", "context": {"cluster": "c"}}], "current-context": "x"}))
+            cfg = load_config(path=None, env={}, overrides={
+                "cql-store-type": "scylla", "rate-limit-elements-per-second": 0, "resync-period": "0s",
+                "kube-config-path": str(kc), "scylla-cql-store": {"hosts": f"127.0.0.1:{srv.port}"},
+                "runtime": {"worker-processes": 2}, "gpu": {"local-telemetry": True, "sample-interval": "100ms"}})
+            app = ShardedApplication(cfg, report_decisions=True, log_dir=str(tmp_path), telemetry=tel)
+            decisions = []
+            app.supervisor.decision_hooks.append(decisions.append)
+            try:
+                await app.start()
+                assert await app.wait_for_cache_sync(30)
+                await asyncio.sleep(0.3)  # a mirror update or two
+                failed = []
+                for rid in rids:
+                    p = make_pod(rid, labels, env=env, gpus=1, rv="3", status={
+                        "phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {
+                            "terminated": {"reason": "Error", "exitCode": 1,
+                                           "message": "torch.OutOfMemoryError: HIP out of memory. Tried to allocate 8.00 GiB"}}}]})
+                    failed.append(("MODIFIED", p))
+                await ctl.apply(failed)
+                for _ in range(300):
+                    if sum(1 for d in decisions if d.outcome == "applied") >= len(rids):
+                        break
+                    await asyncio.sleep(0.05)
+                assert {worker_of(r, 2) for r in rids} == {0, 1}  # both workers took part
+                for rid in rids:
+                    row = await store.read_checkpoint(ALGORITHM, rid)
+                    assert row.lifecycle_stage == LifecycleStage.FAILED, (rid, row)
+                    trace = json.loads(row.algorithm_failure_details)
+                    assert trace["class"] == "hbm-oom", trace
+                    g = trace["gpu"]["gpus"][0]
+                    assert g["index"] == 3 and g["vram_peak_mb"] == 294000, g
+            finally:
+                await app.stop(drain_timeout=5)
+                await store.close()
+                srv.stop()
+                await ctl.close()
+
+    arun(go(), timeout=90)
