@@ -49,6 +49,25 @@ def test_monitor_sees_mi355x(telemetry):
     assert telemetry.samples >= 2
 
 
+def test_native_history_mirrors_into_worker_view(telemetry, stress_exe):
+    """The replica's one amd-smi monitor forwarded to a shard worker (RemoteTelemetry):
+    the mirrored VRAM peak of a real 16 GiB hold equals the native monitor's."""
+    from nexus_supervisor_amd.gpu.telemetry import RemoteTelemetry, telemetry_message
+
+    mirror, since = RemoteTelemetry(), {}
+    t0 = time.time()
+    mirror.update(json.loads(json.dumps(telemetry_message(telemetry, since))))
+    p = subprocess.run([stress_exe, "hold", "--gib", "16", "--seconds", "1.0"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    time.sleep(0.3)
+    mirror.update(json.loads(json.dumps(telemetry_message(telemetry, since))))
+    t1 = time.time()
+    gi = telemetry.devices()[0]["index"]
+    native = telemetry.peak_between(gi, t0, t1)
+    assert native > 16_000 and mirror.peak_between(gi, t0, t1) == native
+    assert len(telemetry.history(gi, t0)) >= 5
+
+
 def _run_oom(exe, tmp_path, env_extra):
     log = tmp_path / "termination.log"
     env = dict(os.environ, **env_extra)
