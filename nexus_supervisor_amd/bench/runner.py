@@ -204,6 +204,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             from ..obs.pprof import Sampler
 
             sampler = Sampler(hz=199).start()
+            pool = getattr(getattr(harness, "app", None), "pool", None)
+            if pool is not None:  # shard workers profile themselves over the same window
+                pool.broadcast({"op": "pprof", "on": True, "hz": 199})
         barrier_sync()
         t0 = time.perf_counter()
         c0 = time.process_time()
@@ -226,6 +229,16 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
                 f.write(prof.encode_gz())
             with open(cfg.pprof_out + ".top.txt", "w") as f:
                 f.write(prof.top(40))
+            pool = getattr(getattr(harness, "app", None), "pool", None)
+            if pool is not None:
+                import os
+
+                pool.broadcast({"op": "pprof", "on": False, "path": cfg.pprof_out})
+                want = [f"{cfg.pprof_out}.w{w.index}.top.txt" for w in pool.workers]
+                for _ in range(100):
+                    if all(os.path.exists(x) for x in want):
+                        break
+                    await asyncio.sleep(0.05)
         sync = getattr(harness, "sync_metrics", None)
         if sync is not None:
             await sync()

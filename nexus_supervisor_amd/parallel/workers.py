@@ -588,6 +588,7 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
 
     sync_task = asyncio.create_task(announce_sync())
     drain = 10.0
+    profiler = None
     try:
         while True:
             msg = await chan.recv()
@@ -600,6 +601,8 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
                 send_metrics(int(msg.get("seq", 0)))
             elif op == "gpu" and remote_tel is not None:
                 remote_tel.update(msg)
+            elif op == "pprof":
+                profiler = _pprof_op(msg, profiler, cfg.runtime.worker_index)
             elif op == "stop":
                 drain = float(msg.get("drain", drain))
                 break
@@ -617,6 +620,26 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
             pass
         chan.close()
     return 0
+
+
+def _pprof_op(msg: Dict[str, Any], profiler, index: int):
+    """``{"op": "pprof", "on": true}`` starts the CPU sampler (SIGPROF, this event loop);
+    ``{"on": false, "path": P}`` stops it and writes ``P.w<index>.pb.gz`` + ``.top.txt``."""
+    from ..obs.pprof import Sampler
+
+    if msg.get("on"):
+        if profiler is None:
+            profiler = Sampler(hz=int(msg.get("hz", 199))).start()
+        return profiler
+    if profiler is not None:
+        prof = profiler.stop()
+        path = msg.get("path")
+        if path:
+            with open(f"{path}.w{index}.pb.gz", "wb") as f:
+                f.write(prof.encode_gz())
+            with open(f"{path}.w{index}.top.txt", "w") as f:
+                f.write(prof.top(40))
+    return None
 
 
 def worker_main() -> int:
