@@ -1,5 +1,5 @@
-"""HDR-style log-linear latency histogram (pure Python; a C++ twin lives in
-``csrc/native.cpp`` for the hot path).
+"""HDR-style log-linear latency histogram (pure Python, O(1) record; the hot path
+records a handful per decision).
 
 Values are recorded in integer microseconds.  Buckets have a fixed relative
 precision: each power-of-two range ``[2^k, 2^(k+1))`` is split into

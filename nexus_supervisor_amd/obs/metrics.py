@@ -36,6 +36,7 @@ class Metrics:
         self.hists: Dict[str, Dict[LabelKey, LatencyHistogram]] = {}
         self.help: Dict[str, str] = {}
         self.statsd: Optional["DogStatsd"] = None
+        self._h0: Dict[str, LatencyHistogram] = {}  # unlabelled series: one dict probe per observation
 
     def describe(self, name: str, text: str) -> None:
         self.help[name] = text
@@ -44,7 +45,7 @@ class Metrics:
         d = self.counters.get(name)
         if d is None:
             d = self.counters[name] = {}
-        k = _lk(labels)
+        k = _lk(labels) if labels else ()
         d[k] = d.get(k, 0.0) + value
         if self.statsd is not None:
             self.statsd.count(name, value, labels)
@@ -58,6 +59,13 @@ class Metrics:
             self.statsd.gauge(name, value, labels)
 
     def observe_seconds(self, name: str, seconds: float, labels: Optional[Dict[str, str]] = None) -> None:
+        if not labels:
+            h = self._h0.get(name)
+            if h is not None:
+                h.record(seconds * 1e6)
+                if self.statsd is not None:
+                    self.statsd.timing(name, seconds * 1e3, None)
+                return
         d = self.hists.get(name)
         if d is None:
             d = self.hists[name] = {}
@@ -65,6 +73,8 @@ class Metrics:
         h = d.get(k)
         if h is None:
             h = d[k] = LatencyHistogram()
+        if not k:
+            self._h0[name] = h
         h.record(seconds * 1e6)
         if self.statsd is not None:
             self.statsd.timing(name, seconds * 1e3, labels)

@@ -25,6 +25,12 @@ class CheckpointStore:
     async def read_checkpoint(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
         raise NotImplementedError
 
+    async def read_status(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
+        """The row's key and ``lifecycle_stage`` only — all the owned-columns write path
+        needs (``is_finished`` and the CAS guard).  Stores that can project the read
+        (CQL: ``SELECT lifecycle_stage``) override this; the default reads the full row."""
+        return await self.read_checkpoint(algorithm, request_id)
+
     async def upsert_checkpoint(self, checkpoint: CheckpointedRequest) -> None:
         raise NotImplementedError
 

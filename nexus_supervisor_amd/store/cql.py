@@ -795,6 +795,9 @@ class CqlCheckpointStore(CheckpointStore):
         ft = f"{keyspace}.{table}"
         cols = ", ".join(COLUMN_NAMES)
         self.q_read = f"SELECT {cols} FROM {ft} WHERE algorithm = ? AND id = ?"
+        # projected read for the owned-columns path: one text column instead of 19
+        # (no timestamp decoding, ~10x smaller response)
+        self.q_read_status = f"SELECT lifecycle_stage FROM {ft} WHERE algorithm = ? AND id = ?"
         self.q_insert = f"INSERT INTO {ft} ({cols}) VALUES ({', '.join('?' for _ in COLUMN_NAMES)})"
         self.q_update_failure = (f"UPDATE {ft} SET lifecycle_stage = ?, algorithm_failure_cause = ?, "
                                  f"algorithm_failure_details = ?, last_modified = ? WHERE algorithm = ? AND id = ?")
@@ -837,8 +840,8 @@ class CqlCheckpointStore(CheckpointStore):
             self.session.local_dc = info.get("local_dc", self.session.local_dc)
             self.session.contact_points = [(hid, 0) for hid in info.get("contact_points", [])] or self.session.contact_points
         await self.session.connect()
-        await asyncio.gather(*(self.session.prepare(q) for q in (self.q_read, self.q_insert, self.q_update_failure,
-                                                                  self.q_update_stage)))
+        await asyncio.gather(*(self.session.prepare(q) for q in (self.q_read, self.q_read_status, self.q_insert,
+                                                                  self.q_update_failure, self.q_update_stage)))
 
     async def close(self) -> None:
         await self.session.close()
@@ -849,6 +852,13 @@ class CqlCheckpointStore(CheckpointStore):
         if not rows.rows:
             return None
         return CheckpointedRequest(*rows.rows[0])
+
+    async def read_status(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
+        self.reads += 1
+        rows = await self.session.execute(self.q_read_status, (algorithm, request_id), consistency=self.cl)
+        if not rows.rows:
+            return None
+        return CheckpointedRequest(algorithm, request_id, rows.rows[0][0])
 
     async def upsert_checkpoint(self, checkpoint: CheckpointedRequest) -> None:
         self.writes += 1

@@ -405,7 +405,10 @@ class Supervisor:
         if r.action not in STAGE_FOR_ACTION:
             raise ValueError(f"unknown analysis result action: {r.action}")
         try:
-            cp = await self.store.read_checkpoint(r.algorithm, r.request_id)
+            # the owned-columns write needs only the stage; the full-row upsert (reference
+            # UpsertCheckpoint of the deep copy) needs every column
+            read = self.store.read_checkpoint if compat.full_row_upsert else self.store.read_status
+            cp = await read(r.algorithm, r.request_id)
         except Exception as exc:
             self.log.error(exc, "no checkpoint exists for the provided request, job will be deleted without metadata saved",
                            requestId=r.request_id, algorithm=r.algorithm)

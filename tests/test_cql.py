@@ -116,6 +116,11 @@ def test_owned_columns_update_keeps_other_columns(seeded, arun):
         await st.update_status(ALGORITHM, row.id, LifecycleStage.RUNNING, None, None, now, set_failure=False)
         got = await st.read_checkpoint(ALGORITHM, row.id)
         assert got.lifecycle_stage == "RUNNING" and got.algorithm_failure_cause == "cause"
+        # projected stage read (owned-columns path): key + stage only
+        lite = await st.read_status(ALGORITHM, row.id)
+        assert (lite.algorithm, lite.id, lite.lifecycle_stage) == (ALGORITHM, row.id, "RUNNING")
+        assert lite.payload_uri is None and not lite.is_finished()
+        assert await st.read_status(ALGORITHM, "missing") is None
         await st.close()
 
     arun(go())
