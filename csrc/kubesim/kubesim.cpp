@@ -34,12 +34,17 @@
 // nexus-kubesim [--host 127.0.0.1] [--port 0] [--ready-file F] [--history N]
 //               [--bookmark-ms 1000] [--token T]
 #include <arpa/inet.h>
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <fcntl.h>
+#include <malloc.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <signal.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
+#include <sys/uio.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -62,6 +67,65 @@
 using kjson::Value;
 
 namespace {
+
+// ------------------------------------------------------------ CPU sampler (diagnostics)
+// NEXUS_KUBESIM_PROF=<file>: SIGPROF every 1 ms of process CPU time records the stack;
+// at exit every sample is written as "module+offset" frames (leaf first), one line per
+// sample, for tools/native_prof.py to symbolise.  Off unless the variable is set.
+namespace prof {
+constexpr int kMaxSamples = 1 << 17;
+constexpr int kDepth = 12;
+void* g_frames[kMaxSamples][kDepth];
+unsigned char g_depth[kMaxSamples];
+volatile int g_n = 0;
+std::string g_path;
+
+void on_sigprof(int) {
+  int i = g_n;
+  if (i >= kMaxSamples) return;
+  g_n = i + 1;
+  g_depth[i] = static_cast<unsigned char>(backtrace(g_frames[i], kDepth));
+}
+
+void start() {
+  const char* p = getenv("NEXUS_KUBESIM_PROF");
+  if (!p || !*p) return;
+  g_path = p;
+  void* warm[2];
+  backtrace(warm, 2);  // first call loads the unwinder: not inside the handler
+  struct sigaction sa {};
+  sa.sa_handler = on_sigprof;
+  sa.sa_flags = SA_RESTART;
+  sigaction(SIGPROF, &sa, nullptr);
+  itimerval it{};
+  it.it_interval.tv_usec = 1000;
+  it.it_value.tv_usec = 1000;
+  setitimer(ITIMER_PROF, &it, nullptr);
+}
+
+void dump() {
+  if (g_path.empty()) return;
+  itimerval off{};
+  setitimer(ITIMER_PROF, &off, nullptr);
+  FILE* f = fopen(g_path.c_str(), "w");
+  if (!f) return;
+  int n = g_n;
+  for (int i = 0; i < n; ++i) {
+    // frames 0-1 are the handler and the signal trampoline
+    for (int d = 2; d < g_depth[i]; ++d) {
+      Dl_info info{};
+      uintptr_t a = reinterpret_cast<uintptr_t>(g_frames[i][d]);
+      if (dladdr(g_frames[i][d], &info) && info.dli_fname)
+        fprintf(f, "%s%s+0x%lx", d > 2 ? " " : "", info.dli_fname,
+                static_cast<unsigned long>(a - reinterpret_cast<uintptr_t>(info.dli_fbase) - (d > 2 ? 1 : 0)));
+      else
+        fprintf(f, "%s?+0x%lx", d > 2 ? " " : "", static_cast<unsigned long>(a));
+    }
+    fputc('\n', f);
+  }
+  fclose(f);
+}
+}  // namespace prof
 
 // ============================================================ options / clock
 struct Options {
@@ -286,7 +350,17 @@ struct Watch {
   bool bookmarks;
   int64_t deadline_ms;
   int64_t last_ms;
-  std::string pending;  // lines committed this loop iteration, sent as one chunk
+  std::string pending;  // control lines (ERROR / BOOKMARK) for the next chunk
+  // event lines committed this loop iteration: shared with the history, sent as one
+  // chunk straight from these buffers (sendmsg iovecs; no per-watch copy)
+  std::vector<std::shared_ptr<const std::string>> lines;
+  size_t lines_bytes = 0;
+  bool idle() const { return pending.empty() && lines.empty(); }
+  void clear() {
+    pending.clear();
+    lines.clear();
+    lines_bytes = 0;
+  }
 };
 
 struct KindStore {
@@ -318,7 +392,7 @@ std::string okey(std::string_view ns, std::string_view name) {
   return k;
 }
 
-void watch_push(Watch* w, const std::string& line);
+void watch_push(Watch* w, const std::shared_ptr<const std::string>& line);
 
 void record(int kind, const char* etype, const Obj& o) {
   std::string line;
@@ -336,7 +410,7 @@ void record(int kind, const char* etype, const Obj& o) {
     ks.history.pop_front();
   }
   for (Watch* w : ks.watchers)
-    if ((w->ns.empty() || w->ns == o.ns) && matches(*o.attrs, w->sel)) watch_push(w, *lp);
+    if ((w->ns.empty() || w->ns == o.ns) && matches(*o.attrs, w->sel)) watch_push(w, lp);
 }
 
 // Fills metadata defaults, assigns the next resourceVersion, serialises and indexes.
@@ -827,6 +901,7 @@ struct Conn {
   std::string out;
   Watch* watch = nullptr;
   bool close_after = false;
+  uint32_t mask = EPOLLIN | EPOLLRDHUP;  // registered epoll interest (skip redundant epoll_ctl)
 };
 
 int g_ep = -1;
@@ -836,10 +911,13 @@ std::set<Conn*> g_dirty;  // connections with queued output
 void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
 void interest(Conn& c) {
+  uint32_t want = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0u : static_cast<uint32_t>(EPOLLOUT));
+  if (want == c.mask) return;  // one syscall per response saved on the hot path
   epoll_event ev{};
-  ev.events = EPOLLIN | EPOLLRDHUP | (c.out.empty() ? 0u : static_cast<uint32_t>(EPOLLOUT));
+  ev.events = want;
   ev.data.fd = c.fd;
   epoll_ctl(g_ep, EPOLL_CTL_MOD, c.fd, &ev);
+  c.mask = want;
 }
 
 void end_watch(Conn& c, bool terminate_chunked) {
@@ -852,11 +930,12 @@ void end_watch(Conn& c, bool terminate_chunked) {
       break;
     }
   if (terminate_chunked) {
-    if (!w->pending.empty()) {
+    if (!w->idle()) {
       char hdr[24];
-      snprintf(hdr, sizeof hdr, "%zx\r\n", w->pending.size());
+      snprintf(hdr, sizeof hdr, "%zx\r\n", w->pending.size() + w->lines_bytes);
       c.out += hdr;
       c.out += w->pending;
+      for (auto& l : w->lines) c.out += *l;
       c.out += "\r\n";
     }
     c.out += "0\r\n\r\n";
@@ -877,23 +956,77 @@ void close_conn(int fd) {
   g_conns.erase(it);
 }
 
-void watch_push(Watch* w, const std::string& line) {
-  w->pending += line;
-  auto it = g_conns.find(w->fd);
-  if (it != g_conns.end()) g_dirty.insert(it->second.get());
+void watch_push(Watch* w, const std::shared_ptr<const std::string>& line) {
+  if (w->idle()) {
+    auto it = g_conns.find(w->fd);
+    if (it != g_conns.end()) g_dirty.insert(it->second.get());
+  }
+  w->lines_bytes += line->size();
+  w->lines.push_back(line);
 }
 
-// move each watch's pending lines into its connection as one chunk; write out
-bool flush(Conn& c) {
-  if (c.watch && !c.watch->pending.empty()) {
-    char hdr[24];
-    snprintf(hdr, sizeof hdr, "%zx\r\n", c.watch->pending.size());
-    c.out += hdr;
-    c.out += c.watch->pending;
+// Sends a watch's committed lines as one chunk.  With nothing queued ahead of it the
+// chunk goes out as iovecs over the shared line buffers; whatever the socket does not
+// take is copied into c.out.  false = connection error.
+bool flush_watch(Conn& c) {
+  Watch* w = c.watch;
+  char hdr[24];
+  int hl = snprintf(hdr, sizeof hdr, "%zx\r\n", w->pending.size() + w->lines_bytes);
+  w->last_ms = mono_ms();
+  if (!c.out.empty()) {  // keep the byte order: append behind what is queued
+    c.out.append(hdr, static_cast<size_t>(hl));
+    c.out += w->pending;
+    for (auto& l : w->lines) c.out += *l;
     c.out += "\r\n";
-    c.watch->pending.clear();
-    c.watch->last_ms = mono_ms();
+    w->clear();
+    return true;
   }
+  static char crlf[] = "\r\n";
+  std::vector<iovec> iov;
+  iov.reserve(w->lines.size() + 3);
+  iov.push_back({hdr, static_cast<size_t>(hl)});
+  if (!w->pending.empty()) iov.push_back({w->pending.data(), w->pending.size()});
+  for (auto& l : w->lines) iov.push_back({const_cast<char*>(l->data()), l->size()});
+  iov.push_back({crlf, 2});
+  size_t i = 0;
+  bool ok = true;
+  while (i < iov.size()) {
+    msghdr m{};
+    m.msg_iov = &iov[i];
+    m.msg_iovlen = std::min<size_t>(iov.size() - i, 1024);  // IOV_MAX
+    ssize_t n = sendmsg(c.fd, &m, MSG_NOSIGNAL);
+    ++g_stats.sends;
+    if (n > 0) {
+      g_stats.send_bytes += static_cast<uint64_t>(n);
+      size_t k = static_cast<size_t>(n);
+      while (k > 0) {
+        if (k >= iov[i].iov_len) {
+          k -= iov[i].iov_len;
+          ++i;
+        } else {
+          iov[i].iov_base = static_cast<char*>(iov[i].iov_base) + k;
+          iov[i].iov_len -= k;
+          k = 0;
+        }
+      }
+      continue;
+    }
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      ++g_stats.eagain;
+      break;
+    }
+    if (n < 0 && errno == EINTR) continue;
+    ok = false;
+    break;
+  }
+  for (; ok && i < iov.size(); ++i) c.out.append(static_cast<const char*>(iov[i].iov_base), iov[i].iov_len);
+  w->clear();
+  return ok;
+}
+
+// write out a connection's queued bytes (and its watch's committed lines)
+bool flush(Conn& c) {
+  if (c.watch && !c.watch->idle() && !flush_watch(c)) return false;
   size_t off = 0;
   while (off < c.out.size()) {
     ssize_t n = send(c.fd, c.out.data() + off, c.out.size() - off, MSG_NOSIGNAL);
@@ -1103,7 +1236,10 @@ void h_watch(Conn& c, const Request& r, int kind, const std::string& ns) {
     }
     for (size_t i = lo; i < ks.history.size(); ++i) {
       const Hist& h = ks.history[i];
-      if ((ns.empty() || h.ns == ns) && matches(*h.attrs, w->sel)) w->pending += *h.line;
+      if ((ns.empty() || h.ns == ns) && matches(*h.attrs, w->sel)) {
+        w->lines_bytes += h.line->size();
+        w->lines.push_back(h.line);
+      }
     }
   }
   ks.watchers.push_back(w);
@@ -1159,7 +1295,7 @@ void h_apply(Conn& c, const Request& r) {
     // compaction that overtakes the watchers: undelivered lines are lost, resuming
     // streams get 410 Gone and must re-list (exercises the informer's relist diff)
     for (auto& kv : g_conns)
-      if (kv.second->watch) kv.second->watch->pending.clear();
+      if (kv.second->watch) kv.second->watch->clear();
     for (int k = 0; k < NKINDS; ++k) expire_kind(k);
     close_watches(-1);
   }
@@ -1269,11 +1405,21 @@ void handle(Conn& c, Request& r) {
 
 // parses as many complete requests as the buffer holds; false = protocol error (close)
 bool on_input(Conn& c) {
+  // requests are consumed by advancing `at`; the buffer is compacted once at the end
+  // (erasing each request from the front made a pipelined burst O(n^2) in bytes moved)
+  size_t at = 0;
+  struct Compact {
+    std::string& in;
+    size_t& at;
+    ~Compact() {
+      if (at) in.erase(0, at);
+    }
+  } compact{c.in, at};
   while (!c.watch) {
-    size_t he = c.in.find("\r\n\r\n");
-    if (he == std::string::npos) return c.in.size() < (1u << 20);
+    size_t he = c.in.find("\r\n\r\n", at);
+    if (he == std::string::npos) return c.in.size() - at < (1u << 20);
     Request r;
-    std::string_view head(c.in.data(), he);
+    std::string_view head(c.in.data() + at, he - at);
     size_t le = head.find("\r\n");
     std::string_view rl = head.substr(0, le);
     size_t s1 = rl.find(' '), s2 = rl.rfind(' ');
@@ -1322,12 +1468,12 @@ bool on_input(Conn& c) {
     if (chunked) {
       c.close_after = true;
       respond(c, 411, status_body(411, "LengthRequired", "chunked request bodies are not supported"));
-      c.in.clear();
+      at = c.in.size();
       return true;
     }
     if (c.in.size() < he + 4 + clen) return true;  // body incomplete
     r.body = c.in.substr(he + 4, clen);
-    c.in.erase(0, he + 4 + clen);
+    at = he + 4 + clen;
     try {
       handle(c, r);
     } catch (const std::exception& e) {
@@ -1370,6 +1516,13 @@ int main(int argc, char** argv) {
     }
   }
   signal(SIGPIPE, SIG_IGN);
+  // Keep freed memory in the heap: bulk applies allocate and free megabytes per step, and
+  // glibc's default trimming hands it back to the kernel only to fault it in again
+  // (brk + page faults were a quarter of the simulator's CPU time).
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+  mallopt(M_TOP_PAD, 64 << 20);
+  mallopt(M_MMAP_THRESHOLD, 1 << 30);
+  prof::start();
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);
 
@@ -1450,6 +1603,9 @@ int main(int argc, char** argv) {
           ssize_t r = recv(fd, buf, sizeof buf, 0);
           if (r > 0) {
             c.in.append(buf, static_cast<size_t>(r));
+            // a short read drained the socket: skip the EAGAIN probe (level-triggered
+            // epoll reports anything that arrives later)
+            if (static_cast<size_t>(r) < sizeof buf) break;
             continue;
           }
           if (r == 0) dead = true;
@@ -1473,7 +1629,7 @@ int main(int argc, char** argv) {
         if (!w) continue;
         if (now >= w->deadline_ms) {
           ended.push_back(kv.second.get());
-        } else if (w->bookmarks && w->pending.empty() && now - w->last_ms >= g_opt.bookmark_ms) {
+        } else if (w->bookmarks && w->idle() && now - w->last_ms >= g_opt.bookmark_ms) {
           w->pending = std::string("{\"type\":\"BOOKMARK\",\"object\":{\"kind\":\"") + KINDS[w->kind].kind +
                        "\",\"apiVersion\":\"" + KINDS[w->kind].api_version + "\",\"metadata\":{\"resourceVersion\":\"" +
                        std::to_string(g_rv) + "\"}}}\n";
@@ -1491,5 +1647,6 @@ int main(int argc, char** argv) {
   }
   for (auto& kv : g_conns) close(kv.first);
   close(lfd);
+  prof::dump();
   return 0;
 }

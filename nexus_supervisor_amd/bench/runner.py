@@ -211,6 +211,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         t0 = time.perf_counter()
         c0 = time.process_time()
         x0 = harness.external_cpu()
+        sim_stats = getattr(harness, "sim_stats", None)
+        s0 = await sim_stats() if sim_stats is not None else None
         await run_steps(cfg.steps)
         barrier_sync()
         elapsed = time.perf_counter() - t0
@@ -219,6 +221,11 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         x1 = harness.external_cpu()
         for k in x1:
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
+        s1 = await sim_stats() if s0 else None
+        if s0 and s1:
+            n_ev = max(cfg.events * cfg.steps, 1)
+            for k in ("requests", "loops", "sends"):
+                cpu[f"kubesim_{k}_per_event"] = round((s1.get(k, 0) - s0.get(k, 0)) / n_ev, 3)
         workers = [v for k, v in cpu.items() if k.startswith("worker")]
         if workers:
             cpu["workers_util_sum"] = round(sum(workers), 3)

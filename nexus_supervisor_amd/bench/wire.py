@@ -64,6 +64,7 @@ class WireHarness:
         with open(ready) as f:
             info = json.load(f)
         self.ctl = info["ctl"]
+        self.api = info["api"]
         self.sim_pid = info.get("sim_pid")
         self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=600))
         async with self.http.post(self.ctl + "/bench/init", json={
@@ -130,9 +131,19 @@ class WireHarness:
                 with open(f"/proc/{proc.pid}/stat") as f:
                     parts = f.read().rsplit(")", 1)[1].split()
                 out[name] = (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
+                if name in ("kubesim", "cqlsrv"):  # kernel share: the native servers are syscall-bound
+                    out[name + "_sys"] = int(parts[12]) / os.sysconf("SC_CLK_TCK")
             except (OSError, AttributeError, IndexError):
                 pass
         return out
+
+    async def sim_stats(self):
+        """The apiserver simulator's counters (requests, event-loop iterations, send calls)."""
+        try:
+            async with self.http.get(self.api + "/sim/stats") as r:
+                return await r.json(content_type=None)
+        except Exception:  # noqa: BLE001 - diagnostics only
+            return None
 
     async def stop(self) -> None:
         try:
