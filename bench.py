@@ -54,9 +54,10 @@ def parse_args(argv=None):
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
     ap.add_argument("--workers", type=int, default=256)
-    ap.add_argument("--procs", type=int, default=6,
-                    help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport)")
-    ap.add_argument("--inflight", type=int, default=3, help="steps pushed ahead of acknowledgement")
+    ap.add_argument("--procs", type=int, default=0,
+                    help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport); "
+                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 12")
+    ap.add_argument("--inflight", type=int, default=4, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--no-pregen", action="store_true",
                     help="generate each step's synthetic traffic on demand instead of before the timed region")
     ap.add_argument("--kube-connections", type=int, default=256)
@@ -69,6 +70,30 @@ def parse_args(argv=None):
     ap.add_argument("--pprof-out", default="", help="write a pprof profile of the timed steps (rank 0)")
     ap.add_argument("--cql-latency-us", type=int, default=0, help="inject CQL server response latency")
     return ap.parse_args(argv)
+
+
+def cpu_share() -> float:
+    """CPUs this process may use: affinity mask, capped by a cgroup-v2 quota if one is set."""
+    try:
+        n = float(len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        n = float(os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, int(quota) / int(period))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def auto_procs(local_world: int) -> int:
+    """Shard-worker processes per replica: the rank's CPU share minus 4 (simulated
+    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 12].
+    MI355X sweep (profiles/r1_sweep_procs12_mi355x.json): throughput rises to 12
+    workers, where the single-threaded apiserver simulator saturates."""
+    return max(1, min(12, int(cpu_share() / max(local_world, 1)) - 4))
 
 
 def real_hbm_oom(local_rank: int, workdir: str):
@@ -101,6 +126,8 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.procs <= 0:
+        args.procs = auto_procs(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
 
     import torch
 
