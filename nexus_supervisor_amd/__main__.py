@@ -18,6 +18,9 @@ import sys
 
 
 def main(argv=None) -> int:
+    from .utils.covtrace import install_from_env
+
+    install_from_env()  # child-process coverage for tools/coverage_gate.py (no-op unless enabled)
     argv = list(sys.argv[1:] if argv is None else argv)
     cmd = argv.pop(0) if argv and not argv[0].startswith("-") else "supervisor"
     if cmd == "supervisor":

@@ -415,8 +415,9 @@ class Supervisor:
             if compat.delete_on_read_error and failing:
                 try:
                     await self._delete_job(r.request_id)
-                except Exception:
-                    pass
+                except Exception as del_exc:  # noqa: BLE001 - the read error is what is retried
+                    self.log.error(del_exc, "failed to delete an algorithm submission after a checkpoint read error",
+                                   requestId=r.request_id, algorithm=r.algorithm)
             raise
         stamps["read"] = wall()
         key = (r.algorithm, r.request_id)

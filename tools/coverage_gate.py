@@ -6,8 +6,9 @@ file 70 / package 70 / total 75, with excluded paths).
 tracer: executable lines come from the compiled code objects of every module
 under ``nexus_supervisor_amd/`` (``co_lines``), executed lines from a
 ``sys.settrace``/``threading.settrace`` hook that only instruments frames of
-those files.  pytest runs in-process; child processes (the native CQL server,
-the bench cluster process) are not traced.
+those files.  pytest runs in-process; package child processes (``python -m
+nexus_supervisor_amd …``: shard workers) trace themselves when ``NEXUS_COVERAGE_DIR``
+is set (``nexus_supervisor_amd/utils/covtrace.py``) and their lines are merged.
 
     python tools/coverage_gate.py [--config .testcoverage.yml] [--report FILE] [-- pytest args]
 
@@ -113,6 +114,10 @@ def main(argv: List[str] = None) -> int:
                 files[p] = rel
 
     tracer = Tracer(files)
+    import tempfile
+
+    child_dir = tempfile.mkdtemp(prefix="nexus-cov-")
+    os.environ["NEXUS_COVERAGE_DIR"] = child_dir
     os.chdir(ROOT)
     sys.path.insert(0, ROOT)
     import pytest
@@ -122,6 +127,18 @@ def main(argv: List[str] = None) -> int:
         rc = pytest.main(pytest_args)
     finally:
         tracer.stop()
+
+    real = {os.path.realpath(p): p for p in files}
+    for name in os.listdir(child_dir):
+        try:
+            with open(os.path.join(child_dir, name)) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for fn, lines in doc.items():
+            p = real.get(os.path.realpath(fn))
+            if p is not None:
+                tracer.hits[p].update(lines)
 
     per_file = {}
     missing: Dict[str, List[int]] = {}
