@@ -233,6 +233,7 @@ def main(argv=None) -> int:
                 "cql_latency_us": args.cql_latency_us,
                 "stages_ms": res.get("stages"),
                 "cpu_util_rank0": res.get("cpu"),
+                "step_done_ms_rank0": res.get("step_done_ms"),
                 "baseline": "reference derived ceiling 10 decisions/s (Helm defaults; BASELINE.md)",
             },
         }

@@ -1110,7 +1110,7 @@ struct Request {
   std::string method, path;
   std::map<std::string, std::string> query;
   std::string auth;
-  std::string body;
+  std::string_view body;  // points into the connection's input buffer (valid while handled)
   bool close = false;
 };
 
@@ -1262,7 +1262,7 @@ void close_watches(int only_kind) {
 void h_apply(Conn& c, const Request& r) {
   int64_t t0 = mono_ns();
   size_t pos = 0, n = 0;
-  const std::string& b = r.body;
+  std::string_view b = r.body;
   while (pos < b.size()) {
     size_t nl = b.find('\n', pos);
     if (nl == std::string::npos) nl = b.size();
@@ -1472,7 +1472,7 @@ bool on_input(Conn& c) {
       return true;
     }
     if (c.in.size() < he + 4 + clen) return true;  // body incomplete
-    r.body = c.in.substr(he + 4, clen);
+    r.body = std::string_view(c.in.data() + he + 4, clen);  // no copy: c.in is compacted after the loop
     at = he + 4 + clen;
     try {
       handle(c, r);
@@ -1522,6 +1522,11 @@ int main(int argc, char** argv) {
   mallopt(M_TRIM_THRESHOLD, 1 << 30);
   mallopt(M_TOP_PAD, 64 << 20);
   mallopt(M_MMAP_THRESHOLD, 1 << 30);
+  // No fastbins: every object line / JSON text is a >1 KiB "large" request, and glibc
+  // consolidates all fastbin chunks before serving one — with the many small key / name
+  // strings freed in between, that consolidation was most of malloc's time.  Small
+  // chunks still go through the per-thread tcache.
+  mallopt(M_MXFAST, 0);
   prof::start();
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);

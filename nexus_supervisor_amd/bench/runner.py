@@ -178,6 +178,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         sup.classifier.evidence_provider = pod_evidence_provider(telemetry)
         sup.decision_hooks.append(tracker)
 
+        done_at: List[float] = []  # completion time of each timed step (diagnostics)
+
         async def run_steps(n: int) -> None:
             """Push ``n`` steps with at most ``cfg.inflight`` unacknowledged at a time."""
             pending: List[StepState] = []
@@ -187,6 +189,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
                     await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
                 except asyncio.TimeoutError:
                     tracker.abandon(st)
+                if tracker.record:
+                    done_at.append(time.perf_counter())
 
             for _ in range(n):
                 while len(pending) >= cfg.inflight:
@@ -216,6 +220,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         await run_steps(cfg.steps)
         barrier_sync()
         elapsed = time.perf_counter() - t0
+        step_done_ms = [round(1000.0 * (t - t0), 1) for t in done_at]
         cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3),
                "supervisor_max_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1)}
         x1 = harness.external_cpu()
@@ -261,7 +266,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
             "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
-            "probe": probe}
+            "probe": probe, "step_done_ms": step_done_ms}
 
 
 async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dict[str, Any]:
