@@ -111,3 +111,30 @@ def test_xgmi_link_down_and_ecc_are_gpu_faults():
         if expect == "XGMI_LINK_DOWN":
             assert g["xgmi_links_down"] == 2 and g["xgmi_links_total"] == 7
         assert not [e for e in tel.snapshot()[0]["events"]]
+
+
+def test_oom_keyword_prefilter_matches_full_pattern_scan():
+    """The literal-keyword prefilter never hides a signature the regex lists would find."""
+    from hypothesis import given, settings, strategies as st
+
+    from nexus_supervisor_amd.gpu import oom as O
+
+    def full(patterns, text):
+        for p in patterns:
+            m = p.search(text)
+            if m:
+                return m.group(0)
+        return None
+
+    fragments = ["hipErrorOutOfMemory", "HIP out of memory", "CUDA OUT OF MEMORY", "OutOfMemoryError", "hipMallocManaged",
+                 " failed", "RCCL", "NCCL", " out of memory", "HSA_STATUS_ERROR_OUT_OF_RESOURCES", "GPU", "MemoryError",
+                 "std::bad_alloc", "Cannot allocate memory", "Memory cgroup", "OOMKilled", "RESOURCE_EXHAUSTED: ",
+                 "Out of memory while trying to allocate", "Back-off pulling image", " ", "\n", "x"]
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.lists(st.sampled_from(fragments), max_size=8).map("".join))
+    def check(text):
+        assert O.hbm_signature(text) == full(O.HBM_PATTERNS, text)
+        assert O.host_signature(text) == full(O.HOST_PATTERNS, text)
+
+    check()
