@@ -72,27 +72,13 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def cpu_share() -> float:
-    """CPUs this process may use: affinity mask, capped by a cgroup-v2 quota if one is set."""
-    try:
-        n = float(len(os.sched_getaffinity(0)))
-    except (AttributeError, OSError):
-        n = float(os.cpu_count() or 1)
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            quota, period = f.read().split()[:2]
-        if quota != "max":
-            n = min(n, int(quota) / int(period))
-    except (OSError, ValueError):
-        pass
-    return n
-
-
 def auto_procs(local_world: int) -> int:
     """Shard-worker processes per replica: the rank's CPU share minus 4 (simulated
     apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 12].
     MI355X sweep (profiles/r1_sweep_procs12_mi355x.json): throughput rises to 12
     workers, where the single-threaded apiserver simulator saturates."""
+    from nexus_supervisor_amd.utils.cpus import cpu_share
+
     return max(1, min(12, int(cpu_share() / max(local_world, 1)) - 4))
 
 

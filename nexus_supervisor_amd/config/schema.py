@@ -161,7 +161,8 @@ class RuntimeConfig:
     gc_refreeze_interval: float = field(default=600.0, metadata=_k("gc-refreeze-interval", "duration"))  # 0 = never
     # process-per-core runtime: this many shard-worker processes, each owning the runs whose
     # job name hashes to it (informers filter at ingest), under one coordinating parent that
-    # holds the lease and serves /metrics; 1 = single-process supervisor
+    # holds the lease and serves /metrics; 1 = single-process supervisor; 0 = one per CPU of
+    # the container's share (cgroup quota / affinity) minus one for the parent
     worker_processes: int = field(default=1, metadata=_k("worker-processes"))
     # set by the coordinator in each worker process (not a user knob)
     worker_index: int = field(default=0, metadata=_k("worker-index"))
@@ -235,8 +236,12 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
     if cfg.sharding.shards < 1 or not 0 <= cfg.sharding.shard_index < cfg.sharding.shards:
         raise ConfigError("sharding.shard-index must be in [0, shards)")
     rt = cfg.runtime
+    if rt.worker_processes == 0:
+        from ..utils.cpus import auto_worker_processes
+
+        rt.worker_processes = auto_worker_processes()
     if rt.worker_processes < 1 or not 0 <= rt.worker_index < rt.worker_processes:
-        raise ConfigError("runtime.worker-processes must be >= 1 and runtime.worker-index in [0, worker-processes)")
+        raise ConfigError("runtime.worker-processes must be >= 0 (0 = auto) and runtime.worker-index in [0, worker-processes)")
     if not 0 < cfg.gpu.hbm_oom_fraction <= 1:
         raise ConfigError("gpu.hbm-oom-fraction must be in (0, 1]")
     if cfg.leader_election.enabled:

@@ -111,3 +111,22 @@ def test_format_duration_roundtrip():
         assert parse_duration(format_duration(parse_duration(s))) == pytest.approx(parse_duration(s))
     assert format_duration(90) == "1m30s"
     assert format_duration(0.1) == "100ms"
+
+
+def test_worker_processes_auto_from_cpu_share(tmp_path, monkeypatch):
+    from nexus_supervisor_amd.utils import cpus
+
+    quota = tmp_path / "cpu.max"
+    quota.write_text("350000 100000\n")  # a 3.5-CPU Kubernetes limit
+    monkeypatch.setattr(os, "sched_getaffinity", lambda _pid: set(range(64)))
+    assert cpus.cpu_share(str(quota)) == pytest.approx(3.5)
+    quota.write_text("max 100000\n")
+    assert cpus.cpu_share(str(quota)) == 64
+    assert cpus.cpu_share(str(tmp_path / "missing")) == 64
+    assert cpus.auto_worker_processes(share=3.5) == 2 and cpus.auto_worker_processes(share=1.0) == 1
+    monkeypatch.setattr(cpus, "CPU_MAX", str(tmp_path / "missing"))
+    monkeypatch.setattr(cpus.cpu_share, "__defaults__", (str(tmp_path / "missing"),))
+    c = load_config(env={"NEXUS__RUNTIME__WORKER_PROCESSES": "0"})
+    assert c.runtime.worker_processes == 63
+    with pytest.raises(ConfigError):
+        load_config(env={"NEXUS__RUNTIME__WORKER_PROCESSES": "-1"})
