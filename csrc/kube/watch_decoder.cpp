@@ -14,6 +14,9 @@
 //   ["list", sub]                 array: project every element with `sub`
 //   ["prefix", "p1", "p2", ...]   object: keep entries whose key starts with a prefix
 //   ["map", sub]                  object: keep all keys, project every value with `sub`
+//   {"$deleted": sub, ...}        (watch envelope) project "object" with `sub` instead when
+//                                 "type" is "DELETED" and precedes it: a deletion needs only
+//                                 the object's identity, the informer already holds the rest
 // A non-object value where an object projection was expected is kept whole (so
 // Status objects in ERROR events survive any kind's schema).
 #define PY_SSIZE_T_CLEAN
@@ -37,6 +40,7 @@ struct Proj {
   enum Kind { KEEP, OBJECT, LIST, PREFIX, MAP } kind = KEEP;
   std::vector<std::pair<std::string, std::unique_ptr<Proj>>> fields;  // OBJECT (small: linear scan)
   std::unique_ptr<Proj> elem;                                         // LIST / MAP
+  std::unique_ptr<Proj> on_deleted;                                   // OBJECT: "object" of a DELETED envelope
   std::vector<std::string> prefixes;                                  // PREFIX
 
   const Proj* field(std::string_view k) const {
@@ -59,6 +63,10 @@ std::unique_ptr<Proj> compile(PyObject* spec) {
       if (!s) return nullptr;
       auto sub = compile(v);
       if (!sub) return nullptr;
+      if (std::string_view(s, static_cast<size_t>(n)) == "$deleted") {
+        p->on_deleted = std::move(sub);
+        continue;
+      }
       p->fields.emplace_back(std::string(s, static_cast<size_t>(n)), std::move(sub));
     }
     return p;
@@ -427,11 +435,20 @@ class Parser {
   }
 
   PyObject* object_proj(const Proj* p) {
+    bool deleted = false;
     return object_loop([&](PyObject* d, std::string_view k) {
       const Proj* sub = p->field(k);
       if (!sub) {
         skip();
         return true;
+      }
+      if (p->on_deleted) {
+        if (k == "type") {
+          ws();
+          deleted = n_ - i_ >= 9 && std::memcmp(s_ + i_, "\"DELETED\"", 9) == 0;
+        } else if (deleted && k == "object") {
+          sub = p->on_deleted.get();
+        }
       }
       return set_item(d, k, value(sub->kind == Proj::KEEP ? nullptr : sub));
     });

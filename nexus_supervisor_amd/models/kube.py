@@ -239,9 +239,18 @@ def finish_pod(pod: Dict[str, Any]) -> Dict[str, Any]:
 FINISHERS: Dict[str, Any] = {"Pod": None, "Job": None, "Event": None, "Lease": None}  # env is derived lazily
 
 
+# A DELETED watch event only removes the object from the informer cache (which holds the
+# full last version for any handler): decode its identity and labels, skip the rest.
+_DELETED = dict(_STATUS_FIELDS, metadata={"name": True, "namespace": True, "uid": True, "resourceVersion": True,
+                                          "labels": True, "deletionTimestamp": True})
+
+
+_DELETED_BY_KIND = {"Event": dict(_DELETED, involvedObject=True)}  # shard filters route events by it
+
+
 def watch_projection(kind: str) -> Any:
     p = PROJECTIONS.get(kind)
-    return True if p is None else {"type": True, "object": p}
+    return True if p is None else {"type": True, "object": p, "$deleted": _DELETED_BY_KIND.get(kind, _DELETED)}
 
 
 def list_projection(kind: str) -> Any:

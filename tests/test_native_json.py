@@ -42,3 +42,34 @@ def test_specials_default_and_errors():
     with pytest.raises(ValueError):
         K.dumps(a)
     assert K.dumps("\x01 é") == json.dumps("\x01 é", ensure_ascii=False).encode()
+
+
+def test_deleted_watch_events_decode_identity_only():
+    """DELETED envelopes project "object" to identity + labels (Events keep involvedObject
+    for the shard filter); other types, and envelopes with "object" first, keep the full
+    projection."""
+    import json as _json
+
+    from nexus_supervisor_amd import _kube_native as K
+    from nexus_supervisor_amd.models import kube
+
+    pod = {"kind": "Pod", "apiVersion": "v1",
+           "metadata": {"name": "p", "namespace": "ns", "uid": "u", "resourceVersion": "5", "labels": {"a": "b"},
+                        "annotations": {"x": "y"}},
+           "spec": {"nodeName": "n", "containers": [{"name": "c", "env": [{"name": "X", "value": "1"}]}]},
+           "status": {"phase": "Failed"}}
+    d = K.ProjectedDecoder(kube.watch_projection("Pod"))
+    (full,) = d.feed((_json.dumps({"type": "MODIFIED", "object": pod}) + "\n").encode())
+    (gone,) = d.feed((_json.dumps({"type": "DELETED", "object": pod}) + "\n").encode())
+    assert full["object"]["spec"]["nodeName"] == "n" and full["object"]["status"]["phase"] == "Failed"
+    assert gone["type"] == "DELETED" and set(gone["object"]) == {"kind", "apiVersion", "metadata"}
+    assert gone["object"]["metadata"] == {"name": "p", "namespace": "ns", "uid": "u", "resourceVersion": "5",
+                                          "labels": {"a": "b"}}
+    (late,) = d.feed((_json.dumps({"object": pod, "type": "DELETED"}) + "\n").encode())
+    assert late["object"]["spec"]["nodeName"] == "n"  # type after object: cannot know, keep all
+    ev = {"kind": "Event", "metadata": {"name": "e", "namespace": "ns", "resourceVersion": "7"},
+          "involvedObject": {"kind": "Job", "name": "j"}, "reason": "BackoffLimitExceeded", "count": 3,
+          "source": {"component": "job-controller"}}
+    (ge,) = K.ProjectedDecoder(kube.watch_projection("Event")).feed((_json.dumps({"type": "DELETED", "object": ev}) + "\n").encode())
+    assert ge["object"]["involvedObject"] == {"kind": "Job", "name": "j"}
+    assert "source" not in ge["object"] and "count" not in ge["object"]
