@@ -52,6 +52,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <map>
 #include <memory>
@@ -207,7 +208,45 @@ int kind_by_name(std::string_view k) {
 // ============================================================ selectors
 // Selectable attributes of an object: its labels plus a fixed set of field paths
 // (prefixed "\x01f:" so they never collide with a label key).
-using Attrs = std::vector<std::pair<std::string, std::string>>;
+// Packed into one buffer ([u32 len][key][u32 len][value]...): one allocation per object
+// version instead of two strings per attribute (allocation was a quarter of the
+// simulator's time under the benchmark's churn).
+class Attrs {
+ public:
+  void add(std::string_view k, std::string_view v) {
+    put(k);
+    put(v);
+  }
+  void reserve(size_t bytes) { buf_.reserve(bytes); }
+  bool find(std::string_view k, std::string_view& v) const {
+    size_t i = 0;
+    while (i < buf_.size()) {
+      std::string_view key = get(i);
+      std::string_view val = get(i);
+      if (key == k) {
+        v = val;
+        return true;
+      }
+    }
+    return false;
+  }
+
+ private:
+  void put(std::string_view x) {
+    uint32_t n = static_cast<uint32_t>(x.size());
+    buf_.append(reinterpret_cast<const char*>(&n), sizeof n);
+    buf_.append(x.data(), x.size());
+  }
+  std::string_view get(size_t& i) const {
+    uint32_t n;
+    std::memcpy(&n, buf_.data() + i, sizeof n);
+    i += sizeof n;
+    std::string_view x(buf_.data() + i, n);
+    i += n;
+    return x;
+  }
+  std::string buf_;
+};
 const char* const FIELD_PATHS[][3] = {{"metadata", "name", nullptr},        {"metadata", "namespace", nullptr},
                                       {"spec", "nodeName", nullptr},        {"status", "phase", nullptr},
                                       {"involvedObject", "kind", nullptr}, {"involvedObject", "name", nullptr},
@@ -219,7 +258,7 @@ std::shared_ptr<const Attrs> attrs_of(const Value& obj) {
   const Value* labels = md ? md->get("labels") : nullptr;
   if (labels && labels->t == Value::OBJ)
     for (auto& kv : labels->o)
-      if (kv.second.t == Value::STR) a->emplace_back(kv.first, kv.second.s);
+      if (kv.second.t == Value::STR) a->add(kv.first, kv.second.s);
   for (auto& fp : FIELD_PATHS) {
     const Value* cur = &obj;
     std::string key = "\x01" "f:";
@@ -229,7 +268,7 @@ std::shared_ptr<const Attrs> attrs_of(const Value& obj) {
       if (i) key += '.';
       key += fp[i];
     }
-    if (cur && cur->t == Value::STR) a->emplace_back(key, cur->s);
+    if (cur && cur->t == Value::STR) a->add(key, cur->s);
   }
   return a;
 }
@@ -280,17 +319,13 @@ void parse_selector(std::string_view sel, bool fields, Selector& out) {
 
 bool matches(const Attrs& a, const Selector& sel) {
   for (auto& r : sel) {
-    const std::string* v = nullptr;
-    for (auto& kv : a)
-      if (kv.first == r.key) {
-        v = &kv.second;
-        break;
-      }
+    std::string_view v;
+    bool has = a.find(r.key, v);
     switch (r.op) {
-      case '=': if (!v || *v != r.val) return false; break;
-      case '!': if (v && *v == r.val) return false; break;
-      case 'e': if (!v) return false; break;
-      case 'n': if (v) return false; break;
+      case '=': if (!has || v != r.val) return false; break;
+      case '!': if (has && v == r.val) return false; break;
+      case 'e': if (!has) return false; break;
+      case 'n': if (has) return false; break;
     }
   }
   return true;
@@ -376,6 +411,8 @@ int64_t g_rv = 1000;
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0;
   uint64_t loops = 0, sends = 0, send_bytes = 0, eagain = 0;
+  // wall time spent per phase of the event loop (ns): where a saturated simulator goes
+  int64_t apply_ns = 0, request_ns = 0, flush_ns = 0, recv_ns = 0, busy_ns = 0;
 } g_stats;
 
 struct Snapshot {
@@ -728,15 +765,17 @@ class RawScan {
 
 std::shared_ptr<const Attrs> attrs_raw(const Raw& r) {
   auto a = std::make_shared<Attrs>();
-  a->reserve(r.labels.size() + 8);
-  for (auto& kv : r.labels) a->emplace_back(std::string(kv.first), std::string(kv.second));
+  size_t bytes = 8 * 40;
+  for (auto& kv : r.labels) bytes += kv.first.size() + kv.second.size() + 8;
+  a->reserve(bytes + r.name.size() + r.ns.size() + r.node.size() + r.iname.size());
+  for (auto& kv : r.labels) a->add(kv.first, kv.second);
   const std::pair<const char*, std::string_view> fields[] = {
       {"\x01" "f:metadata.name", r.name},  {"\x01" "f:metadata.namespace", r.ns},
       {"\x01" "f:spec.nodeName", r.node},   {"\x01" "f:status.phase", r.phase},
       {"\x01" "f:involvedObject.kind", r.ikind}, {"\x01" "f:involvedObject.name", r.iname},
       {"\x01" "f:reason", r.reason},       {"\x01" "f:type", r.type}};
   for (auto& f : fields)
-    if (f.second.data()) a->emplace_back(f.first, std::string(f.second));
+    if (f.second.data()) a->add(f.first, f.second);
   return a;
 }
 
@@ -1299,6 +1338,7 @@ void h_apply(Conn& c, const Request& r) {
     for (int k = 0; k < NKINDS; ++k) expire_kind(k);
     close_watches(-1);
   }
+  g_stats.apply_ns += mono_ns() - t0;
   char buf[160];
   snprintf(buf, sizeof buf, "{\"applied\":%zu,\"rv\":%lld,\"t_push\":%.9f}", n, static_cast<long long>(g_rv),
            static_cast<double>(t0) / 1e9);
@@ -1316,6 +1356,9 @@ void handle(Conn& c, Request& r) {
                       ",\"deleted\":" + std::to_string(g_stats.deleted) + ",\"applied\":" + std::to_string(g_stats.applied) +
                       ",\"loops\":" + std::to_string(g_stats.loops) + ",\"sends\":" + std::to_string(g_stats.sends) +
                       ",\"send_bytes\":" + std::to_string(g_stats.send_bytes) + ",\"eagain\":" + std::to_string(g_stats.eagain) +
+                      ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
+                      ",\"flush_ns\":" + std::to_string(g_stats.flush_ns) + ",\"recv_ns\":" + std::to_string(g_stats.recv_ns) +
+                      ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
                       ",\"objects\":{";
       for (int k = 0; k < NKINDS; ++k) {
         if (k) s += ',';
@@ -1474,11 +1517,13 @@ bool on_input(Conn& c) {
     if (c.in.size() < he + 4 + clen) return true;  // body incomplete
     r.body = std::string_view(c.in.data() + he + 4, clen);  // no copy: c.in is compacted after the loop
     at = he + 4 + clen;
+    int64_t th = mono_ns();
     try {
       handle(c, r);
     } catch (const std::exception& e) {
       respond(c, 400, status_body(400, "BadRequest", e.what()));
     }
+    g_stats.request_ns += mono_ns() - th;  // includes bulk applies (apply_ns is their share)
     if (c.close_after) return true;
   }
   return true;
@@ -1576,6 +1621,7 @@ int main(int argc, char** argv) {
   char buf[1 << 16];
   while (!g_stop) {
     int n = epoll_wait(g_ep, evs.data(), static_cast<int>(evs.size()), 100);
+    int64_t t_loop = mono_ns();
     ++g_stats.loops;
     if (n < 0 && errno != EINTR) {
       perror("epoll_wait");
@@ -1604,6 +1650,7 @@ int main(int argc, char** argv) {
       Conn& c = *it->second;
       bool dead = false;
       if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+        int64_t tr = mono_ns();
         while (true) {
           ssize_t r = recv(fd, buf, sizeof buf, 0);
           if (r > 0) {
@@ -1617,6 +1664,7 @@ int main(int argc, char** argv) {
           else if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) dead = true;
           break;
         }
+        g_stats.recv_ns += mono_ns() - tr;
         if (!dead && !on_input(c)) dead = true;
       }
       if (dead) {
@@ -1644,11 +1692,14 @@ int main(int argc, char** argv) {
       for (Conn* c : ended) end_watch(*c, true);
     }
     if (!g_dirty.empty()) {
+      int64_t tf = mono_ns();
       std::vector<Conn*> dirty(g_dirty.begin(), g_dirty.end());
       g_dirty.clear();
       for (Conn* c : dirty)
         if (!flush(*c)) close_conn(c->fd);
+      g_stats.flush_ns += mono_ns() - tf;
     }
+    g_stats.busy_ns += mono_ns() - t_loop;
   }
   for (auto& kv : g_conns) close(kv.first);
   close(lfd);

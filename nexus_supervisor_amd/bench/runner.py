@@ -231,6 +231,11 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             n_ev = max(cfg.events * cfg.steps, 1)
             for k in ("requests", "loops", "sends"):
                 cpu[f"kubesim_{k}_per_event"] = round((s1.get(k, 0) - s0.get(k, 0)) / n_ev, 3)
+            # event-loop phases (µs per pod failure): busy = everything but epoll_wait;
+            # request includes apply (the synthetic traffic injection)
+            for k in ("busy", "apply", "request", "recv", "flush"):
+                if f"{k}_ns" in s1:
+                    cpu[f"kubesim_{k}_us_per_event"] = round((s1[f"{k}_ns"] - s0.get(f"{k}_ns", 0)) / 1000.0 / n_ev, 2)
         workers = [v for k, v in cpu.items() if k.startswith("worker")]
         if workers:
             cpu["workers_util_sum"] = round(sum(workers), 3)
