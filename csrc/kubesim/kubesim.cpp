@@ -280,6 +280,21 @@ struct Req {
 };
 using Selector = std::vector<Req>;
 
+std::string_view trim_view(std::string_view s) {
+  size_t b = 0, e = s.size();
+  while (b < e && isspace(static_cast<unsigned char>(s[b]))) ++b;
+  while (e > b && isspace(static_cast<unsigned char>(s[e - 1]))) --e;
+  return s.substr(b, e - b);
+}
+
+// ASCII case-insensitive equality; `lower` must already be lower case
+bool iequals(std::string_view s, std::string_view lower) {
+  if (s.size() != lower.size()) return false;
+  for (size_t i = 0; i < s.size(); ++i)
+    if (static_cast<char>(tolower(static_cast<unsigned char>(s[i]))) != lower[i]) return false;
+  return true;
+}
+
 std::string trim(std::string_view s) {
   size_t b = 0, e = s.size();
   while (b < e && isspace(static_cast<unsigned char>(s[b]))) ++b;
@@ -1399,9 +1414,14 @@ void handle(Conn& c, Request& r) {
   if (r.method == "DELETE" && !name.empty()) {
     std::string prop = "Background";
     if (!r.body.empty()) {
-      Value b = kjson::parse(r.body);
-      std::string p(b.path({"propagationPolicy"}));
-      if (!p.empty()) prop = p;
+      // DeleteOptions: only propagationPolicy matters here; a plain scan for its string
+      // value (an enum, never escaped) instead of a DOM parse per DELETE
+      size_t k = r.body.find("\"propagationPolicy\"");
+      size_t c = k == std::string_view::npos ? k : r.body.find(':', k + 19);
+      size_t q1 = c == std::string_view::npos ? c : r.body.find('"', c + 1);
+      size_t q2 = q1 == std::string_view::npos ? q1 : r.body.find('"', q1 + 1);
+      if (q2 != std::string_view::npos && q2 > q1 + 1) prop = std::string(r.body.substr(q1 + 1, q2 - q1 - 1));
+      else if (k == std::string_view::npos) kjson::parse(r.body);  // still reject malformed bodies
     }
     std::string qp = q(r, "propagationPolicy");
     if (!qp.empty()) prop = qp;
@@ -1495,17 +1515,15 @@ bool on_input(Conn& c) {
       pos = e + 2;
       size_t colon = line.find(':');
       if (colon == std::string_view::npos) continue;
-      std::string name(line.substr(0, colon));
-      for (auto& ch : name) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
-      std::string val = trim(line.substr(colon + 1));
-      if (name == "content-length") clen = static_cast<size_t>(atol(val.c_str()));
-      else if (name == "authorization") r.auth = val;
-      else if (name == "transfer-encoding" && val.find("chunked") != std::string::npos) chunked = true;
-      else if (name == "connection") {
-        std::string v = val;
-        for (auto& ch : v) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
-        if (v == "close") r.close = true;
-        else if (v == "keep-alive") r.close = false;
+      // header names / connection tokens compared case-insensitively in place (no copies)
+      std::string_view name = line.substr(0, colon);
+      std::string_view val = trim_view(line.substr(colon + 1));
+      if (iequals(name, "content-length")) clen = static_cast<size_t>(strtoull(std::string(val).c_str(), nullptr, 10));
+      else if (iequals(name, "authorization")) r.auth = std::string(val);
+      else if (iequals(name, "transfer-encoding") && val.find("chunked") != std::string_view::npos) chunked = true;
+      else if (iequals(name, "connection")) {
+        if (iequals(val, "close")) r.close = true;
+        else if (iequals(val, "keep-alive")) r.close = false;
       }
     }
     if (chunked) {
