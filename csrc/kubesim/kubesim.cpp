@@ -383,10 +383,36 @@ void splice_rv(Obj& o, int64_t rv) {
   o.rv_len = r.size();
 }
 
+// One watch line, `{"type":"<T>","object":` + object text + `}\n`, kept as the static type
+// prefix plus the object's own immutable (shared) text: recording a change copies nothing,
+// and a watch chunk goes out as three iovecs per line over the store's buffers.
+struct Line {
+  const std::string* prefix;
+  std::shared_ptr<const std::string> json;
+  size_t size() const { return prefix->size() + json->size() + 2; }
+};
+
+const std::string* line_prefix(const char* etype) {
+  static const std::string added = "{\"type\":\"ADDED\",\"object\":";
+  static const std::string modified = "{\"type\":\"MODIFIED\",\"object\":";
+  static const std::string deleted = "{\"type\":\"DELETED\",\"object\":";
+  if (etype[0] == 'A') return &added;
+  if (etype[0] == 'M') return &modified;
+  return &deleted;
+}
+
+char g_line_end[] = "}\n";
+
+void append_line(std::string& out, const Line& l) {
+  out += *l.prefix;
+  out += *l.json;
+  out.append(g_line_end, 2);
+}
+
 struct Hist {
   int64_t rv;
   std::string ns;
-  std::shared_ptr<const std::string> line;
+  Line line;
   std::shared_ptr<const Attrs> attrs;
 };
 
@@ -403,7 +429,7 @@ struct Watch {
   std::string pending;  // control lines (ERROR / BOOKMARK) for the next chunk
   // event lines committed this loop iteration: shared with the history, sent as one
   // chunk straight from these buffers (sendmsg iovecs; no per-watch copy)
-  std::vector<std::shared_ptr<const std::string>> lines;
+  std::vector<Line> lines;
   size_t lines_bytes = 0;
   bool idle() const { return pending.empty() && lines.empty(); }
   void clear() {
@@ -444,17 +470,10 @@ std::string okey(std::string_view ns, std::string_view name) {
   return k;
 }
 
-void watch_push(Watch* w, const std::shared_ptr<const std::string>& line);
+void watch_push(Watch* w, const Line& line);
 
 void record(int kind, const char* etype, const Obj& o) {
-  std::string line;
-  line.reserve(o.json->size() + 32);
-  line += "{\"type\":\"";
-  line += etype;
-  line += "\",\"object\":";
-  line += *o.json;
-  line += "}\n";
-  auto lp = std::make_shared<const std::string>(std::move(line));
+  Line lp{line_prefix(etype), o.json};
   KindStore& ks = g_store[kind];
   ks.history.push_back(Hist{o.rv, o.ns, lp, o.attrs});
   while (ks.history.size() > g_opt.history) {
@@ -860,7 +879,7 @@ bool apply_raw(std::string_view line) {
   auto it = ks.objs.find(key);
   const Obj* prev = it == ks.objs.end() ? nullptr : &it->second;
   Obj o = finish_raw(r, line, ob, oe, prev);
-  if (kind == K_POD) {
+  if (kind == K_POD && !(prev && prev->job == o.job)) {  // job label unchanged: index stays
     if (prev) index_pod(*prev, false);
     index_pod(o, true);
   }
@@ -912,7 +931,7 @@ int update(int kind, Value& doc, bool check_rv, std::string* out_json, std::stri
   std::string want(md.path({"resourceVersion"}));
   if (check_rv && !want.empty() && want != std::to_string(it->second.rv)) return 2;
   Obj o = finish(kind, doc, &it->second, src);
-  if (kind == K_POD) {
+  if (kind == K_POD && it->second.job != o.job) {
     index_pod(it->second, false);
     index_pod(o, true);
   }
@@ -989,7 +1008,7 @@ void end_watch(Conn& c, bool terminate_chunked) {
       snprintf(hdr, sizeof hdr, "%zx\r\n", w->pending.size() + w->lines_bytes);
       c.out += hdr;
       c.out += w->pending;
-      for (auto& l : w->lines) c.out += *l;
+      for (auto& l : w->lines) append_line(c.out, l);
       c.out += "\r\n";
     }
     c.out += "0\r\n\r\n";
@@ -1010,12 +1029,12 @@ void close_conn(int fd) {
   g_conns.erase(it);
 }
 
-void watch_push(Watch* w, const std::shared_ptr<const std::string>& line) {
+void watch_push(Watch* w, const Line& line) {
   if (w->idle()) {
     auto it = g_conns.find(w->fd);
     if (it != g_conns.end()) g_dirty.insert(it->second.get());
   }
-  w->lines_bytes += line->size();
+  w->lines_bytes += line.size();
   w->lines.push_back(line);
 }
 
@@ -1030,17 +1049,22 @@ bool flush_watch(Conn& c) {
   if (!c.out.empty()) {  // keep the byte order: append behind what is queued
     c.out.append(hdr, static_cast<size_t>(hl));
     c.out += w->pending;
-    for (auto& l : w->lines) c.out += *l;
+    for (auto& l : w->lines) append_line(c.out, l);
     c.out += "\r\n";
     w->clear();
     return true;
   }
   static char crlf[] = "\r\n";
-  std::vector<iovec> iov;
-  iov.reserve(w->lines.size() + 3);
+  static std::vector<iovec> iov;  // single-threaded event loop: reused across flushes
+  iov.clear();
+  iov.reserve(3 * w->lines.size() + 3);
   iov.push_back({hdr, static_cast<size_t>(hl)});
   if (!w->pending.empty()) iov.push_back({w->pending.data(), w->pending.size()});
-  for (auto& l : w->lines) iov.push_back({const_cast<char*>(l->data()), l->size()});
+  for (auto& l : w->lines) {
+    iov.push_back({const_cast<char*>(l.prefix->data()), l.prefix->size()});
+    iov.push_back({const_cast<char*>(l.json->data()), l.json->size()});
+    iov.push_back({g_line_end, 2});
+  }
   iov.push_back({crlf, 2});
   size_t i = 0;
   bool ok = true;
@@ -1291,7 +1315,7 @@ void h_watch(Conn& c, const Request& r, int kind, const std::string& ns) {
     for (size_t i = lo; i < ks.history.size(); ++i) {
       const Hist& h = ks.history[i];
       if ((ns.empty() || h.ns == ns) && matches(*h.attrs, w->sel)) {
-        w->lines_bytes += h.line->size();
+        w->lines_bytes += h.line.size();
         w->lines.push_back(h.line);
       }
     }
