@@ -229,14 +229,7 @@ class SharedInformer:
                 backoff = 0.2
                 while True:
                     try:
-                        async for etype, obj in self.lw.watch(self._rv):
-                            if etype == ERROR:
-                                code = (obj or {}).get("code")
-                                if code == 410:
-                                    raise WatchGone()
-                                log.warning("%s watch error object: %s", self.kind, obj)
-                                break
-                            self._apply(etype, obj)
+                        await self._watch_once()
                     except WatchGone:
                         log.info("%s watch expired (410) at rv=%s, re-listing", self.kind, self._rv)
                         break
@@ -248,6 +241,35 @@ class SharedInformer:
                 log.warning("%s list/watch failed: %s; retrying in %.1fs", self.kind, exc, backoff)
                 await asyncio.sleep(backoff * (1 + random.random() * 0.2))
                 backoff = min(backoff * 2, 30.0)
+
+    def _watch_error(self, obj) -> None:
+        if (obj or {}).get("code") == 410:
+            raise WatchGone()
+        log.warning("%s watch error object: %s", self.kind, obj)
+
+    async def _watch_once(self) -> None:
+        """One watch stream from the last resourceVersion: returns on a clean end or an error
+        object, raises :class:`WatchGone` on 410.  A transport with ``watch_batches`` (the
+        watch hub's per-worker feed) hands over one list per received frame, applied in one
+        loop instead of one async-generator step per line; either way the loop yields to the
+        pipeline every 64 lines."""
+        batches = getattr(self.lw, "watch_batches", None)
+        if batches is None:
+            async for etype, obj in self.lw.watch(self._rv):
+                if etype == ERROR:
+                    return self._watch_error(obj)
+                self._apply(etype, obj)
+            return
+        n = 0
+        apply = self._apply
+        async for batch in batches(self._rv):
+            for etype, obj in batch:
+                if etype == ERROR:
+                    return self._watch_error(obj)
+                apply(etype, obj)
+                n += 1
+                if not n & 63:
+                    await asyncio.sleep(0)
 
     async def _resync_loop(self):
         while True:

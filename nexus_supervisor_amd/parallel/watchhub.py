@@ -241,6 +241,30 @@ class HubListWatch(ListWatch):
             it.setdefault("kind", self.kind)
         return items, rv
 
+    async def watch_batches(self, resource_version: str):
+        """The :meth:`watch` stream as one list of ``(type, object)`` per hub frame (the
+        informer's batched path: no async-generator step per line)."""
+        from .. import _kube_native
+
+        decoder = _kube_native.ProjectedDecoder(self._watch_proj)
+        kind = self.kind
+        while True:
+            ftype, payload = await self.queue.get()
+            if ftype == SNAPSHOT:
+                self._pending = payload
+                yield [("ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": "hub re-listed"})]
+                return
+            if ftype == 0:
+                raise ConnectionError("watch hub closed")
+            batch = []
+            for ev in decoder.feed(payload):
+                obj = ev.get("object") or {}
+                if obj.get("kind") is None:
+                    obj["kind"] = kind
+                batch.append((ev.get("type", ""), obj))
+            if batch:
+                yield batch
+
     async def watch(self, resource_version: str):
         from .. import _kube_native
 

@@ -172,6 +172,59 @@ def test_watch_splitter_routes_lines_and_list_items():
         sp_pod.split_list(b'{"kind":"Status"}')
 
 
+def test_hub_feed_batched_watch_matches_per_line(arun):
+    """HubListWatch.watch_batches (one list per frame, the informer's path) yields the same
+    (type, object) stream as the per-line watch(), and a newer snapshot ends both with a 410
+    that leaves the snapshot pending for the informer's re-list."""
+    from nexus_supervisor_amd.informer.informer import SharedInformer
+    from nexus_supervisor_amd.parallel.watchhub import LINES, SNAPSHOT, HubListWatch
+
+    labels = LabelConfig()
+    pods = [make_pod(f"job-{i}", labels) for i in range(100)]
+    frames = [(LINES, b"".join(_line("ADDED", p) for p in pods[:70])),
+              (LINES, b"".join(_line("DELETED", p) for p in pods[70:])),
+              (SNAPSHOT, b"77\n" + _kube_native.dumps([pods[0]]))]
+
+    async def drain(batched):
+        q = asyncio.Queue()
+        for f in frames:
+            q.put_nowait(f)
+        lw = HubListWatch("Pod", q)
+        got = []
+        if batched:
+            async for batch in lw.watch_batches("1"):
+                got.extend(batch)
+        else:
+            async for item in lw.watch("1"):
+                got.append(item)
+        items, rv = await lw.list()
+        return got, items, rv
+
+    async def informer_run():
+        q = asyncio.Queue()
+        q.put_nowait((SNAPSHOT, b"5\n[]"))
+        for f in frames:
+            q.put_nowait(f)
+        inf = SharedInformer("Pod", HubListWatch("Pod", q))
+        task = inf.start()
+        for _ in range(200):
+            await asyncio.sleep(0.01)
+            if inf.relists >= 2:
+                break
+        task.cancel()
+        return inf
+
+    per_line = arun(drain(False))
+    batched = arun(drain(True))
+    assert per_line == batched
+    got, items, rv = batched
+    assert [t for t, _ in got] == ["ADDED"] * 70 + ["DELETED"] * 30 + ["ERROR"]
+    assert got[-1][1]["code"] == 410 and rv == "77" and len(items) == 1
+    inf = arun(informer_run())
+    assert inf.relists == 2 and inf.watch_events == 100  # frames applied, then the new snapshot
+    assert len(inf.indexer.values()) == 1
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("hub", [True, False], ids=["watch-hub", "per-worker-watch"])
 def test_two_worker_replica_reference_parity(arun, tmp_path, hub):
