@@ -370,26 +370,18 @@ void locate_rv(Obj& o) {
   }
 }
 
-// same object text with another resourceVersion (no parse / re-serialise)
-void splice_rv(Obj& o, int64_t rv) {
-  std::string r = std::to_string(rv);
-  auto j = std::make_shared<std::string>();
-  j->reserve(o.json->size() + 4);
-  j->append(*o.json, 0, o.rv_off);
-  j->append(r);
-  j->append(*o.json, o.rv_off + o.rv_len, std::string::npos);
-  o.json = std::move(j);
-  o.rv = rv;
-  o.rv_len = r.size();
-}
-
 // One watch line, `{"type":"<T>","object":` + object text + `}\n`, kept as the static type
 // prefix plus the object's own immutable (shared) text: recording a change copies nothing,
 // and a watch chunk goes out as three iovecs per line over the store's buffers.
+// A DELETED line carries the deletion's resourceVersion in `rv`, replacing the digits at
+// json[rv_off, rv_off + rv_len) when sent (the removed object's text is not copied).
 struct Line {
   const std::string* prefix;
   std::shared_ptr<const std::string> json;
-  size_t size() const { return prefix->size() + json->size() + 2; }
+  uint32_t rv_off = 0, rv_len = 0;
+  uint8_t rvn = 0;
+  char rv[23];
+  size_t size() const { return prefix->size() + json->size() - rv_len + rvn + 2; }
 };
 
 const std::string* line_prefix(const char* etype) {
@@ -405,7 +397,13 @@ char g_line_end[] = "}\n";
 
 void append_line(std::string& out, const Line& l) {
   out += *l.prefix;
-  out += *l.json;
+  if (l.rvn) {
+    out.append(*l.json, 0, l.rv_off);
+    out.append(l.rv, l.rvn);
+    out.append(*l.json, l.rv_off + l.rv_len, std::string::npos);
+  } else {
+    out += *l.json;
+  }
   out.append(g_line_end, 2);
 }
 
@@ -472,10 +470,18 @@ std::string okey(std::string_view ns, std::string_view name) {
 
 void watch_push(Watch* w, const Line& line);
 
-void record(int kind, const char* etype, const Obj& o) {
+// `new_rv` > 0: a deletion at that resourceVersion of `o` (text still at o.rv), spliced on send
+void record(int kind, const char* etype, const Obj& o, int64_t new_rv = 0) {
   Line lp{line_prefix(etype), o.json};
+  int64_t rv = o.rv;
+  if (new_rv > 0) {
+    rv = new_rv;
+    lp.rv_off = static_cast<uint32_t>(o.rv_off);
+    lp.rv_len = static_cast<uint32_t>(o.rv_len);
+    lp.rvn = static_cast<uint8_t>(snprintf(lp.rv, sizeof lp.rv, "%lld", static_cast<long long>(new_rv)));
+  }
   KindStore& ks = g_store[kind];
-  ks.history.push_back(Hist{o.rv, o.ns, lp, o.attrs});
+  ks.history.push_back(Hist{rv, o.ns, lp, o.attrs});
   while (ks.history.size() > g_opt.history) {
     ks.compacted = ks.history.front().rv;
     ks.history.pop_front();
@@ -948,14 +954,14 @@ bool remove(int kind, const std::string& ns, const std::string& name, const std:
   g_store[kind].objs.erase(it);
   if (kind == K_POD) index_pod(o, false);
   if (o.rv_off != std::string::npos) {
-    splice_rv(o, ++g_rv);
+    record(kind, "DELETED", o, ++g_rv);  // new resourceVersion spliced in on send
   } else {
     Value doc = kjson::parse(*o.json);
     o.rv = ++g_rv;
     doc.at("metadata").at("resourceVersion") = Value::str(std::to_string(o.rv));
     o.json = std::make_shared<const std::string>(kjson::dump(doc));
+    record(kind, "DELETED", o);
   }
-  record(kind, "DELETED", o);
   ++g_stats.deleted;
   if (kind == K_JOB && (propagation == "Background" || propagation == "Foreground")) {
     auto pit = g_pods_by_job.find(okey(ns, name));
@@ -1057,12 +1063,19 @@ bool flush_watch(Conn& c) {
   static char crlf[] = "\r\n";
   static std::vector<iovec> iov;  // single-threaded event loop: reused across flushes
   iov.clear();
-  iov.reserve(3 * w->lines.size() + 3);
+  iov.reserve(5 * w->lines.size() + 3);
   iov.push_back({hdr, static_cast<size_t>(hl)});
   if (!w->pending.empty()) iov.push_back({w->pending.data(), w->pending.size()});
-  for (auto& l : w->lines) {
+  for (auto& l : w->lines) {  // pointers into w->lines stay valid until w->clear()
     iov.push_back({const_cast<char*>(l.prefix->data()), l.prefix->size()});
-    iov.push_back({const_cast<char*>(l.json->data()), l.json->size()});
+    char* j = const_cast<char*>(l.json->data());
+    if (l.rvn) {
+      iov.push_back({j, l.rv_off});
+      iov.push_back({const_cast<char*>(l.rv), l.rvn});
+      iov.push_back({j + l.rv_off + l.rv_len, l.json->size() - l.rv_off - l.rv_len});
+    } else {
+      iov.push_back({j, l.json->size()});
+    }
     iov.push_back({g_line_end, 2});
   }
   iov.push_back({crlf, 2});

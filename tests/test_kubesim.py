@@ -105,6 +105,14 @@ def test_resource_versions_spliced_consistently(arun):
             assert [e for e, _, _ in lines] == ["MODIFIED", "DELETED"]
             assert lines[0][1] == str(r2["rv"]) and int(lines[1][1]) > r2["rv"]
             assert lines[1][2]["status"] == {"phase": "Running"} and lines[1][2]["metadata"]["uid"] == pod["metadata"]["uid"]
+            # a watch resumed from the history replays the same DELETED line (its RV is
+            # spliced into the removed object's text on send, not stored as a copy)
+            replay = []
+            async for et, o in c.watch("Pod", "nexus", str(r2["rv"]), timeout_seconds=1):
+                replay.append((et, o["metadata"]["resourceVersion"], o))
+                if et == "DELETED":
+                    break
+            assert replay == lines[1:]
             # server-owned metadata missing: inserted into the client's text (uid, timestamp, RV)
             bare = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "bare", "namespace": "nexus"}}
             r3 = await ctl.apply([("ADDED", bare)])
