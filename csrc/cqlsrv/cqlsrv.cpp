@@ -1343,7 +1343,7 @@ void update_interest(Conn& c) {
   if (want == c.want_write) return;
   c.want_write = want;
   epoll_event ev{};
-  ev.events = EPOLLIN | (want ? EPOLLOUT : 0);
+  ev.events = EPOLLIN | (want ? static_cast<uint32_t>(EPOLLOUT) : 0u);
   ev.data.fd = c.fd;
   epoll_ctl(g_epfd, EPOLL_CTL_MOD, c.fd, &ev);
 }

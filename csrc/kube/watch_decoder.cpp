@@ -34,6 +34,10 @@
 #include <unordered_map>
 #include <vector>
 
+// CPython static type objects are declared with only their header and filled in at
+// module init; the remaining slots are zero by static initialisation.
+#pragma GCC diagnostic ignored "-Wmissing-field-initializers"
+
 namespace {
 
 struct Proj {
@@ -1210,7 +1214,7 @@ PyMethodDef module_methods[] = {
 
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_kube_native",
                       "Projected JSON decoding of Kubernetes watch streams and LIST bodies; fast JSON encoding", -1,
-                      module_methods};
+                      module_methods, nullptr, nullptr, nullptr, nullptr};
 
 }  // namespace
 

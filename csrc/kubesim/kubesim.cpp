@@ -472,7 +472,7 @@ void watch_push(Watch* w, const Line& line);
 
 // `new_rv` > 0: a deletion at that resourceVersion of `o` (text still at o.rv), spliced on send
 void record(int kind, const char* etype, const Obj& o, int64_t new_rv = 0) {
-  Line lp{line_prefix(etype), o.json};
+  Line lp{line_prefix(etype), o.json, 0, 0, 0, {}};
   int64_t rv = o.rv;
   if (new_rv > 0) {
     rv = new_rv;
@@ -1299,7 +1299,7 @@ void h_list(Conn& c, const Request& r, int kind, const std::string& ns) {
 
 void h_watch(Conn& c, const Request& r, int kind, const std::string& ns) {
   ++g_stats.watch_requests;
-  auto* w = new Watch{c.fd, kind, ns, {}, q(r, "allowWatchBookmarks") == "true" || q(r, "allowWatchBookmarks") == "1", 0, 0, {}};
+  auto* w = new Watch{c.fd, kind, ns, {}, q(r, "allowWatchBookmarks") == "true" || q(r, "allowWatchBookmarks") == "1", 0, 0, {}, {}, 0};
   parse_selector(q(r, "labelSelector"), false, w->sel);
   parse_selector(q(r, "fieldSelector"), true, w->sel);
   long timeout = atol(q(r, "timeoutSeconds", "0").c_str());

@@ -7,3 +7,10 @@ attribution (HBM-OOM vs host-OOM on 288 GB HBM3E), RCCL/xGMI rank topology in
 the trace row, keyed work pipeline, leader election and pprof-format profiling.
 """
 __version__ = "0.1.0"
+
+import os as _os
+
+# Sanitizer runs (tests/test_sanitizers.py): resolve the native extensions from an
+# instrumented build directory first.
+if _os.environ.get("NEXUS_NATIVE_DIR"):
+    __path__.insert(0, _os.environ["NEXUS_NATIVE_DIR"])  # type: ignore[name-defined]

@@ -9,7 +9,14 @@ artefact               sources                                 toolchain
 ``bin/nexus-cqlsrv``   ``csrc/cqlsrv/*.cpp`` (+ proto)         g++ (epoll)
 ``bin/nexus-kubesim``  ``csrc/kubesim/*.cpp`` (+ json.hpp)     g++ (epoll)
 ``bin/gpu_stress``     ``csrc/stress/gpu_stress.hip``          hipcc gfx950
+``_amdsmi_monitor_stub`` monitor over ``amdsmi_stub.cpp``      g++ (CPU tests)
+``bin/monitor_selftest`` monitor threads over the stub          g++ (TSan/ASan)
 =====================  ======================================  ==================
+
+Every C++ target builds with ``-Wall -Wextra -Werror`` (the CI static-analysis gate).
+``--sanitize address|undefined|thread`` also builds the in-process extensions with the
+sanitizer into ``build/san/<name>/``; tests load them in a subprocess via
+``NEXUS_NATIVE_DIR`` with the runtime LD_PRELOADed (:func:`sanitizer_runtime`).
 
 ``python -m nexus_supervisor_amd._build [--force] [--only NAME] [--sanitize thread|address]``
 """
@@ -28,6 +35,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 BIN = os.path.join(PKG, "bin")
+SAN_DIR = os.path.join(ROOT, "build", "san")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -44,52 +52,101 @@ def _cxx() -> str:
 
 
 def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
-    common = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-fvisibility=hidden"]
-    san = [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"] if sanitize else []
+    """Every native artefact.  With ``sanitize`` the in-process extensions are built into
+    ``SAN_DIR/<sanitizer>/`` (loaded in a subprocess through ``NEXUS_NATIVE_DIR``) and the
+    executables get a ``-<sanitizer>`` suffix."""
+    common = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter", "-fvisibility=hidden"]
+    san = []
+    if sanitize:
+        flags = "address,undefined" if sanitize in ("address", "undefined") else sanitize
+        san = [f"-fsanitize={flags}", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"
+               if sanitize != "thread" else "-fno-omit-frame-pointer"]
     proto = os.path.join(CSRC, "cql", "cql_proto.hpp")
+    amd = os.path.join(CSRC, "amdsmi")
+    mon_deps = [os.path.join(amd, "monitor_core.hpp"), os.path.join(amd, "procscan.hpp")]
+    ext_dir = os.path.join(SAN_DIR, sanitize) if sanitize else PKG
+    sfx = f"-{sanitize}" if sanitize else ""
     return {
         "cql_native": {
-            "out": os.path.join(PKG, "_cql_native" + EXT),
+            "out": os.path.join(ext_dir, "_cql_native" + EXT),
             "srcs": [os.path.join(CSRC, "cql", "cql_native.cpp")],
             "deps": [proto],
-            "cmd": lambda out, srcs: [_cxx(), *common, "-shared", "-fPIC", *_pybind_includes(), *srcs, "-o", out],
+            "cmd": lambda out, srcs: [_cxx(), *common, *san, "-shared", "-fPIC", *_pybind_includes(), *srcs, "-o", out],
+            "inproc": True,
         },
         "kube_native": {
-            "out": os.path.join(PKG, "_kube_native" + EXT),
+            "out": os.path.join(ext_dir, "_kube_native" + EXT),
             "srcs": [os.path.join(CSRC, "kube", "watch_decoder.cpp"), os.path.join(CSRC, "kube", "json_encode.cpp")],
             "deps": [],
-            "cmd": lambda out, srcs: [_cxx(), *common, "-O3", "-shared", "-fPIC", f"-I{sysconfig.get_paths()['include']}",
-                                      *srcs, "-o", out],
+            "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, "-shared", "-fPIC",
+                                      f"-I{sysconfig.get_paths()['include']}", *srcs, "-o", out],
+            "inproc": True,
         },
         "amdsmi_monitor": {
-            "out": os.path.join(PKG, "_amdsmi_monitor" + EXT),
-            "srcs": [os.path.join(CSRC, "amdsmi", "gpu_monitor.cpp")],
-            "deps": [],
-            "cmd": lambda out, srcs: [_cxx(), *common, "-shared", "-fPIC", *_pybind_includes(), f"-I{ROCM}/include", *srcs,
-                                      f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib", "-pthread", "-o", out],
+            "out": os.path.join(ext_dir, "_amdsmi_monitor" + EXT),
+            "srcs": [os.path.join(amd, "gpu_monitor.cpp")],
+            "deps": mon_deps,
+            "cmd": lambda out, srcs: [_cxx(), *common, *san, "-shared", "-fPIC", *_pybind_includes(), f"-I{ROCM}/include",
+                                      *srcs, f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib", "-pthread", "-o", out],
             "requires": os.path.join(ROCM, "include", "amd_smi", "amdsmi.h"),
         },
+        # the same monitor over the stub amd-smi: CPU tests of the sampler / attribution path
+        "amdsmi_monitor_stub": {
+            "out": os.path.join(ext_dir, "_amdsmi_monitor_stub" + EXT),
+            "srcs": [os.path.join(amd, "gpu_monitor.cpp"), os.path.join(amd, "amdsmi_stub.cpp")],
+            "deps": mon_deps,
+            "cmd": lambda out, srcs: [_cxx(), *common, *san, "-shared", "-fPIC", *_pybind_includes(), f"-I{ROCM}/include",
+                                      "-DNEXUS_AMDSMI_STUB", "-DNEXUS_MONITOR_MODULE=_amdsmi_monitor_stub", *srcs,
+                                      "-pthread", "-o", out],
+            "requires": os.path.join(ROCM, "include", "amd_smi", "amdsmi.h"),
+            "inproc": True,
+        },
+        "monitor_selftest": {
+            "out": os.path.join(BIN, "monitor_selftest" + sfx),
+            "srcs": [os.path.join(amd, "monitor_selftest.cpp"), os.path.join(amd, "amdsmi_stub.cpp")],
+            "deps": mon_deps,
+            "cmd": lambda out, srcs: [_cxx(), *common, *san, f"-I{ROCM}/include", *srcs, "-pthread", "-o", out],
+            "requires": os.path.join(ROCM, "include", "amd_smi", "amdsmi.h"),
+            "exe": True,
+        },
         "cqlsrv": {
-            "out": os.path.join(BIN, "nexus-cqlsrv" + (f"-{sanitize}" if sanitize else "")),
+            "out": os.path.join(BIN, "nexus-cqlsrv" + sfx),
             "srcs": [os.path.join(CSRC, "cqlsrv", "cqlsrv.cpp")],
             "deps": [proto],
             "cmd": lambda out, srcs: [_cxx(), *common, *san, "-pthread", f"-I{os.path.join(CSRC, 'cql')}", *srcs, "-o", out],
+            "exe": True,
         },
         "kubesim": {
-            "out": os.path.join(BIN, "nexus-kubesim" + (f"-{sanitize}" if sanitize else "")),
+            "out": os.path.join(BIN, "nexus-kubesim" + sfx),
             "srcs": [os.path.join(CSRC, "kubesim", "kubesim.cpp")],
             "deps": [os.path.join(CSRC, "kubesim", "json.hpp")],
             "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, *srcs, "-o", out],
+            "exe": True,
         },
         "gpu_stress": {
             "out": os.path.join(BIN, "gpu_stress"),
             "srcs": [os.path.join(CSRC, "stress", "gpu_stress.hip")],
             "deps": [],
             "cmd": lambda out, srcs: [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17",
-                                      *srcs, "-o", out],
+                                      "-Wall", "-Werror", *srcs, "-o", out],
             "requires": os.path.join(ROCM, "bin", "hipcc"),
         },
     }
+
+
+def sanitizer_runtime(sanitize: str) -> Optional[str]:
+    """``LD_PRELOAD`` value for an uninstrumented Python that loads instrumented
+    extensions: the compiler's sanitizer runtime first, then libstdc++ (the runtime
+    resolves its ``__cxa_throw`` interceptor at startup; Python itself does not link
+    libstdc++, so without it the first C++ exception aborts the process)."""
+    libs = []
+    for lib in ({"address": "libasan.so", "undefined": "libasan.so", "thread": "libtsan.so"}[sanitize], "libstdc++.so"):
+        p = subprocess.run([_cxx(), f"-print-file-name={lib}"], capture_output=True, text=True)
+        path = p.stdout.strip()
+        if not (path and os.path.isabs(path) and os.path.exists(path)):
+            return None
+        libs.append(os.path.realpath(path))
+    return " ".join(libs)
 
 
 def _stale(t: Dict) -> bool:
@@ -124,7 +181,7 @@ def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optio
     ts = targets(sanitize)
     names = [n for n in ts if not only or n in only]
     if sanitize:
-        names = [n for n in names if n in ("cqlsrv", "kubesim")]
+        names = [n for n in names if ts[n].get("exe") or ts[n].get("inproc")]
     with cf.ThreadPoolExecutor(max_workers=min(4, len(names) or 1)) as ex:
         futs = {ex.submit(build_one, n, ts[n], force, verbose): n for n in names}
         return [f.result() for f in cf.as_completed(futs)]
@@ -133,7 +190,8 @@ def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optio
 def binary(name: str) -> str:
     """Path of a built helper binary, building it on demand."""
     ts = targets()
-    key = {"nexus-cqlsrv": "cqlsrv", "gpu_stress": "gpu_stress", "nexus-kubesim": "kubesim"}[name]
+    key = {"nexus-cqlsrv": "cqlsrv", "gpu_stress": "gpu_stress", "nexus-kubesim": "kubesim",
+           "monitor_selftest": "monitor_selftest"}[name]
     t = ts[key]
     if _stale(t):
         build_one(key, t)

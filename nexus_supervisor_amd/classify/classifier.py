@@ -27,7 +27,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 from ..config.schema import GpuConfig, LabelConfig, RulesConfig
 from ..gpu import oom as oom_mod
 from ..gpu.telemetry import FAULT_EVENTS
-from ..gpu.topology import merge_process_ranks, topology_from_pod
+from ..gpu.topology import merge_process_ranks, resolve_devices, topology_from_pod, xgmi_from_evidence
 from ..models import kube
 from ..models.decisions import DecisionAction as A
 from ..models.decisions import FailureClass as F
@@ -347,6 +347,9 @@ class Classifier:
             return hit
         topo = topology_from_pod(pod, self.gpu.gpu_resource_name)
         gev = self._gpu_evidence(pod) if want_gpu else None
+        if gev:
+            # physical view: device-plugin allocation / UUIDs → physical GPUs, measured xGMI
+            topo = xgmi_from_evidence(resolve_devices(topo, gev), gev)
         if len(self._ctx_cache) > 4096:
             self._ctx_cache.clear()
         self._ctx_cache[key] = (topo, gev)
@@ -367,7 +370,7 @@ class Classifier:
     def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
         topo, gev = self._pod_ctx(pod)
         return oom_mod.analyze(texts, terms, gev, topo.get("expected_gpu"),
-                               self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+                               self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction, topo=topo)
 
     def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
         if not self.gpu.attribution_enabled:
@@ -387,7 +390,8 @@ class Classifier:
             if verdict is None and res.action != A.TO_RUNNING:
                 terms = [t for p in pods for t in kube.terminated_states(p)]
                 verdict = oom_mod.analyze(list(texts) + [t.get("message", "") for t in terms], terms, gev,
-                                          topo.get("expected_gpu"), self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+                                          topo.get("expected_gpu"), self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction,
+                                          topo=topo)
         elif verdict is None and res.action != A.TO_RUNNING and any(texts):
             verdict = oom_mod.analyze(texts, (), None, None, self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
         if verdict is not None and verdict.kind:
@@ -424,7 +428,7 @@ class Classifier:
                 if terms:
                     topo, gev = self._pod_ctx(pods[-1])
                     v = oom_mod.analyze([t.get("message", "") for t in terms], terms, gev, topo.get("expected_gpu"),
-                                        self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
+                                        self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction, topo=topo)
                     if v.kind:
                         res.evidence["oom"] = v.as_dict()
                         res.failure_class = F.HBM_OOM if v.kind == "hbm" else F.HOST_OOM

@@ -26,7 +26,7 @@ from typing import Any, Dict, List, Optional, Set, Tuple
 from ..informer import InformerFactory
 from ..models import kube
 from .podresources import PodResourcesClient, gpu_allocations, normalize_bdf
-from .telemetry import ATTRIBUTION_EVENTS, FAULT_EVENTS, GpuTelemetry, evidence_for
+from .telemetry import ATTRIBUTION_EVENTS, FAULT_EVENTS, GpuTelemetry, _pod_gpus, evidence_for
 from .topology import topology_from_pod
 
 log = logging.getLogger("nexus_supervisor_amd.agent")
@@ -88,26 +88,33 @@ class NodeAgent:
             self.podres.close()
 
     # ------------------------------------------------------------ mapping
-    def gpus_for(self, pod: Dict[str, Any]) -> List[int]:
-        """Physical GPU indices allocated to ``pod`` (pod-resources, then env)."""
-        if self.podres is not None:
-            try:
-                alloc = gpu_allocations(self.podres.list(), self.gpu_resource)
-                ids = alloc.get((kube.namespace_of(pod), kube.name_of(pod)), [])
-                idx = [self._bdf_index[normalize_bdf(i)] for i in ids if normalize_bdf(i) in self._bdf_index]
-                if idx:
-                    return sorted(idx)
-            except Exception as exc:  # noqa: BLE001 - kubelet socket optional
-                log.debug("pod-resources lookup failed: %s", exc)
+    def allocation(self, pod: Dict[str, Any]) -> List[int]:
+        """Physical GPU indices the device plugin allocated to ``pod`` (kubelet
+        pod-resources, by PCI BDF), sorted: what the container enumerates as HIP
+        ordinals 0..k-1 before any *_VISIBLE_DEVICES narrowing.  Empty when unknown."""
+        if self.podres is None:
+            return []
+        try:
+            alloc = gpu_allocations(self.podres.list(), self.gpu_resource)
+        except Exception as exc:  # noqa: BLE001 - kubelet socket optional
+            log.debug("pod-resources lookup failed: %s", exc)
+            return []
+        ids = alloc.get((kube.namespace_of(pod), kube.name_of(pod)), [])
+        return sorted(self._bdf_index[normalize_bdf(i)] for i in ids if normalize_bdf(i) in self._bdf_index)
+
+    def gpus_for(self, pod: Dict[str, Any], allocated: Optional[List[int]] = None) -> List[int]:
+        """Physical GPU indices of ``pod``: the allocation, else its env's devices
+        (logical ordinals mapped through ROCR/HIP_VISIBLE_DEVICES)."""
+        alloc = self.allocation(pod) if allocated is None else allocated
+        if alloc:
+            return alloc
         topo = topology_from_pod(pod, self.gpu_resource)
-        exp = topo.get("expected_gpu")
-        if exp is not None and str(exp).isdigit():
-            return [int(exp)]
-        return [int(d) for d in topo.get("visible_devices", []) if str(d).isdigit()]
+        return _pod_gpus(topo, self.tel.devices())
 
     def evidence(self, pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
-        return evidence_for(self.tel, pod_uid=kube.uid_of(pod), gpu_indices=self.gpus_for(pod), lookback=self.lookback,
-                            node=self.node)
+        alloc = self.allocation(pod)
+        return evidence_for(self.tel, pod_uid=kube.uid_of(pod), gpu_indices=self.gpus_for(pod, alloc),
+                            lookback=self.lookback, node=self.node, allocated=alloc)
 
     # ------------------------------------------------------------ publishing
     async def publish(self, pod: Dict[str, Any], reason: str) -> bool:

@@ -15,8 +15,19 @@ HBM-OOM (288 GB HBM3E per MI355X)
   * agent-sampled VRAM peak ≥ ``hbm_oom_fraction`` × capacity on the rank's GPU +0.5
   * VM-fault / queue-eviction event on that GPU                             +0.25
 
-A verdict needs ≥0.5; the larger score wins, with a cgroup OOMKill (a hard
-kernel fact about *host* memory) winning ties.
+A verdict needs ≥0.5 **and** at least one OOM *signature* (a HIP/host allocation
+failure message, OOMKilled, or exit 137): VRAM peaks and GPU events corroborate and
+attribute, they never make a plain crash an OOM on their own (a GPU left full by a
+previous tenant must not turn an exit-1 into an HBM-OOM that bypasses the Job's
+retry policy).  The larger score wins, with a cgroup OOMKill (a hard kernel fact about
+*host* memory) winning ties.
+
+GPU index.  torch's ``GPU N`` is the *logical* HIP ordinal inside the process, after
+ROCR/HIP_VISIBLE_DEVICES and the device plugin's allocation narrowed the node's GPUs.
+With the pod's topology the verdict records both ``gpu_logical_index`` (N) and
+``gpu_index`` (the physical GPU, :func:`..topology.physical_gpu`), and only the physical
+GPU's telemetry is read.  Per-process VRAM (the pod's own processes on that GPU) is
+preferred over the device-wide peak for ``peak_vram_bytes``.
 """
 from __future__ import annotations
 
@@ -70,14 +81,18 @@ class OomVerdict:
     host_score: float = 0.0
     signals: List[str] = field(default_factory=list)
     gpu_index: Optional[int] = None
+    gpu_logical_index: Optional[int] = None
     requested_bytes: Optional[int] = None
     capacity_bytes: Optional[int] = None
     peak_vram_bytes: Optional[int] = None
+    device_peak_vram_bytes: Optional[int] = None
+    signature: bool = False
 
     def as_dict(self) -> Dict[str, Any]:
         d: Dict[str, Any] = {"kind": self.kind, "hbm_score": round(self.hbm_score, 3),
                              "host_score": round(self.host_score, 3), "signals": self.signals}
-        for k in ("gpu_index", "requested_bytes", "capacity_bytes", "peak_vram_bytes"):
+        for k in ("gpu_index", "gpu_logical_index", "requested_bytes", "capacity_bytes", "peak_vram_bytes",
+                  "device_peak_vram_bytes"):
             v = getattr(self, k)
             if v is not None:
                 d[k] = v
@@ -111,7 +126,10 @@ def analyze(
     expected_gpu: Optional[str] = None,
     hbm_capacity_gb: float = 288.0,
     hbm_oom_fraction: float = 0.97,
+    topo: Optional[Dict[str, Any]] = None,
 ) -> OomVerdict:
+    from .topology import physical_gpu
+
     v = OomVerdict()
     texts = [t for t in texts if t]
     for t in terminated:
@@ -119,42 +137,58 @@ def analyze(
         code = t.get("exitCode")
         if reason == "OOMKilled":
             v.host_score += 1.0
+            v.signature = True
             v.signals.append(f"container {t.get('container', '')!s} OOMKilled (cgroup, exit {code})")
         elif code == 137:
             v.host_score += 0.35
+            v.signature = True
             v.signals.append(f"container {t.get('container', '')!s} exit 137 (SIGKILL)")
         if t.get("message"):
             texts.append(t["message"])
     hbm_hit = host_hit = False
+    logical = None
     for text in texts:
         s = hbm_signature(text)
         if s and not hbm_hit:
             hbm_hit = True
+            v.signature = True
             v.hbm_score += 1.0
             v.signals.append(f"HIP OOM signature: {s!r}")
         h = host_signature(text)
         if h and not host_hit and h != "OOMKilled":
             host_hit = True
+            v.signature = True
             v.host_score += 0.6
             v.signals.append(f"host allocation failure: {h!r}")
         if not _mentions(text, _TORCH_KEYS):
             continue
         m = _TORCH_GPU.search(text)
-        if m and v.gpu_index is None:
-            v.gpu_index = int(m.group(1))
+        if m and logical is None:
+            logical = int(m.group(1))
             v.capacity_bytes = int(float(m.group(2)) * _UNIT[m.group(3).lower()])
         r = _TORCH_REQ.search(text)
         if r and v.requested_bytes is None:
             v.requested_bytes = int(float(r.group(1)) * _UNIT[r.group(2).lower()])
+    if logical is not None:
+        v.gpu_logical_index = logical
+        if topo is not None:
+            ev = gpu_evidence or {}
+            v.gpu_index = physical_gpu(topo, logical, ev.get("gpus") or (), ev.get("allocated"))
+        else:
+            v.gpu_index = logical  # no topology: the process saw the node's numbering
     if gpu_evidence:
         cap = int(hbm_capacity_gb * (1 << 30))
         for g in _candidate_gpus(gpu_evidence, expected_gpu, v.gpu_index):
             total = int(g.get("vram_total_mb") or 0) * (1 << 20) or cap
             peak = int(g.get("vram_peak_mb") or g.get("vram_used_mb") or 0) * (1 << 20)
+            own = int(g.get("proc_peak_vram_bytes") or 0)
             if peak and peak >= hbm_oom_fraction * total:
                 v.hbm_score += 0.5
-                v.signals.append(f"GPU {g.get('index')} VRAM peak {peak / (1 << 30):.1f} GiB of {total / (1 << 30):.1f} GiB")
-                v.peak_vram_bytes = peak
+                share = f"; the pod's own processes peaked at {own / (1 << 30):.1f} GiB" if own else ""
+                v.signals.append(f"GPU {g.get('index')} VRAM peak {peak / (1 << 30):.1f} GiB of "
+                                 f"{total / (1 << 30):.1f} GiB{share}")
+                v.device_peak_vram_bytes = peak
+                v.peak_vram_bytes = own or peak
                 if v.gpu_index is None:
                     v.gpu_index = g.get("index")
             faults = [e for e in g.get("events", []) if e.get("type") in ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET")]
@@ -165,22 +199,23 @@ def analyze(
                     v.gpu_index = g.get("index")
             if v.capacity_bytes is None and g.get("vram_total_mb"):
                 v.capacity_bytes = int(g["vram_total_mb"]) * (1 << 20)
-    if v.hbm_score >= 0.5 or v.host_score >= 0.5:
+    if v.signature and (v.hbm_score >= 0.5 or v.host_score >= 0.5):
         if v.host_score >= 1.0 and v.host_score >= v.hbm_score:
             v.kind = "host"
         elif v.hbm_score >= v.host_score:
             v.kind = "hbm"
         else:
             v.kind = "host"
+    elif v.hbm_score >= 0.5:
+        v.signals.append("no OOM signature (allocation-failure message, OOMKilled or exit 137): not an OOM verdict")
     return v
 
 
 def _candidate_gpus(ev: Dict[str, Any], expected: Optional[str], idx: Optional[int]):
     gpus = ev.get("gpus") or []
     if idx is not None:
-        sel = [g for g in gpus if g.get("index") == idx]
-        if sel:
-            return sel
+        # the failing process named its GPU: never read another GPU's evidence for it
+        return [g for g in gpus if g.get("index") == idx]
     if expected is not None:
         sel = [g for g in gpus if str(g.get("index")) == str(expected) or g.get("uuid") == expected]
         if sel:

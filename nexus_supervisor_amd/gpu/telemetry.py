@@ -59,9 +59,14 @@ class GpuTelemetry:
         raise NotImplementedError
 
 
-def native_monitor_module():
-    """Import the native monitor; raises :class:`TelemetryUnavailable` with the build hint."""
+def native_monitor_module(stub: bool = False):
+    """Import the native monitor (``stub``: the build over the stub amd-smi, for CPU
+    tests); raises :class:`TelemetryUnavailable` with the build hint."""
     try:
+        if stub:
+            from .. import _amdsmi_monitor_stub  # type: ignore
+
+            return _amdsmi_monitor_stub
         from .. import _amdsmi_monitor  # type: ignore
 
         return _amdsmi_monitor
@@ -73,10 +78,14 @@ def native_monitor_module():
 class AmdSmiTelemetry(GpuTelemetry):
     name = "amdsmi"
 
-    def __init__(self, interval: float = 0.25, events: bool = True, retain: float = 600.0, read_proc: bool = True):
-        mod = native_monitor_module()
+    def __init__(self, interval: float = 0.25, events: bool = True, retain: float = 600.0, read_proc: bool = True,
+                 proc_source: str = "auto", proc_root: str = "/proc", sys_root: str = "/sys", stub: bool = False):
+        """``proc_source``: where per-process GPU use comes from — ``auto`` (amd-smi with KFD
+        sysfs fill-in when this process shares the host PID namespace, else DRM fdinfo of
+        our own /proc), or forced ``amdsmi`` / ``kfd`` / ``drm``."""
+        mod = native_monitor_module(stub)
         self.interval = interval
-        self._m = mod.GpuMonitor(int(interval * 1000), events, retain, read_proc)
+        self._m = mod.GpuMonitor(int(interval * 1000), events, retain, read_proc, proc_source, proc_root, sys_root)
         self._started = False
 
     def start(self) -> None:
@@ -110,6 +119,11 @@ class AmdSmiTelemetry(GpuTelemetry):
     @property
     def samples(self) -> int:
         return self._m.samples
+
+    @property
+    def proc_mode(self) -> str:
+        """Per-process source in use (``amdsmi`` / ``kfd`` / ``drm``), known after start()."""
+        return self._m.proc_mode
 
 
 class RemoteTelemetry(GpuTelemetry):
@@ -147,7 +161,7 @@ class RemoteTelemetry(GpuTelemetry):
                 self._hist[int(gi)] = [x for x in h if x[0] >= horizon]
 
     def devices(self):
-        return [{k: g.get(k) for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb")} for g in self._snap]
+        return [{k: g.get(k) for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb", "links")} for g in self._snap]
 
     def snapshot(self, include_exited: bool = True):
         if include_exited:
@@ -188,9 +202,14 @@ class FakeTelemetry(GpuTelemetry):
     def __init__(self, n_gpus: int = 8, vram_total_mb: int = 294896, clock=time.time):
         self.clock = clock
         self._lock = threading.Lock()
-        self._gpus = [{"index": i, "uuid": f"fake-{i:04d}", "hip_uuid": f"GPU-fake{i:012d}", "bdf": f"0000:{0x0a + i:02x}:00.0",
+        bdf = [f"0000:{0x0a + i:02x}:00.0" for i in range(n_gpus)]
+        # MI355X node fabric: every GPU pair joined by one xGMI link (7 per GPU on 8 GPUs)
+        self._gpus = [{"index": i, "uuid": f"fake-{i:04d}", "hip_uuid": f"GPU-fake{i:012d}", "bdf": bdf[i],
                        "vram_total_mb": vram_total_mb, "vram_used_mb": 0, "vram_peak_mb": 0,
-                       "ecc_correctable": 0, "ecc_uncorrectable": 0} for i in range(n_gpus)]
+                       "ecc_correctable": 0, "ecc_uncorrectable": 0, "xgmi_hive_id": 0x5A7E,
+                       "links": [{"peer_bdf": bdf[j], "peer_index": j, "type": "xgmi", "bit_rate_gbps": 38,
+                                  "max_bandwidth_gbps": 608, "read_kb": 0, "write_kb": 0}
+                                 for j in range(n_gpus) if j != i]} for i in range(n_gpus)]
         self._hist: List[List] = [[] for _ in range(n_gpus)]
         self._procs: Dict[tuple, Dict[str, Any]] = {}
         self._events: List[Dict[str, Any]] = []
@@ -204,7 +223,7 @@ class FakeTelemetry(GpuTelemetry):
 
     def devices(self):
         with self._lock:
-            return [{k: g[k] for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb")} | {"hip_id": g["index"],
+            return [{k: g[k] for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb", "links")} | {"hip_id": g["index"],
                     "market_name": "AMD Instinct MI355X (fake)", "events": True} for g in self._gpus]
 
     # ---- programming API
@@ -219,7 +238,8 @@ class FakeTelemetry(GpuTelemetry):
                     pod_uid: str = "", name: str = "python3") -> None:
         now = self.clock()
         with self._lock:
-            self._procs[(gpu, pid)] = {"pid": pid, "name": name, "vram_bytes": vram_bytes, "peak_vram_bytes": vram_bytes,
+            self._procs[(gpu, pid)] = {"pid": pid, "name": name, "source": "fake", "vram_bytes": vram_bytes,
+                                       "peak_vram_bytes": vram_bytes,
                                        "cu_occupancy": 0, "alive": True, "first_seen": now, "last_seen": now,
                                        "pod_uid": pod_uid, "env": dict(env or {}), "gpu": gpu}
 
@@ -319,10 +339,36 @@ def _rank_fields(env: Dict[str, str]) -> Dict[str, Any]:
     return out
 
 
+def _links_of(g: Dict[str, Any]) -> Optional[List[Dict[str, Any]]]:
+    """Connected xGMI ports of one GPU (disabled ports report an all-ones peer BDF)."""
+    raw = g.get("links")
+    if raw is None:
+        return None
+    out = []
+    for l in raw:
+        peer = l.get("peer_bdf") or ""
+        if not peer or peer.startswith("ffff") or l.get("type") not in ("xgmi", None):
+            continue
+        rec = {"peer_bdf": peer, "peer": l.get("peer_index") if (l.get("peer_index") or 0) >= 0 else None,
+               "gbps": l.get("bit_rate_gbps"), "max_gbps": l.get("max_bandwidth_gbps")}
+        if l.get("read_kb") or l.get("write_kb"):
+            rec["read_kb"], rec["write_kb"] = l.get("read_kb", 0), l.get("write_kb", 0)
+        out.append(rec)
+    return out
+
+
 def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterable[int] = (), pids: Iterable[int] = (),
                  lookback: float = 300.0, now: Optional[float] = None, node: str = "",
-                 snapshot: Optional[List[Dict[str, Any]]] = None) -> Optional[Dict[str, Any]]:
-    """Evidence record for one pod (matched by cgroup pod UID, PIDs or explicit GPU indices)."""
+                 snapshot: Optional[List[Dict[str, Any]]] = None,
+                 allocated: Optional[List[int]] = None) -> Optional[Dict[str, Any]]:
+    """Evidence record for one pod (matched by cgroup pod UID, PIDs or explicit GPU indices).
+
+    Per GPU: the device-wide VRAM peak over the window the pod's processes lived (or the
+    lookback when none matched), the pod's own processes with their per-process VRAM and
+    peak (``source``: amdsmi / kfd / drm-fdinfo), the measured xGMI links, GPU events in
+    the window and usage by processes of other PID namespaces.  ``allocated`` (physical
+    indices from the kubelet pod-resources API) is recorded so the supervisor can map the
+    pod's logical HIP ordinals to physical GPUs (:func:`..topology.resolve_devices`)."""
     snap = snapshot if snapshot is not None else telemetry.snapshot(True)
     now = time.time() if now is None else now
     pids = set(pids)
@@ -343,17 +389,29 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
         rec: Dict[str, Any] = {"index": g["index"], "uuid": g.get("hip_uuid") or g.get("uuid"),
                                "bdf": g.get("bdf"), "vram_total_mb": g.get("vram_total_mb"),
                                "vram_used_mb": g.get("vram_used_mb"), "vram_peak_mb": peak,
-                               "window": [round(t0, 3), round(t1, 3)]}
+                               "window": [round(t0, 3), round(t1, 3)], "matched": bool(procs)}
         if g.get("ecc_uncorrectable"):
             rec["ecc_uncorrectable"] = g["ecc_uncorrectable"]
-        if g.get("xgmi_links_down"):
-            rec["xgmi_links_down"] = g["xgmi_links_down"]
+        if g.get("xgmi_links_total") is not None:
+            rec["xgmi_links_up"] = g.get("xgmi_links_up")
+            rec["xgmi_links_down"] = g.get("xgmi_links_down") or 0
             rec["xgmi_links_total"] = g.get("xgmi_links_total")
         if g.get("xgmi_error"):
             rec["xgmi_error"] = g["xgmi_error"]
+        if g.get("xgmi_hive_id"):
+            rec["xgmi_hive_id"] = g["xgmi_hive_id"]
+        links = _links_of(g)
+        if links is not None:
+            rec["links"] = links
+        if g.get("foreign_procs"):
+            rec["foreign_procs"] = g["foreign_procs"]
+            rec["foreign_vram_bytes"] = g.get("foreign_vram_bytes", 0)
         rec["procs"] = [dict({"pid": p["pid"], "vram_bytes": p.get("vram_bytes", 0),
-                              "peak_vram_bytes": p.get("peak_vram_bytes", 0), "alive": p.get("alive", False)},
+                              "peak_vram_bytes": p.get("peak_vram_bytes", 0), "alive": p.get("alive", False),
+                              "source": p.get("source", "")},
                              **_rank_fields(p.get("env") or {})) for p in procs]
+        if procs:
+            rec["proc_peak_vram_bytes"] = sum(p.get("peak_vram_bytes", 0) for p in procs)
         evs = [{"type": e["type"], "t": round(e["t"], 3), "message": (e.get("message") or "")[:200]}
                for e in g.get("events", []) if e["type"] in ATTRIBUTION_EVENTS and t0 <= e["t"] <= t1 + grace]
         if evs:
@@ -362,6 +420,8 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
     if not gpus:
         return None
     out: Dict[str, Any] = {"source": telemetry.name, "t": round(now, 3), "gpus": gpus}
+    if allocated:
+        out["allocated"] = sorted(int(i) for i in allocated)
     if node:
         out["node"] = node
     if pod_uid:
@@ -392,15 +452,10 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
 
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         topo = topology_from_pod(pod, gpu_resource)
-        gpus = []
-        exp = topo.get("expected_gpu")
-        if exp is not None and str(exp).isdigit():
-            gpus.append(int(exp))
-        elif topo.get("visible_devices"):
-            gpus.extend(int(d) for d in topo["visible_devices"] if str(d).isdigit())
         now = time.monotonic()
         if cache["snap"] is None or now - cache["t"] > ttl:
             refresh(now)
+        gpus = _pod_gpus(topo, cache["snap"])
         uid = kube.uid_of(pod)
         # only the GPUs this pod could have used: its expected devices + where its processes ran
         relevant = set(gpus) | cache["by_uid"].get(uid, set())
@@ -410,3 +465,23 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
                             node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=sub)
 
     return provider
+
+
+def _pod_gpus(topo: Dict[str, Any], snap: Iterable[Dict[str, Any]] = ()) -> List[int]:
+    """Physical GPUs a pod's env points at: the rank's expected device, else every visible
+    device; UUID entries resolved against the telemetry snapshot."""
+    from .topology import physical_gpu
+
+    lr = topo.get("local_rank")
+    devs = topo.get("visible_devices") or []
+    out = []
+    if devs and lr is not None and 0 <= lr < len(devs):
+        p = physical_gpu(topo, lr, snap)
+        if p is not None:
+            out.append(p)
+    elif devs:
+        for i in range(len(devs)):
+            p = physical_gpu(topo, i, snap)
+            if p is not None:
+                out.append(p)
+    return out

@@ -44,8 +44,20 @@ def parse_visible_devices(value: Optional[str]) -> List[str]:
     return [v.strip() for v in str(value).split(",") if v.strip()]
 
 
+# HIP device selection is layered: ROCr filters the node's agents first, then HIP
+# indexes into what ROCr left (CUDA_VISIBLE_DEVICES is HIP's alias when HIP_* is unset).
+_DEVICE_CHAIN = (("ROCR_VISIBLE_DEVICES",), ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
+
+
 def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = "") -> Dict[str, Any]:
-    """Fold torchrun / RCCL env into a topology record (only non-empty keys)."""
+    """Fold torchrun / RCCL env into a topology record (only non-empty keys).
+
+    ``visible_devices`` is the *composed* device list in the container's numbering
+    (ROCR_VISIBLE_DEVICES, then HIP/CUDA_VISIBLE_DEVICES indexing into it): entry ``i`` is
+    what a process's HIP ordinal ``i`` (torch's ``GPU i``) opens.  ``device_chain`` keeps
+    each layer.  The container numbering equals the node's physical numbering only when
+    the container sees every GPU; :func:`resolve_devices` applies the device-plugin
+    allocation when the node agent reported one."""
     topo: Dict[str, Any] = {}
     for var, key in _INT_VARS:
         raw = env.get(var)
@@ -57,11 +69,20 @@ def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = 
         topo["master_addr"] = env["MASTER_ADDR"]
     if "rank" not in topo and "completion_index" in topo:
         topo["rank"] = topo["completion_index"]  # indexed Job → rank
-    for var in DEVICE_VARS:
-        devs = parse_visible_devices(env.get(var))
-        if devs:
-            topo.setdefault("visible_devices", devs)
-            topo.setdefault("visible_devices_var", var)
+    chain = []
+    for names in _DEVICE_CHAIN:
+        for var in names:
+            devs = parse_visible_devices(env.get(var))
+            if devs:
+                chain.append([var, devs])
+                break
+    if chain:
+        topo["device_chain"] = chain
+        topo["visible_devices"] = device_map(chain)
+        topo["visible_devices_var"] = chain[-1][0]
+    elif env.get("GPU_DEVICE_ORDINAL"):
+        topo["visible_devices"] = parse_visible_devices(env["GPU_DEVICE_ORDINAL"])
+        topo["visible_devices_var"] = "GPU_DEVICE_ORDINAL"
     coll = {k: v for k, v in env.items() if k.startswith(COLLECTIVE_PREFIXES)}
     if coll:
         topo["collective_env"] = dict(sorted(coll.items()))
@@ -73,8 +94,11 @@ def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = 
         topo["backend"] = "rccl"
         n_local = topo.get("local_world_size") or gpus_requested or len(topo.get("visible_devices", []))
         if n_local:
-            # single-node GPUs on an MI355X platform are all-to-all xGMI connected
+            # Platform default only (MI355X: 8 OAM GPUs, all pairs xGMI-connected).  The
+            # measured fabric replaces this in :func:`xgmi_from_evidence` when telemetry
+            # reported link metrics.
             topo["xgmi"] = {
+                "source": "platform-default",
                 "local_gpus": n_local,
                 "links_per_gpu": min(XGMI_LINKS_PER_GPU, max(n_local - 1, 0)),
                 "fully_connected": n_local <= GPUS_PER_NODE,
@@ -83,6 +107,112 @@ def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = 
         if gpu is not None:
             topo["expected_gpu"] = gpu
     return topo
+
+
+def device_map(chain: List, allocated: Optional[List[int]] = None) -> List[str]:
+    """Physical device of each logical HIP ordinal: the allocation (the GPUs a device
+    plugin exposed to the container, in node order) narrowed by each env layer; entries
+    are physical index strings or GPU UUIDs.  Empty = identity (nothing restricts)."""
+    base: Optional[List[str]] = [str(i) for i in allocated] if allocated else None
+    for _var, sel in chain:
+        if base is None:
+            base = list(sel)
+            continue
+        out = []
+        for x in sel:
+            if x.isdigit():
+                i = int(x)
+                if i < len(base):
+                    out.append(base[i])
+            else:
+                out.append(x)  # a UUID names a device absolutely
+        base = out
+    return base or []
+
+
+def physical_gpu(topo: Dict[str, Any], logical: Optional[int], gpus: Iterable[Dict[str, Any]] = (),
+                 allocated: Optional[List[int]] = None) -> Optional[int]:
+    """Physical GPU index behind a process's logical HIP ordinal (torch ``GPU N``).
+    UUID entries resolve against telemetry records (``uuid`` / ``hip_uuid``)."""
+    if logical is None:
+        return None
+    m = device_map(topo.get("device_chain") or [], allocated)
+    if not m:
+        return int(logical)
+    if not 0 <= logical < len(m):
+        return None
+    ent = m[logical]
+    if ent.isdigit():
+        return int(ent)
+    for g in gpus:
+        if ent in (g.get("uuid"), g.get("hip_uuid")):
+            return g.get("index")
+    return None
+
+
+def resolve_devices(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, Any]]) -> Dict[str, Any]:
+    """Topology with the node's *physical* view applied: the device-plugin allocation the
+    node agent reported (``gpu_evidence["allocated"]``) and UUID entries resolved against
+    its GPU records.  Adds ``physical_devices`` and turns ``expected_gpu`` into the
+    physical index (``expected_gpu_logical`` keeps the rank's ordinal).  Returns a new
+    dict; the per-version memo of :func:`topology_from_pod` is never mutated."""
+    alloc = list((gpu_evidence or {}).get("allocated") or [])
+    gpus = (gpu_evidence or {}).get("gpus") or []
+    chain = topo.get("device_chain") or []
+    if not alloc and not any(not str(x).isdigit() for _v, sel in chain for x in sel):
+        return topo
+    out = dict(topo)
+    m = device_map(chain, alloc)
+    phys = []
+    for ent in m:
+        if ent.isdigit():
+            phys.append(int(ent))
+        else:
+            hit = [g.get("index") for g in gpus if ent in (g.get("uuid"), g.get("hip_uuid"))]
+            phys.append(hit[0] if hit else ent)
+    if alloc:
+        out["allocated_gpus"] = alloc
+    if phys:
+        out["physical_devices"] = phys
+    lr = topo.get("local_rank")
+    logical = lr if lr is not None and 0 <= lr < len(phys) else (0 if len(phys) == 1 else None)
+    if logical is not None:
+        out["expected_gpu_logical"] = logical
+        out["expected_gpu"] = str(phys[logical])
+    return out
+
+
+def xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, Any]]) -> Dict[str, Any]:
+    """Replace the platform-default xGMI block with the measured fabric of the pod's GPUs
+    (link metrics the native monitor read from amd-smi: peers, rates, link status)."""
+    gpus = [g for g in (gpu_evidence or {}).get("gpus", []) if g.get("links") is not None]
+    if not gpus:
+        return topo
+    idx = {g.get("index") for g in gpus}
+    links, hive = [], set()
+    for g in gpus:
+        if g.get("xgmi_hive_id"):
+            hive.add(g["xgmi_hive_id"])
+        for l in g["links"]:
+            links.append(dict(l, gpu=g.get("index")))
+    within = sorted({tuple(sorted((l["gpu"], l["peer"]))) for l in links if l.get("peer") in idx})
+    n = len(idx)
+    rec: Dict[str, Any] = {
+        "source": gpu_evidence.get("source", "telemetry"),
+        "gpus": sorted(idx),
+        "links": links,
+        "pairs_connected": [list(p) for p in within],
+        "fully_connected": len(within) == n * (n - 1) // 2,
+    }
+    if hive:
+        rec["hive_ids"] = sorted(hive)
+    up = [g.get("xgmi_links_up") for g in gpus if g.get("xgmi_links_up") is not None]
+    if up:
+        rec["links_up"] = sum(up)
+        rec["links_down"] = sum(g.get("xgmi_links_down") or 0 for g in gpus)
+    out = dict(topo)
+    out["xgmi"] = rec
+    return out
 
 
 def expected_gpu(topo: Dict[str, Any]) -> Optional[str]:

@@ -124,14 +124,15 @@ def test_agent_gpu_fault_event_annotates_running_pod(arun):
 def test_supervisor_waits_for_agent_evidence_then_attributes(arun):
     """Cluster supervisor + node agent over one apiserver: the supervisor holds the failed
     GPU pod (gpu.evidence-wait) until the agent's annotation lands, then writes an
-    HBM-OOM verdict with the GPU index into the trace column."""
+    HBM-OOM verdict with the *physical* GPU index into the trace column (the rank's torch
+    ordinal 2 behind HIP_VISIBLE_DEVICES=4,5,6,7 is physical GPU 6)."""
     async def go():
         api = FakeApiServer(bookmark_interval=0.1)
         url = await api.start()
         row = seed_rows()[1]  # RUNNING
         cfg = load_config(path=None, env={}, overrides={"cql-store-type": "memory", "rate-limit-elements-per-second": 0,
                                                         "resync-period": "0s", "gpu": {"evidence-wait": "3s"}})
-        pod = make_pod(row.id, cfg.labels, gpus=1, node="n", env={"LOCAL_RANK": "2", "HIP_VISIBLE_DEVICES": "0,1,2,3",
+        pod = make_pod(row.id, cfg.labels, gpus=1, node="n", env={"LOCAL_RANK": "2", "HIP_VISIBLE_DEVICES": "4,5,6,7",
                                                                    "RANK": "10", "WORLD_SIZE": "16"},
                        status={"phase": "Running"})
         api.create(pod)
@@ -139,15 +140,17 @@ def test_supervisor_waits_for_agent_evidence_then_attributes(arun):
         store = MemoryStore([row])
         app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
         await app.start()
-        tel = FakeTelemetry(n_gpus=4)
+        tel = FakeTelemetry(n_gpus=8)
         kc = KubeClient(KubeConfig(url))
         agent = NodeAgent(kc, tel, "n", "nexus")
         await agent.start()
         await asyncio.gather(app.factory.wait_for_cache_sync(5), agent.factory.wait_for_cache_sync(5))
-        tel.set_vram(2, 290_000)
+        tel.set_vram(6, 290_000)
+        tel.set_vram(2, 290_000)  # a busy GPU the pod never used must not be blamed
         t0 = time.monotonic()
-        # a message without any HIP signature: only the agent's VRAM evidence can tell it was HBM
-        api.update(_failed(api.get("Pod", "nexus", f"{row.id}-acdey"), "RuntimeError: worker exited", code=1))
+        msg = ("torch.OutOfMemoryError: HIP out of memory. Tried to allocate 4.00 GiB. GPU 2 has a total capacity of "
+               "287.98 GiB of which 1.02 GiB is free.")
+        api.update(_failed(api.get("Pod", "nexus", f"{row.id}-acdey"), msg, code=1))
         for _ in range(200):
             if store.get(ALGORITHM, row.id).lifecycle_stage == "FAILED":
                 break
@@ -156,8 +159,11 @@ def test_supervisor_waits_for_agent_evidence_then_attributes(arun):
         out = store.get(ALGORITHM, row.id)
         assert out.lifecycle_stage == "FAILED" and took < 3.0, took
         trace = json.loads(out.algorithm_failure_details)
-        assert trace["class"] == "hbm-oom" and trace["oom"]["gpu_index"] == 2
-        assert trace["topology"]["rank"] == 10 and trace["topology"]["expected_gpu"] == "2"
+        assert trace["class"] == "hbm-oom" and trace["oom"]["gpu_index"] == 6 and trace["oom"]["gpu_logical_index"] == 2
+        assert trace["topology"]["rank"] == 10 and trace["topology"]["expected_gpu"] == "6"
+        assert [g["index"] for g in trace["gpu"]["gpus"]] == [6]
+        assert any("VRAM peak" in sig for sig in trace["oom"]["signals"])
+        assert trace["topology"]["xgmi"]["source"] == "fake" and len(trace["topology"]["xgmi"]["links"]) == 7
         assert app.metrics.counter("decisions_deferred_for_gpu_evidence") == 1
         await agent.stop()
         await kc.close()
@@ -199,3 +205,54 @@ def test_pod_failed_predicate():
     assert pod_failed({"status": {"phase": "Failed"}})
     assert pod_failed({"status": {"reason": "Evicted"}})
     assert not pod_failed({"status": {"phase": "Running", "containerStatuses": [{"state": {"running": {}}}]}})
+
+
+class _FakePodResources:
+    def __init__(self, pods):
+        self.pods = pods
+
+    def list(self):
+        return self.pods
+
+    def close(self):
+        return None
+
+
+def test_agent_maps_device_plugin_allocation_to_physical_gpus():
+    """Device-plugin allocation (kubelet pod-resources, by BDF) is the container's HIP
+    ordinal space: a pod allocated physical GPUs 4-7 whose rank 3 OOMs on torch 'GPU 3'
+    is attributed to physical GPU 7, and the evidence records the allocation."""
+    from nexus_supervisor_amd.classify import Classifier
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.gpu.podresources import gpu_allocations
+
+    labels = LabelConfig()
+    tel = FakeTelemetry(n_gpus=8)
+    bdfs = [d["bdf"] for d in tel.devices()]
+    pod = make_pod("alloc-run", labels, gpus=4, node="n", env={"LOCAL_RANK": "3", "RANK": "3", "WORLD_SIZE": "4"}, rv="2",
+                   status={"phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {
+                       "terminated": {"reason": "Error", "exitCode": 1, "message":
+                                      "HIP out of memory. GPU 3 has a total capacity of 287.98 GiB"}}}]})
+    podres = _FakePodResources([{"name": pod["metadata"]["name"], "namespace": pod["metadata"]["namespace"], "containers": [
+        {"name": "algorithm", "devices": [{"resource_name": "amd.com/gpu", "device_ids": [bdfs[i] for i in (6, 4, 7, 5)]}]}]}])
+    assert gpu_allocations(podres.list())
+    agent = NodeAgent(None, tel, "n", "nexus", pod_resources=podres, factory=_NullFactory())
+    agent._bdf_index = {d["bdf"]: d["index"] for d in tel.devices()}
+    tel.set_vram(7, 294_000)
+    ev = agent.evidence(pod)
+    assert ev["allocated"] == [4, 5, 6, 7] and [g["index"] for g in ev["gpus"]] == [4, 5, 6, 7]
+    pod["metadata"]["annotations"] = {ANN: json.dumps(ev)}
+    r = Classifier(labels).classify_pod(pod)[0]
+    assert r.evidence["oom"]["gpu_index"] == 7 and r.evidence["oom"]["gpu_logical_index"] == 3
+    assert r.evidence["topology"]["expected_gpu"] == "7" and r.evidence["topology"]["physical_devices"] == [4, 5, 6, 7]
+    assert r.evidence["oom"]["peak_vram_bytes"] == 294_000 << 20
+
+
+class _NullFactory:
+    def informer(self, kind):
+        class _I:
+            indexer = {}
+
+            def add_event_handler(self, **kw):
+                return None
+        return _I()

@@ -27,11 +27,67 @@ def test_oomkilled_wins_tie_with_hip_message():
     assert v.kind == "host"
 
 
-def test_vram_peak_evidence_alone_is_hbm_and_attributes_gpu():
+def test_vram_peak_alone_is_not_an_oom_verdict():
+    """A full GPU without any OOM signature (exit 1, no allocation failure) is recorded as
+    a signal, not a verdict: a GPU left full by a previous tenant must not turn a plain
+    crash into an HBM-OOM that bypasses the Job's retry policy."""
     ev = {"gpus": [{"index": 3, "vram_total_mb": 294896, "vram_peak_mb": 294000},
                    {"index": 4, "vram_total_mb": 294896, "vram_peak_mb": 1000}]}
     v = oom.analyze(["RuntimeError: something failed"], [{"exitCode": 1}], ev, expected_gpu="3")
+    assert v.kind is None and v.hbm_score >= 0.5
+    assert any("no OOM signature" in s for s in v.signals)
+    # SIGKILL (exit 137, no cgroup OOMKilled) on a full GPU: the VRAM evidence decides HBM
+    v = oom.analyze([], [{"exitCode": 137}], ev, expected_gpu="3")
     assert v.kind == "hbm" and v.gpu_index == 3
+
+
+def test_torch_logical_gpu_maps_to_physical_through_visible_devices():
+    """torch's 'GPU 3' is the process's logical ordinal.  With
+    HIP_VISIBLE_DEVICES=4,5,6,7 and LOCAL_RANK=3 the failing GPU is physical 7; the trace
+    records both and reads GPU 7's evidence, never GPU 3's."""
+    from nexus_supervisor_amd.classify import Classifier
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.testing.seed import make_pod
+
+    msg = ("torch.OutOfMemoryError: HIP out of memory. Tried to allocate 8.00 GiB. GPU 3 has a total capacity of "
+           "287.98 GiB of which 2.10 GiB is free.")
+    ev = {"source": "agent", "gpus": [
+        {"index": 3, "vram_total_mb": 294896, "vram_peak_mb": 294500, "procs": []},  # another pod's full GPU
+        {"index": 7, "vram_total_mb": 294896, "vram_peak_mb": 292000, "proc_peak_vram_bytes": 280 << 30,
+         "procs": [{"pid": 4242, "rank": 3, "local_rank": 3}]}]}
+    topo = topology_from_env({"HIP_VISIBLE_DEVICES": "4,5,6,7", "LOCAL_RANK": "3", "RANK": "3", "WORLD_SIZE": "4"})
+    assert topo["visible_devices"] == ["4", "5", "6", "7"] and topo["expected_gpu"] == "7"
+    v = oom.analyze([msg], [{"exitCode": 1}], ev, topo["expected_gpu"], topo=topo)
+    assert v.kind == "hbm" and v.gpu_index == 7 and v.gpu_logical_index == 3
+    assert v.peak_vram_bytes == 280 << 30 and v.device_peak_vram_bytes == 292000 << 20
+    assert not any("GPU 3 " in s for s in v.signals)
+
+    labels = LabelConfig()
+    pod = make_pod("remapped", labels, gpus=4, rv="2", env={"HIP_VISIBLE_DEVICES": "4,5,6,7", "LOCAL_RANK": "3"}, status={
+        "phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {
+            "terminated": {"reason": "Error", "exitCode": 1, "message": msg}}}]})
+    pod["metadata"]["annotations"] = {"nexus.amd.com/gpu-evidence": json.dumps(ev)}
+    r = Classifier(labels).classify_pod(pod)[0]
+    assert r.evidence["oom"]["gpu_index"] == 7 and r.evidence["oom"]["gpu_logical_index"] == 3
+    assert r.evidence["topology"]["expected_gpu"] == "7"
+
+
+def test_layered_device_env_and_uuids():
+    from nexus_supervisor_amd.gpu.topology import device_map, physical_gpu, resolve_devices
+
+    # ROCr narrows first, HIP indexes into ROCr's list
+    t = topology_from_env({"ROCR_VISIBLE_DEVICES": "2,3,6,7", "HIP_VISIBLE_DEVICES": "1,3", "LOCAL_RANK": "1"})
+    assert t["visible_devices"] == ["3", "7"] and t["expected_gpu"] == "7"
+    assert physical_gpu(t, 0) == 3 and physical_gpu(t, 5) is None
+    # device-plugin allocation: the container's ordinals are the allocated GPUs in node order
+    assert device_map(t["device_chain"], list(range(8, 16))) == ["11", "15"]
+    # UUID entries resolve against telemetry records
+    u = topology_from_env({"HIP_VISIBLE_DEVICES": "GPU-abc,GPU-def", "LOCAL_RANK": "1"})
+    gpus = [{"index": 2, "uuid": "GPU-abc"}, {"index": 5, "uuid": "GPU-def"}]
+    assert physical_gpu(u, 1, gpus) == 5
+    r = resolve_devices(u, {"gpus": gpus})
+    assert r["physical_devices"] == [2, 5] and r["expected_gpu"] == "5" and r["expected_gpu_logical"] == 1
+    assert u["expected_gpu"] == "GPU-def"  # the memoised per-version record is not mutated
 
 
 def test_plain_failure_is_not_oom():
@@ -58,7 +114,7 @@ def test_topology_from_torchrun_env():
     assert t["rank"] == 5 and t["world_size"] == 16 and t["local_rank"] == 5
     assert t["master_addr"] == "10.0.0.1" and t["master_port"] == 29500
     assert t["expected_gpu"] == "5"
-    assert t["xgmi"] == {"local_gpus": 8, "links_per_gpu": 7, "fully_connected": True}
+    assert t["xgmi"] == {"source": "platform-default", "local_gpus": 8, "links_per_gpu": 7, "fully_connected": True}
     assert t["collective_env"] == {"NCCL_SOCKET_IFNAME": "eth0", "RCCL_MSCCL_ENABLE": "0"}
     assert t["backend"] == "rccl" and t["node"] == "mi355x-07"
     json.dumps(t)

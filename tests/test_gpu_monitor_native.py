@@ -1,0 +1,157 @@
+"""The native GPU monitor's attribution path on CPU (round 2, VERDICT weak #1-#3).
+
+``_amdsmi_monitor_stub`` is ``csrc/amdsmi/gpu_monitor.cpp`` built over the stub amd-smi
+(``amdsmi_stub.cpp``): the real sampler and event threads, the DRM-fdinfo / KFD-sysfs
+process scanners (``procscan.hpp``) and the xGMI link metrics run against a fake procfs /
+sysfs tree.  The fdinfo fixture is verbatim from an MI355X gpurun box
+(``tools/probe_kfd.py``)."""
+import os
+import time
+
+import pytest
+
+from nexus_supervisor_amd.testing.fakeprocfs import FakeProcFs, stub_bdf
+
+M = pytest.importorskip("nexus_supervisor_amd._amdsmi_monitor_stub")
+FIXTURE = os.path.join(os.path.dirname(__file__), "fixtures", "drm_fdinfo_mi355x.txt")
+UID = "0f3e2b6a-1111-2222-3333-444455556666"
+
+
+def test_parse_real_mi355x_fdinfo():
+    r = M.parse_drm_fdinfo(open(FIXTURE).read())
+    assert r["amdgpu"] and r["pdev"] == "0000:f4:00.0" and r["client_id"] == 4911448
+    assert r["vram_bytes"] == 8536236 * 1024  # the 8 GiB hold of gpu_stress
+    assert r["gtt_bytes"] == 8232 * 1024
+    assert not M.parse_drm_fdinfo("pos:\t0\nflags:\t02\n")["amdgpu"]
+
+
+def test_drm_scanner_and_kfd_sysfs(tmp_path):
+    fs = FakeProcFs(str(tmp_path), n_gpus=2)
+    fs.add_process(4242, {0: 8 << 30, 1: 1 << 30}, pod_uid=UID)
+    fs.add_process(77, {})  # /dev/kfd only: not a GPU user
+    sc = M.DrmScanner(fs.proc, 4)
+    uses = sorted((u["pid"], u["bdf"], u["vram_bytes"]) for u in sc.scan())
+    assert uses == [(4242, stub_bdf(0), 8 << 30), (4242, stub_bdf(1), 1 << 30)]
+    # fd tables are re-listed only for new PIDs / every `rescan_every` scans; VRAM every scan
+    fs.set_vram(4242, 0, 100 << 30)
+    before = sc.fd_scans
+    assert max(u["vram_bytes"] for u in sc.scan()) == 100 << 30 and sc.fd_scans == before
+    fs.end_process(4242)
+    assert sc.scan() == []
+    assert M.kfd_gpu_bdfs(fs.sys) == {27852: stub_bdf(0), 28852: stub_bdf(1)}
+    fs.add_process(5, {1: 3 << 30})
+    assert [(u["pid"], u["bdf"], u["vram_bytes"]) for u in M.kfd_proc_usage(fs.sys)] == [(5, stub_bdf(1), 3 << 30)]
+    assert M.host_pid_namespace(fs.proc) is False
+
+
+def _monitor(fs, source):
+    from nexus_supervisor_amd.gpu.telemetry import AmdSmiTelemetry
+
+    t = AmdSmiTelemetry(interval=0.01, proc_source=source, proc_root=fs.proc, sys_root=fs.sys, stub=True)
+    t.start()
+    return t
+
+
+def _wait(pred, timeout=3.0):
+    end = time.time() + timeout
+    while time.time() < end:
+        v = pred()
+        if v:
+            return v
+        time.sleep(0.01)
+    return pred()
+
+
+@pytest.mark.parametrize("source", ["auto", "drm", "kfd"])
+def test_monitor_attributes_pod_processes_without_amdsmi_pids(tmp_path, source):
+    """In a private PID namespace (a container without hostPID — the gpurun box) amd-smi's
+    host PIDs are only tallied as foreign; the pod's own processes come from DRM fdinfo
+    (or KFD sysfs), with cgroup pod UID, rank env and per-process VRAM peaks."""
+    from nexus_supervisor_amd.gpu.telemetry import evidence_for
+
+    fs = FakeProcFs(str(tmp_path), n_gpus=2)
+    env = {"RANK": "3", "LOCAL_RANK": "1", "WORLD_SIZE": "8", "HIP_VISIBLE_DEVICES": "0,1", "PATH": "/bin"}
+    fs.add_process(4242, {1: 200 << 30}, env=env, pod_uid=UID)
+    M.stub_set_proc(1, 2_946_842, 9 << 30)  # a host-PID entry amd-smi reports
+    tel = _monitor(fs, source)
+    try:
+        assert tel.proc_mode == ("drm" if source == "auto" else source)
+        snap = _wait(lambda: [g for g in tel.snapshot() if g["procs"]])
+        g = snap[0]
+        assert g["index"] == 1 and [p["pid"] for p in g["procs"]] == [4242]
+        p = g["procs"][0]
+        assert p["pod_uid"] == UID and p["env"] == {k: v for k, v in env.items() if k != "PATH"}
+        assert p["source"] == ("kfd" if source == "kfd" else "drm-fdinfo")
+        if source != "kfd":
+            assert g["foreign_procs"] == 1 and g["foreign_vram_bytes"] == 9 << 30
+        fs.set_vram(4242, 1, 280 << 30)
+        _wait(lambda: tel.snapshot()[1]["procs"][0]["peak_vram_bytes"] == 280 << 30)
+        fs.set_vram(4242, 1, 1 << 30)
+        ev = _wait(lambda: evidence_for(tel, pod_uid=UID))
+        rec = ev["gpus"][0]
+        assert rec["matched"] and rec["proc_peak_vram_bytes"] == 280 << 30
+        assert rec["procs"][0]["rank"] == 3 and rec["procs"][0]["source"] == p["source"]
+        # measured xGMI: the stub node's peer link plus six unconnected ports filtered out
+        assert [l["peer"] for l in rec["links"]] == [0] and rec["links"][0]["max_gbps"] == 608
+        assert rec["xgmi_links_up"] == 7 and rec["xgmi_hive_id"]
+    finally:
+        tel.stop()
+        M.stub_end_proc(1, 2_946_842)
+
+
+def test_monitor_events_links_and_stub_hooks(tmp_path):
+    fs = FakeProcFs(str(tmp_path), n_gpus=2)
+    tel = _monitor(fs, "drm")
+    try:
+        devs = tel.devices()
+        assert [d["bdf"] for d in devs] == [stub_bdf(0), stub_bdf(1)]
+        assert devs[0]["links"][0]["peer_index"] == 1 and devs[0]["links"][0]["type"] == "xgmi"
+        M.stub_push_event(0, "VMFAULT", "page fault at 0xdead")
+        evs = _wait(lambda: tel.drain_events())
+        assert evs[0]["type"] == "VMFAULT" and evs[0]["gpu"] == 0
+        M.stub_set_links_down(1, 2)
+        got = _wait(lambda: [e for e in tel.drain_events() if e["type"] == "XGMI_LINK_DOWN"])
+        assert got and got[0]["gpu"] == 1
+        M.stub_set_vram(0, 290_000)
+        t0 = time.time()
+        _wait(lambda: tel.peak_between(0, t0 - 1, time.time()) == 290_000)
+    finally:
+        tel.stop()
+        M.stub_set_links_down(1, 0)
+        M.stub_set_vram(0, 283)
+
+
+def test_classifier_attributes_through_native_monitor(tmp_path):
+    """End to end on CPU: the native (stub) monitor's evidence for a failing pod names the
+    physical GPU its processes ran on and the per-process VRAM peak."""
+    import json
+
+    from nexus_supervisor_amd.classify import Classifier, render_trace
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.gpu.telemetry import pod_evidence_provider
+    from nexus_supervisor_amd.testing.seed import make_pod
+
+    fs = FakeProcFs(str(tmp_path), n_gpus=2)
+    fs.add_process(4242, {1: 286 << 30}, env={"LOCAL_RANK": "0", "HIP_VISIBLE_DEVICES": "1"}, pod_uid=UID)
+    M.stub_set_vram(1, 294_000)
+    tel = _monitor(fs, "drm")
+    try:
+        _wait(lambda: tel.snapshot()[1]["procs"])
+        labels = LabelConfig()
+        c = Classifier(labels)
+        c.evidence_provider = pod_evidence_provider(tel, lookback=30)
+        pod = make_pod("native-run", labels, gpus=1, rv="2", env={"LOCAL_RANK": "0", "HIP_VISIBLE_DEVICES": "1"}, status={
+            "phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {"terminated": {
+                "reason": "Error", "exitCode": 1, "message": "hipErrorOutOfMemory: HIP out of memory. GPU 0 has a total "
+                                                            "capacity of 287.98 GiB"}}}]})
+        pod["metadata"]["uid"] = UID
+        r = c.classify_pod(pod)[0]
+        trace = json.loads(render_trace(r))
+        assert trace["class"] == "hbm-oom"
+        assert trace["oom"]["gpu_index"] == 1 and trace["oom"]["gpu_logical_index"] == 0
+        assert trace["oom"]["peak_vram_bytes"] == 286 << 30
+        assert trace["gpu"]["gpus"][0]["procs"][0]["source"] == "drm-fdinfo"
+        assert trace["topology"]["xgmi"]["source"] == "amdsmi"
+    finally:
+        tel.stop()
+        M.stub_set_vram(1, 283)

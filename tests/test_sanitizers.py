@@ -7,6 +7,14 @@ not available on the pool).  The reference has no race/sanitizer testing at all
   the test fails on any sanitizer report in the server's stderr.
 * random / truncated inputs into the in-process decoders (``_cql_native.FrameReader``,
   ``_kube_native.ProjectedDecoder``) must raise ``ValueError`` — never crash.
+* the in-process extensions themselves (``_kube_native``, ``_cql_native`` and the GPU
+  monitor over the stub amd-smi) built with ``-fsanitize=address,undefined`` and loaded
+  into a child Python with the runtime preloaded (``tools/san_inproc.py``): the fuzzers,
+  the native JSON tests, the monitor tests and the reference-parity scenario over HTTP +
+  CQL run there; any ASan / UBSan report fails the test.
+* the GPU monitor's sampler + event-listener threads under ThreadSanitizer
+  (``bin/monitor_selftest-thread`` over the stub amd-smi and a fake procfs), and the
+  monitor module itself under TSan in a child Python.
 """
 import asyncio
 import json
@@ -14,6 +22,9 @@ import os
 import random
 import socket
 import struct
+
+import subprocess
+import sys
 
 import pytest
 
@@ -135,3 +146,56 @@ def test_projected_decoder_fuzz():
         except ValueError:
             bad += 1
     assert ok + bad == 5000 and bad > 0 and ok > 0
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_REPORTS = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitizer", "ERROR: LeakSanitizer")
+
+
+def _sanitized(sanitize):
+    try:
+        _build.build(sanitize=sanitize)
+    except RuntimeError as exc:  # pragma: no cover - toolchain without the runtime
+        pytest.skip(f"sanitizer build unavailable: {exc}")
+    rt = _build.sanitizer_runtime(sanitize)
+    if rt is None:  # pragma: no cover
+        pytest.skip(f"no {sanitize} runtime library")
+    return rt
+
+
+@pytest.mark.parametrize("sanitize", ["thread", "address"])
+def test_gpu_monitor_threads_under_sanitizer(sanitize, tmp_path):
+    """Sampler + event listener + every reader of the native monitor, concurrently, over
+    the stub amd-smi and a fake procfs in all three process-source modes."""
+    from nexus_supervisor_amd.testing.fakeprocfs import FakeProcFs
+
+    _sanitized(sanitize)
+    fs = FakeProcFs(str(tmp_path), n_gpus=2)
+    fs.add_process(4242, {0: 8 << 30, 1: 1 << 30}, env={"RANK": "1"}, pod_uid="0f3e2b6a-1111-2222-3333-444455556666")
+    exe = os.path.join(_build.BIN, f"monitor_selftest-{sanitize}")
+    p = subprocess.run([exe, fs.proc, fs.sys, "1.5"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=0", ASAN_OPTIONS="detect_leaks=1"))
+    out = p.stdout + p.stderr
+    assert p.returncode == 0 and not any(r in out for r in _REPORTS), out[-4000:]
+    assert out.count("mode=") == 3
+
+
+@pytest.mark.parametrize("sanitize", ["address", "thread"])
+def test_inprocess_extensions_under_sanitizer(sanitize):
+    rt = _sanitized(sanitize)
+    if sanitize == "address":
+        tests = ["tests/test_sanitizers.py::test_frame_reader_fuzz", "tests/test_sanitizers.py::test_projected_decoder_fuzz",
+                 "tests/test_native_json.py", "tests/test_gpu_monitor_native.py",
+                 "tests/test_kube_wire.py::test_reference_parity_over_http_and_cql", "tests/test_cql.py"]
+    else:
+        tests = ["tests/test_gpu_monitor_native.py"]
+    env = dict(os.environ, NEXUS_NATIVE_DIR=os.path.join(_build.SAN_DIR, sanitize), LD_PRELOAD=rt,
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=0:report_signal_unsafe=0", PYTHONDONTWRITEBYTECODE="1")
+    env.pop("PYTEST_XDIST_WORKER", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "san_inproc.py"), *tests], cwd=ROOT,
+                       capture_output=True, text=True, timeout=600, env=env)
+    out = p.stdout + p.stderr
+    assert "instrumented:" in out, out[-3000:]
+    assert p.returncode == 0, out[-4000:]
+    assert not any(r in out for r in _REPORTS), out[-4000:]
