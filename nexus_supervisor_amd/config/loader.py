@@ -18,6 +18,7 @@ keep the default rather than decoding to zero.
 from __future__ import annotations
 
 import dataclasses
+import logging
 import os
 from typing import Any, Dict, Mapping, Optional, get_type_hints
 
@@ -76,7 +77,9 @@ def _is_unset(value) -> bool:
     return value is None or (isinstance(value, str) and value.strip() == "")
 
 
-def _apply(obj, data: Mapping[str, Any], env: Mapping[str, str], path=()):
+def _apply(obj, data: Mapping[str, Any], env: Mapping[str, str], path=(), unknown: Optional[list] = None):
+    """Fill ``obj`` from ``data`` + env.  Unknown keys raise, or are collected into
+    ``unknown`` (dotted paths) when a list is given."""
     hints = get_type_hints(type(obj))
     known = set()
     for f in dataclasses.fields(obj):
@@ -87,7 +90,7 @@ def _apply(obj, data: Mapping[str, Any], env: Mapping[str, str], path=()):
         sub = getattr(obj, f.name)
         if dataclasses.is_dataclass(sub):
             sub_data = data.get(key) if isinstance(data, Mapping) else None
-            _apply(sub, sub_data if isinstance(sub_data, Mapping) else {}, env, fpath)
+            _apply(sub, sub_data if isinstance(sub_data, Mapping) else {}, env, fpath, unknown)
             continue
         kind = f.metadata.get("kind")
         if isinstance(data, Mapping) and key in data and not (_is_unset(data[key]) and kind != "list"):
@@ -98,9 +101,11 @@ def _apply(obj, data: Mapping[str, Any], env: Mapping[str, str], path=()):
         if ev is not None and ev.strip() != "":
             setattr(obj, f.name, _coerce(ev, ftype, kind, env_name(fpath)))
     if isinstance(data, Mapping):
-        unknown = set(data) - known
-        if unknown:
-            raise ConfigError(f"unknown config keys at {'.'.join(path) or '<root>'}: {sorted(unknown)}")
+        extra = set(data) - known
+        if extra and unknown is None:
+            raise ConfigError(f"unknown config keys at {'.'.join(path) or '<root>'}: {sorted(extra)}")
+        if extra:
+            unknown.extend(".".join(path + (k,)) for k in sorted(extra))
 
 
 def _read_yaml(path: str) -> Dict[str, Any]:
@@ -132,6 +137,9 @@ def load_config(
     """Load a :class:`SupervisorConfig` from defaults, YAML files and ``NEXUS__`` env.
 
     ``overrides`` is a kebab-keyed mapping applied after the files (tests use it).
+    Unknown keys are logged and ignored, as viper does for the reference (an appconfig
+    with keys of a newer or older release still starts); ``NEXUS_CONFIG_STRICT=1`` makes
+    them fatal.
     """
     env = os.environ if env is None else env
     data: Dict[str, Any] = {}
@@ -149,7 +157,12 @@ def load_config(
     if overrides:
         data = _deep_merge(data, overrides)
     cfg = SupervisorConfig()
-    _apply(cfg, data, env)
+    strict = str(env.get("NEXUS_CONFIG_STRICT", "")).strip().lower() in _TRUE
+    unknown: list = []
+    _apply(cfg, data, env, unknown=None if strict else unknown)
+    if unknown:
+        logging.getLogger("nexus_supervisor_amd.config").warning(
+            "ignoring unknown config keys (set NEXUS_CONFIG_STRICT=1 to refuse them): %s", ", ".join(unknown))
     return validate(cfg) if do_validate else cfg
 
 

@@ -77,8 +77,14 @@ class CompatConfig:
     delete_on_read_error: bool = field(default=False, metadata=_k("delete-on-read-error"))
     # NotFound on Job DELETE counts as success (fixes retry hazard)
     delete_not_found_ok: bool = field(default=True, metadata=_k("delete-not-found-ok"))
-    # conditional write: only move rows that are still unfinished (LWT)
-    conditional_update: bool = field(default=False, metadata=_k("conditional-update"))
+    # conditional writes (LWT ``IF lifecycle_stage IN (<unfinished stages>)``): a write never
+    # moves a row out of a finished stage, so a deposed leader's queued decision cannot
+    # overwrite what the new leader (or another component: CANCELLED) wrote.
+    #   auto   — ToRunning always conditional; failure writes conditional when leader
+    #            election is enabled (HA) — the default
+    #   always — every write conditional; never — none (reference behaviour)
+    # true / false are accepted as always / never.
+    conditional_update: str = field(default="auto", metadata=_k("conditional-update"))
 
 
 @dataclass
@@ -128,6 +134,36 @@ class GpuConfig:
     # hold a failed GPU pod's decision this long for the node agent's evidence annotation
     # (0 = decide immediately on whatever is there)
     evidence_wait: float = field(default=0.0, metadata=_k("evidence-wait", "duration"))
+
+
+@dataclass
+class StagesConfig:
+    """nexus-core ``models.LifecycleStage*`` strings and ``IsFinished()`` set (SURVEY §8 q1:
+    only BUFFERED / RUNNING / CANCELLED are attested by the reference's seed data, the
+    rest are unverifiable offline) — pinned per deployment."""
+
+    new: str = field(default="NEW", metadata=_k("new"))
+    buffered: str = field(default="BUFFERED", metadata=_k("buffered"))
+    running: str = field(default="RUNNING", metadata=_k("running"))
+    completed: str = field(default="COMPLETED", metadata=_k("completed"))
+    failed: str = field(default="FAILED", metadata=_k("failed"))
+    scheduling_failed: str = field(default="SCHEDULING_FAILED", metadata=_k("scheduling-failed"))
+    deadline_exceeded: str = field(default="DEADLINE_EXCEEDED", metadata=_k("deadline-exceeded"))
+    cancelled: str = field(default="CANCELLED", metadata=_k("cancelled"))
+    # stage strings for which IsFinished() is true (may name stages this build does not model,
+    # e.g. one added by a newer nexus-core); empty = the five terminal stages above
+    finished: List[str] = field(default_factory=list, metadata=_k("finished", "list"))
+
+    def mapping(self):
+        return {"NEW": self.new, "BUFFERED": self.buffered, "RUNNING": self.running, "COMPLETED": self.completed,
+                "FAILED": self.failed, "SCHEDULING_FAILED": self.scheduling_failed,
+                "DEADLINE_EXCEEDED": self.deadline_exceeded, "CANCELLED": self.cancelled}
+
+    def apply(self) -> None:
+        """Make these the process-wide stage strings (models.checkpoint)."""
+        from ..models.checkpoint import configure_lifecycle_stages
+
+        configure_lifecycle_stages(self.mapping(), self.finished or None)
 
 
 @dataclass
@@ -206,6 +242,7 @@ class SupervisorConfig:
     async_job_delete: bool = field(default=True, metadata=_k("async-job-delete"))
     compat: CompatConfig = field(default_factory=CompatConfig, metadata=_k("compat"))
     labels: LabelConfig = field(default_factory=LabelConfig, metadata=_k("labels"))
+    stages: StagesConfig = field(default_factory=StagesConfig, metadata=_k("stages"))
     rules: RulesConfig = field(default_factory=RulesConfig, metadata=_k("rules"))
     gpu: GpuConfig = field(default_factory=GpuConfig, metadata=_k("gpu"))
     leader_election: LeaderElectionConfig = field(default_factory=LeaderElectionConfig, metadata=_k("leader-election"))
@@ -229,6 +266,16 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("rate-limit-elements-burst must be >= 1")
     if cfg.failure_rate_base_delay < 0 or cfg.failure_rate_max_delay < cfg.failure_rate_base_delay:
         raise ConfigError("failure-rate-max-delay must be >= failure-rate-base-delay >= 0")
+    cu = str(cfg.compat.conditional_update).strip().lower()
+    cfg.compat.conditional_update = {"true": "always", "1": "always", "yes": "always", "on": "always",
+                                     "false": "never", "0": "never", "no": "never", "off": "never"}.get(cu, cu)
+    if cfg.compat.conditional_update not in ("auto", "always", "never"):
+        raise ConfigError("compat.conditional-update must be auto|always|never")
+    st = cfg.stages.mapping()
+    if any(not v for v in st.values()) or len(set(st.values())) != len(st):
+        raise ConfigError("stages: every lifecycle stage needs a distinct non-empty string")
+    if set(cfg.stages.finished) & {st["NEW"], st["BUFFERED"], st["RUNNING"]}:
+        raise ConfigError("stages.finished cannot contain new / buffered / running")
     if cfg.rules.evicted_policy not in ("fail", "observe"):
         raise ConfigError("rules.evicted-policy must be fail|observe")
     if cfg.rules.trace_format not in ("raw", "json", "auto"):

@@ -6,9 +6,12 @@ indexes).  The Python model mirrors nexus-core ``models.CheckpointedRequest``
 (used at ``/root/reference/services/supervisor.go:264-370``).
 
 Stage strings other than BUFFERED / RUNNING / CANCELLED (seen in the seed data,
-``checkpoints.cql:35,44,98``) cannot be verified offline; they are
-plain module constants so a deployment can pin them via
-:func:`configure_lifecycle_stages`.
+``checkpoints.cql:35,44,98``) cannot be verified offline, so they and
+the finished set are configuration (``stages:`` section, :class:`..config.schema.StagesConfig`)
+applied process-wide by :func:`configure_lifecycle_stages` — every supervisor and
+shard-worker process applies its config's section at construction.  Readers go
+through the class attributes / :func:`finished_stages` at call time, never through a
+copy taken at import.
 """
 from __future__ import annotations
 
@@ -29,28 +32,42 @@ class LifecycleStage:
     CANCELLED = "CANCELLED"
 
 
+DEFAULT_STAGES: Dict[str, str] = {a: getattr(LifecycleStage, a) for a in vars(LifecycleStage) if a.isupper()}
 # nexus-core ``CheckpointedRequest.IsFinished()``: proven for CANCELLED
 # (/root/reference/services/supervisor_test.go:473-540), presumed for terminal stages.
-FINISHED_STAGES = frozenset(
-    {
-        LifecycleStage.COMPLETED,
-        LifecycleStage.FAILED,
-        LifecycleStage.SCHEDULING_FAILED,
-        LifecycleStage.DEADLINE_EXCEEDED,
-        LifecycleStage.CANCELLED,
-    }
-)
+TERMINAL_ATTRS = ("COMPLETED", "FAILED", "SCHEDULING_FAILED", "DEADLINE_EXCEEDED", "CANCELLED")
+UNFINISHED_ATTRS = ("NEW", "BUFFERED", "RUNNING")
 
 
-def configure_lifecycle_stages(mapping: Dict[str, str], finished: Optional[Iterable[str]] = None) -> None:
-    """Override stage strings (``{"FAILED": "FAILED_V2", ...}``) and the finished set."""
+def _terminal_set() -> frozenset:
+    return frozenset(getattr(LifecycleStage, a) for a in TERMINAL_ATTRS)
+
+
+FINISHED_STAGES = _terminal_set()
+
+
+def finished_stages() -> frozenset:
+    """The current finished set (reads the module state at call time)."""
+    return FINISHED_STAGES
+
+
+def unfinished_stages() -> Tuple[str, ...]:
+    """Stages a run can still leave: the conditional-write guard (``IF lifecycle_stage IN``)."""
+    return tuple(s for s in (getattr(LifecycleStage, a) for a in UNFINISHED_ATTRS) if s not in FINISHED_STAGES)
+
+
+def configure_lifecycle_stages(mapping: Optional[Dict[str, str]] = None, finished: Optional[Iterable[str]] = None) -> None:
+    """Set the stage strings (``{"FAILED": "FAILED_V2", ...}``, attributes not named keep
+    their defaults) and the finished set.  ``finished`` None rebuilds the set from the
+    terminal attributes, so remapping only ``FAILED`` moves it in the set too."""
     global FINISHED_STAGES
-    for attr, value in mapping.items():
-        if not hasattr(LifecycleStage, attr):
+    mapping = dict(mapping or {})
+    for attr in mapping:
+        if attr not in DEFAULT_STAGES:
             raise KeyError(attr)
-        setattr(LifecycleStage, attr, value)
-    if finished is not None:
-        FINISHED_STAGES = frozenset(finished)
+    for attr, default in DEFAULT_STAGES.items():
+        setattr(LifecycleStage, attr, mapping.get(attr) or default)
+    FINISHED_STAGES = frozenset(finished) if finished else _terminal_set()
 
 
 KEYSPACE = "nexus"

@@ -88,11 +88,12 @@ class PipelineStage:
         self._pending: Dict[Hashable, Deque[_Entry]] = {}
         self._ready: Deque[Hashable] = collections.deque()
         self._active: set = set()       # keys held by a worker or waiting out a backoff
+        self._running: set = set()      # keys a worker is processing right now
         # idle workers park on their own future; a signal wakes exactly one (a shared
         # Event would wake every idle worker per item: 256 wakeups for one decision)
         self._waiters: Deque[asyncio.Future] = collections.deque()
         self._tasks = []
-        self._timers = set()
+        self._timers: Dict[Hashable, asyncio.TimerHandle] = {}  # backoff retries by key
         self._closed = False
         self._idle: Optional[asyncio.Event] = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None
@@ -164,6 +165,7 @@ class PipelineStage:
                 self._pending.pop(key, None)
                 continue
             self._active.add(key)
+            self._running.add(key)
             entry = q[0]
             delay = self.bucket.reserve()
             if delay > 0:
@@ -171,8 +173,10 @@ class PipelineStage:
             try:
                 out = await self.processor(entry.item)
             except asyncio.CancelledError:
+                self._running.discard(key)
                 raise
             except BaseException as exc:  # noqa: BLE001 - every failure is retried / dead-lettered
+                self._running.discard(key)
                 self.stats.failed_attempts += 1
                 nfail = self.backoff.failures(key) + 1
                 if self.max_retries and nfail > self.max_retries:
@@ -192,6 +196,7 @@ class PipelineStage:
                 log.debug("%s: retry key %s in %.3fs (%s)", self.name, key, wait, exc)
                 self._schedule_retry(key, wait)
                 continue
+            self._running.discard(key)
             self.stats.processed += 1
             self.backoff.forget(key)
             q.popleft()
@@ -215,7 +220,7 @@ class PipelineStage:
     def _schedule_retry(self, key, wait):
         # key stays in _active: later items of the same key cannot overtake the retried one
         def fire():
-            self._timers.discard(h)
+            self._timers.pop(key, None)
             self._active.discard(key)
             if self._pending.get(key):
                 self._ready.appendleft(key)
@@ -224,8 +229,7 @@ class PipelineStage:
                 self._pending.pop(key, None)
                 self._check_idle()
 
-        h = self._loop.call_later(wait, fire)
-        self._timers.add(h)
+        self._timers[key] = self._loop.call_later(wait, fire)
 
     # ---------------------------------------------------------------- lifecycle
     async def start(self, post_start: Optional[Callable[[], Awaitable[None]]] = None) -> None:
@@ -254,7 +258,7 @@ class PipelineStage:
         self._closed = True
         if drain:
             await self.join(timeout)
-        for h in list(self._timers):
+        for h in list(self._timers.values()):
             h.cancel()
         self._timers.clear()
         self._pending.clear()
@@ -265,6 +269,29 @@ class PipelineStage:
             t.cancel()
         await asyncio.gather(*self._tasks, return_exceptions=True)
         self._tasks = []
+
+    def clear(self) -> int:
+        """Drop every queued item and every backoff retry (fencing on lost leadership);
+        items a worker is processing right now finish (their processor checks the fence
+        itself).  Returns the number of items dropped."""
+        dropped = 0
+        for key, q in list(self._pending.items()):
+            if key in self._running:
+                while len(q) > 1:
+                    q.pop()
+                    dropped += 1
+                continue
+            dropped += len(q)
+            del self._pending[key]
+            h = self._timers.pop(key, None)
+            if h is not None:
+                h.cancel()
+            self._active.discard(key)
+            self.backoff.forget(key)
+        self._ready.clear()
+        self.stats.dropped_closed += dropped
+        self._check_idle()
+        return dropped
 
     # ---------------------------------------------------------------- introspection
     def depth(self) -> int:

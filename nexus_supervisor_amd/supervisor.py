@@ -35,7 +35,8 @@ from .config.schema import SupervisorConfig
 from .informer import InformerFactory, label_index
 from .kube.errors import NotFound
 from .models import kube
-from .models.checkpoint import FINISHED_STAGES, LifecycleStage
+from .models import checkpoint as _cp
+from .models.checkpoint import LifecycleStage
 from .models.decisions import Decision, DecisionAction as A, RunStatusAnalysisResult
 from .obs.logging import KLogger
 from .obs.metrics import Metrics
@@ -64,6 +65,10 @@ class JobClient:
 
 class CasConflict(Exception):
     """Conditional write lost a race; the item is retried (re-read + re-decide)."""
+
+
+class Fenced(Exception):
+    """This replica lost its lease (or its shard) after the decision was dequeued."""
 
 
 def parse_k8s_time(ts: Optional[str]) -> Optional[float]:
@@ -107,6 +112,7 @@ class Supervisor:
         wall: Callable[[], float] = time.time,
     ):
         self.cfg = cfg
+        cfg.stages.apply()  # process-wide stage strings / finished set (stages: section)
         self.namespace = cfg.resource_namespace
         self.store = store
         self.jobs = jobs
@@ -129,6 +135,11 @@ class Supervisor:
         self._sweeper: Optional[asyncio.Task] = None
         self.decision_hooks: List[Callable[[Decision], None]] = []
         self.active = not cfg.leader_election.enabled  # leader gating flips this
+        # fencing epoch: bumped on every loss of leadership; a decision dequeued under an
+        # older epoch never writes or deletes (see set_active)
+        self.epoch = 0
+        self._label_check_at = 0.0
+        self.label_mismatch = False
         self._unfinished_cache: Optional[Tuple[str, ...]] = None
         self.gc_tuner = GcTuner.from_config(cfg.runtime, self.metrics)
         self.worker_shard = None
@@ -210,12 +221,36 @@ class Supervisor:
             await asyncio.gather(*pending, return_exceptions=True)
 
     def set_active(self, active: bool) -> None:
-        """Leader gating: on gaining leadership replay the caches (idempotent) so nothing
-        decided while standby is lost (SURVEY §5.3 'replay on restart')."""
+        """Leader gating.  On gaining leadership replay the caches (idempotent) so nothing
+        decided while standby is lost (SURVEY §5.3 'replay on restart').  On losing it,
+        *fence*: bump the epoch (in-flight decisions check it right before their write
+        and their Job DELETE), drop every queued and backing-off decision, cancel the
+        background DELETEs and forget the decided-stage cache — the new leader owns those
+        runs now (ADVICE r1 app.py:106).  The conditional write
+        (``compat.conditional-update``) covers a write already on the wire."""
         was = self.active
         self.active = active
         if active and not was:
             self.replay()
+        elif was and not active:
+            self.fence()
+
+    def fence(self) -> int:
+        self.epoch += 1
+        dropped = self.pipeline.clear() if self.pipeline is not None else 0
+        for t in list(self._deletes):
+            t.cancel()
+        self._deletes.clear()
+        self._gpu_wait.clear()
+        self._parked.clear()
+        self._applied.clear()
+        self.metrics.inc("fenced_decisions_dropped", dropped)
+        self.metrics.inc("fencings")
+        self.log.info("leadership lost: fenced in-flight work", dropped=dropped, epoch=self.epoch)
+        return dropped
+
+    def _fenced(self, epoch: int) -> bool:
+        return not self.active or epoch != self.epoch
 
     def replay(self) -> None:
         for ev in self.event_informer.indexer.values():
@@ -316,9 +351,13 @@ class Supervisor:
         inv = ev.get("involvedObject") or {}
         grace = self.cfg.rules.stale_event_grace
         if grace <= 0:
-            self.log.info("Algorithm object not found - stale event", requestId=inv.get("name"), reason=ev.get("reason"),
-                          message=ev.get("message"))
-            self.metrics.inc("events_stale")
+            if self.cfg.informer_label_selector:
+                self.metrics.inc("events_unmatched")
+                self.log.v(2).info("event object not in the Nexus caches, dropped", requestId=inv.get("name"))
+            else:
+                self.log.info("Algorithm object not found - stale event", requestId=inv.get("name"),
+                              reason=ev.get("reason"), message=ev.get("message"))
+                self.metrics.inc("events_stale")
             return
         key = (inv.get("kind", ""), inv.get("name", ""))
         lst = self._parked.setdefault(key, [])
@@ -341,11 +380,14 @@ class Supervisor:
     async def _sweep_parked(self):
         tick = max(0.02, min(1.0, self.cfg.rules.stale_event_grace / 4 or 1.0,
                              self.cfg.gpu.evidence_wait / 4 if self.cfg.gpu.evidence_wait > 0 else 1.0))
+        selected = self.cfg.informer_label_selector
         while True:
             await asyncio.sleep(tick)
             if self._gpu_wait:
                 self._expire_gpu_waits()
             now = time.monotonic()
+            if now >= self._label_check_at:
+                self._check_labels(now)
             ws = self.worker_shard
             for key in list(self._parked):
                 lst = [p for p in self._parked[key] if p[0] > now]
@@ -353,12 +395,47 @@ class Supervisor:
                 if dropped and ws is not None and key[0] == "Pod" and ws.owner_of_pod(key[1]) not in (None, ws.index):
                     dropped = 0  # another shard worker owns that pod: not stale, just not ours
                 if dropped:
-                    self.metrics.inc("events_stale", dropped)
-                    self.log.info("Algorithm object not found - stale event", kind=key[0], requestId=key[1])
+                    if selected:
+                        # label-selected caches hold only Nexus runs: an event whose object never
+                        # showed up is almost always about a non-Nexus Pod/Job of the namespace —
+                        # counted, logged at V(2) only
+                        self.metrics.inc("events_unmatched", dropped)
+                        self.log.v(2).info("event object not in the Nexus caches, dropped", kind=key[0], name=key[1])
+                    else:
+                        self.metrics.inc("events_stale", dropped)
+                        self.log.info("Algorithm object not found - stale event", kind=key[0], requestId=key[1])
                 if lst:
                     self._parked[key] = lst
                 else:
                     del self._parked[key]
+
+    def _check_labels(self, now: float) -> None:
+        """Loud startup check for a label-key mismatch: the label keys
+        are unverifiable offline guesses, and with server-side selectors a wrong guess
+        leaves the Pod/Job caches empty so every decision is silently dropped.  Events
+        naming Pods/Jobs while both caches stay empty means the selector matches nothing."""
+        synced = all(i.has_synced() for i in (self.event_informer, self.pod_informer, self.job_informer))
+        if not synced or not self.cfg.informer_label_selector or not self.active:
+            self._label_check_at = now + 5.0
+            return
+        self._label_check_at = now + 60.0
+        if len(self.pod_informer.indexer) or len(self.job_informer.indexer):
+            if self.label_mismatch:
+                self.label_mismatch = False
+                self.metrics.set("label_selector_mismatch", 0.0)
+            return
+        named = sum(1 for ev in self.event_informer.indexer.values()
+                    if (ev.get("involvedObject") or {}).get("kind") in ("Pod", "Job"))
+        if named < 3:
+            return
+        self.label_mismatch = True
+        self.metrics.set("label_selector_mismatch", 1.0)
+        lb = self.cfg.labels
+        self.log.warning("LABEL MISMATCH: the namespace has Events about Pods/Jobs but no Pod or Job matches the "
+                         "Nexus label selector - every decision would be dropped. Check labels.nexus-component / "
+                         "labels.algorithm-run-value against the labels your Nexus runs carry.",
+                         selector=f"{lb.nexus_component_label}={lb.algorithm_run_value}", events=named,
+                         namespace=self.namespace)
 
     # ------------------------------------------------------------------ submit
     def _submit(self, r: RunStatusAnalysisResult, origin: float, recv: float) -> None:
@@ -369,7 +446,8 @@ class Supervisor:
         if not self.owns(key):
             return
         applied = self._applied.get(key)
-        if applied is not None and (applied in FINISHED_STAGES or (r.action == A.TO_RUNNING and applied == LifecycleStage.RUNNING)):
+        if applied is not None and (applied in _cp.FINISHED_STAGES
+                                    or (r.action == A.TO_RUNNING and applied == LifecycleStage.RUNNING)):
             self.metrics.inc("decisions_suppressed")
             return
         if self.cfg.observability.stage_timestamps:
@@ -380,8 +458,13 @@ class Supervisor:
         self.pipeline.receive(r)
 
     # ------------------------------------------------------------------ actuate
-    def _unfinished_stages(self):
-        return tuple(s for s in (LifecycleStage.NEW, LifecycleStage.BUFFERED, LifecycleStage.RUNNING) if s not in FINISHED_STAGES)
+    def _conditional(self, running: bool) -> bool:
+        mode = self.cfg.compat.conditional_update
+        if mode == "always":
+            return True
+        if mode == "never":
+            return False
+        return running or self.cfg.leader_election.enabled
 
     async def _delete_job(self, name: str) -> bool:
         try:
@@ -402,8 +485,12 @@ class Supervisor:
         if stamps is not None and "dequeue" not in stamps:
             stamps["dequeue"] = wall()
         failing = r.action in A.FAILING
+        epoch = self.epoch
         if r.action not in STAGE_FOR_ACTION:
             raise ValueError(f"unknown analysis result action: {r.action}")
+        if self._fenced(epoch):
+            self.metrics.inc("decisions_fenced")
+            return Decision(r, "fenced", None, False)
         try:
             # the owned-columns write needs only the stage; the full-row upsert (reference
             # UpsertCheckpoint of the deep copy) needs every column
@@ -435,6 +522,8 @@ class Supervisor:
             # a crash between write and delete (or a failed delete) — finish the delete
             if r.pending_delete or (failing and cp.lifecycle_stage in _FAILED_STAGES()
                                     and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is not None):
+                if self._fenced(epoch):
+                    return Decision(r, "fenced", cp.lifecycle_stage, False)
                 deleted = await self._delete_job(r.request_id)
                 r.pending_delete = False
             self._remember(key, cp.lifecycle_stage)
@@ -446,7 +535,11 @@ class Supervisor:
             if cp.lifecycle_stage == LifecycleStage.RUNNING and not compat.full_row_upsert:
                 self._remember(key, stage)
                 return Decision(r, "skipped-already-running", stage, False)
-            await self._write(cp, stage, None, None, now_dt, set_failure=False)
+            if self._fenced(epoch):
+                self.metrics.inc("decisions_fenced")
+                return Decision(r, "fenced", None, False)
+            if not await self._write(cp, stage, None, None, now_dt, set_failure=False, running=True):
+                return await self._lost_race(r, key)
             stamps["ack"] = wall()
             stamps["ack_mono"] = time.monotonic()
             self._observe(r)
@@ -460,16 +553,23 @@ class Supervisor:
         # lose the decision for good — the Job's pods are garbage-collected, so the replay
         # after failover has nothing to re-decide from.  Written-then-crashed instead leaves
         # a failed row whose Job still exists, which the replay finishes (finished path).
+        if self._fenced(epoch):
+            self.metrics.inc("decisions_fenced")
+            return Decision(r, "fenced", None, False)
         try:
-            await self._write(cp, stage, cause, details, now_dt, set_failure=True)
+            written = await self._write(cp, stage, cause, details, now_dt, set_failure=True)
         except Exception as exc:
             self.log.error(exc, "failed to update algorithm submission status", requestId=r.request_id, algorithm=r.algorithm)
             raise
+        if not written:
+            return await self._lost_race(r, key)
         stamps["ack"] = wall()
         stamps["ack_mono"] = time.monotonic()
         self._observe(r)
         self._remember(key, stage)
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
+        if self._fenced(epoch):  # durable, but the Job now belongs to the new leader's replay
+            return Decision(r, "applied", stage, False)
         if self.cfg.async_job_delete:
             # the decision is durable; the Job DELETE must not hold a worker (and with it
             # every later decision) hostage to API-server latency
@@ -518,20 +618,34 @@ class Supervisor:
             if ack is not None:
                 self.metrics.observe_seconds("stage_delete", self.wall() - ack)
             return
+        if not self.active:
+            return  # fenced: the new leader's replay owns this Job
         self.metrics.inc("job_delete_retries")
         t = asyncio.ensure_future(self._delete_with_retry(r, first_delay=self.cfg.failure_rate_base_delay))
         self._deletes.add(t)
         t.add_done_callback(self._deletes.discard)
 
     async def _delete_with_retry(self, r: RunStatusAnalysisResult, first_delay: float = 0.0) -> None:
+        """Background Job DELETE after a durable failure write.  The key is already marked
+        finished, so a later failing decision would be suppressed: this loop is the only
+        thing left that removes the Job (and frees its amd.com/gpu) — it never gives up
+        while this replica leads and the Job is still cached (ADVICE r1 supervisor.py:545).
+        After ``max-retries`` attempts the backoff keeps doubling up to 60 s."""
         c = self.cfg
-        delay = c.failure_rate_base_delay
+        delay = c.failure_rate_base_delay or 0.05
+        cap = c.failure_rate_max_delay
         attempt = 0
+        epoch = self.epoch
         if first_delay > 0:
             attempt = 1
             await asyncio.sleep(first_delay)
-            delay = min(delay * 2, c.failure_rate_max_delay)
+            delay = min(delay * 2, cap)
         while True:
+            if self._fenced(epoch):
+                return
+            if attempt and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is None \
+                    and self.job_informer.has_synced():
+                return  # gone from the cache: deleted by someone else (or our earlier attempt landed)
             attempt += 1
             try:
                 await self._delete_job(r.request_id)
@@ -542,16 +656,19 @@ class Supervisor:
             except asyncio.CancelledError:
                 raise
             except Exception as exc:  # noqa: BLE001 - retried with backoff
+                if c.max_retries and attempt == c.max_retries:
+                    self.metrics.inc("job_deletes_slow")
+                    self.log.error(exc, "algorithm submission still not deleted; retrying with a longer backoff",
+                                   requestId=r.request_id, algorithm=r.algorithm, attempts=attempt)
                 if c.max_retries and attempt >= c.max_retries:
-                    self.metrics.inc("job_deletes_failed")
-                    self.log.error(exc, "giving up deleting an algorithm submission", requestId=r.request_id,
-                                   algorithm=r.algorithm)
-                    return
+                    cap = max(cap, 60.0)
                 self.metrics.inc("job_delete_retries")
                 await asyncio.sleep(delay)
-                delay = min(delay * 2, c.failure_rate_max_delay)
+                delay = min(delay * 2, cap)
 
-    async def _write(self, cp, stage, cause, details, now_dt, set_failure):
+    async def _write(self, cp, stage, cause, details, now_dt, set_failure, running=False) -> bool:
+        """Write the decision; False when the conditional write found the row already
+        moved to a finished stage (by another leader, shard owner or component)."""
         compat = self.cfg.compat
         if compat.full_row_upsert:
             clone = cp.deep_copy()
@@ -562,12 +679,24 @@ class Supervisor:
             clone.last_modified = now_dt
             await self.store.upsert_checkpoint(clone)
             return True
-        only_if = (cp.lifecycle_stage,) if compat.conditional_update else None
+        only_if = None
+        if self._conditional(running) and cp.lifecycle_stage is not None:
+            only_if = _cp.unfinished_stages()
+            if cp.lifecycle_stage not in only_if:
+                only_if = only_if + (cp.lifecycle_stage,)
         applied = await self.store.update_status(cp.algorithm, cp.id, stage, cause, details, now_dt,
                                                  only_if_stages=only_if, set_failure=set_failure)
-        if only_if is not None and not applied:
-            raise CasConflict(f"checkpoint {cp.algorithm}/{cp.id} changed concurrently")
-        return True
+        return bool(applied) or only_if is None
+
+    async def _lost_race(self, r: RunStatusAnalysisResult, key) -> Decision:
+        """The conditional write was not applied: re-read; a finished row is final (another
+        writer got there first), anything else is retried through the pipeline backoff."""
+        self.metrics.inc("conditional_write_rejected")
+        cp = await self.store.read_status(r.algorithm, r.request_id)
+        if cp is not None and cp.is_finished():
+            self._remember(key, cp.lifecycle_stage)
+            return Decision(r, "skipped-finished", cp.lifecycle_stage, False)
+        raise CasConflict(f"checkpoint {r.algorithm}/{r.request_id} changed concurrently")
 
     def _remember(self, key, stage):
         self._applied[key] = stage

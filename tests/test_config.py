@@ -83,8 +83,9 @@ def test_validation():
         load_config(env={}, overrides={"failure-rate-base-delay": "2s", "failure-rate-max-delay": "1s"})
     with pytest.raises(ConfigError):
         load_config(env={"NEXUS__WORKERS": "two"})
-    with pytest.raises(ConfigError):
-        load_config(env={}, overrides={"no-such-key": 1})
+    with pytest.raises(ConfigError):  # unknown keys: warned by default, fatal in strict mode
+        load_config(env={"NEXUS_CONFIG_STRICT": "1"}, overrides={"no-such-key": 1})
+    assert load_config(env={}, overrides={"no-such-key": 1}).workers == 2
 
 
 def test_redacted_masks_secrets():
