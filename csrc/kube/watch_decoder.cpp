@@ -692,8 +692,16 @@ class Scan {
   }
 };
 
+// A pod's placement: its worker inside the replica and the replica-shard hash of its
+// run (kept raw so a later change of the owned shard set re-evaluates it).
+struct PodOwner {
+  int worker;
+  uint32_t rhash;
+  bool labeled;
+};
+
 struct Owners {
-  std::unordered_map<std::string, int> pod;
+  std::unordered_map<std::string, PodOwner> pod;
   std::deque<std::pair<double, std::string>> gone;
 };
 
@@ -707,12 +715,27 @@ typedef struct {
   Owners* owners;
   unsigned long long passed;
   unsigned long long dropped;
+  // replica sharding (parallel/sharding.py): runs whose crc32(job name, rseed) % rcount
+  // is not in `owned` belong to another replica and are dropped before decode
+  int rcount;
+  uint32_t rseed;
+  std::vector<uint8_t>* owned;
+  unsigned long long foreign;
 } Router;
 
 enum Role { ROLE_NONE = 0, ROLE_JOB, ROLE_POD, ROLE_EVENT };
 
 int owner_of(const Router* r, std::string_view key) {
   return static_cast<int>(crc32_update(r->seed, key.data(), key.size()) % static_cast<uint32_t>(r->count));
+}
+
+uint32_t replica_hash(const Router* r, std::string_view key) {
+  return crc32_update(r->rseed, key.data(), key.size());
+}
+
+bool replica_owns_hash(const Router* r, uint32_t h) {
+  if (r->rcount <= 1) return true;
+  return (*r->owned)[h % static_cast<uint32_t>(r->rcount)] != 0;
 }
 
 void expire_owners(Router* r) {
@@ -729,6 +752,12 @@ void expire_owners(Router* r) {
 // item.  -1 = every worker must see it (bookmarks, errors, unparsable lines, Events about a
 // Pod not seen yet).  Pod lines also record the pod's owner for Pod-Event routing.
 constexpr int OWNER_ALL = -1;
+constexpr int OWNER_NONE = -2;  // another replica's run: nobody here sees it
+
+int pod_owner_now(const Router* r, const PodOwner& po) {
+  if (po.labeled && !replica_owns_hash(r, po.rhash)) return OWNER_NONE;
+  return po.worker;
+}
 
 int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
   static const char* const P_TYPE[] = {"type"};
@@ -743,29 +772,35 @@ int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
   std::string_view v;
   if (role == ROLE_JOB) {
     if (!sc.find(P_NAME, d, v)) return OWNER_ALL;  // BOOKMARK / ERROR / unparsable
+    if (!replica_owns_hash(r, replica_hash(r, v))) return OWNER_NONE;
     return owner_of(r, v);
   }
   if (role == ROLE_POD) {
     std::string_view name;
     if (!sc.find(P_NAME, d, name)) return OWNER_ALL;
     const char* E_JOB[] = {"object", "metadata", "labels", r->job_label->c_str()};
-    int owner = sc.find(envelope ? E_JOB : E_JOB + 1, d + 1, v) ? owner_of(r, v) : 0;
+    PodOwner po{0, 0, false};
+    if (sc.find(envelope ? E_JOB : E_JOB + 1, d + 1, v)) po = PodOwner{owner_of(r, v), replica_hash(r, v), true};
     std::string key(name);
-    r->owners->pod[key] = owner;
+    r->owners->pod[key] = po;
     std::string_view type;
     if (envelope && sc.find(P_TYPE, 1, type) && type == "DELETED")
       r->owners->gone.emplace_back(mono_s() + r->forget_after, key);
     expire_owners(r);
-    return owner;
+    return pod_owner_now(r, po);
   }
   if (role == ROLE_EVENT) {
     std::string_view kind;
     if (!sc.find(P_IKIND, d, kind)) return OWNER_ALL;
     if (!sc.find(P_INAME, d, v)) return OWNER_ALL;
-    if (kind == "Job") return owner_of(r, v);
+    if (kind == "Job") {
+      if (!replica_owns_hash(r, replica_hash(r, v))) return OWNER_NONE;
+      return owner_of(r, v);
+    }
     if (kind == "Pod") {
       auto it = r->owners->pod.find(std::string(v));
-      return it == r->owners->pod.end() ? OWNER_ALL : it->second;  // unknown pod: everyone parks it
+      // unknown pod: everyone parks it until the pod shows up
+      return it == r->owners->pod.end() ? OWNER_ALL : pod_owner_now(r, it->second);
     }
     return 0;
   }
@@ -775,12 +810,14 @@ int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
 // true = this worker owns (or must see) the watch line
 bool route_line(Router* r, int role, const char* s, size_t n) {
   int owner = route_owner(r, role, s, n, true);
+  if (owner == OWNER_NONE) ++r->foreign;
   return owner == OWNER_ALL || owner == r->index;
 }
 
 void Router_dealloc(Router* self) {
   delete self->job_label;
   delete self->owners;
+  delete self->owned;
   Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
 }
 
@@ -794,6 +831,10 @@ PyObject* Router_new(PyTypeObject* type, PyObject*, PyObject*) {
     self->job_label = new std::string("batch.kubernetes.io/job-name");
     self->owners = new Owners();
     self->passed = self->dropped = 0;
+    self->rcount = 1;
+    self->rseed = 0;
+    self->owned = new std::vector<uint8_t>(1, 1);
+    self->foreign = 0;
   }
   return reinterpret_cast<PyObject*>(self);
 }
@@ -829,29 +870,70 @@ PyObject* Router_pod_owner(Router* self, PyObject* arg) {
   if (!s) return nullptr;
   auto it = self->owners->pod.find(std::string(s, static_cast<size_t>(n)));
   if (it == self->owners->pod.end()) Py_RETURN_NONE;
-  return PyLong_FromLong(it->second);
+  return PyLong_FromLong(pod_owner_now(self, it->second));
 }
 
+// note_pod(name, owner[, deleted[, job]]) — job: the pod's run (job name) for replica sharding
 PyObject* Router_note_pod(Router* self, PyObject* args) {
   const char* name;
   int owner;
   int deleted = 0;
-  if (!PyArg_ParseTuple(args, "si|p", &name, &owner, &deleted)) return nullptr;
-  self->owners->pod[name] = owner;
+  const char* job = nullptr;
+  Py_ssize_t job_n = 0;
+  if (!PyArg_ParseTuple(args, "si|pz#", &name, &owner, &deleted, &job, &job_n)) return nullptr;
+  PodOwner po{owner, 0, false};
+  if (job) po = PodOwner{owner, replica_hash(self, std::string_view(job, static_cast<size_t>(job_n))), true};
+  self->owners->pod[name] = po;
   if (deleted) self->owners->gone.emplace_back(mono_s() + self->forget_after, name);
   expire_owners(self);
   Py_RETURN_NONE;
 }
 
+// set_replica(count, seed, owned) — replica shards: drop runs of shards not in `owned`
+PyObject* Router_set_replica(Router* self, PyObject* args) {
+  int count;
+  unsigned long seed;
+  PyObject* owned;
+  if (!PyArg_ParseTuple(args, "ikO", &count, &seed, &owned)) return nullptr;
+  if (count < 1) {
+    PyErr_SetString(PyExc_ValueError, "count must be >= 1");
+    return nullptr;
+  }
+  std::vector<uint8_t> bits(static_cast<size_t>(count), 0);
+  PyObject* it = PyObject_GetIter(owned);
+  if (!it) return nullptr;
+  PyObject* item;
+  while ((item = PyIter_Next(it)) != nullptr) {
+    long k = PyLong_AsLong(item);
+    Py_DECREF(item);
+    if (k == -1 && PyErr_Occurred()) break;
+    if (k < 0 || k >= count) {
+      PyErr_SetString(PyExc_ValueError, "owned shard out of range [0, count)");
+      break;
+    }
+    bits[static_cast<size_t>(k)] = 1;
+  }
+  Py_DECREF(it);
+  if (PyErr_Occurred()) return nullptr;
+  self->rcount = count;
+  self->rseed = static_cast<uint32_t>(seed);
+  *self->owned = std::move(bits);
+  Py_RETURN_NONE;
+}
+
 PyObject* Router_stats(Router* self, void*) {
-  return Py_BuildValue("{s:K,s:K,s:n}", "passed", self->passed, "dropped", self->dropped, "pods",
-                       static_cast<Py_ssize_t>(self->owners->pod.size()));
+  return Py_BuildValue("{s:K,s:K,s:K,s:n}", "passed", self->passed, "dropped", self->dropped, "foreign",
+                       self->foreign, "pods", static_cast<Py_ssize_t>(self->owners->pod.size()));
 }
 
 PyMethodDef Router_methods[] = {
     {"owner_of", reinterpret_cast<PyCFunction>(Router_owner_of), METH_O, "Owner worker of a job name"},
-    {"pod_owner", reinterpret_cast<PyCFunction>(Router_pod_owner), METH_O, "Owner worker of a pod seen so far (or None)"},
-    {"note_pod", reinterpret_cast<PyCFunction>(Router_note_pod), METH_VARARGS, "Record a pod's owner (name, owner[, deleted])"},
+    {"pod_owner", reinterpret_cast<PyCFunction>(Router_pod_owner), METH_O,
+     "Owner worker of a pod seen so far (None = unknown, -2 = another replica's run)"},
+    {"note_pod", reinterpret_cast<PyCFunction>(Router_note_pod), METH_VARARGS,
+     "Record a pod's owner (name, owner[, deleted[, job name]])"},
+    {"set_replica", reinterpret_cast<PyCFunction>(Router_set_replica), METH_VARARGS,
+     "Replica sharding: (shard count, seed, owned shard indexes)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef Router_getset[] = {{"stats", reinterpret_cast<getter>(Router_stats), nullptr, nullptr, nullptr},
@@ -967,6 +1049,10 @@ PyObject* Splitter_feed(Splitter* self, PyObject* arg) {
       continue;
     }
     int owner = route_owner(r, self->role, line, n, true);
+    if (owner == OWNER_NONE) {
+      ++r->foreign;
+      continue;
+    }
     if (owner == OWNER_ALL) {
       for (auto& o : outs) {
         o.append(line, n);
@@ -1007,6 +1093,10 @@ PyObject* Splitter_split_list(Splitter* self, PyObject* arg) {
   std::vector<std::string> outs(static_cast<size_t>(r->count), std::string("["));
   for (auto& it : items) {
     int owner = route_owner(r, self->role, s + it.first, it.second - it.first, false);
+    if (owner == OWNER_NONE) {
+      ++r->foreign;
+      continue;
+    }
     for (int w = 0; w < r->count; ++w) {
       if (owner != OWNER_ALL && owner != w) continue;
       std::string& o = outs[static_cast<size_t>(w)];

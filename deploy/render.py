@@ -184,6 +184,8 @@ FUNCS = {
     "printf": lambda fmt, *a: re.sub(r"%[vsd]", "{}", fmt).format(*a),
     "eq": lambda a, b: a == b,
     "ne": lambda a, b: a != b,
+    "gt": lambda a, b: a > b,
+    "lt": lambda a, b: a < b,
     "not": lambda a: not _truthy(a),
     "and": lambda *a: all(_truthy(x) for x in a),
     "or": lambda *a: next((x for x in a if _truthy(x)), a[-1] if a else None),

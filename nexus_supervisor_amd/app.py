@@ -38,6 +38,21 @@ def build_store(cfg: SupervisorConfig) -> CheckpointStore:
     return CqlCheckpointStore.from_config(cfg)
 
 
+def _identity(cfg: SupervisorConfig) -> str:
+    le = cfg.leader_election
+    return le.identity or os.environ.get("POD_NAME") or f"{socket.gethostname()}-{os.getpid()}"
+
+
+def make_shard_leases(cfg: SupervisorConfig, kube, on_change, metrics):
+    """``sharding.mode: lease``: the replica's :class:`~.ha.shards.ShardLeaseManager`."""
+    from .ha.shards import ShardLeaseManager
+
+    le, sh = cfg.leader_election, cfg.sharding
+    return ShardLeaseManager(kube, cfg.resource_namespace, le.lease_name, _identity(cfg), sh.shards,
+                             replicas=sh.replicas, lease_duration=le.lease_duration, renew_deadline=le.renew_deadline,
+                             retry_period=le.retry_period, on_change=on_change, metrics=metrics)
+
+
 def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
     from .kube.client import KubeListWatch
 
@@ -69,6 +84,7 @@ class Application:
                                      logger=self.log, metrics=self.metrics)
         self.telemetry = telemetry
         self.elector = None
+        self.shard_leases = None
         self.http = None
         self._stopped = asyncio.Event()
 
@@ -93,20 +109,24 @@ class Application:
 
             self.http = ObsServer(self)
             await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
-        if cfg.leader_election.enabled:
+        if cfg.sharding.mode == "lease":
+            # one Lease per shard replaces the single leader lease (ha/shards.py)
+            self.shard_leases = make_shard_leases(cfg, self.kube, self.supervisor.set_shards, self.metrics)
+        elif cfg.leader_election.enabled:
             from .ha.leader import LeaderElector, LeaseLock
 
             le = cfg.leader_election
-            identity = le.identity or os.environ.get("POD_NAME") or f"{socket.gethostname()}-{os.getpid()}"
             self.supervisor.active = False
             self.elector = LeaderElector(
-                LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, identity),
+                LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, _identity(cfg)),
                 lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
                 on_started_leading=lambda: self.supervisor.set_active(True),
                 on_stopped_leading=lambda: self.supervisor.set_active(False), metrics=self.metrics)
         await self.supervisor.start()
         if self.elector is not None:
             self.elector.start()
+        if self.shard_leases is not None:
+            self.shard_leases.start()
 
     def ready(self) -> bool:
         return self.factory is not None and all(i.has_synced() for i in self.factory.informers.values())
@@ -117,6 +137,8 @@ class Application:
     async def stop(self, drain_timeout: float = 10.0) -> None:
         if self.elector is not None:
             await self.elector.stop(release=True)
+        if self.shard_leases is not None:
+            await self.shard_leases.stop(release=True)
         await self.supervisor.stop(drain=True, timeout=drain_timeout)
         if self.http is not None:
             await self.http.stop()
@@ -175,8 +197,12 @@ class ShardedApplication:
         self.merged_metrics = self.metrics
         self.store = None
         self.elector = None
+        self.shard_leases = None
         self.http = None
         self.hub = None
+        from .parallel.sharding import ShardSet
+
+        self.shards = ShardSet.from_config(cfg)
         self.telemetry = telemetry
         self._owns_telemetry = telemetry is None
         self._gpu_task: Optional[asyncio.Task] = None
@@ -200,7 +226,10 @@ class ShardedApplication:
         self.log.info("Starting Nexus Supervisor", version=__version__, namespace=cfg.resource_namespace,
                       store=cfg.cql_store_type, worker_processes=self.pool.count)
         le = cfg.leader_election
-        await self.pool.start(active=not le.enabled)
+        lease_mode = cfg.sharding.mode == "lease"
+        if lease_mode:
+            self.pool.owned_shards = []  # nothing until a shard lease is won
+        await self.pool.start(active=lease_mode or not le.enabled)
         if self.pool.remote_gpu:
             if self.telemetry is None:
                 from .gpu.telemetry import make_telemetry
@@ -226,20 +255,34 @@ class ShardedApplication:
 
             self.http = ObsServer(self)
             await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
-        if le.enabled:
-            from .ha.leader import LeaderElector, LeaseLock
-
+        if lease_mode or le.enabled:
             if self.kube is None:
                 from .kube.client import KubeClient, KubeConfig
 
                 self.kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
-            identity = le.identity or os.environ.get("POD_NAME") or f"{socket.gethostname()}-{os.getpid()}"
+        if lease_mode:
+            self.shard_leases = make_shard_leases(cfg, self.kube, self.set_shards, self.metrics)
+            self.shard_leases.start()
+        elif le.enabled:
+            from .ha.leader import LeaderElector, LeaseLock
+
             self.elector = LeaderElector(
-                LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, identity),
+                LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, _identity(cfg)),
                 lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
                 on_started_leading=lambda: self.pool.set_active(True),
                 on_stopped_leading=lambda: self.pool.set_active(False), metrics=self.metrics)
             self.elector.start()
+
+    def set_shards(self, owned) -> None:
+        """Shard leases won / lost: the workers fence and replay, the hub re-routes and
+        re-lists so the workers receive the runs of gained shards."""
+        gained, lost = self.shards.update(owned)
+        self.pool.set_shards(owned)
+        if self.hub is not None:
+            self.hub.set_shards(self.shards)
+            if gained or lost:
+                asyncio.ensure_future(self.hub.resync())
+        self.metrics.set("shards_owned", float(len(self.shards.owned or ())))
 
     def ready(self) -> bool:
         return self.pool.all_synced()
@@ -255,6 +298,8 @@ class ShardedApplication:
     async def stop(self, drain_timeout: float = 10.0) -> None:
         if self.elector is not None:
             await self.elector.stop(release=True)
+        if self.shard_leases is not None:
+            await self.shard_leases.stop(release=True)
         if self.hub is not None:
             await self.hub.stop()
         if self._gpu_task is not None:

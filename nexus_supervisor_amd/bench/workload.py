@@ -29,11 +29,11 @@ from __future__ import annotations
 import datetime as _dt
 import random
 import uuid
-import zlib
 from typing import Any, Dict, List, Optional, Tuple
 
 from ..config.schema import LabelConfig
 from ..models.checkpoint import CheckpointedRequest, LifecycleStage
+from ..parallel.sharding import shard_of as _shard_of
 from ..testing.seed import make_event, make_job, make_pod, run_labels
 
 DEFAULT_HIP_OOM = ("hipErrorOutOfMemory: HIP out of memory. Tried to allocate 4.00 GiB. GPU 0 has a total capacity of "
@@ -50,8 +50,8 @@ MIX: Tuple[Tuple[str, float, str], ...] = (
 
 
 def shard_of(algorithm: str, request_id: str, shards: int) -> int:
-    """Same hash as ``Supervisor.owns`` (crc32 of ``algorithm\\0id``)."""
-    return zlib.crc32(f"{algorithm}\x00{request_id}".encode()) % shards if shards > 1 else 0
+    """Replica shard of a run, as ``Supervisor.owns`` computes it (``parallel/sharding.py``)."""
+    return _shard_of(request_id, shards)
 
 
 class Workload:

@@ -178,10 +178,18 @@ class LeaderElectionConfig:
 
 @dataclass
 class ShardingConfig:
-    """Consistent-hash sharding of runs across active replicas (0/1 shard = off)."""
+    """Hash sharding of runs across replicas (``parallel/sharding.py``; 1 shard = off).
+
+    ``static``: this replica owns ``shard-index`` (StatefulSet ordinal).  ``lease``: one
+    Lease per shard (``<leader-election.lease-name>-shard-<k>``, leader-election timings);
+    each replica holds up to its fair share ``ceil(shards / replicas)`` and takes over any
+    shard left unheld for a full lease duration, so shards fail over individually."""
 
     shards: int = field(default=1, metadata=_k("shards"))
     shard_index: int = field(default=0, metadata=_k("shard-index"))
+    mode: str = field(default="static", metadata=_k("mode"))  # static | lease
+    # expected replica count (Helm replicaCount) for the lease-mode fair share; 0 = greedy
+    replicas: int = field(default=0, metadata=_k("replicas"))
 
 
 @dataclass
@@ -282,6 +290,10 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("rules.trace-format must be raw|json|auto")
     if cfg.sharding.shards < 1 or not 0 <= cfg.sharding.shard_index < cfg.sharding.shards:
         raise ConfigError("sharding.shard-index must be in [0, shards)")
+    if cfg.sharding.mode not in ("static", "lease"):
+        raise ConfigError("sharding.mode must be static|lease")
+    if cfg.sharding.replicas < 0:
+        raise ConfigError("sharding.replicas must be >= 0 (0 = greedy)")
     rt = cfg.runtime
     if rt.worker_processes == 0:
         from ..utils.cpus import auto_worker_processes
@@ -291,7 +303,7 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("runtime.worker-processes must be >= 0 (0 = auto) and runtime.worker-index in [0, worker-processes)")
     if not 0 < cfg.gpu.hbm_oom_fraction <= 1:
         raise ConfigError("gpu.hbm-oom-fraction must be in (0, 1]")
-    if cfg.leader_election.enabled:
+    if cfg.leader_election.enabled or cfg.sharding.mode == "lease":
         le = cfg.leader_election
         if not le.lease_duration > le.renew_deadline > le.retry_period > 0:
             raise ConfigError("leader-election: lease-duration > renew-deadline > retry-period > 0 required")

@@ -162,6 +162,24 @@ class LeaderElector:
         self._observe({"holderIdentity": self.identity}, now)
         return True
 
+    async def observe(self) -> bool:
+        """Read the lease without competing for it (caller does not hold it); True when
+        nobody holds a live lease (never created, released, or not renewed for a full lease
+        duration as observed locally — the same expiry rule :meth:`try_acquire_or_renew`
+        applies)."""
+        lease = await self.lock.get()
+        now = self.clock()
+        if lease is None:
+            return True
+        spec = lease.get("spec") or {}
+        record = (spec.get("holderIdentity"), spec.get("renewTime"), spec.get("leaseTransitions"))
+        if record != self._observed_record:
+            self._observe(spec, now, record)
+        holder = spec.get("holderIdentity") or ""
+        duration = float(spec.get("leaseDurationSeconds") or self.lease_duration)
+        # our own identity on a lease we do not hold any more (renewal timed out): ours to retake
+        return not holder or holder == self.identity or now >= self._observed_at + duration
+
     def _observe(self, spec, now, record=None):
         self._observed_record = record
         self._observed_at = now

@@ -113,6 +113,14 @@ class SharedInformer:
                 self._resync_task = asyncio.create_task(self._resync_loop(), name=f"resync-{self.kind}")
         return self._task
 
+    def relist(self) -> None:
+        """Restart list+watch now (a changed ingest filter: objects it used to drop must be
+        listed again; the re-list diff dispatches them as adds)."""
+        if self._task is None:
+            return
+        self._task.cancel()
+        self._task = asyncio.create_task(self._run(), name=f"informer-{self.kind}")
+
     async def stop(self) -> None:
         for t in (self._task, self._resync_task):
             if t is not None:

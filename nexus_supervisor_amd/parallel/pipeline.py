@@ -270,12 +270,16 @@ class PipelineStage:
         await asyncio.gather(*self._tasks, return_exceptions=True)
         self._tasks = []
 
-    def clear(self) -> int:
-        """Drop every queued item and every backoff retry (fencing on lost leadership);
-        items a worker is processing right now finish (their processor checks the fence
-        itself).  Returns the number of items dropped."""
+    def clear(self, predicate: Optional[Callable[[Hashable], bool]] = None) -> int:
+        """Drop every queued item and every backoff retry (fencing on lost leadership),
+        or only those of keys ``predicate`` accepts (a lost replica shard); items a worker
+        is processing right now finish (their processor checks the fence itself).
+        Returns the number of items dropped."""
         dropped = 0
+        gone = set()
         for key, q in list(self._pending.items()):
+            if predicate is not None and not predicate(key):
+                continue
             if key in self._running:
                 while len(q) > 1:
                     q.pop()
@@ -283,12 +287,17 @@ class PipelineStage:
                 continue
             dropped += len(q)
             del self._pending[key]
+            gone.add(key)
             h = self._timers.pop(key, None)
             if h is not None:
                 h.cancel()
             self._active.discard(key)
             self.backoff.forget(key)
-        self._ready.clear()
+        if predicate is None:
+            self._ready.clear()
+        elif gone:
+            # a dropped key re-received later is queued afresh: no stale duplicate may stay
+            self._ready = collections.deque(k for k in self._ready if k not in gone)
         self.stats.dropped_closed += dropped
         self._check_idle()
         return dropped

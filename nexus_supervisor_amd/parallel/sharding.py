@@ -1,0 +1,77 @@
+"""Replica sharding: which supervisor replica owns a run.
+
+The reference scales by adding replicas that all process every event
+(``/root/reference/.helm/values.yaml:124-125`` "Increase to support higher (1000+)
+pod numbers"): N replicas do N times the work and race on every row.  This build
+partitions runs over ``sharding.shards`` shards instead; a replica owns a *set* of
+shards, fixed (``sharding.mode: static`` → ``{shard-index}``) or held through one
+Lease per shard (``mode: lease``, :mod:`..ha.shards`), so a dead replica's shards
+fail over one by one to the survivors.
+
+The shard of a run is a function of the Job name (= request id) alone, the one key
+every Job, Pod (``batch.kubernetes.io/job-name`` label) and Job Event carries: the
+native watch router (``csrc/kube/watch_decoder.cpp`` ``ShardRouter.set_replica``)
+drops another replica's lines from the raw bytes, before anything is decoded, so a
+replica watching the whole namespace pays only a key scan for the runs it does not
+own.  ``SHARD_SEED`` decorrelates replica shards from the worker placement inside a
+replica (:data:`.workers._SEED`).
+"""
+from __future__ import annotations
+
+import zlib
+from typing import FrozenSet, Iterable, Optional, Tuple
+
+SHARD_SEED = 0x5BD1E995
+
+
+def shard_of(request_id: str, shards: int) -> int:
+    """Replica shard of a run (its Job name); must match the native router."""
+    if shards <= 1:
+        return 0
+    return zlib.crc32(request_id.encode(), SHARD_SEED) % shards
+
+
+class ShardSet:
+    """The shards this replica currently owns, with a fencing epoch per shard.
+
+    ``owned`` None means "every shard" (sharding off).  An epoch is bumped whenever the
+    shard is lost, so a decision dequeued before the loss never writes after it."""
+
+    def __init__(self, shards: int = 1, owned: Optional[Iterable[int]] = None):
+        self.shards = max(1, int(shards))
+        self.owned: Optional[FrozenSet[int]] = None if owned is None or self.shards <= 1 else frozenset(owned)
+        self.epochs = [0] * self.shards
+
+    @classmethod
+    def from_config(cls, cfg) -> "ShardSet":
+        s = cfg.sharding
+        if s.shards <= 1:
+            return cls(1)
+        if s.mode == "lease":
+            return cls(s.shards, ())  # nothing until a shard lease is won
+        return cls(s.shards, (s.shard_index,))
+
+    @property
+    def enabled(self) -> bool:
+        return self.owned is not None
+
+    def of(self, request_id: str) -> int:
+        return shard_of(request_id, self.shards)
+
+    def owns(self, request_id: str) -> bool:
+        return self.owned is None or shard_of(request_id, self.shards) in self.owned
+
+    def token(self, request_id: str) -> int:
+        return self.epochs[shard_of(request_id, self.shards)] if self.owned is not None else 0
+
+    def update(self, owned: Iterable[int]) -> Tuple[FrozenSet[int], FrozenSet[int]]:
+        """Replace the owned set; returns (gained, lost) and fences the lost shards."""
+        new = frozenset(int(k) for k in owned)
+        if any(not 0 <= k < self.shards for k in new):
+            raise ValueError(f"shard index out of range [0, {self.shards})")
+        old = self.owned if self.owned is not None else frozenset(range(self.shards))
+        self.owned = new
+        lost = old - new
+        for k in lost:
+            self.epochs[k] += 1
+        return new - old, lost

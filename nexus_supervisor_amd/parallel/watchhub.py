@@ -72,11 +72,25 @@ class WatchHub:
         self.drain = drain
         self.metrics = metrics
         self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label)
+        from .sharding import ShardSet
+
+        self.set_shards(ShardSet.from_config(cfg))
         self.tasks: Dict[str, asyncio.Task] = {}
         self.relists = 0
         self.bytes_routed = 0
         self.selector = (f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
                          if cfg.informer_label_selector else "")
+
+    def set_shards(self, shards) -> None:
+        """Replica shard set: lines of runs this replica does not own are dropped in the
+        splitter (before any decode, in any worker).  A change takes effect for lines
+        routed from now on; :meth:`resync` re-lists so gained runs reach the workers."""
+        from .sharding import SHARD_SEED
+
+        if shards.enabled:
+            self.router.set_replica(shards.shards, SHARD_SEED, sorted(shards.owned))
+        else:
+            self.router.set_replica(1, SHARD_SEED, [0])
 
     def start(self) -> None:
         for i, kind in enumerate(KINDS):

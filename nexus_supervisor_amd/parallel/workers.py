@@ -25,6 +25,7 @@ threads:
 
 Control channel: one ``socketpair`` per worker, newline-delimited JSON.
 Parent → worker: ``{"op": "active", "v": bool}``, ``{"op": "metrics", "seq": n}``,
+``{"op": "shards", "owned": [k, ...]}`` (replica shard leases won / lost),
 ``{"op": "stop", "drain": seconds}``.  Worker → parent: ``{"op": "synced"}``,
 ``{"op": "dec", "d": [[request_id, algorithm, outcome, ack_mono, stage], ...]}``,
 ``{"op": "metrics", "seq": n, "s": state}``, ``{"op": "exit"}``.  A worker whose
@@ -51,7 +52,8 @@ from ..models.decisions import Decision, RunStatusAnalysisResult
 from ..obs.histogram import LatencyHistogram
 from ..obs.metrics import Metrics
 
-_SEED = 0x2545F491  # decorrelates worker placement from replica sharding (crc32 of algorithm\0id)
+_SEED = 0x2545F491  # decorrelates worker placement from replica sharding (sharding.SHARD_SEED)
+_FOREIGN = -2  # pod owner: another replica's run (native router OWNER_NONE)
 _LINE_LIMIT = 64 << 20
 
 
@@ -63,16 +65,20 @@ def worker_of(request_id: str, count: int) -> int:
 
 
 class WorkerShard:
-    """Ingest filter of worker ``index`` of ``count`` (installed on the Event/Pod/Job informers)."""
+    """Ingest filter of worker ``index`` of ``count`` (installed on the Event/Pod/Job informers),
+    and of the replica's shard set (``shards``: runs of other replicas are dropped)."""
 
     def __init__(self, index: int, count: int, job_name_label: str, forget_after: float = 120.0,
-                 clock: Callable[[], float] = time.monotonic):
+                 clock: Callable[[], float] = time.monotonic, shards=None):
+        from .sharding import ShardSet
+
         self.index = index
         self.count = count
         self.job_name_label = job_name_label
         self.forget_after = forget_after
         self.clock = clock
-        self.pod_owner: Dict[str, int] = {}
+        self.shards = shards if shards is not None else ShardSet(1)
+        self.pod_owner: Dict[str, Tuple[int, str]] = {}  # pod name → (worker, run)
         self._gone: Deque[Tuple[float, str]] = collections.deque()
         try:  # native pre-decode filter (csrc/kube/watch_decoder.cpp ShardRouter)
             from .._kube_native import ShardRouter
@@ -80,27 +86,38 @@ class WorkerShard:
             self.native = ShardRouter(index, count, _SEED, job_name_label, forget_after)
         except ImportError:  # pragma: no cover - pure-Python fallback filters after decode
             self.native = None
+        self.sync_replica()
+
+    def sync_replica(self) -> None:
+        """Push the replica's current shard set into the native router."""
+        if self.native is not None and self.shards.enabled:
+            from .sharding import SHARD_SEED
+
+            self.native.set_replica(self.shards.shards, SHARD_SEED, sorted(self.shards.owned))
 
     def of(self, request_id: str) -> int:
         return zlib.crc32(request_id.encode(), _SEED) % self.count
 
+    def _owner(self, request_id: str) -> int:
+        return self.of(request_id) if self.shards.owns(request_id) else _FOREIGN
+
     def accept_job(self, obj: Dict[str, Any], etype: str) -> bool:
-        return self.of(kube.name_of(obj)) == self.index
+        return self._owner(kube.name_of(obj)) == self.index
 
     def accept_pod(self, obj: Dict[str, Any], etype: str) -> bool:
         meta = obj.get("metadata") or {}
         rid = (meta.get("labels") or {}).get(self.job_name_label)
-        owner = self.of(rid) if rid else 0
+        worker = self.of(rid) if rid else 0
         name = meta.get("name", "")
         if etype == "DELETED":
             # events about a deleted pod may still be in flight on the event watch
             self._gone.append((self.clock() + self.forget_after, name))
-        self.pod_owner[name] = owner
+        self.pod_owner[name] = (worker, rid or "")
         if self.native is not None:
-            self.native.note_pod(name, owner, etype == "DELETED")
+            self.native.note_pod(name, worker, etype == "DELETED", rid)
         if self._gone:
             self._expire()
-        return owner == self.index
+        return (worker if not rid or self.shards.owns(rid) else _FOREIGN) == self.index
 
     def _expire(self) -> None:
         now = self.clock()
@@ -113,17 +130,21 @@ class WorkerShard:
         inv = obj.get("involvedObject") or {}
         kind = inv.get("kind")
         if kind == "Job":
-            return self.of(inv.get("name", "")) == self.index
+            return self._owner(inv.get("name", "")) == self.index
         if kind == "Pod":
             owner = self.owner_of_pod(inv.get("name", ""))
             return owner is None or owner == self.index  # unknown pod: park everywhere until it shows up
         return self.index == 0
 
     def owner_of_pod(self, name: str) -> Optional[int]:
-        owner = self.pod_owner.get(name)
-        if owner is None and self.native is not None:
-            owner = self.native.pod_owner(name)  # pods dropped before decode are only known natively
-        return owner
+        """Worker owning a pod seen so far; None = unknown, -2 = another replica's run."""
+        seen = self.pod_owner.get(name)
+        if seen is not None:
+            worker, rid = seen
+            return worker if not rid or self.shards.owns(rid) else _FOREIGN
+        if self.native is not None:
+            return self.native.pod_owner(name)  # pods dropped before decode are only known natively
+        return None
 
     def install(self, sup, routed_upstream: bool = False) -> None:
         """Filter this worker's informers.  ``routed_upstream`` (watch hub): the parent
@@ -269,6 +290,7 @@ class WorkerPool:
         # into every worker (RemoteTelemetry) instead of K monitors per replica
         self.remote_gpu = bool(cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry)
         self.on_restart: Optional[Callable[[int], Any]] = None  # async callback (watch hub resync)
+        self.owned_shards: Optional[List[int]] = None  # lease mode: shards held right now
         self._stopping = False
         self._watchdog: Optional[asyncio.Task] = None
 
@@ -361,6 +383,8 @@ class WorkerPool:
         w.synced.clear()
         w.exited.clear()
         w.reader = asyncio.create_task(self._read(w), name=f"worker-{w.index}-ctl")
+        if self.owned_shards is not None:  # lease mode: the shards this replica holds right now
+            w.chan.send({"op": "shards", "owned": self.owned_shards})
 
     async def _read(self, w: _Worker) -> None:
         while True:
@@ -427,6 +451,13 @@ class WorkerPool:
         for w in self.workers:
             if w.chan is not None:
                 w.chan.send({"op": "active", "v": active})
+
+    def set_shards(self, owned) -> None:
+        """Relay the replica's owned shard set; a worker restarted later gets it at spawn."""
+        self.owned_shards = sorted(owned)
+        for w in self.workers:
+            if w.chan is not None:
+                w.chan.send({"op": "shards", "owned": self.owned_shards})
 
     def all_synced(self) -> bool:
         return all(w.synced.is_set() for w in self.workers)
@@ -599,6 +630,8 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
                 sup.set_active(bool(msg.get("v")))
             elif op == "metrics":
                 send_metrics(int(msg.get("seq", 0)))
+            elif op == "shards":
+                sup.set_shards(msg.get("owned") or ())
             elif op == "gpu" and remote_tel is not None:
                 remote_tel.update(msg)
             elif op == "pprof":

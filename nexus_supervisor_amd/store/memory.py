@@ -18,6 +18,7 @@ class MemoryStore(CheckpointStore):
         self.writes = 0
         self.fail_next_reads = 0
         self.fail_next_writes = 0
+        self.write_log: list = []  # (key, stage) of every applied write (tests: exactly-once checks)
 
     async def _io(self):
         if self.latency:
@@ -39,6 +40,7 @@ class MemoryStore(CheckpointStore):
             self.fail_next_writes -= 1
             raise StoreError("injected write failure")
         self.rows[checkpoint.key] = checkpoint.deep_copy()
+        self.write_log.append((checkpoint.key, checkpoint.lifecycle_stage))
 
     async def update_status(self, algorithm, request_id, lifecycle_stage, failure_cause, failure_details,
                             last_modified: _dt.datetime, only_if_stages=None, set_failure=True) -> bool:
@@ -61,6 +63,7 @@ class MemoryStore(CheckpointStore):
             row.algorithm_failure_details = failure_details
         row.last_modified = last_modified
         self.rows[key] = row
+        self.write_log.append((key, lifecycle_stage))
         return True
 
     def get(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:

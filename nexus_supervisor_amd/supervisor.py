@@ -25,7 +25,6 @@ from __future__ import annotations
 import asyncio
 import datetime as _dt
 import time
-import zlib
 from collections import OrderedDict
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -41,6 +40,7 @@ from .models.decisions import Decision, DecisionAction as A, RunStatusAnalysisRe
 from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
+from .parallel.sharding import ShardSet
 from .store.base import CheckpointStore
 from .utils.gctune import GcTuner
 
@@ -131,10 +131,11 @@ class Supervisor:
         self._applied_cap = 200_000
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
-        self._deletes: set = set()  # in-flight asynchronous Job DELETEs
+        self._deletes: Dict[Any, str] = {}  # in-flight asynchronous Job DELETEs → request id
         self._sweeper: Optional[asyncio.Task] = None
         self.decision_hooks: List[Callable[[Decision], None]] = []
-        self.active = not cfg.leader_election.enabled  # leader gating flips this
+        # leader gating flips this; with shard leases ownership is per shard (self.shards)
+        self.active = not cfg.leader_election.enabled or cfg.sharding.mode == "lease"
         # fencing epoch: bumped on every loss of leadership; a decision dequeued under an
         # older epoch never writes or deletes (see set_active)
         self.epoch = 0
@@ -142,15 +143,17 @@ class Supervisor:
         self.label_mismatch = False
         self._unfinished_cache: Optional[Tuple[str, ...]] = None
         self.gc_tuner = GcTuner.from_config(cfg.runtime, self.metrics)
+        # replica shards owned right now (sharding.*), with a fencing epoch per shard
+        self.shards = ShardSet.from_config(cfg)
         self.worker_shard = None
-        if cfg.runtime.worker_processes > 1:
+        self.hub_fed = all(type(i.lw).__name__ == "HubListWatch"
+                           for i in (self.event_informer, self.pod_informer, self.job_informer))
+        if cfg.runtime.worker_processes > 1 or self.shards.enabled:
             from .parallel.workers import WorkerShard
 
             self.worker_shard = WorkerShard(cfg.runtime.worker_index, cfg.runtime.worker_processes,
-                                            cfg.labels.job_name_label)
-            hub_fed = all(type(i.lw).__name__ == "HubListWatch"
-                          for i in (self.event_informer, self.pod_informer, self.job_informer))
-            self.worker_shard.install(self, routed_upstream=hub_fed)
+                                            cfg.labels.job_name_label, shards=self.shards)
+            self.worker_shard.install(self, routed_upstream=self.hub_fed)
         m = self.metrics
         m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
@@ -249,27 +252,112 @@ class Supervisor:
         self.log.info("leadership lost: fenced in-flight work", dropped=dropped, epoch=self.epoch)
         return dropped
 
-    def _fenced(self, epoch: int) -> bool:
-        return not self.active or epoch != self.epoch
+    def _token(self, request_id: str) -> Tuple[int, int]:
+        """Fencing token of a run: the replica epoch and its shard's epoch."""
+        return self.epoch, self.shards.token(request_id)
 
-    def replay(self) -> None:
-        for ev in self.event_informer.indexer.values():
-            self._on_event_add(ev)
-        for job in self.job_informer.indexer.values():
-            self._on_job_add(job)
-        for pod in self.pod_informer.indexer.values():
-            self._on_pod_add(pod)
+    def _fenced(self, token: Tuple[int, int], request_id: str) -> bool:
+        return not self.active or token != self._token(request_id) or not self.shards.owns(request_id)
+
+    def set_shards(self, owned) -> Tuple[frozenset, frozenset]:
+        """New owned replica-shard set (lease mode: a shard lease won or lost).  Lost shards
+        are fenced like a lost leadership, but only for their runs: their queued and
+        backing-off decisions are dropped, their background DELETEs cancelled and their
+        objects purged from the caches (so a later regain re-adds them).  Gained shards
+        are replayed from whatever the caches hold, and informers that filter at ingest
+        re-list to pick up the runs they used to drop (the watch hub re-lists upstream)."""
+        gained, lost = self.shards.update(owned)
+        if self.worker_shard is not None:
+            self.worker_shard.sync_replica()
+        if lost:
+            self.fence_shards(lost)
+        if gained:
+            self.metrics.inc("shards_gained", len(gained))
+            self.replay(lambda rid: self.shards.of(rid) in gained)
+            if self.worker_shard is not None and not self.hub_fed:
+                for inf in (self.event_informer, self.pod_informer, self.job_informer):
+                    inf.relist()
+        self.metrics.set("shards_owned", float(len(self.shards.owned or ())))
+        if gained or lost:
+            self.log.info("replica shards changed", owned=sorted(self.shards.owned or ()), gained=sorted(gained),
+                          lost=sorted(lost))
+        return gained, lost
+
+    def fence_shards(self, lost) -> int:
+        of = self.shards.of
+        dropped = self.pipeline.clear(lambda key: of(key[1]) in lost) if self.pipeline is not None else 0
+        for t, rid in list(self._deletes.items()):
+            if of(rid) in lost:
+                t.cancel()
+                self._deletes.pop(t, None)
+        for key in [k for k in self._applied if of(k[1]) in lost]:
+            del self._applied[key]
+        self._purge(lambda rid: of(rid) in lost)
+        self.metrics.inc("fenced_decisions_dropped", dropped)
+        self.metrics.inc("shards_lost", len(lost))
+        return dropped
+
+    def _purge(self, lost_run: Callable[[str], bool]) -> None:
+        """Forget cached objects of runs this replica no longer owns (no handlers fire)."""
+        label = self.cfg.labels.job_name_label
+        ns = self.namespace
+        lost_pods = set()
+        for pod in list(self.pod_informer.indexer.values()):
+            rid = ((pod.get("metadata") or {}).get("labels") or {}).get(label)
+            if rid and lost_run(rid):
+                lost_pods.add(kube.name_of(pod))
+                self.pod_informer.indexer.delete(pod)
+        for job in list(self.job_informer.indexer.values()):
+            if lost_run(kube.name_of(job)):
+                self.job_informer.indexer.delete(job)
+        for ev in list(self.event_informer.indexer.values()):
+            inv = ev.get("involvedObject") or {}
+            if (inv.get("kind") == "Job" and lost_run(inv.get("name", ""))) or \
+                    (inv.get("kind") == "Pod" and inv.get("name") in lost_pods):
+                self.event_informer.indexer.delete(ev)
+        for key in [k for k in self._parked if k[0] == "Job" and lost_run(k[1])]:
+            del self._parked[key]
+        for key in [k for k in self._gpu_wait if self._gpu_wait_run(k, ns, lost_run)]:
+            del self._gpu_wait[key]
+
+    def _gpu_wait_run(self, key, ns, lost_run) -> bool:
+        pod = self.pod_informer.indexer.get(key)
+        rid = ((pod or {}).get("metadata") or {}).get("labels", {}).get(self.cfg.labels.job_name_label) if pod else None
+        return pod is None or (rid is not None and lost_run(rid))
+
+    def replay(self, run_filter: Optional[Callable[[str], bool]] = None) -> None:
+        """Re-decide every cached object (``run_filter``: only runs it accepts)."""
+        if run_filter is None:
+            for ev in list(self.event_informer.indexer.values()):
+                self._on_event_add(ev)
+            for job in list(self.job_informer.indexer.values()):
+                self._on_job_add(job)
+            for pod in list(self.pod_informer.indexer.values()):
+                self._on_pod_add(pod)
+            return
+        label = self.cfg.labels.job_name_label
+        for ev in list(self.event_informer.indexer.values()):
+            inv = ev.get("involvedObject") or {}
+            name = inv.get("name", "")
+            if inv.get("kind") == "Pod":
+                pod = self.pod_informer.indexer.get_by_name(self.namespace, name)
+                name = ((pod or {}).get("metadata") or {}).get("labels", {}).get(label, "") if pod else ""
+            if name and run_filter(name):
+                self._on_event_add(ev)
+        for job in list(self.job_informer.indexer.values()):
+            if run_filter(kube.name_of(job)):
+                self._on_job_add(job)
+        for pod in list(self.pod_informer.indexer.values()):
+            rid = ((pod.get("metadata") or {}).get("labels") or {}).get(label)
+            if rid and run_filter(rid):
+                self._on_pod_add(pod)
 
     # ------------------------------------------------------------------ ownership
     def owns(self, key: Tuple[str, str]) -> bool:
         ws = self.worker_shard
-        if ws is not None and ws.of(key[1]) != ws.index:
+        if ws is not None and ws.count > 1 and ws.of(key[1]) != ws.index:
             return False
-        s = self.cfg.sharding
-        if s.shards <= 1:
-            return True
-        h = zlib.crc32(f"{key[0]}\x00{key[1]}".encode())
-        return h % s.shards == s.shard_index
+        return self.shards.owns(key[1])
 
     # ------------------------------------------------------------------ handlers
     def _on_event_add(self, ev: Dict[str, Any]) -> None:
@@ -392,8 +480,14 @@ class Supervisor:
             for key in list(self._parked):
                 lst = [p for p in self._parked[key] if p[0] > now]
                 dropped = len(self._parked[key]) - len(lst)
-                if dropped and ws is not None and key[0] == "Pod" and ws.owner_of_pod(key[1]) not in (None, ws.index):
-                    dropped = 0  # another shard worker owns that pod: not stale, just not ours
+                if dropped and ws is not None and key[0] == "Pod":
+                    owner = ws.owner_of_pod(key[1])
+                    if owner not in (None, ws.index):
+                        dropped = 0  # another shard worker (or replica) owns that pod: not stale, just not ours
+                    elif owner is None and self.hub_fed and ws.index != 0:
+                        # the hub broadcast an event about a pod it had not routed yet to every
+                        # worker: only worker 0 accounts for it (ADVICE r1 workers.py:131)
+                        dropped = 0
                 if dropped:
                     if selected:
                         # label-selected caches hold only Nexus runs: an event whose object never
@@ -464,7 +558,8 @@ class Supervisor:
             return True
         if mode == "never":
             return False
-        return running or self.cfg.leader_election.enabled
+        # HA: a single lease or shard leases (a deposed owner may still hold a decision)
+        return running or self.cfg.leader_election.enabled or self.cfg.sharding.mode == "lease"
 
     async def _delete_job(self, name: str) -> bool:
         try:
@@ -485,10 +580,11 @@ class Supervisor:
         if stamps is not None and "dequeue" not in stamps:
             stamps["dequeue"] = wall()
         failing = r.action in A.FAILING
-        epoch = self.epoch
+        rid = r.request_id
+        epoch = self._token(rid)
         if r.action not in STAGE_FOR_ACTION:
             raise ValueError(f"unknown analysis result action: {r.action}")
-        if self._fenced(epoch):
+        if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)
         try:
@@ -522,7 +618,7 @@ class Supervisor:
             # a crash between write and delete (or a failed delete) — finish the delete
             if r.pending_delete or (failing and cp.lifecycle_stage in _FAILED_STAGES()
                                     and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is not None):
-                if self._fenced(epoch):
+                if self._fenced(epoch, rid):
                     return Decision(r, "fenced", cp.lifecycle_stage, False)
                 deleted = await self._delete_job(r.request_id)
                 r.pending_delete = False
@@ -535,7 +631,7 @@ class Supervisor:
             if cp.lifecycle_stage == LifecycleStage.RUNNING and not compat.full_row_upsert:
                 self._remember(key, stage)
                 return Decision(r, "skipped-already-running", stage, False)
-            if self._fenced(epoch):
+            if self._fenced(epoch, rid):
                 self.metrics.inc("decisions_fenced")
                 return Decision(r, "fenced", None, False)
             if not await self._write(cp, stage, None, None, now_dt, set_failure=False, running=True):
@@ -553,7 +649,7 @@ class Supervisor:
         # lose the decision for good — the Job's pods are garbage-collected, so the replay
         # after failover has nothing to re-decide from.  Written-then-crashed instead leaves
         # a failed row whose Job still exists, which the replay finishes (finished path).
-        if self._fenced(epoch):
+        if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)
         try:
@@ -568,7 +664,7 @@ class Supervisor:
         self._observe(r)
         self._remember(key, stage)
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
-        if self._fenced(epoch):  # durable, but the Job now belongs to the new leader's replay
+        if self._fenced(epoch, rid):  # durable, but the Job now belongs to the new leader's replay
             return Decision(r, "applied", stage, False)
         if self.cfg.async_job_delete:
             # the decision is durable; the Job DELETE must not hold a worker (and with it
@@ -591,15 +687,18 @@ class Supervisor:
             # the retrying coroutine below
             fut = nowait(self.namespace, r.request_id, "Background")
             if fut is not None:
-                self._deletes.add(fut)
+                self._deletes[fut] = r.request_id
                 fut.add_done_callback(lambda f, r=r: self._delete_settled(r, f))
                 return
         t = asyncio.ensure_future(self._delete_with_retry(r))
-        self._deletes.add(t)
-        t.add_done_callback(self._deletes.discard)
+        self._deletes[t] = r.request_id
+        t.add_done_callback(self._delete_done)
+
+    def _delete_done(self, t) -> None:
+        self._deletes.pop(t, None)
 
     def _delete_settled(self, r: RunStatusAnalysisResult, fut) -> None:
-        self._deletes.discard(fut)
+        self._deletes.pop(fut, None)
         if fut.cancelled():
             return
         exc = fut.exception()
@@ -618,12 +717,12 @@ class Supervisor:
             if ack is not None:
                 self.metrics.observe_seconds("stage_delete", self.wall() - ack)
             return
-        if not self.active:
-            return  # fenced: the new leader's replay owns this Job
+        if not self.active or not self.shards.owns(r.request_id):
+            return  # fenced: the new leader's (shard owner's) replay owns this Job
         self.metrics.inc("job_delete_retries")
         t = asyncio.ensure_future(self._delete_with_retry(r, first_delay=self.cfg.failure_rate_base_delay))
-        self._deletes.add(t)
-        t.add_done_callback(self._deletes.discard)
+        self._deletes[t] = r.request_id
+        t.add_done_callback(self._delete_done)
 
     async def _delete_with_retry(self, r: RunStatusAnalysisResult, first_delay: float = 0.0) -> None:
         """Background Job DELETE after a durable failure write.  The key is already marked
@@ -635,13 +734,14 @@ class Supervisor:
         delay = c.failure_rate_base_delay or 0.05
         cap = c.failure_rate_max_delay
         attempt = 0
-        epoch = self.epoch
+        rid = r.request_id
+        epoch = self._token(rid)
         if first_delay > 0:
             attempt = 1
             await asyncio.sleep(first_delay)
             delay = min(delay * 2, cap)
         while True:
-            if self._fenced(epoch):
+            if self._fenced(epoch, rid):
                 return
             if attempt and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is None \
                     and self.job_informer.has_synced():

@@ -152,3 +152,29 @@ def test_kindload_manifests_seed_and_wait(arun):
         assert res["apply_to_checkpoint_p50_ms"] > 0
     finally:
         srv.stop()
+
+
+def test_reference_rbac_keys_are_honoured():
+    """VERDICT r1 missing #6: the reference chart's rbac.clusterRole.supervisor.* and
+    rbac.clusterRoleBindings.* (/root/reference/.helm/values.yaml:34-53) are not ignored."""
+    vals = {"rbac": {"clusterRole": {"supervisor": {"create": True, "additionalLabels": {"team": "ml"},
+                                                    "additionalAnnotations": {"note": "x"}}},
+                     "clusterRoleBindings": {"create": True}}}
+    k = _by_kind(render_docs(CHART, values=vals))
+    role = k["ClusterRole"][0]
+    assert role["metadata"]["labels"]["team"] == "ml" and role["metadata"]["annotations"]["note"] == "x"
+    assert k["ClusterRoleBinding"][0]["roleRef"]["kind"] == "ClusterRole"
+    vals["rbac"]["clusterRoleBindings"]["create"] = False
+    k = _by_kind(render_docs(CHART, values=vals))
+    assert "ClusterRole" in k and "ClusterRoleBinding" not in k
+    vals["rbac"]["clusterRole"]["supervisor"]["create"] = False
+    k = _by_kind(render_docs(CHART, values=vals))
+    assert "ClusterRole" not in k and all(r["metadata"]["name"].endswith("gpu-agent") for r in k.get("Role", []))
+
+
+def test_sharding_values_render_lease_mode():
+    docs = render_docs(CHART, values={"supervisor": {"replicas": 3, "highAvailability": {"sharding": {"shards": 6}}}})
+    env = _env(_by_kind(docs)["Deployment"][0]["spec"]["template"]["spec"]["containers"][0])
+    cfg = load_config(path=None, env={k: v for k, v in env.items() if k.startswith("NEXUS__") and v is not None})
+    assert cfg.sharding.shards == 6 and cfg.sharding.mode == "lease" and cfg.sharding.replicas == 3
+    assert "NEXUS__SHARDING__SHARDS" not in _env(_by_kind(render_docs(CHART))["Deployment"][0]["spec"]["template"]["spec"]["containers"][0])

@@ -1,0 +1,361 @@
+"""Replica sharding (``parallel/sharding.py``) and per-shard leases (``ha/shards.py``).
+
+VERDICT r1 next-round #7: horizontal scale that can actually be deployed with HA —
+one Lease per shard, a dead owner's shard moves within the lease duration, and no
+run is lost or written twice.  The reference scales by running more replicas that
+all process everything (``/root/reference/.helm/values.yaml:124-125``)."""
+import asyncio
+import collections
+import json
+import time
+
+from nexus_supervisor_amd import _kube_native
+from nexus_supervisor_amd.app import Application
+from nexus_supervisor_amd.bench.workload import Workload
+from nexus_supervisor_amd.config import load_config
+from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig
+from nexus_supervisor_amd.parallel.pipeline import PipelineStage
+from nexus_supervisor_amd.parallel.sharding import SHARD_SEED, ShardSet, shard_of
+from nexus_supervisor_amd.parallel.workers import _SEED
+from nexus_supervisor_amd.store.memory import MemoryStore
+from nexus_supervisor_amd.testing.fake_apiserver import FakeApiServer
+
+LABEL = "batch.kubernetes.io/job-name"
+
+
+def _ids(n_per_shard, shards=2):
+    out = collections.defaultdict(list)
+    i = 0
+    while any(len(out[k]) < n_per_shard for k in range(shards)):
+        rid = f"run-{i:05d}"
+        i += 1
+        k = shard_of(rid, shards)
+        if len(out[k]) < n_per_shard:
+            out[k].append(rid)
+    return out
+
+
+def _line(etype, obj):
+    return (json.dumps({"type": etype, "object": obj}) + "\n").encode()
+
+
+def test_shard_set_epochs_and_hash():
+    s = ShardSet(4, [1, 2])
+    rid = next(r for r in (f"x{i}" for i in range(100)) if shard_of(r, 4) == 2)
+    assert s.owns(rid) and s.token(rid) == 0
+    gained, lost = s.update([0, 1])
+    assert gained == {0} and lost == {2}
+    assert not s.owns(rid) and s.token(rid) == 1  # a decision holding token 0 is fenced
+    assert ShardSet(1).owns("anything") and not ShardSet(1).enabled
+    assert all(0 <= shard_of(f"r{i}", 3) < 3 for i in range(50))
+
+
+def test_native_router_drops_other_replicas_runs_before_decode():
+    ids = _ids(3)
+    router = _kube_native.ShardRouter(0, 2, _SEED, LABEL)
+    router.set_replica(2, SHARD_SEED, [0])
+    jobs = _kube_native.WatchSplitter(router, "job")
+    pods = _kube_native.WatchSplitter(router, "pod")
+    events = _kube_native.WatchSplitter(router, "event")
+    body = b"".join(_line("ADDED", {"kind": "Job", "metadata": {"name": r, "resourceVersion": "1"}})
+                    for k in (0, 1) for r in ids[k])
+    outs, _rv, errors = jobs.feed(body)
+    text = b"".join(outs).decode()
+    assert not errors
+    assert all(r in text for r in ids[0]) and not any(r in text for r in ids[1])
+    # each owned run goes to exactly one worker (the in-replica placement)
+    for r in ids[0]:
+        assert sum(r.encode() in o for o in outs) == 1
+    pod_body = b"".join(_line("ADDED", {"kind": "Pod", "metadata": {"name": f"{r}-w0", "resourceVersion": "2",
+                                                                   "labels": {LABEL: r}}})
+                        for k in (0, 1) for r in ids[k])
+    outs, _rv, _e = pods.feed(pod_body)
+    assert not any(r.encode() in b"".join(outs) for r in ids[1])
+    foreign_pod = f"{ids[1][0]}-w0"
+    assert router.pod_owner(foreign_pod) == -2
+    # a Pod Event follows its pod's owner: another replica's pod → dropped everywhere
+    ev = {"kind": "Event", "metadata": {"name": "e1", "resourceVersion": "3"},
+          "involvedObject": {"kind": "Pod", "name": foreign_pod}, "reason": "OOMKilling"}
+    outs, _rv, _e = events.feed(_line("ADDED", ev))
+    assert not any(outs)
+    # unknown pod: every worker parks it until the pod shows up
+    ev2 = dict(ev, involvedObject={"kind": "Pod", "name": "never-seen"})
+    outs, _rv, _e = events.feed(_line("ADDED", ev2))
+    assert all(outs)
+    assert router.stats["foreign"] >= 5
+    # gaining the shard re-evaluates what the router already knows about its pods
+    router.set_replica(2, SHARD_SEED, [0, 1])
+    assert router.pod_owner(foreign_pod) in (0, 1)
+    outs, _rv, _e = events.feed(_line("ADDED", ev))
+    assert sum(bool(o) for o in outs) == 1
+    # LIST bodies are split the same way
+    router.set_replica(2, SHARD_SEED, [1])
+    listing = json.dumps({"metadata": {"resourceVersion": "9"}, "items": [
+        {"kind": "Job", "metadata": {"name": r}} for k in (0, 1) for r in ids[k]]}).encode()
+    rv, parts = jobs.split_list(listing)
+    items = [it["metadata"]["name"] for p in parts for it in json.loads(p)]
+    assert rv == "9" and sorted(items) == sorted(ids[1])
+
+
+def test_pipeline_clear_with_predicate_keeps_other_keys(arun):
+    async def go():
+        done = []
+        release = asyncio.Event()
+
+        async def proc(item):
+            await release.wait()
+            done.append(item)
+
+        p = PipelineStage("t", proc, workers=1, elements_per_second=0, burst=10, key_fn=lambda x: x)
+        await p.start()
+        for k in ("a", "b", "c", "d"):
+            p.receive(k)
+        await asyncio.sleep(0.01)  # "a" is running, the rest queued
+        dropped = p.clear(lambda key: key in ("b", "d"))
+        assert dropped == 2
+        p.receive("b")  # re-received after the drop: queued once
+        release.set()
+        assert await p.join(2)
+        assert sorted(done) == ["a", "b", "c"] and done.count("b") == 1
+        await p.stop()
+
+    arun(go())
+
+
+def _cfg(ident, extra=None):
+    over = {"cql-store-type": "memory", "workers": 8, "rate-limit-elements-per-second": 0, "resync-period": "0s",
+            "rules": {"stale-event-grace": "2s"},
+            "leader-election": {"identity": ident, "lease-duration": "800ms", "renew-deadline": "500ms",
+                                "retry-period": "100ms"}}
+    over.update(extra or {})
+    return load_config(path=None, env={}, overrides=over)
+
+
+async def _wait(pred, timeout):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if pred():
+            return True
+        await asyncio.sleep(0.05)
+    return pred()
+
+
+def _push(api, wl, store, n, expected):
+    failed, traffic, rows = wl.step(n)
+    for r in rows:
+        store.rows[r.key] = r.deep_copy()
+    for etype, obj in traffic:
+        (api.create if etype == "ADDED" else api.update)(obj)
+    for rid in failed:
+        expected[rid] = wl.expected[rid]
+
+
+def _check_exactly_once(store, wl, expected):
+    stages = {rid: store.get(wl.algorithm, rid).lifecycle_stage for rid in expected}
+    wrong = {rid: (s, expected[rid]) for rid, s in stages.items() if s != expected[rid]}
+    writes = collections.Counter(key[1] for key, _stage in store.write_log)
+    twice = {rid: writes[rid] for rid in expected if writes[rid] != 1}
+    return wrong, twice
+
+
+def test_static_shards_split_the_namespace_and_write_each_run_once(arun):
+    """Two replicas with ``sharding.shards: 2`` over one namespace: each caches and decides
+    only its own half (ingest filter), and every failed run is written exactly once."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        wl = Workload(concurrent_jobs=120, seed=3)
+        objs, rows = wl.initial()
+        store = MemoryStore(rows)
+        for o in objs:
+            api.create(o)
+        apps = []
+        for i in range(2):
+            cfg = _cfg(f"s{i}", {"sharding": {"shards": 2, "shard-index": i}})
+            app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+            await app.start()
+            apps.append(app)
+        for a in apps:
+            assert await a.wait_for_cache_sync(10)
+        jobs = [len(a.supervisor.job_informer.indexer) for a in apps]
+        assert sum(jobs) == 120 and all(j > 20 for j in jobs), jobs
+        expected = {}
+        _push(api, wl, store, 60, expected)
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 15)
+        await asyncio.sleep(0.3)  # late duplicates would land now
+        wrong, twice = _check_exactly_once(store, wl, expected)
+        assert not wrong and not twice, (wrong, twice)
+        for a in apps:
+            await a.stop(drain_timeout=1)
+        await api.stop()
+
+    arun(go(), timeout=60)
+
+
+def test_shard_leases_fail_over_individually_without_loss_or_double_writes(arun):
+    """Three replicas, two shards (fair share 1 each, one standby).  Killing a shard owner
+    (no lease release) moves exactly that shard to the standby within the lease duration;
+    runs failing during the gap are decided by the new owner; nothing is written twice."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        wl = Workload(concurrent_jobs=200, seed=11)
+        objs, rows = wl.initial()
+        store = MemoryStore(rows)
+        for o in objs:
+            api.create(o)
+        apps = {}
+        for ident in ("rep-a", "rep-b", "rep-c"):
+            cfg = _cfg(ident, {"sharding": {"shards": 2, "mode": "lease", "replicas": 3}})
+            app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+            await app.start()
+            apps[ident] = app
+
+        def owners():
+            return {k: [i for i, a in apps.items() if k in a.shard_leases.owned] for k in (0, 1)}
+
+        assert await _wait(lambda: all(len(v) == 1 for v in owners().values()), 5), owners()
+        own = owners()
+        assert own[0] != own[1]  # fair share: one shard each, the third replica stands by
+        standby = next(i for i in apps if i not in own[0] + own[1])
+        expected = {}
+        _push(api, wl, store, 40, expected)
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 15)
+        # the owner of shard 1 dies holding its lease
+        victim_id = own[1][0]
+        victim = apps.pop(victim_id)
+        await victim.shard_leases.stop(release=False)
+        await victim.stop(drain_timeout=0.2)
+        t0 = time.monotonic()
+        _push(api, wl, store, 40, expected)  # failures of both shards during the gap
+        assert await _wait(lambda: owners()[1] == [standby], 5), owners()
+        took = time.monotonic() - t0
+        # lease duration (0.8 s) + up to two retry periods of observation
+        assert took < 0.8 + 0.5, took
+        assert owners()[0] == own[0]  # the surviving owner kept its shard throughout
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 15)
+        await asyncio.sleep(0.3)
+        wrong, twice = _check_exactly_once(store, wl, expected)
+        assert not wrong and not twice, (wrong, twice)
+        lease = api.get("Lease", "nexus", "nexus-supervisor-leader-shard-1")
+        assert lease["spec"]["holderIdentity"] == standby
+        for a in apps.values():
+            await a.stop(drain_timeout=1)
+        await api.stop()
+
+    arun(go(), timeout=60)
+
+
+def test_last_survivor_takes_orphaned_shards(arun):
+    """With the fair share at one shard, a lone survivor still takes a shard nobody renews
+    for a full lease duration (orphaned), so the namespace is never left uncovered."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        wl = Workload(concurrent_jobs=60, seed=5)
+        objs, rows = wl.initial()
+        store = MemoryStore(rows)
+        for o in objs:
+            api.create(o)
+        cfg = _cfg("lonely", {"sharding": {"shards": 2, "mode": "lease", "replicas": 2}})
+        app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+        await app.start()
+        assert await _wait(lambda: len(app.shard_leases.owned) == 1, 3)
+        assert await _wait(lambda: len(app.shard_leases.owned) == 2, 4)  # after a lease duration
+        expected = {}
+        _push(api, wl, store, 30, expected)
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 15)
+        await app.stop(drain_timeout=1)
+        # released on shutdown
+        for k in (0, 1):
+            assert api.get("Lease", "nexus", f"nexus-supervisor-leader-shard-{k}")["spec"]["holderIdentity"] == ""
+        await api.stop()
+
+    arun(go(), timeout=60)
+
+
+def test_shard_leases_with_worker_processes_and_watch_hub(arun, tmp_path):
+    """Lease mode on process-per-core replicas: the parent holds the shard leases, its
+    watch hub drops the other replica's runs before decode, and when the other replica
+    dies the survivor's hub re-lists and its workers decide the orphaned shard's runs."""
+    from nexus_supervisor_amd.app import ShardedApplication
+    from nexus_supervisor_amd.bench.wire import schema_statements
+    from nexus_supervisor_amd.store.cql import CqlCheckpointStore, CqlSession
+    from nexus_supervisor_amd.testing.cqlsrv import CqlServer
+
+    srv = CqlServer(exec_statements=schema_statements()).start()
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(json.dumps({"clusters": [{"name": "c", "cluster": {"server": url}}],
+                                  "contexts": [{"name": "x", "context": {"cluster": "c"}}], "current-context": "x"}))
+        wl = Workload(concurrent_jobs=120, seed=21)
+        objs, rows = wl.initial()
+        st = CqlCheckpointStore(CqlSession([srv.address]))
+        await st.connect()
+        await st.upsert_many(rows)
+        for o in objs:
+            api.create(o)
+        apps = {}
+        try:
+            for ident in ("hub-a", "hub-b"):
+                cfg = _cfg(ident, {"cql-store-type": "scylla", "kube-config-path": str(kc),
+                                   "scylla-cql-store": {"hosts": f"127.0.0.1:{srv.port}"},
+                                   "runtime": {"worker-processes": 2},
+                                   "sharding": {"shards": 2, "mode": "lease", "replicas": 2}})
+                app = ShardedApplication(cfg)
+                await app.start()
+                apps[ident] = app
+            for a in apps.values():
+                assert await a.wait_for_cache_sync(30)
+            assert await _wait(lambda: sorted(k for a in apps.values() for k in a.shards.owned or ()) == [0, 1], 5)
+            expected = {}
+
+            async def decided():
+                got = {}
+                for rid, stage in expected.items():
+                    row = await st.read_checkpoint(wl.algorithm, rid)
+                    got[rid] = row.lifecycle_stage if row else None
+                return {r: (g, expected[r]) for r, g in got.items() if g != expected[r]}
+
+            async def wait_decided(timeout):
+                deadline = time.monotonic() + timeout
+                bad = await decided()
+                while bad and time.monotonic() < deadline:
+                    await asyncio.sleep(0.1)
+                    bad = await decided()
+                return bad
+
+            async def push(n):
+                failed, traffic, new_rows = wl.step(n)
+                await st.upsert_many(new_rows)
+                for etype, obj in traffic:
+                    (api.create if etype == "ADDED" else api.update)(obj)
+                for rid in failed:
+                    expected[rid] = wl.expected[rid]
+
+            await push(30)
+            assert not await wait_decided(20)
+            # each hub routed only its own shard's runs to its workers
+            for a in apps.values():
+                assert a.hub.router.stats["foreign"] > 0
+            victim = apps.pop("hub-a")
+            survivor = apps["hub-b"]
+            await victim.shard_leases.stop(release=False)
+            await victim.stop(drain_timeout=0.5)
+            await push(30)
+            assert await _wait(lambda: survivor.shards.owned == {0, 1}, 6), survivor.shards.owned
+            bad = await wait_decided(30)
+            assert not bad, list(bad.items())[:3]
+        finally:
+            for a in apps.values():
+                await a.stop(drain_timeout=1)
+            await st.close()
+            await api.stop()
+
+    try:
+        arun(go(), timeout=120)
+    finally:
+        srv.stop()
