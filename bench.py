@@ -69,6 +69,9 @@ def parse_args(argv=None):
     ap.add_argument("--json-out", default="")
     ap.add_argument("--pprof-out", default="", help="write a pprof profile of the timed steps (rank 0)")
     ap.add_argument("--cql-latency-us", type=int, default=0, help="inject CQL server response latency")
+    ap.add_argument("--cluster", choices=("auto", "shared", "per-rank"), default="auto",
+                    help="shared = one apiserver + one CQL server for all ranks, each replica watching the whole "
+                         "namespace and owning its shard (default for N>1); per-rank = independent copies")
     return ap.parse_args(argv)
 
 
@@ -144,18 +147,29 @@ def main(argv=None) -> int:
         if has_gpu:
             torch.cuda.synchronize(device)
 
+    def share(obj):
+        """rank 0's object on every rank (shared-cluster rendezvous)."""
+        if dist is None:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    cluster = args.cluster if args.cluster != "auto" else ("shared" if world > 1 else "per-rank")
     cfg = BenchConfig(rank=rank, world=world, local_rank=local_rank, jobs=args.jobs, events=args.events,
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
-                      pregen=not args.no_pregen,
+                      pregen=not args.no_pregen, cluster=cluster,
                       pprof_out=args.pprof_out if rank == 0 else "")
-    res = asyncio.run(run_rank(cfg, barrier_sync))
+    res = asyncio.run(run_rank(cfg, barrier_sync, share))
 
     elapsed = res["elapsed"]
-    stats = torch.tensor([elapsed, float(res["events"]), float(res["errors"])], dtype=torch.float64, device=device)
+    rb = res.get("readback") or {}
+    stats = torch.tensor([elapsed, float(res["events"]), float(res["errors"]), float(res["wrong_stage"]),
+                          float(rb.get("checked", 0)), float(rb.get("wrong", 0))], dtype=torch.float64, device=device)
     lat = torch.tensor(res["latencies_ms"], dtype=torch.float64, device=device)
     if dist is not None:
         mx = stats.clone()
@@ -172,9 +186,11 @@ def main(argv=None) -> int:
         allat = torch.cat(gathered)
         allat = allat[~torch.isnan(allat)]
         max_elapsed, total_events, total_errors = mx[0].item(), sm[1].item(), sm[2].item()
+        wrong_stage, rb_checked, rb_wrong = sm[3].item(), sm[4].item(), sm[5].item()
     else:
         allat = lat
         max_elapsed, total_events, total_errors = elapsed, float(res["events"]), float(res["errors"])
+        wrong_stage, rb_checked, rb_wrong = float(res["wrong_stage"]), float(rb.get("checked", 0)), float(rb.get("wrong", 0))
     allat = allat.cpu()
 
     if rank == 0:
@@ -199,11 +215,18 @@ def main(argv=None) -> int:
             # open-loop latency at the north-star churn rate (1000 pod-fail events/min), rank 0
             "latency_at_rate": res.get("probe"),
             "errors": int(total_errors),
+            # correctness of what was measured: decisions whose written stage differs from the
+            # workload's expected stage, and timed rows read back from the store afterwards
+            "wrong_stage": int(wrong_stage),
+            "readback": {"checked": int(rb_checked), "wrong": int(rb_wrong),
+                         "examples_rank0": rb.get("examples", [])[:3] + res.get("wrong_examples", [])[:3]},
+            "supervisor_cpu_us_per_event_rank0": (res.get("cpu") or {}).get("supervisor_cpu_us_per_event"),
             "config": {
                 "model": "nexus-supervisor (informer→classify→CQL write), 1 replica-shard per GPU-job slot",
                 "global_batch": args.events * world,
                 "seq_len": None,
                 "parallelism": f"shard{world}x{args.procs if args.transport == 'wire' else 1}proc",
+                "cluster": cluster if args.transport == "wire" else "in-process",
                 "concurrent_jobs_per_rank": args.jobs,
                 "events_per_step_per_rank": args.events,
                 "transport": args.transport,

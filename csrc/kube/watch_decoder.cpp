@@ -729,8 +729,19 @@ int owner_of(const Router* r, std::string_view key) {
   return static_cast<int>(crc32_update(r->seed, key.data(), key.size()) % static_cast<uint32_t>(r->count));
 }
 
+// murmur3 finaliser over the CRC: CRC32 is affine in its seed, so without it the replica
+// shard would be correlated with the worker placement (parallel/sharding.py shard_of)
+uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
 uint32_t replica_hash(const Router* r, std::string_view key) {
-  return crc32_update(r->rseed, key.data(), key.size());
+  return fmix32(crc32_update(r->rseed, key.data(), key.size()));
 }
 
 bool replica_owns_hash(const Router* r, uint32_t h) {

@@ -7,11 +7,18 @@ generator, and the "receiver" role that inserts each new run's checkpoint row
 into the CQL store before the run's pods exist (what nexus's receiver does
 upstream of the supervisor).  A small control API drives it:
 
-``POST /bench/init {"jobs": N, "seed": s, ..., "pregen": P, "events": E}``
-                                                    create the live runs (+ rows) and
-                                                    pre-generate P steps of E failures
-``POST /bench/step {"events": E}``                fail E runs, replace them; returns
-                                                    ``{"rids": [...], "t_push": monotonic}``
+``POST /bench/init {"jobs": N, "seed": s, "shards": S, "shard_indexes": [k, ...],
+                   "pregen": P, "events": E}``
+                                                    one workload per listed replica shard
+                                                    (N live runs each, + rows) and P
+                                                    pre-generated steps of E failures each
+``POST /bench/step {"events": E, "shard": k}``    fail E runs of shard k, replace them;
+                                                    ``{"rids": [...], "t_push": monotonic,
+                                                    "expected": {rid: stage}}``
+
+Per-rank mode lists one shard (the rank's own cluster); shared mode (``bench.py
+--cluster shared``) lists every shard: one apiserver and one CQL server for the whole
+node, every replica watching the whole namespace and owning its shard of it.
 
 ``python -m nexus_supervisor_amd.bench.cluster_proc --ready-file F --cql HOST:PORT``
 """
@@ -64,7 +71,15 @@ async def amain(args) -> None:
     host, _, port = args.cql.partition(":")
     store = CqlCheckpointStore(CqlSession([(host, int(port))], connections_per_host=2, consistency="ONE"), consistency="ONE")
     await store.connect()
-    state = {"wl": None}
+    shards = {}  # replica shard → _Shard
+    state = {}
+
+    class _Shard:
+        def __init__(self, wl):
+            self.wl = wl
+            self.pregen = collections.deque()
+            self.next = None
+            self.lock = asyncio.Lock()
 
     async def write_rows(rows):
         # the receiver's inserts as UNLOGGED batches of 64 rows, 8 batches in flight
@@ -73,35 +88,41 @@ async def amain(args) -> None:
 
     async def h_init(req):
         p = await req.json()
-        wl = Workload(p.get("jobs", 10_000), rank=p.get("rank", 0), world=p.get("world", 1), seed=p.get("seed", 0),
-                      hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=p.get("shards", 1),
-                      shard_index=p.get("shard_index", 0))
-        objs, rows = wl.initial()
-        await write_rows(rows)
-        await apply([("ADDED", o) for o in objs])
-        state["wl"] = wl
-        # synthetic input generated up front (like a data loader's pre-built batches): the
-        # failures of the next `pregen` steps of `events` each, their replacement runs' rows
-        # inserted (the receiver writes a run's row before its pods exist) and their watch
-        # traffic encoded, so a timed step costs the generator one HTTP request
-        pregen, events = int(p.get("pregen", 0)), int(p.get("events", 0))
-        queue = state["pregen"] = collections.deque()
-        if pregen and events and simctl is not None:
-            for _ in range(pregen):
-                failed, traffic, rows = wl.step(events)
-                await write_rows(rows)
-                queue.append((events, failed, encode_events(traffic)))
+        n_shards = int(p.get("shards", 1))
+        indexes = p.get("shard_indexes")
+        if indexes is None:
+            indexes = [int(p.get("shard_index", 0))]
+        total = 0
+        for k in indexes:
+            # per-rank mode: the rank's workload (rank = its shard); shared mode: one per shard
+            wl = Workload(p.get("jobs", 10_000), rank=k if len(indexes) > 1 else p.get("rank", 0),
+                          world=p.get("world", 1), seed=p.get("seed", 0),
+                          hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=n_shards, shard_index=k)
+            objs, rows = wl.initial()
+            await write_rows(rows)
+            await apply([("ADDED", o) for o in objs])
+            sh = shards[k] = _Shard(wl)
+            total += len(objs)
+            # synthetic input generated up front (like a data loader's pre-built batches): the
+            # failures of the next `pregen` steps of `events` each, their replacement runs' rows
+            # inserted (the receiver writes a run's row before its pods exist) and their watch
+            # traffic encoded, so a timed step costs the generator one HTTP request
+            pregen, events = int(p.get("pregen", 0)), int(p.get("events", 0))
+            if pregen and events and simctl is not None:
+                for _ in range(pregen):
+                    failed, traffic, rows = wl.step(events)
+                    await write_rows(rows)
+                    sh.pregen.append((events, failed, encode_events(traffic)))
         # the simulated cluster holds the same 10k-run heap as the supervisor: keep it out
         # of full collections so the generator never paces the measured process
         gc.collect()
         gc.freeze()
         gc.set_threshold(20000, 20, 20)
-        return web.json_response({"objects": len(objs), "rows": len(rows)})
+        return web.json_response({"objects": total, "shards": sorted(shards)})
 
-    async def prepare(events: int):
+    async def prepare(wl, events: int):
         # generate the next step's traffic and insert its replacement runs' rows ahead of
         # time (overlapped with the supervisor working on the current step)
-        wl = state["wl"]
         failed, traffic, rows = wl.step(events)
         await write_rows(rows)
         return failed, traffic
@@ -112,19 +133,23 @@ async def amain(args) -> None:
             cp.enable()
         p = await req.json()
         events = int(p["events"])
-        wl = state["wl"]
-        queue = state.get("pregen")
-        if queue and queue[0][0] == events and "next" not in state:
+        sh = shards[int(p["shard"])] if "shard" in p else next(iter(shards.values()))
+        async with sh.lock:  # one step of a shard at a time (shards run concurrently)
+            return web.json_response(await _step(sh, events))
+
+    async def _step(sh, events):
+        wl = sh.wl
+        queue = sh.pregen
+        if queue and queue[0][0] == events and sh.next is None:
             _, failed, body = queue.popleft()
             doc = await simctl.apply_raw(body)
-            return web.json_response({"rids": failed, "t_push": doc["t_push"],
-                                      "expected": {r: wl.expected[r] for r in failed}})
+            return {"rids": failed, "t_push": doc["t_push"], "expected": {r: wl.expected[r] for r in failed}}
         if queue:
             # a step of another size (latency probe): the pre-generated steps' runs are live
             # in the workload already, so they must exist in the cluster before we diverge
             while queue:
                 await simctl.apply_raw(queue.popleft()[2])
-        nxt = state.pop("next", None)
+        nxt, sh.next = sh.next, None
         if nxt is not None and nxt[0] == events:
             failed, traffic = await nxt[1]
         else:
@@ -133,10 +158,10 @@ async def amain(args) -> None:
                 # already live in the workload, so they must exist in the cluster too
                 _f, stale = await nxt[1]
                 await apply([(e, o) for e, o in stale if e == "ADDED" and o.get("kind") in ("Pod", "Job")])
-            failed, traffic = await prepare(events)
+            failed, traffic = await prepare(wl, events)
         t_push = await apply(traffic)
-        state["next"] = (events, asyncio.ensure_future(prepare(events)))
-        return web.json_response({"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}})
+        sh.next = (events, asyncio.ensure_future(prepare(wl, events)))
+        return {"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}}
 
     async def h_stats(req):
         if simctl is not None:

@@ -43,6 +43,7 @@ class BenchConfig:
     probe_rate_per_min: float = 1000.0
     procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
     pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
+    cluster: str = "per-rank"  # per-rank | shared (one apiserver + one CQL server for all ranks)
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -67,13 +68,18 @@ class Tracker:
 
     Several steps may be in flight at once (the generator runs ahead of the
     supervisor, as a live cluster would); each step completes when every run it
-    failed has been acknowledged by the store."""
+    failed has been acknowledged by the store.  Every acknowledged decision is checked
+    against the stage the workload expects for that failure (``wrong_stage``), and the
+    timed runs are remembered for the read-back check against the store afterwards."""
 
     def __init__(self):
-        self.acks: Dict[str, Tuple[float, str]] = {}
+        self.acks: Dict[str, Tuple[float, str, Optional[str]]] = {}
         self.owner: Dict[str, "StepState"] = {}
         self.latencies: List[float] = []
         self.errors = 0
+        self.wrong_stage = 0
+        self.wrong_examples: List[Tuple[str, Optional[str], str]] = []
+        self.checked: Dict[str, str] = {}  # timed run → expected stage (read-back)
         self.record = False
 
     def __call__(self, d: Decision):
@@ -82,12 +88,14 @@ class Tracker:
         t = d.result.stamps.get("ack_mono") or time.monotonic()
         st = self.owner.pop(rid, None)
         if st is None:
-            self.acks[rid] = (t, d.outcome)  # ack raced ahead of the step response
+            self.acks[rid] = (t, d.outcome, d.new_stage)  # ack raced ahead of the step response
             return
-        st.settle(self, rid, t, d.outcome)
+        st.settle(self, rid, t, d.outcome, d.new_stage)
 
-    def arm(self, rids: List[str], t_push: float) -> "StepState":
-        st = StepState(set(rids), t_push, self.record)
+    def arm(self, rids: List[str], t_push: float, expected: Optional[Dict[str, str]] = None) -> "StepState":
+        st = StepState(set(rids), t_push, self.record, expected or {})
+        if self.record and expected:
+            self.checked.update(expected)
         for rid in rids:
             a = self.acks.pop(rid, None)
             if a is not None:
@@ -107,20 +115,27 @@ class Tracker:
 
 
 class StepState:
-    __slots__ = ("waiting", "t_push", "record", "done")
+    __slots__ = ("waiting", "t_push", "record", "done", "expected")
 
-    def __init__(self, waiting, t_push, record):
+    def __init__(self, waiting, t_push, record, expected):
         self.waiting = waiting
         self.t_push = t_push
         self.record = record
+        self.expected = expected
         self.done = asyncio.Event()
 
-    def settle(self, tr: Tracker, rid: str, t: float, outcome: str) -> None:
+    def settle(self, tr: Tracker, rid: str, t: float, outcome: str, stage: Optional[str] = None) -> None:
         self.waiting.discard(rid)
+        want = self.expected.get(rid)
         if outcome != "applied":
             tr.errors += 1
-        elif self.record:
-            tr.latencies.append((t - self.t_push) * 1000.0)
+        else:
+            if want is not None and stage != want:
+                tr.wrong_stage += 1
+                if len(tr.wrong_examples) < 5:
+                    tr.wrong_examples.append((rid, stage, want))
+            if self.record:
+                tr.latencies.append((t - self.t_push) * 1000.0)
         if not self.waiting:
             self.done.set()
 
@@ -149,7 +164,18 @@ class InProcHarness:
         t = time.monotonic()
         for etype, obj in traffic:
             self.cluster.push(obj, etype)
-        return failed, t
+        return failed, t, {r: self.wl.expected[r] for r in failed}
+
+    async def read_stages(self, algorithm: str, rids: List[str]) -> Dict[str, Optional[str]]:
+        out = {}
+        for rid in rids:
+            row = self.store.get(algorithm, rid)
+            out[rid] = row.lifecycle_stage if row else None
+        return out
+
+    @property
+    def algorithm(self) -> str:
+        return self.wl.algorithm
 
     async def stop(self):
         await self.cluster.stop()
@@ -158,7 +184,10 @@ class InProcHarness:
         return {}
 
 
-async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[str, Any]:
+async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
+                   share: Optional[Callable[[Any], Any]] = None) -> Dict[str, Any]:
+    """One rank of the bench.  ``share(obj)`` returns rank 0's ``obj`` on every rank (the
+    shared-cluster rendezvous); ``barrier_sync`` brackets the timed region."""
     from ..gpu.telemetry import FakeTelemetry, make_telemetry, pod_evidence_provider
 
     sc = supervisor_config(cfg)
@@ -169,7 +198,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
     else:
         from .wire import WireHarness
 
-        harness = WireHarness(sc, cfg, cfg.workdir, telemetry=telemetry)
+        harness = WireHarness(sc, cfg, cfg.workdir, telemetry=telemetry, share=share, barrier=barrier_sync)
     tracker = Tracker()
     sampler = None
     try:
@@ -195,14 +224,15 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             for _ in range(n):
                 while len(pending) >= cfg.inflight:
                     await finish(pending.pop(0))
-                failed, t_push = await harness.step(cfg.events)
-                pending.append(tracker.arm(failed, t_push))
+                failed, t_push, expected = await harness.step(cfg.events)
+                pending.append(tracker.arm(failed, t_push, expected))
             for st in pending:
                 await finish(st)
 
         await run_steps(cfg.warmup)
         gc.collect()
-        tracker.errors = 0
+        tracker.errors = tracker.wrong_stage = 0
+        tracker.wrong_examples.clear()
         tracker.record = True
         if cfg.pprof_out:
             from ..obs.pprof import Sampler
@@ -228,7 +258,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
         s1 = await sim_stats() if s0 else None
         if s0 and s1:
-            n_ev = max(cfg.events * cfg.steps, 1)
+            # shared cluster: the simulator serves every rank's failures
+            n_ev = max(cfg.events * cfg.steps * (cfg.world if getattr(harness, "shared", False) else 1), 1)
             for k in ("requests", "loops", "sends"):
                 cpu[f"kubesim_{k}_per_event"] = round((s1.get(k, 0) - s0.get(k, 0)) / n_ev, 3)
             # event-loop phases (µs per pod failure): busy = everything but epoll_wait;
@@ -239,6 +270,16 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         workers = [v for k, v in cpu.items() if k.startswith("worker")]
         if workers:
             cpu["workers_util_sum"] = round(sum(workers), 3)
+        # supervisor CPU per pod failure: the replica's processes (coordinating parent — here
+        # also the bench driver — plus its shard workers), whole-run CPU seconds ÷ failures
+        n_ev = max(cfg.events * cfg.steps, 1)
+        sup_cpu = cpu["supervisor_util"] * elapsed + sum(workers) * elapsed
+        cpu["supervisor_cpu_us_per_event"] = round(sup_cpu * 1e6 / n_ev, 1)
+        if workers:
+            cpu["worker_cpu_us_per_event"] = round(sum(workers) * elapsed * 1e6 / n_ev, 1)
+        rss = getattr(harness, "replica_rss_mb", None)
+        if rss is not None:
+            cpu.update(rss())
         if sampler is not None:
             prof = sampler.stop()
             sampler = None
@@ -260,6 +301,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         if sync is not None:
             await sync()
         stages = _stage_breakdown(sup)
+        readback = await _read_back(harness, tracker)
         probe = None
         if cfg.probe_events > 0:
             probe = await _latency_probe(harness, tracker, cfg)
@@ -269,6 +311,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None]) -> Dict[s
         await harness.stop()
         telemetry.stop()
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
+            "wrong_stage": tracker.wrong_stage, "wrong_examples": tracker.wrong_examples, "readback": readback,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
             "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
             "probe": probe, "step_done_ms": step_done_ms}
@@ -287,8 +330,8 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         delay = start + i * interval - loop.time()
         if delay > 0:
             await asyncio.sleep(delay)
-        failed, t_push = await harness.step(1)
-        states.append(tracker.arm(failed, t_push))
+        failed, t_push, expected = await harness.step(1)
+        states.append(tracker.arm(failed, t_push, expected))
     for st in states:
         try:
             await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
@@ -301,6 +344,19 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     q = lambda p: lat[min(len(lat) - 1, int(round(p * (len(lat) - 1))))]  # noqa: E731
     return {"rate_per_min": cfg.probe_rate_per_min, "events": len(lat), "p50_ms": round(q(0.5), 3),
             "p99_ms": round(q(0.99), 3), "max_ms": round(lat[-1], 3)}
+
+
+async def _read_back(harness, tracker: "Tracker") -> Dict[str, Any]:
+    """After the timed steps: read every timed run's row back from the store and compare
+    its lifecycle stage with the stage the workload expects (the decision reports say
+    what the supervisor *meant* to write; this checks what the store *holds*)."""
+    read = getattr(harness, "read_stages", None)
+    if read is None or not tracker.checked:
+        return {"checked": 0}
+    rids = list(tracker.checked)
+    got = await read(harness.algorithm, rids)
+    wrong = [(r, got.get(r), tracker.checked[r]) for r in rids if got.get(r) != tracker.checked[r]]
+    return {"checked": len(rids), "wrong": len(wrong), "examples": wrong[:5]}
 
 
 def _stage_breakdown(sup) -> Dict[str, Any]:

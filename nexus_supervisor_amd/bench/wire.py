@@ -6,6 +6,13 @@ Process layout per rank::
     nexus-cqlsrv  ◄── CQL v4 ──  supervisor (rank process)  ── HTTP list/watch/DELETE ──►  cluster_proc
          ▲                                                                                  (apiserver +
          └──────────────────────────── CQL v4 (receiver inserts new rows) ───────────────── workload)
+
+``cluster="per-rank"``: every rank runs its own CQL server and cluster process holding
+only its shard's runs (N independent copies).  ``cluster="shared"`` (``bench.py``'s
+default for N>1): rank 0 starts ONE CQL server and ONE cluster process (one apiserver)
+holding every shard's runs; every rank's replica watches the whole namespace with
+``sharding.shards = N`` and its hub drops the other replicas' runs — the cost of a
+sharded replica filtering the shared stream is inside the measurement.
 """
 from __future__ import annotations
 
@@ -15,7 +22,7 @@ import os
 import subprocess
 import sys
 import time
-from typing import List, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import aiohttp
 
@@ -35,7 +42,8 @@ def schema_statements(ks: str = "nexus", table: str = "checkpoints") -> List[str
 class WireHarness:
     store_name = "cql (nexus-cqlsrv over TCP)"
 
-    def __init__(self, sc: SupervisorConfig, cfg, workdir: str, telemetry=None):
+    def __init__(self, sc: SupervisorConfig, cfg, workdir: str, telemetry=None,
+                 share: Optional[Callable[[Any], Any]] = None, barrier: Optional[Callable[[], None]] = None):
         self.sc = sc
         self.telemetry = telemetry
         self.cfg = cfg
@@ -45,17 +53,26 @@ class WireHarness:
         self.app: Application = None
         self.ctl = ""
         self.http: aiohttp.ClientSession = None
+        self.shared = cfg.cluster == "shared" and cfg.world > 1
+        self.share = share or (lambda obj: obj)
+        self.barrier = barrier or (lambda: None)
+        self.owner = not self.shared or cfg.rank == 0  # this rank runs the harness servers
+        self.cql_port = 0
+        self.readback: Optional[CqlCheckpointStore] = None
 
-    async def start(self) -> None:
-        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=self.cfg.cql_latency_us).start()
+    async def _start_cluster(self) -> dict:
+        cfg = self.cfg
+        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=cfg.cql_latency_us).start()
         ready = os.path.join(self.workdir, "cluster.ready")
         if os.path.exists(ready):
             os.unlink(ready)
         env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
         self._log = open(os.path.join(self.workdir, "cluster.log"), "ab")
+        # the apiserver's watch cache scales with the traffic it must hold (every shard's)
+        history = 50_000 * (cfg.world if self.shared else 1)
         self.proc = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd.bench.cluster_proc", "--cql",
-                                      f"127.0.0.1:{self.cql.port}", "--ready-file", ready], env=env,
-                                     stdout=self._log, stderr=self._log, start_new_session=True)
+                                      f"127.0.0.1:{self.cql.port}", "--ready-file", ready, "--history", str(history)],
+                                     env=env, stdout=self._log, stderr=self._log, start_new_session=True)
         deadline = time.monotonic() + 120
         while not os.path.exists(ready):
             if self.proc.poll() is not None or time.monotonic() > deadline:
@@ -63,20 +80,29 @@ class WireHarness:
             await asyncio.sleep(0.05)
         with open(ready) as f:
             info = json.load(f)
+        info["cql_port"] = self.cql.port
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=900)) as http:
+            async with http.post(info["ctl"] + "/bench/init", json={
+                    "jobs": cfg.jobs, "seed": cfg.seed, "rank": cfg.rank, "world": cfg.world, "shards": cfg.world,
+                    "shard_indexes": list(range(cfg.world)) if self.shared else [cfg.rank],
+                    "hip_oom_message": cfg.hip_oom_message,
+                    "pregen": cfg.warmup + cfg.steps if cfg.pregen else 0, "events": cfg.events}) as r:
+                r.raise_for_status()
+                await r.json()
+        return info
+
+    async def start(self) -> None:
+        info = await self._start_cluster() if self.owner else None
+        if self.shared:
+            info = self.share(info)  # rank 0's harness addresses to every rank
         self.ctl = info["ctl"]
         self.api = info["api"]
-        self.sim_pid = info.get("sim_pid")
+        self.cql_port = info["cql_port"]
+        self.sim_pid = info.get("sim_pid") if self.owner else None
         self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=600))
-        async with self.http.post(self.ctl + "/bench/init", json={
-                "jobs": self.cfg.jobs, "seed": self.cfg.seed, "rank": self.cfg.rank, "world": self.cfg.world,
-                "shards": self.cfg.world, "shard_index": self.cfg.rank,
-                "hip_oom_message": self.cfg.hip_oom_message,
-                "pregen": self.cfg.warmup + self.cfg.steps if self.cfg.pregen else 0, "events": self.cfg.events}) as r:
-            r.raise_for_status()
-            await r.json()
         sc = self.sc
         sc.cql_store_type = "scylla"
-        sc.scylla_cql_store.hosts = [f"127.0.0.1:{self.cql.port}"]
+        sc.scylla_cql_store.hosts = [f"127.0.0.1:{self.cql_port}"]
         sc.scylla_cql_store.consistency = "LOCAL_QUORUM"
         if self.cfg.procs > 1:
             # process-per-core replica: the workers build their own clients from the config
@@ -94,7 +120,7 @@ class WireHarness:
             self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir, telemetry=self.telemetry)
         else:
             kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)
-            store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql.port)],
+            store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql_port)],
                                                   connections_per_host=sc.scylla_cql_store.connections_per_host))
             self.app = Application(sc, kube=kube, store=store)
         await self.app.start()
@@ -106,11 +132,43 @@ class WireHarness:
     def supervisor(self):
         return self.app.supervisor
 
-    async def step(self, events: int) -> Tuple[List[str], float]:
-        async with self.http.post(self.ctl + "/bench/step", json={"events": events}) as r:
+    async def step(self, events: int) -> Tuple[List[str], float, Dict[str, str]]:
+        async with self.http.post(self.ctl + "/bench/step", json={"events": events, "shard": self.cfg.rank}) as r:
             r.raise_for_status()
             doc = await r.json()
-        return doc["rids"], doc["t_push"]
+        return doc["rids"], doc["t_push"], doc.get("expected") or {}
+
+    algorithm = "bench-algorithm"
+
+    async def read_stages(self, algorithm: str, rids: List[str]) -> Dict[str, Optional[str]]:
+        """Rows as the CQL server holds them (the bench's read-back check)."""
+        if self.readback is None:
+            self.readback = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql_port)], connections_per_host=2))
+            await self.readback.connect()
+        out: Dict[str, Optional[str]] = {}
+
+        async def one(rid):
+            row = await self.readback.read_status(algorithm, rid)
+            out[rid] = row.lifecycle_stage if row else None
+
+        for i in range(0, len(rids), 512):
+            await asyncio.gather(*(one(r) for r in rids[i:i + 512]))
+        return out
+
+    def replica_rss_mb(self) -> Dict[str, float]:
+        """Resident memory of the replica: this (parent) process plus its shard workers."""
+        def rss(pid):
+            try:
+                with open(f"/proc/{pid}/status") as f:
+                    for line in f:
+                        if line.startswith("VmRSS:"):
+                            return int(line.split()[1]) / 1024.0
+            except OSError:
+                pass
+            return 0.0
+        pool = getattr(self.app, "pool", None)
+        workers = sum(rss(p) for p in pool.pids()) if pool is not None else 0.0
+        return {"replica_rss_mb": round(rss(os.getpid()) + workers, 1), "workers_rss_mb": round(workers, 1)}
 
     async def sync_metrics(self) -> None:
         refresh = getattr(self.app, "refresh_metrics", None)
@@ -150,8 +208,12 @@ class WireHarness:
             if self.app is not None:
                 await self.app.stop(drain_timeout=5)
         finally:
+            if self.readback is not None:
+                await self.readback.close()
             if self.http is not None:
                 await self.http.close()
+            if self.shared:
+                self.barrier()  # every rank's replica is down before the shared servers go
             if self.proc is not None and self.proc.poll() is None:
                 self.proc.terminate()
                 try:

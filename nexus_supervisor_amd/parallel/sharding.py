@@ -24,11 +24,24 @@ from typing import FrozenSet, Iterable, Optional, Tuple
 SHARD_SEED = 0x5BD1E995
 
 
+def _fmix32(h: int) -> int:
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
 def shard_of(request_id: str, shards: int) -> int:
-    """Replica shard of a run (its Job name); must match the native router."""
+    """Replica shard of a run (its Job name); must match the native router.
+
+    CRC32 is affine: for equal-length keys crc32(x, a) ^ crc32(x, b) is a constant, so
+    a second CRC seed alone would correlate the replica shard with the worker placement
+    (``crc32(x, _SEED) % K``) — with 2 shards and 2 workers every run of a replica would
+    land on one worker.  The murmur3 finaliser breaks the linearity."""
     if shards <= 1:
         return 0
-    return zlib.crc32(request_id.encode(), SHARD_SEED) % shards
+    return _fmix32(zlib.crc32(request_id.encode(), SHARD_SEED)) % shards
 
 
 class ShardSet:

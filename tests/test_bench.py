@@ -26,6 +26,11 @@ def _check(out, n, steps, warmup, events):
     assert out["value"] > 0 and out["config"]["global_batch"] == events * n
     assert abs(out["vs_baseline"] - out["value"] / 10.0) < 0.05
     assert out["p50_ms"] is not None and out["p99_ms"] >= out["p50_ms"]
+    # the bench checks what it measured: every decision wrote the workload's expected stage,
+    # and every timed run's row reads back with that stage
+    assert out["wrong_stage"] == 0, out["readback"]
+    assert out["readback"]["checked"] == steps * events * n and out["readback"]["wrong"] == 0, out["readback"]
+    assert out["supervisor_cpu_us_per_event_rank0"] > 0
 
 
 @pytest.mark.slow
@@ -71,8 +76,10 @@ def test_bench_two_ranks_torchrun_gloo():
 
 @pytest.mark.slow
 def test_bench_two_ranks_wire_worker_processes():
-    """The driver's N>1 path on the default (wire) transport: each rank a 2-process replica
-    over its own kubesim + CQL server, MAX-over-ranks timing, one JSON line."""
+    """The driver's N>1 path on the default (wire) transport: the shared cluster — ONE
+    apiserver simulator and ONE CQL server for both ranks, each rank a 2-process replica
+    watching the whole namespace with ``sharding.shards = 2`` — MAX-over-ranks timing,
+    one JSON line, every timed run read back with its expected stage."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -88,7 +95,7 @@ def test_bench_two_ranks_wire_worker_processes():
     out = json.loads(lines[0])
     _check(out, 2, 2, 1, 50)
     cfg = out["config"]
-    assert cfg["parallelism"] == "shard2x2proc" and cfg["worker_processes"] == 2
+    assert cfg["parallelism"] == "shard2x2proc" and cfg["worker_processes"] == 2 and cfg["cluster"] == "shared"
     assert cfg["stages_ms"]["receive_to_checkpoint"]["count"] >= 150  # merged from both workers
     assert {"worker0_util", "worker1_util"} <= set(cfg["cpu_util_rank0"])
 

@@ -359,3 +359,26 @@ def test_shard_leases_with_worker_processes_and_watch_hub(arun, tmp_path):
         arun(go(), timeout=120)
     finally:
         srv.stop()
+
+
+def test_replica_shard_is_independent_of_worker_placement():
+    """CRC32 is affine in its seed: the replica hash must not correlate with the worker
+    placement inside a replica, or one worker would get all of a replica's runs."""
+    import random
+    import zlib
+
+    rng = random.Random(1)
+    counts = collections.Counter()
+    for _ in range(4000):
+        rid = "%08x-%04x-4%03x-8%03x-%012x" % (rng.getrandbits(32), rng.getrandbits(16), rng.getrandbits(12),
+                                              rng.getrandbits(12), rng.getrandbits(48))
+        counts[(shard_of(rid, 2), zlib.crc32(rid.encode(), _SEED) % 2)] += 1
+    assert len(counts) == 4 and min(counts.values()) > 800, counts
+    # the native router agrees with the Python hash
+    router = _kube_native.ShardRouter(0, 1, _SEED, LABEL)
+    router.set_replica(3, SHARD_SEED, [1])
+    split = _kube_native.WatchSplitter(router, "job")
+    ids = [f"job-{i}" for i in range(60)]
+    outs, _rv, _e = split.feed(b"".join(_line("ADDED", {"metadata": {"name": r}}) for r in ids))
+    kept = {json.loads(x)["object"]["metadata"]["name"] for x in outs[0].splitlines()}
+    assert kept == {r for r in ids if shard_of(r, 3) == 1}
