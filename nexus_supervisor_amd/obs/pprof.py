@@ -279,3 +279,111 @@ def decode_profile(data: bytes) -> Dict[str, object]:
             period = v
     return {"strings": strings, "samples": samples, "sample_count": values, "locations": locations,
             "functions": functions, "period": period}
+
+
+def _pb_fields(b: bytes):
+    i = 0
+    while i < len(b):
+        k, i = _read_varint(b, i)
+        f, wt = k >> 3, k & 7
+        if wt == 0:
+            v, i = _read_varint(b, i)
+            yield f, v
+        elif wt == 2:
+            ln, i = _read_varint(b, i)
+            yield f, b[i:i + ln]
+            i += ln
+        else:
+            raise ValueError(f"unsupported wire type {wt}")
+
+
+def _read_varint(b: bytes, i: int):
+    shift = v = 0
+    while True:
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << shift
+        if not c & 0x80:
+            return v, i
+        shift += 7
+
+
+def _packed(v) -> List[int]:
+    if isinstance(v, int):
+        return [v]
+    out, j = [], 0
+    while j < len(v):
+        x, j = _read_varint(v, j)
+        out.append(x)
+    return out
+
+
+def load_profile(data: bytes) -> Profile:
+    """Decode a profile written by :meth:`Profile.encode` back into stacks (merging)."""
+    if data[:2] == b"\x1f\x8b":
+        data = gzip.decompress(data)
+    strings: List[str] = []
+    funcs: Dict[int, Tuple[int, int, int]] = {}
+    locs: Dict[int, Tuple[int, int]] = {}
+    samples: List[Tuple[List[int], int]] = []
+    period = duration = 0
+    for f, v in _pb_fields(data):
+        if f == 6:
+            strings.append(v.decode())
+        elif f == 2:
+            ids: List[int] = []
+            n = 0
+            for sf, sv in _pb_fields(v):
+                if sf == 1:
+                    ids += _packed(sv)
+                elif sf == 2:
+                    n = _packed(sv)[0]
+            samples.append((ids, n))
+        elif f == 4:
+            lid = fid = line = 0
+            for sf, sv in _pb_fields(v):
+                if sf == 1:
+                    lid = sv
+                elif sf == 4:
+                    for lf, lv in _pb_fields(sv):
+                        if lf == 1:
+                            fid = lv
+                        elif lf == 2:
+                            line = lv
+            locs[lid] = (fid, line)
+        elif f == 5:
+            fid = name = fname = first = 0
+            for sf, sv in _pb_fields(v):
+                if sf == 1:
+                    fid = sv
+                elif sf == 2:
+                    name = sv
+                elif sf == 4:
+                    fname = sv
+                elif sf == 5:
+                    first = sv
+            funcs[fid] = (name, fname, first)
+        elif f == 10:
+            duration = v
+        elif f == 12:
+            period = v
+    prof = Profile(period or 1)
+    prof.duration_ns = duration
+    for ids, n in samples:
+        stack = []
+        for lid in ids:
+            fid, line = locs[lid]
+            name, fname, first = funcs[fid]
+            stack.append((strings[fname], strings[name], first, line))
+        prof.add(tuple(stack), n)
+    return prof
+
+
+def merge_profiles(profiles) -> Profile:
+    """Sum several profiles (e.g. every shard worker of a replica) into one."""
+    profiles = list(profiles)
+    out = Profile(profiles[0].period_ns if profiles else 1)
+    for p in profiles:
+        out.stacks.update(p.stacks)
+        out.duration_ns = max(out.duration_ns, p.duration_ns)
+    return out

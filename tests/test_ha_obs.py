@@ -200,3 +200,15 @@ def test_signal_sampler_is_cpu_time_based():
     import signal as _signal
 
     assert _signal.getsignal(_signal.SIGPROF) in (_signal.SIG_DFL, None) or callable(_signal.getsignal(_signal.SIGPROF))
+
+
+def test_profile_decode_and_merge_roundtrip():
+    from nexus_supervisor_amd.obs.pprof import load_profile, merge_profiles
+
+    p = Profile(5_000_000)
+    p.add((("a.py", "leaf", 1, 3), ("a.py", "root", 10, 12)), 7)
+    p.add((("b.py", "other", 2, 5),), 3)
+    q = load_profile(p.encode_gz())
+    assert q.stacks == p.stacks and q.period_ns == p.period_ns
+    m = merge_profiles([q, load_profile(p.encode())])
+    assert sum(m.stacks.values()) == 20 and "leaf (a.py)" in m.top(5)
