@@ -36,6 +36,11 @@ app.kubernetes.io/instance: {{ .Release.Name }}
 
 {{- define "nexus.image" -}}
 {{- printf "%s:%s" .Values.image.repository (default (printf "v%s" .Chart.AppVersion) .Values.image.tag) -}}
+{{- end }}
+
+{{/* node agent image: ROCm base (amd-smi), linux/amd64 (deploy/Dockerfile) */}}
+{{- define "nexus.agentImage" -}}
+{{- printf "%s:%s" .Values.agent.image.repository (default (printf "v%s" .Chart.AppVersion) .Values.agent.image.tag) -}}
 {{- end -}}
 
 {{- define "nexus.roleName" -}}

@@ -6,7 +6,7 @@ re-designed: asyncio control plane, native C++ CQL wire codec, amd-smi GPU
 attribution (HBM-OOM vs host-OOM on 288 GB HBM3E), RCCL/xGMI rank topology in
 the trace row, keyed work pipeline, leader election and pprof-format profiling.
 """
-__version__ = "0.1.0"
+from .buildmeta import APP_VERSION as __version__, BUILD_NUMBER as __build__  # noqa: E402,F401
 
 import os as _os
 

@@ -61,10 +61,9 @@ def main(argv=None) -> int:
         # child process (never exec): keeps signal handling simple for callers
         return subprocess.call([binary("nexus-cqlsrv")] + argv)
     if cmd == "version":
-        from . import __version__
+        from .buildmeta import main as version
 
-        print(__version__)
-        return 0
+        return version(argv)
     print(__doc__, file=sys.stderr)
     return 2
 

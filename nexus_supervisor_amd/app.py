@@ -18,11 +18,11 @@ import socket
 import sys
 from typing import Optional
 
-from . import __version__
+from . import __build__, __version__
 from .config import load_config, redacted
 from .config.schema import CQL_STORE_MEMORY, SupervisorConfig
 from .informer import InformerFactory
-from .obs.logging import KLogger, configure_logging
+from .obs.logging import KLogger, configure_logging, shutdown_logging
 from .obs.metrics import DogStatsd, Metrics
 from .store.base import CheckpointStore
 from .supervisor import JobClient, Supervisor
@@ -90,7 +90,7 @@ class Application:
 
     async def start(self) -> None:
         cfg = self.cfg
-        self.log.info("Starting Nexus Supervisor", version=__version__, namespace=cfg.resource_namespace,
+        self.log.info("Starting Nexus Supervisor", version=__version__, build=__build__, namespace=cfg.resource_namespace,
                       store=cfg.cql_store_type)
         await self.store.connect()
         if self.telemetry is None and cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry:
@@ -223,7 +223,7 @@ class ShardedApplication:
 
     async def start(self) -> None:
         cfg = self.cfg
-        self.log.info("Starting Nexus Supervisor", version=__version__, namespace=cfg.resource_namespace,
+        self.log.info("Starting Nexus Supervisor", version=__version__, build=__build__, namespace=cfg.resource_namespace,
                       store=cfg.cql_store_type, worker_processes=self.pool.count)
         le = cfg.leader_election
         lease_mode = cfg.sharding.mode == "lease"
@@ -345,6 +345,8 @@ def main(argv=None) -> int:
         loop = asyncio.get_running_loop()
         for sig in (signal.SIGTERM, signal.SIGINT):
             loop.add_signal_handler(sig, stop.set)
+        if metrics.statsd is not None:
+            metrics.statsd.attach(loop)
         try:
             app = make_application(cfg, logger=log, metrics=metrics)
         except Exception as exc:  # noqa: BLE001 - fatal init (klog.FlushAndExit analog)
@@ -357,7 +359,12 @@ def main(argv=None) -> int:
             return 1
         return 0
 
-    return asyncio.run(amain())
+    try:
+        return asyncio.run(amain())
+    finally:
+        if metrics.statsd is not None:
+            metrics.statsd.close()
+        shutdown_logging()
 
 
 if __name__ == "__main__":

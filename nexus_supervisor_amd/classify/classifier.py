@@ -448,9 +448,15 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
     doc = {"message": res.run_status_trace, "reason": res.reason, "class": res.failure_class,
            "source": res.evidence.get("source", "")}
     doc.update(extra)
+    gpu, topo = doc.get("gpu"), doc.get("topology")
+    if gpu and topo and (topo.get("xgmi") or {}).get("links") is not None:
+        # the measured links are listed once, under topology.xgmi (with their GPU index)
+        doc["gpu"] = dict(gpu, gpus=[{k: v for k, v in g.items() if k != "links"} for g in gpu.get("gpus", ())])
+    # key order is the (deterministic) construction order: sorting every object doubled the
+    # cost of the largest per-decision serialisation (profiles/r2_*_pprof_*)
     if _native_dumps is not None:
-        return _native_dumps(doc, sort_keys=True, default=str).decode()
-    return json.dumps(doc, sort_keys=True, separators=(",", ":"), default=str, ensure_ascii=False)
+        return _native_dumps(doc, default=str).decode()
+    return json.dumps(doc, separators=(",", ":"), default=str, ensure_ascii=False)
 
 
 try:  # compact UTF-8 JSON (csrc/kube/json_encode.cpp); same document as the json fallback

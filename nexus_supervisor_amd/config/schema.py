@@ -266,6 +266,12 @@ class ConfigError(ValueError):
 def validate(cfg: SupervisorConfig) -> SupervisorConfig:
     if cfg.cql_store_type not in CQL_STORE_TYPES:
         raise ConfigError(f"unknown store type {cfg.cql_store_type}")
+    from ..obs.logging import parse_level
+
+    try:
+        parse_level(cfg.log_level)
+    except ValueError as exc:
+        raise ConfigError(str(exc)) from None
     if cfg.workers < 1:
         raise ConfigError(f"workers must be >= 1, got {cfg.workers}")
     if cfg.rate_limit_elements_per_second < 0:

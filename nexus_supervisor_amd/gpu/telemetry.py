@@ -17,6 +17,7 @@ classifies on event reasons only); this is the north-star extension.
 """
 from __future__ import annotations
 
+import bisect
 import os
 import threading
 import time
@@ -138,7 +139,7 @@ class RemoteTelemetry(GpuTelemetry):
         self.interval = interval
         self.retain = retain
         self._snap: List[Dict[str, Any]] = []
-        self._hist: Dict[int, List] = {}
+        self._hist: Dict[int, _PeakSeries] = {}
         self.source = ""
         self.updates = 0
 
@@ -155,10 +156,11 @@ class RemoteTelemetry(GpuTelemetry):
             self._snap = msg["snap"]
         horizon = (msg.get("t") or time.time()) - self.retain
         for gi, samples in (msg.get("hist") or {}).items():
-            h = self._hist.setdefault(int(gi), [])
-            h.extend((float(t), int(mb)) for t, mb in samples)
-            if h and h[0][0] < horizon:
-                self._hist[int(gi)] = [x for x in h if x[0] >= horizon]
+            h = self._hist.get(int(gi))
+            if h is None:
+                h = self._hist[int(gi)] = _PeakSeries()
+            h.extend(samples)
+            h.trim(horizon)
 
     def devices(self):
         return [{k: g.get(k) for k in ("index", "uuid", "hip_uuid", "bdf", "vram_total_mb", "links")} for g in self._snap]
@@ -172,7 +174,61 @@ class RemoteTelemetry(GpuTelemetry):
         return []
 
     def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:
-        return max((mb for t, mb in self._hist.get(int(gpu_index), ()) if t0 <= t <= t1), default=0)
+        h = self._hist.get(int(gpu_index))
+        return h.peak(t0, t1) if h is not None else 0
+
+
+class _PeakSeries:
+    """Time-ordered VRAM samples with per-block maxima: a window peak costs a bisect plus
+    at most two partial blocks, not a scan of the retained history (the supervisor asks
+    for a 300 s lookback peak per failed GPU pod)."""
+
+    B = 64
+
+    def __init__(self):
+        self.t: List[float] = []
+        self.v: List[int] = []
+        self.bmax: List[int] = []
+
+    def __len__(self) -> int:
+        return len(self.t)
+
+    def extend(self, samples) -> None:
+        t, v, bmax, B = self.t, self.v, self.bmax, self.B
+        for ts, mb in samples:
+            ts, mb = float(ts), int(mb)
+            if t and ts < t[-1]:
+                continue  # out of order (a resent sample): the series stays sorted
+            if len(t) % B == 0:
+                bmax.append(mb)
+            elif mb > bmax[-1]:
+                bmax[-1] = mb
+            t.append(ts)
+            v.append(mb)
+
+    def trim(self, horizon: float) -> None:
+        i = bisect.bisect_left(self.t, horizon)
+        if i >= self.B:  # drop whole blocks only (keeps the block alignment)
+            cut = (i // self.B) * self.B
+            del self.t[:cut]
+            del self.v[:cut]
+            del self.bmax[:cut // self.B]
+
+    def peak(self, t0: float, t1: float) -> int:
+        lo = bisect.bisect_left(self.t, t0)
+        hi = bisect.bisect_right(self.t, t1)
+        if lo >= hi:
+            return 0
+        B, v = self.B, self.v
+        b0, b1 = -(-lo // B), hi // B  # whole blocks [b0, b1)
+        if b0 >= b1:
+            return max(v[lo:hi])
+        best = max(self.bmax[b0:b1])
+        if lo < b0 * B:
+            best = max(best, max(v[lo:b0 * B]))
+        if b1 * B < hi:
+            best = max(best, max(v[b1 * B:hi]))
+        return best
 
 
 def telemetry_message(tel: GpuTelemetry, since: Dict[int, float]) -> Dict[str, Any]:
@@ -360,7 +416,8 @@ def _links_of(g: Dict[str, Any]) -> Optional[List[Dict[str, Any]]]:
 def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterable[int] = (), pids: Iterable[int] = (),
                  lookback: float = 300.0, now: Optional[float] = None, node: str = "",
                  snapshot: Optional[List[Dict[str, Any]]] = None,
-                 allocated: Optional[List[int]] = None) -> Optional[Dict[str, Any]]:
+                 allocated: Optional[List[int]] = None,
+                 links: Optional[Dict[int, Any]] = None) -> Optional[Dict[str, Any]]:
     """Evidence record for one pod (matched by cgroup pod UID, PIDs or explicit GPU indices).
 
     Per GPU: the device-wide VRAM peak over the window the pod's processes lived (or the
@@ -400,9 +457,9 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
             rec["xgmi_error"] = g["xgmi_error"]
         if g.get("xgmi_hive_id"):
             rec["xgmi_hive_id"] = g["xgmi_hive_id"]
-        links = _links_of(g)
-        if links is not None:
-            rec["links"] = links
+        glinks = links[g["index"]] if links is not None and g["index"] in links else _links_of(g)
+        if glinks is not None:
+            rec["links"] = glinks
         if g.get("foreign_procs"):
             rec["foreign_procs"] = g["foreign_procs"]
             rec["foreign_vram_bytes"] = g.get("foreign_vram_bytes", 0)
@@ -448,7 +505,8 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
                 u = p.get("pod_uid")
                 if u:
                     by_uid.setdefault(u, set()).add(g["index"])
-        cache.update(t=now, snap=snap, by_uid=by_uid, by_index={g["index"]: g for g in snap})
+        cache.update(t=now, snap=snap, by_uid=by_uid, by_index={g["index"]: g for g in snap},
+                     links={g["index"]: _links_of(g) for g in snap})
 
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         topo = topology_from_pod(pod, gpu_resource)
@@ -462,7 +520,8 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
         by_index = cache["by_index"]
         sub = [by_index[i] for i in sorted(relevant) if i in by_index]
         return evidence_for(telemetry, pod_uid=uid, gpu_indices=gpus, lookback=lookback,
-                            node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=sub)
+                            node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=sub,
+                            links=cache["links"])
 
     return provider
 

@@ -12,7 +12,7 @@ views are merged by :func:`merge_process_ranks`.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, Iterable, List, Optional
+from typing import Any, Dict, Iterable, List, Optional, Tuple
 
 from ..models import kube
 
@@ -49,7 +49,32 @@ def parse_visible_devices(value: Optional[str]) -> List[str]:
 _DEVICE_CHAIN = (("ROCR_VISIBLE_DEVICES",), ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
 
 
+# every variable _topology_from_env reads (besides the collective prefixes)
+_READ_VARS = frozenset([v for v, _k in _INT_VARS] + [v for names in _DEVICE_CHAIN for v in names]
+                       + ["GPU_DEVICE_ORDINAL"])
+_ENV_MEMO: Dict[Tuple, Dict[str, Any]] = {}
+
+
 def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = "") -> Dict[str, Any]:
+    """:func:`_topology_from_env`, memoised on the variables it reads except ``MASTER_ADDR``
+    (unique per run; re-attached to a shallow copy).  Every run of a job template on a
+    node folds the same rank/device/collective env: the fold is done once.  The result
+    is shared and must not be mutated (callers build new dicts, as everywhere here)."""
+    key = (tuple(sorted((k, v) for k, v in env.items()
+                        if k != "MASTER_ADDR" and (k in _READ_VARS or k.startswith(COLLECTIVE_PREFIXES)))),
+           gpus_requested, node)
+    topo = _ENV_MEMO.get(key)
+    if topo is None:
+        if len(_ENV_MEMO) > 4096:
+            _ENV_MEMO.clear()
+        topo = _ENV_MEMO[key] = _topology_from_env({k: v for k, v in key[0]}, gpus_requested, node)
+    addr = env.get("MASTER_ADDR")
+    if addr:
+        return dict(topo, master_addr=addr) if topo else _topology_from_env(env, gpus_requested, node)
+    return topo
+
+
+def _topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = "") -> Dict[str, Any]:
     """Fold torchrun / RCCL env into a topology record (only non-empty keys).
 
     ``visible_devices`` is the *composed* device list in the container's numbering

@@ -18,6 +18,16 @@ from typing import Any, Dict, Optional
 
 _LEVELS = {"TRACE": (logging.DEBUG, 9), "DEBUG": (logging.DEBUG, 4), "INFO": (logging.INFO, 0),
            "WARN": (logging.WARNING, 0), "WARNING": (logging.WARNING, 0), "ERROR": (logging.ERROR, 0)}
+LOG_LEVELS = tuple(_LEVELS)
+
+
+def parse_level(level: str):
+    """(python level, klog verbosity) of a ``log-level`` string; unknown → ValueError
+    (the reference fails start-up on a logger it cannot configure, ``main.go:22-24``)."""
+    key = (level or "INFO").strip().upper()
+    if key not in _LEVELS:
+        raise ValueError(f"unknown log-level {level!r} (one of {', '.join(LOG_LEVELS)})")
+    return _LEVELS[key]
 
 
 class JsonFormatter(logging.Formatter):
@@ -85,15 +95,32 @@ class _V:
         return self.level <= self.parent.verbosity
 
 
-def configure_logging(level: str = "INFO", stream=None, static: Optional[Dict[str, Any]] = None) -> KLogger:
+def configure_logging(level: str = "INFO", stream=None, static: Optional[Dict[str, Any]] = None,
+                      env: Optional[Dict[str, str]] = None) -> KLogger:
     """Configure the root ``nexus_supervisor_amd`` logger (telemetry.ConfigureLogger analog,
-    ``/root/reference/main.go:15``)."""
-    pylevel, verbosity = _LEVELS.get((level or "INFO").strip().upper(), (logging.INFO, 0))
+    ``/root/reference/main.go:15``): JSON lines on stdout, plus the batched Datadog HTTP
+    sink when the ``DATADOG__*`` variables are set (``obs/datadog.py``)."""
+    pylevel, verbosity = parse_level(level)
     root = logging.getLogger("nexus_supervisor_amd")
     root.setLevel(pylevel)
-    root.handlers[:] = []
+    shutdown_logging()
     h = logging.StreamHandler(stream or sys.stdout)
     h.setFormatter(JsonFormatter(static))
     root.addHandler(h)
+    from .datadog import DatadogLogHandler
+
+    dd = DatadogLogHandler.from_env(env)
+    if dd is not None:
+        dd.setFormatter(JsonFormatter(static))
+        root.addHandler(dd)
     root.propagate = False
     return KLogger("nexus_supervisor_amd", verbosity)
+
+
+def shutdown_logging() -> None:
+    """Flush and detach the handlers (the Datadog sink ships what is still queued)."""
+    root = logging.getLogger("nexus_supervisor_amd")
+    for h in list(root.handlers):
+        root.removeHandler(h)
+        if not isinstance(h, logging.StreamHandler):
+            h.close()

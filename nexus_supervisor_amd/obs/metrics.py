@@ -218,6 +218,23 @@ class DogStatsd:
         except OSError:
             self.dropped += 1
 
+    def attach(self, loop) -> None:
+        """Flush on a timer too (not only when the next metric is emitted), so the tail of a
+        burst reaches the agent within ``flush_interval`` even if the process goes idle."""
+        self._loop = loop
+
+        def tick():
+            if self.sock.fileno() < 0:
+                return
+            if self._buf and time.monotonic() - self._last_flush >= self.flush_interval:
+                self.flush()
+            self._timer = loop.call_later(self.flush_interval, tick)
+
+        self._timer = loop.call_later(self.flush_interval, tick)
+
     def close(self) -> None:
+        timer = getattr(self, "_timer", None)
+        if timer is not None:
+            timer.cancel()
         self.flush()
         self.sock.close()

@@ -697,15 +697,27 @@ def worker_main() -> int:
         loop = asyncio.get_running_loop()
         for sig in (signal.SIGTERM, signal.SIGINT):
             loop.add_signal_handler(sig, sock.shutdown, socket.SHUT_RD)  # → EOF → drain and exit
+        if sd is not None:
+            sd.attach(loop)
         dfd = os.environ.get("NEXUS_WORKER_DATA_FD")
         return await run_worker(cfg, sock, start_active=os.environ.get("NEXUS_WORKER_START_ACTIVE", "1") == "1",
                                 report=os.environ.get("NEXUS_WORKER_REPORT", "0") == "1", logger=log, metrics=metrics,
                                 data_sock=socket.socket(fileno=int(dfd)) if dfd else None,
                                 remote_gpu=os.environ.get("NEXUS_WORKER_REMOTE_GPU", "0") == "1")
 
+    def finish() -> None:
+        from ..obs.logging import shutdown_logging
+
+        if sd is not None:
+            sd.close()
+        shutdown_logging()
+
     prof_path = os.environ.get("NEXUS_WORKER_CPROFILE")
     if not prof_path:
-        return asyncio.run(amain())
+        try:
+            return asyncio.run(amain())
+        finally:
+            finish()
     import cProfile
     import pstats
 

@@ -194,3 +194,26 @@ def test_oom_keyword_prefilter_matches_full_pattern_scan():
         assert O.host_signature(text) == full(O.HOST_PATTERNS, text)
 
     check()
+
+
+def test_peak_series_matches_a_scan():
+    """The mirrored telemetry's window peak (block maxima + bisect) equals a full scan."""
+    import random
+
+    from nexus_supervisor_amd.gpu.telemetry import _PeakSeries
+
+    rng = random.Random(0)
+    s, data, t = _PeakSeries(), [], 0.0
+    for _ in range(2000):
+        t += rng.random()
+        data.append((t, rng.randrange(1000)))
+    s.extend(data[:1000])
+    s.extend(data[1000:])
+    s.extend([(1.0, 5000)])  # out of order: ignored
+    for _ in range(500):
+        a = rng.uniform(-5, t + 5)
+        b = rng.uniform(a, t + 5)
+        assert s.peak(a, b) == max((v for ts, v in data if a <= ts <= b), default=0)
+    s.trim(t / 2)
+    assert s.t[0] <= t / 2 and len(s) < len(data)
+    assert s.peak(t / 2, t) == max(v for ts, v in data if t / 2 <= ts <= t)
