@@ -68,6 +68,7 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--pprof-out", default="", help="write a pprof profile of the timed steps (rank 0)")
+    ap.add_argument("--pprof-hz", type=int, default=199, help="pprof sampling rate (CPU-time Hz)")
     ap.add_argument("--cql-latency-us", type=int, default=0, help="inject CQL server response latency")
     ap.add_argument("--cluster", choices=("auto", "shared", "per-rank"), default="auto",
                     help="shared = one apiserver + one CQL server for all ranks, each replica watching the whole "
@@ -163,7 +164,7 @@ def main(argv=None) -> int:
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster,
-                      pprof_out=args.pprof_out if rank == 0 else "")
+                      pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz)
     res = asyncio.run(run_rank(cfg, barrier_sync, share))
 
     elapsed = res["elapsed"]

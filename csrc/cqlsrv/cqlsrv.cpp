@@ -16,15 +16,29 @@
 // SIGUSR1 drops every client connection; --data FILE keeps a write-ahead log so a
 // killed + restarted server ("Scylla node restart") keeps its rows.
 //
-// One epoll thread; responses delayed by --latency-us go through a timer heap.
+// Scylla shard emulation (--shards N): N shard threads, each with its own epoll loop
+// and connections, and the Scylla protocol extensions a shard-aware driver uses —
+// SUPPORTED carries SCYLLA_SHARD / SCYLLA_NR_SHARDS / SCYLLA_SHARDING_ALGORITHM
+// (biased-token-round-robin) / SCYLLA_SHARDING_IGNORE_MSB / SCYLLA_SHARD_AWARE_PORT,
+// and a connection to the shard-aware port lands on shard (client source port % N).
+// Every EXECUTE with a partition key counts whether it arrived on the shard owning
+// its token (system.cqlsrv_stats shard_hits / shard_misses: a miss is the cross-shard
+// hop real Scylla pays).  The data itself sits behind one lock; the shards parallelise
+// framing, parsing, encoding and socket I/O.  Without --shards: one shard, no
+// extensions.  Responses delayed by --latency-us go through a per-shard timer heap.
 #include <arpa/inet.h>
 #include <csignal>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
+
+#include <atomic>
+#include <mutex>
+#include <thread>
 
 #include <algorithm>
 #include <cerrno>
@@ -61,11 +75,16 @@ struct Options {
   std::vector<std::string> tokens;  // this node's tokens
   std::vector<std::string> peers;   // host:port:token[;token]
   bool verbose = false;
+  int shards = 0;        // Scylla shard emulation: 0 = off (one shard, no extensions)
+  int shard_port = 0;    // shard-aware port (0 = ephemeral) when --shards is given
+  int ignore_msb = 12;   // SCYLLA_SHARDING_IGNORE_MSB
 };
 
 Options g_opt;
-volatile sig_atomic_t g_stop = 0;
-volatile sig_atomic_t g_drop = 0;
+// set from the signal handler, read by every shard thread: lock-free atomics (async-signal-safe)
+std::atomic<int> g_stop{0};
+std::atomic<int> g_drop{0};
+static_assert(std::atomic<int>::is_always_lock_free, "signal flags must be lock-free");
 
 int64_t now_us() {
   return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -624,8 +643,8 @@ struct Prepared {
 };
 
 struct Stats {
-  uint64_t requests = 0, queries = 0, executes = 0, prepares = 0, batches = 0, reads = 0, writes = 0, lwt = 0,
-           errors = 0, injected_errors = 0, connections = 0, dropped = 0;
+  std::atomic<uint64_t> requests{0}, queries{0}, executes{0}, prepares{0}, batches{0}, reads{0}, writes{0}, lwt{0},
+      errors{0}, injected_errors{0}, connections{0}, dropped{0}, shard_hits{0}, shard_misses{0};
 };
 
 class Db {
@@ -1221,10 +1240,11 @@ ResultSet stats_rows() {
   ResultSet rs;
   const Stats& s = g_db.stats;
   std::vector<std::pair<const char*, uint64_t>> kv = {
-      {"requests", s.requests}, {"queries", s.queries}, {"executes", s.executes}, {"prepares", s.prepares},
-      {"batches", s.batches},   {"reads", s.reads},     {"writes", s.writes},     {"lwt", s.lwt},
-      {"errors", s.errors},     {"injected_errors", s.injected_errors},         {"connections", s.connections},
-      {"dropped", s.dropped}};
+      {"requests", s.requests},       {"queries", s.queries},       {"executes", s.executes},
+      {"prepares", s.prepares},       {"batches", s.batches},       {"reads", s.reads},
+      {"writes", s.writes},           {"lwt", s.lwt},               {"errors", s.errors},
+      {"injected_errors", s.injected_errors}, {"connections", s.connections}, {"dropped", s.dropped},
+      {"shard_hits", s.shard_hits},   {"shard_misses", s.shard_misses}};
   for (auto& p : kv) rs.cols.push_back(ColSpec{"system", "cqlsrv_stats", p.first, ty(T_BIGINT)});
   std::vector<Val> row;
   for (auto& p : kv) {
@@ -1323,32 +1343,45 @@ struct Delayed {
   bool operator>(const Delayed& o) const { return due > o.due; }
 };
 
-int g_epfd = -1;
-std::unordered_map<int, std::unique_ptr<Conn>> g_conns;
-std::unordered_map<int, uint64_t> g_gen;  // fd generation (reuse guard for delayed writes)
-std::priority_queue<Delayed, std::vector<Delayed>, std::greater<Delayed>> g_delayed;
-std::mt19937_64 g_rng;
+// One shard: an epoll loop over its own connections (Scylla's shard-per-core model).
+struct Shard {
+  int id = 0;
+  int epfd = -1;
+  int wake = -1;  // eventfd: new connections handed over by the acceptor
+  std::mutex inbox_mu;
+  std::vector<int> inbox;
+  std::unordered_map<int, std::unique_ptr<Conn>> conns;
+  std::unordered_map<int, uint64_t> gen;  // fd generation (reuse guard for delayed writes)
+  std::priority_queue<Delayed, std::vector<Delayed>, std::greater<Delayed>> delayed;
+  std::mt19937_64 rng;
+  uint64_t drop_seen = 0;
+};
+
+std::mutex g_db_mu;  // tables, prepared statements, WAL
+std::atomic<uint64_t> g_drop_gen{0};
+std::vector<std::unique_ptr<Shard>> g_shards;
+int g_shard_port = 0;
 
 void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
-void close_conn(int fd) {
-  epoll_ctl(g_epfd, EPOLL_CTL_DEL, fd, nullptr);
+void close_conn(Shard& s, int fd) {
+  epoll_ctl(s.epfd, EPOLL_CTL_DEL, fd, nullptr);
   close(fd);
-  g_conns.erase(fd);
-  g_gen[fd]++;
+  s.conns.erase(fd);
+  s.gen[fd]++;
 }
 
-void update_interest(Conn& c) {
+void update_interest(Shard& s, Conn& c) {
   bool want = c.out.size() > c.out_off;
   if (want == c.want_write) return;
   c.want_write = want;
   epoll_event ev{};
   ev.events = EPOLLIN | (want ? static_cast<uint32_t>(EPOLLOUT) : 0u);
   ev.data.fd = c.fd;
-  epoll_ctl(g_epfd, EPOLL_CTL_MOD, c.fd, &ev);
+  epoll_ctl(s.epfd, EPOLL_CTL_MOD, c.fd, &ev);
 }
 
-bool flush(Conn& c) {
+bool flush(Shard& s, Conn& c) {
   while (c.out_off < c.out.size()) {
     ssize_t n = ::send(c.fd, c.out.data() + c.out_off, c.out.size() - c.out_off, MSG_NOSIGNAL);
     if (n > 0) {
@@ -1365,17 +1398,25 @@ bool flush(Conn& c) {
     c.out.erase(0, c.out_off);
     c.out_off = 0;
   }
-  update_interest(c);
+  update_interest(s, c);
   return true;
 }
 
-void respond(Conn& c, int16_t stream, uint8_t op, const std::string& body) {
+void respond(Shard& s, Conn& c, int16_t stream, uint8_t op, const std::string& body) {
   std::string f = frame(VERSION_RESP, stream, op, body);
   if (g_opt.latency_us > 0) {
-    g_delayed.push(Delayed{now_us() + g_opt.latency_us, c.fd, g_gen[c.fd], std::move(f)});
+    s.delayed.push(Delayed{now_us() + g_opt.latency_us, c.fd, s.gen[c.fd], std::move(f)});
     return;
   }
   c.out += f;
+}
+
+// Scylla "biased-token-round-robin": shard of a Murmur3 token.
+int shard_of_token(int64_t token) {
+  int n = std::max(1, g_opt.shards);
+  uint64_t z = static_cast<uint64_t>(token) + (1ULL << 63);
+  z <<= g_opt.ignore_msb;
+  return static_cast<int>((static_cast<unsigned __int128>(z) * static_cast<uint64_t>(n)) >> 64);
 }
 
 // Parse [query parameters]; fills values; returns flags.
@@ -1490,23 +1531,38 @@ std::pair<uint8_t, std::string> run_stmt(Conn& c, const Stmt& st, const std::vec
   return {OP_RESULT, void_body()};
 }
 
-void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
+void handle_frame(Shard& sh, Conn& c, const FrameHeader& h, const uint8_t* body) {
   Reader r(body, h.length);
   ++g_db.stats.requests;
   try {
     if ((h.version & 0x7F) != 4) {
-      respond(c, h.stream, OP_ERROR, error_body(ERR_PROTOCOL, "Invalid or unsupported protocol version; only v4 is supported"));
+      respond(sh, c, h.stream, OP_ERROR, error_body(ERR_PROTOCOL, "Invalid or unsupported protocol version; only v4 is supported"));
       return;
     }
     switch (h.opcode) {
       case OP_OPTIONS: {
         Writer w;
-        w.u16(2);
+        bool scylla = g_opt.shards > 0;
+        w.u16(scylla ? 8 : 2);
         w.string("CQL_VERSION");
         w.string_list({"3.3.1"});
         w.string("COMPRESSION");
         w.string_list({});
-        respond(c, h.stream, OP_SUPPORTED, w.buf);
+        if (scylla) {
+          w.string("SCYLLA_SHARD");
+          w.string_list({std::to_string(sh.id)});
+          w.string("SCYLLA_NR_SHARDS");
+          w.string_list({std::to_string(g_opt.shards)});
+          w.string("SCYLLA_PARTITIONER");
+          w.string_list({"org.apache.cassandra.dht.Murmur3Partitioner"});
+          w.string("SCYLLA_SHARDING_ALGORITHM");
+          w.string_list({"biased-token-round-robin"});
+          w.string("SCYLLA_SHARDING_IGNORE_MSB");
+          w.string_list({std::to_string(g_opt.ignore_msb)});
+          w.string("SCYLLA_SHARD_AWARE_PORT");
+          w.string_list({std::to_string(g_shard_port)});
+        }
+        respond(sh, c, h.stream, OP_SUPPORTED, w.buf);
         return;
       }
       case OP_STARTUP: {
@@ -1515,10 +1571,10 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
         if (!g_opt.user.empty()) {
           Writer w;
           w.string("org.apache.cassandra.auth.PasswordAuthenticator");
-          respond(c, h.stream, OP_AUTHENTICATE, w.buf);
+          respond(sh, c, h.stream, OP_AUTHENTICATE, w.buf);
         } else {
           c.authed = true;
-          respond(c, h.stream, OP_READY, std::string());
+          respond(sh, c, h.stream, OP_READY, std::string());
         }
         return;
       }
@@ -1535,15 +1591,15 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
           c.authed = true;
           Writer w;
           w.null_bytes();
-          respond(c, h.stream, OP_AUTH_SUCCESS, w.buf);
+          respond(sh, c, h.stream, OP_AUTH_SUCCESS, w.buf);
         } else {
-          respond(c, h.stream, OP_ERROR, error_body(ERR_BAD_CREDENTIALS, "Provided username " + u + " and/or password are incorrect"));
+          respond(sh, c, h.stream, OP_ERROR, error_body(ERR_BAD_CREDENTIALS, "Provided username " + u + " and/or password are incorrect"));
         }
         return;
       }
       case OP_REGISTER:
         r.string_list();
-        respond(c, h.stream, OP_READY, std::string());
+        respond(sh, c, h.stream, OP_READY, std::string());
         return;
       default: break;
     }
@@ -1551,11 +1607,12 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
     if (!c.authed) throw CqlError(ERR_UNAUTHORIZED, "authentication required");
     if (g_opt.error_rate > 0 && (h.opcode == OP_QUERY || h.opcode == OP_EXECUTE || h.opcode == OP_BATCH)) {
       std::uniform_real_distribution<double> u(0, 1);
-      if (u(g_rng) < g_opt.error_rate) {
+      if (u(sh.rng) < g_opt.error_rate) {
         ++g_db.stats.injected_errors;
         throw CqlError(ERR_OVERLOADED, "Injected overload (--error-rate)");
       }
     }
+    std::lock_guard<std::mutex> lk(g_db_mu);  // the data is shared by every shard
     switch (h.opcode) {
       case OP_QUERY: {
         ++g_db.stats.queries;
@@ -1566,7 +1623,7 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
         Parser p(q);
         Stmt st = p.parse();
         auto res = run_stmt(c, st, vals, (flags & QF_SKIP_METADATA) != 0);
-        respond(c, h.stream, res.first, res.second);
+        respond(sh, c, h.stream, res.first, res.second);
         return;
       }
       case OP_PREPARE: {
@@ -1575,7 +1632,7 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
         std::string id = prepare_id(c.ks, q);
         auto it = g_db.prepared.find(id);
         if (it == g_db.prepared.end()) it = g_db.prepared.emplace(id, prepare(q, c.ks)).first;
-        respond(c, h.stream, OP_RESULT, prepared_body(id, it->second));
+        respond(sh, c, h.stream, OP_RESULT, prepared_body(id, it->second));
         return;
       }
       case OP_EXECUTE: {
@@ -1585,12 +1642,30 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
         if (it == g_db.prepared.end()) {
           Writer w;
           w.short_bytes(id);
-          respond(c, h.stream, OP_ERROR, error_body(ERR_UNPREPARED, "Prepared query with ID not found", w.buf));
+          respond(sh, c, h.stream, OP_ERROR, error_body(ERR_UNPREPARED, "Prepared query with ID not found", w.buf));
           return;
         }
         std::vector<Val> vals;
         uint16_t cl;
         uint8_t flags = read_params(r, vals, cl);
+        if (g_opt.shards > 0 && !it->second.pk_idx.empty()) {
+          // did the driver send this to the shard owning the partition? (a miss is a cross-shard hop)
+          std::vector<std::string> parts;
+          bool full = true;
+          for (auto i : it->second.pk_idx) {
+            if (i >= vals.size() || !vals[i]) {
+              full = false;
+              break;
+            }
+            parts.push_back(*vals[i]);
+          }
+          if (full) {
+            std::string key = composite_routing_key(parts);
+            int64_t tok = murmur3_token(reinterpret_cast<const uint8_t*>(key.data()), key.size());
+            if (shard_of_token(tok) == sh.id) ++g_db.stats.shard_hits;
+            else ++g_db.stats.shard_misses;
+          }
+        }
         if (vals.size() != it->second.bind.size())
           throw CqlError(ERR_INVALID, "There were " + std::to_string(it->second.bind.size()) + " markers(?) in CQL but " +
                                            std::to_string(vals.size()) + " bound variables");
@@ -1598,7 +1673,7 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
         if (!it->second.stmt.ks.empty()) c.ks = it->second.stmt.ks;
         auto res = run_stmt(c, it->second.stmt, vals, (flags & QF_SKIP_METADATA) != 0);
         c.ks = saved;
-        respond(c, h.stream, res.first, res.second);
+        respond(sh, c, h.stream, res.first, res.second);
         return;
       }
       case OP_BATCH: {
@@ -1618,7 +1693,7 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
             if (it == g_db.prepared.end()) {
               Writer w;
               w.short_bytes(id);
-              respond(c, h.stream, OP_ERROR, error_body(ERR_UNPREPARED, "Prepared query with ID not found", w.buf));
+              respond(sh, c, h.stream, OP_ERROR, error_body(ERR_UNPREPARED, "Prepared query with ID not found", w.buf));
               return;
             }
             st = it->second.stmt;
@@ -1643,25 +1718,25 @@ void handle_frame(Conn& c, const FrameHeader& h, const uint8_t* body) {
           std::string sk, ch;
           if (execute(it.first, it.second, c.ks, rs, sk, ch)) last = rs;
         }
-        if (!last.cols.empty()) respond(c, h.stream, OP_RESULT, rows_body(last, false));
-        else respond(c, h.stream, OP_RESULT, void_body());
+        if (!last.cols.empty()) respond(sh, c, h.stream, OP_RESULT, rows_body(last, false));
+        else respond(sh, c, h.stream, OP_RESULT, void_body());
         return;
       }
       default: throw CqlError(ERR_PROTOCOL, "unsupported opcode " + std::to_string(h.opcode));
     }
   } catch (const CqlError& e) {
     ++g_db.stats.errors;
-    respond(c, h.stream, OP_ERROR, error_body(e.code, e.what()));
+    respond(sh, c, h.stream, OP_ERROR, error_body(e.code, e.what()));
   } catch (const ProtocolError& e) {
     ++g_db.stats.errors;
-    respond(c, h.stream, OP_ERROR, error_body(ERR_PROTOCOL, e.what()));
+    respond(sh, c, h.stream, OP_ERROR, error_body(ERR_PROTOCOL, e.what()));
   } catch (const std::exception& e) {
     ++g_db.stats.errors;
-    respond(c, h.stream, OP_ERROR, error_body(ERR_SERVER, e.what()));
+    respond(sh, c, h.stream, OP_ERROR, error_body(ERR_SERVER, e.what()));
   }
 }
 
-bool on_readable(Conn& c) {
+bool on_readable(Shard& sh, Conn& c) {
   char buf[1 << 16];
   while (true) {
     ssize_t n = ::recv(c.fd, buf, sizeof buf, 0);
@@ -1670,7 +1745,7 @@ bool on_readable(Conn& c) {
       FrameHeader h;
       const uint8_t* body;
       try {
-        while (c.in.next(h, body)) handle_frame(c, h, body);
+        while (c.in.next(h, body)) handle_frame(sh, c, h, body);
       } catch (const ProtocolError&) {
         return false;
       }
@@ -1681,7 +1756,106 @@ bool on_readable(Conn& c) {
     if (errno == EAGAIN || errno == EWOULDBLOCK) break;
     return false;
   }
-  return flush(c);
+  return flush(sh, c);
+}
+
+void shard_loop(Shard& s) {
+  std::vector<epoll_event> evs(256);
+  while (!g_stop) {
+    int timeout = -1;
+    if (!s.delayed.empty()) {
+      int64_t dt = s.delayed.top().due - now_us();
+      timeout = dt <= 0 ? 0 : static_cast<int>((dt + 999) / 1000);
+    }
+    if (timeout < 0 || timeout > 200) timeout = 200;
+    int n = epoll_wait(s.epfd, evs.data(), static_cast<int>(evs.size()), timeout);
+    uint64_t dg = g_drop_gen.load();
+    if (dg != s.drop_seen) {
+      s.drop_seen = dg;
+      std::vector<int> fds;
+      for (auto& kv : s.conns) fds.push_back(kv.first);
+      for (int fd : fds) close_conn(s, fd);
+      g_db.stats.dropped += fds.size();
+    }
+    for (int i = 0; i < n; ++i) {
+      int fd = evs[static_cast<size_t>(i)].data.fd;
+      if (fd == s.wake) {
+        uint64_t v;
+        if (read(s.wake, &v, sizeof v) < 0 && errno != EAGAIN) perror("eventfd read");
+        std::vector<int> fresh;
+        {
+          std::lock_guard<std::mutex> lk(s.inbox_mu);
+          fresh.swap(s.inbox);
+        }
+        for (int cfd : fresh) {
+          auto c = std::make_unique<Conn>();
+          c->fd = cfd;
+          epoll_event ev{};
+          ev.events = EPOLLIN;
+          ev.data.fd = cfd;
+          epoll_ctl(s.epfd, EPOLL_CTL_ADD, cfd, &ev);
+          s.conns[cfd] = std::move(c);
+        }
+        continue;
+      }
+      auto it = s.conns.find(fd);
+      if (it == s.conns.end()) continue;
+      Conn& c = *it->second;
+      bool ok = true;
+      if (evs[static_cast<size_t>(i)].events & (EPOLLERR | EPOLLHUP)) ok = false;
+      if (ok && (evs[static_cast<size_t>(i)].events & EPOLLIN)) ok = on_readable(s, c);
+      if (ok && (evs[static_cast<size_t>(i)].events & EPOLLOUT)) ok = flush(s, c);
+      if (!ok) close_conn(s, fd);
+    }
+    if (!s.delayed.empty()) {
+      int64_t t = now_us();
+      std::set<int> touched;
+      while (!s.delayed.empty() && s.delayed.top().due <= t) {
+        const Delayed& d = s.delayed.top();
+        auto it = s.conns.find(d.fd);
+        if (it != s.conns.end() && s.gen[d.fd] == d.gen) {
+          it->second->out += d.bytes;
+          touched.insert(d.fd);
+        }
+        s.delayed.pop();
+      }
+      for (int fd : touched) {
+        auto it = s.conns.find(fd);
+        if (it != s.conns.end() && !flush(s, *it->second)) close_conn(s, fd);
+      }
+    }
+  }
+}
+
+void hand_over(Shard& s, int cfd) {
+  {
+    std::lock_guard<std::mutex> lk(s.inbox_mu);
+    s.inbox.push_back(cfd);
+  }
+  uint64_t one = 1;
+  if (write(s.wake, &one, sizeof one) < 0) perror("eventfd write");
+}
+
+int listen_on(int port, int& bound) {
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, g_opt.host.c_str(), &addr.sin_addr) != 1) {
+    fprintf(stderr, "bad --host\n");
+    exit(2);
+  }
+  if (bind(fd, reinterpret_cast<sockaddr*>(&addr), sizeof addr) != 0 || listen(fd, 1024) != 0) {
+    perror("bind/listen");
+    exit(1);
+  }
+  socklen_t alen = sizeof addr;
+  getsockname(fd, reinterpret_cast<sockaddr*>(&addr), &alen);
+  bound = ntohs(addr.sin_port);
+  set_nonblock(fd);
+  return fd;
 }
 
 void on_signal(int sig) {
@@ -1693,7 +1867,8 @@ void usage() {
   fprintf(stderr,
           "nexus-cqlsrv [--host H] [--port P (0 = ephemeral)] [--user U --password P] [--latency-us N]\n"
           "             [--error-rate F] [--seed N] [--data WAL] [--ready-file PATH] [--dc DC] [--rack R]\n"
-          "             [--tokens t1,t2] [--peer host:port:tok1;tok2]... [--exec FILE.cql] [-v]\n");
+          "             [--tokens t1,t2] [--peer host:port:tok1;tok2]... [--exec FILE.cql] [-v]\n"
+          "             [--shards N [--shard-aware-port P] [--ignore-msb B]]\n");
 }
 
 void exec_file(const std::string& path) {
@@ -1767,13 +1942,15 @@ int main(int argc, char** argv) {
         p = e + 1;
       }
     } else if (a == "--peer") g_opt.peers.push_back(val());
+    else if (a == "--shards") g_opt.shards = std::stoi(val());
+    else if (a == "--shard-aware-port") g_opt.shard_port = std::stoi(val());
+    else if (a == "--ignore-msb") g_opt.ignore_msb = std::stoi(val());
     else if (a == "-v") g_opt.verbose = true;
     else {
       usage();
       return 2;
     }
   }
-  g_rng.seed(g_opt.seed);
   signal(SIGPIPE, SIG_IGN);
   struct sigaction sa {};
   sa.sa_handler = on_signal;
@@ -1799,103 +1976,72 @@ int main(int argc, char** argv) {
     }
   }
 
-  int lfd = socket(AF_INET, SOCK_STREAM, 0);
-  int one = 1;
-  setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-  sockaddr_in addr{};
-  addr.sin_family = AF_INET;
-  addr.sin_port = htons(static_cast<uint16_t>(g_opt.port));
-  if (inet_pton(AF_INET, g_opt.host.c_str(), &addr.sin_addr) != 1) {
-    fprintf(stderr, "bad --host\n");
-    return 2;
+  int lfd = listen_on(g_opt.port, g_opt.port);
+  int sfd = -1;
+  if (g_opt.shards > 0 && g_opt.shard_port >= 0) sfd = listen_on(g_opt.shard_port, g_shard_port);  // -1: none
+  int nshards = std::max(1, g_opt.shards);
+  for (int k = 0; k < nshards; ++k) {
+    auto sh = std::make_unique<Shard>();
+    sh->id = k;
+    sh->epfd = epoll_create1(0);
+    sh->wake = eventfd(0, EFD_NONBLOCK);
+    sh->rng.seed(g_opt.seed + static_cast<uint64_t>(k));
+    epoll_event wev{};
+    wev.events = EPOLLIN;
+    wev.data.fd = sh->wake;
+    epoll_ctl(sh->epfd, EPOLL_CTL_ADD, sh->wake, &wev);
+    g_shards.push_back(std::move(sh));
   }
-  if (bind(lfd, reinterpret_cast<sockaddr*>(&addr), sizeof addr) != 0 || listen(lfd, 1024) != 0) {
-    perror("bind/listen");
-    return 1;
+  int epfd = epoll_create1(0);
+  for (int fd : {lfd, sfd}) {
+    if (fd < 0) continue;
+    epoll_event lev{};
+    lev.events = EPOLLIN;
+    lev.data.fd = fd;
+    epoll_ctl(epfd, EPOLL_CTL_ADD, fd, &lev);
   }
-  socklen_t alen = sizeof addr;
-  getsockname(lfd, reinterpret_cast<sockaddr*>(&addr), &alen);
-  g_opt.port = ntohs(addr.sin_port);
-  set_nonblock(lfd);
-  g_epfd = epoll_create1(0);
-  epoll_event lev{};
-  lev.events = EPOLLIN;
-  lev.data.fd = lfd;
-  epoll_ctl(g_epfd, EPOLL_CTL_ADD, lfd, &lev);
   if (!g_opt.ready_file.empty()) {
     std::string tmp = g_opt.ready_file + ".tmp";
     FILE* f = fopen(tmp.c_str(), "w");
     if (f) {
-      fprintf(f, "%d\n", g_opt.port);
+      fprintf(f, "%d\n%d\n", g_opt.port, g_shard_port);
       fclose(f);
       rename(tmp.c_str(), g_opt.ready_file.c_str());
     }
   }
-  fprintf(stderr, "nexus-cqlsrv listening on %s:%d\n", g_opt.host.c_str(), g_opt.port);
+  fprintf(stderr, "nexus-cqlsrv listening on %s:%d (shards %d, shard-aware port %d)\n", g_opt.host.c_str(), g_opt.port,
+          g_opt.shards, g_shard_port);
   fflush(stderr);
+  std::vector<std::thread> threads;
+  for (auto& sh : g_shards) threads.emplace_back(shard_loop, std::ref(*sh));
 
-  std::vector<epoll_event> evs(256);
+  // acceptor: the regular port spreads connections round-robin over the shards (Scylla
+  // picks the least loaded one); the shard-aware port maps source port % shards
+  int one = 1;
+  size_t rr = 0;
+  std::vector<epoll_event> evs(8);
   while (!g_stop) {
-    int timeout = -1;
-    if (!g_delayed.empty()) {
-      int64_t dt = g_delayed.top().due - now_us();
-      timeout = dt <= 0 ? 0 : static_cast<int>((dt + 999) / 1000);
-    }
-    if (timeout < 0 || timeout > 200) timeout = 200;
-    int n = epoll_wait(g_epfd, evs.data(), static_cast<int>(evs.size()), timeout);
+    int n = epoll_wait(epfd, evs.data(), static_cast<int>(evs.size()), 200);
     if (g_drop) {
       g_drop = 0;
-      std::vector<int> fds;
-      for (auto& kv : g_conns) fds.push_back(kv.first);
-      for (int fd : fds) close_conn(fd);
-      g_db.stats.dropped += fds.size();
+      ++g_drop_gen;
     }
     for (int i = 0; i < n; ++i) {
       int fd = evs[static_cast<size_t>(i)].data.fd;
-      if (fd == lfd) {
-        while (true) {
-          int cfd = accept(lfd, nullptr, nullptr);
-          if (cfd < 0) break;
-          set_nonblock(cfd);
-          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-          auto c = std::make_unique<Conn>();
-          c->fd = cfd;
-          epoll_event ev{};
-          ev.events = EPOLLIN;
-          ev.data.fd = cfd;
-          epoll_ctl(g_epfd, EPOLL_CTL_ADD, cfd, &ev);
-          g_conns[cfd] = std::move(c);
-          ++g_db.stats.connections;
-        }
-        continue;
-      }
-      auto it = g_conns.find(fd);
-      if (it == g_conns.end()) continue;
-      Conn& c = *it->second;
-      bool ok = true;
-      if (evs[static_cast<size_t>(i)].events & (EPOLLERR | EPOLLHUP)) ok = false;
-      if (ok && (evs[static_cast<size_t>(i)].events & EPOLLIN)) ok = on_readable(c);
-      if (ok && (evs[static_cast<size_t>(i)].events & EPOLLOUT)) ok = flush(c);
-      if (!ok) close_conn(fd);
-    }
-    if (!g_delayed.empty()) {
-      int64_t t = now_us();
-      std::set<int> touched;
-      while (!g_delayed.empty() && g_delayed.top().due <= t) {
-        const Delayed& d = g_delayed.top();
-        auto it = g_conns.find(d.fd);
-        if (it != g_conns.end() && g_gen[d.fd] == d.gen) {
-          it->second->out += d.bytes;
-          touched.insert(d.fd);
-        }
-        g_delayed.pop();
-      }
-      for (int fd : touched) {
-        auto it = g_conns.find(fd);
-        if (it != g_conns.end() && !flush(*it->second)) close_conn(fd);
+      while (true) {
+        sockaddr_in peer{};
+        socklen_t plen = sizeof peer;
+        int cfd = accept(fd, reinterpret_cast<sockaddr*>(&peer), &plen);
+        if (cfd < 0) break;
+        set_nonblock(cfd);
+        setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+        ++g_db.stats.connections;
+        size_t k = fd == sfd ? static_cast<size_t>(ntohs(peer.sin_port)) % g_shards.size() : rr++ % g_shards.size();
+        hand_over(*g_shards[k], cfd);
       }
     }
   }
+  for (auto& t : threads) t.join();
   if (g_db.wal) fclose(g_db.wal);
   fprintf(stderr, "nexus-cqlsrv: requests=%llu reads=%llu writes=%llu errors=%llu\n",
           static_cast<unsigned long long>(g_db.stats.requests), static_cast<unsigned long long>(g_db.stats.reads),

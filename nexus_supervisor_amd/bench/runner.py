@@ -44,6 +44,7 @@ class BenchConfig:
     procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
     pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
     cluster: str = "per-rank"  # per-rank | shared (one apiserver + one CQL server for all ranks)
+    pprof_hz: int = 199
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -237,10 +238,10 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         if cfg.pprof_out:
             from ..obs.pprof import Sampler
 
-            sampler = Sampler(hz=199).start()
+            sampler = Sampler(hz=cfg.pprof_hz).start()
             pool = getattr(getattr(harness, "app", None), "pool", None)
             if pool is not None:  # shard workers profile themselves over the same window
-                pool.broadcast({"op": "pprof", "on": True, "hz": 199})
+                pool.broadcast({"op": "pprof", "on": True, "hz": cfg.pprof_hz})
         barrier_sync()
         t0 = time.perf_counter()
         c0 = time.process_time()

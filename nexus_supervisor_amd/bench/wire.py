@@ -62,7 +62,11 @@ class WireHarness:
 
     async def _start_cluster(self) -> dict:
         cfg = self.cfg
-        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=cfg.cql_latency_us).start()
+        # a Scylla node is sharded (one shard per core): the store runs as a sharded node and
+        # the replicas route every request to the owning shard (shard-aware driver); the
+        # shared cluster gets a shard per rank, up to 8
+        shards = max(2, min(8, cfg.world)) if self.shared else 2
+        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=cfg.cql_latency_us, shards=shards).start()
         ready = os.path.join(self.workdir, "cluster.ready")
         if os.path.exists(ready):
             os.unlink(ready)

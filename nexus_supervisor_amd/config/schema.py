@@ -61,6 +61,10 @@ class ScyllaCqlStoreConfig:
     request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))
     connect_timeout: float = field(default=5.0, metadata=_k("connect-timeout", "duration"))
     token_aware: bool = field(default=True, metadata=_k("token-aware"))
+    # Scylla shard-aware routing (scylladb/gocql fork, /root/reference/go.mod:93): one
+    # connection per shard through the shard-aware port, requests to the owning shard
+    shard_aware: bool = field(default=True, metadata=_k("shard-aware"))
+    connections_per_shard: int = field(default=1, metadata=_k("connections-per-shard"))
 
 
 @dataclass

@@ -18,6 +18,14 @@ Design:
   ``system.peers``; the partition key ``((algorithm, id))`` is hashed with
   Cassandra's Murmur3 (native) and the request goes straight to the owner in
   ``local-dc`` (one network hop, no coordinator forwarding).
+* **Scylla shard-aware routing** — what the reference gets from the scylladb/gocql
+  fork it pins (``/root/reference/go.mod:93``): ``OPTIONS`` before ``STARTUP`` reads
+  ``SCYLLA_SHARD`` / ``SCYLLA_NR_SHARDS`` / ``SCYLLA_SHARDING_IGNORE_MSB`` /
+  ``SCYLLA_SHARD_AWARE_PORT``; one connection per shard is opened on the shard-aware
+  port from a local port ``≡ shard (mod nr_shards)`` (or, without that port, by
+  reconnecting until every shard is covered), and each request goes to the
+  connection of the shard owning its token (``biased-token-round-robin``), so the
+  node never forwards it across cores.
 * **retries** — idempotent requests are retried on another host after
   connection loss, ``Overloaded``, ``Unavailable`` or timeouts; hosts that fail
   are reconnected in the background with exponential backoff.
@@ -112,14 +120,26 @@ class _Protocol(asyncio.Protocol):
         self.conn._on_lost(exc)
 
 
+_MASK64 = (1 << 64) - 1
+
+
+def scylla_shard_of(token: int, nr_shards: int, ignore_msb: int) -> int:
+    """Scylla's ``biased-token-round-robin`` sharding: shard of a Murmur3 token."""
+    z = ((token + (1 << 63)) << ignore_msb) & _MASK64
+    return (z * nr_shards) >> 64
+
+
 class CqlConnection:
     """One multiplexed CQL connection."""
 
     MAX_STREAMS = 32768
 
     def __init__(self, host: str, port: int, *, user: str = "", password: str = "", ssl_ctx: Optional[ssl.SSLContext] = None,
-                 server_hostname: Optional[str] = None, request_timeout: float = 5.0, connect_timeout: float = 5.0):
+                 server_hostname: Optional[str] = None, request_timeout: float = 5.0, connect_timeout: float = 5.0,
+                 local_port: int = 0):
         self.host, self.port = host, port
+        self.local_port = local_port  # shard-aware port: the source port selects the shard
+        self.supported: Dict[str, List[str]] = {}
         self.user, self.password = user, password
         self.ssl_ctx, self.server_hostname = ssl_ctx, server_hostname
         self.request_timeout, self.connect_timeout = request_timeout, connect_timeout
@@ -151,6 +171,8 @@ class CqlConnection:
         if self.ssl_ctx is not None:
             kw["ssl"] = self.ssl_ctx
             kw["server_hostname"] = self.server_hostname or self.host
+        if self.local_port:
+            kw["local_addr"] = ("0.0.0.0", self.local_port)
         await asyncio.wait_for(self._loop.create_connection(lambda: _Protocol(self), self.host, self.port, **kw),
                                self.connect_timeout)
         self.closed = False
@@ -163,6 +185,9 @@ class CqlConnection:
                 sock.setsockopt(_s.IPPROTO_TCP, _s.TCP_NODELAY, 1)
             except OSError:
                 pass
+        opts = await self.request(lambda s: N.encode_options(s))
+        if opts[0] == "supported":
+            self.supported = dict(opts[1])
         resp = await self.request(lambda s: N.encode_startup(s, {"CQL_VERSION": "3.0.0"}))
         if resp[0] == "authenticate":
             token = b"\x00" + self.user.encode() + b"\x00" + self.password.encode()
@@ -265,6 +290,10 @@ class CqlConnection:
     def in_flight(self) -> int:
         return len(self._pending)
 
+    def scylla(self, key: str) -> Optional[str]:
+        v = self.supported.get(key)
+        return v[0] if v else None
+
     def close(self) -> None:
         if self._transport is not None:
             self._transport.close()
@@ -300,6 +329,15 @@ class Host:
     failures: int = 0
     next_retry: float = 0.0
     rr: int = 0
+    # Scylla sharding of this node (0 = not sharded / unknown) and its connections by shard
+    nr_shards: int = 0
+    ignore_msb: int = 0
+    shard_conns: List[List[CqlConnection]] = field(default_factory=list)
+
+    def shard_of(self, token: Optional[int]) -> Optional[int]:
+        if token is None or self.nr_shards <= 1:
+            return None
+        return scylla_shard_of(token, self.nr_shards, self.ignore_msb)
 
     @property
     def up(self) -> bool:
@@ -311,9 +349,14 @@ class Host:
             self._up = v
             _HOST_EPOCH[0] += 1
 
-    def pick(self) -> Optional[CqlConnection]:
-        """Least in-flight live connection, scanning from a rotating start (ties spread)."""
+    def pick(self, shard: Optional[int] = None) -> Optional[CqlConnection]:
+        """Least in-flight live connection (of ``shard`` when the node is sharded and has
+        one), scanning from a rotating start (ties spread)."""
         conns = self.conns
+        if shard is not None and shard < len(self.shard_conns):
+            own = [c for c in self.shard_conns[shard] if not c.closed]
+            if own:
+                conns = own
         n = len(conns)
         if n == 1:
             c = conns[0]
@@ -348,7 +391,7 @@ class CqlSession:
                  password: str = "", local_dc: str = "", connections_per_host: int = 2, request_timeout: float = 5.0,
                  connect_timeout: float = 5.0, token_aware: bool = True, consistency: str = "LOCAL_QUORUM",
                  ssl_ctx: Optional[ssl.SSLContext] = None, sni_proxy: Optional[Tuple[str, int]] = None,
-                 max_retries: int = 3, discover: bool = True):
+                 max_retries: int = 3, discover: bool = True, shard_aware: bool = True, connections_per_shard: int = 1):
         if not contact_points:
             raise StoreError("no CQL contact points configured")
         self.contact_points = list(contact_points)
@@ -363,6 +406,9 @@ class CqlSession:
         self.sni_proxy = sni_proxy
         self.max_retries = max_retries
         self.discover = discover
+        self.shard_aware = shard_aware and sni_proxy is None
+        self._sharded = False  # some node advertised Scylla shards
+        self.per_shard = max(1, connections_per_shard)
         self.hosts: Dict[Tuple[str, int], Host] = {}
         self._ring: List[int] = []
         self._ring_hosts: List[Host] = []
@@ -373,27 +419,74 @@ class CqlSession:
         self._plan_key: Optional[Tuple[int, int]] = None
         self._plan_up: List[Host] = []
         self._plan_owner: Dict[int, List[Host]] = {}
-        self.stats = {"requests": 0, "retries": 0, "reprepares": 0, "token_routed": 0}
+        self.stats = {"requests": 0, "retries": 0, "reprepares": 0, "token_routed": 0, "shard_routed": 0}
 
     # -------------------------------------------------------------- lifecycle
-    def _new_conn(self, h: Host) -> CqlConnection:
-        host, port = h.address
+    def _new_conn(self, h: Host, port: Optional[int] = None, local_port: int = 0) -> CqlConnection:
+        host, hport = h.address
         server_hostname = None
         if self.sni_proxy is not None:
             server_hostname = h.host_id or host
-            host, port = self.sni_proxy
-        return CqlConnection(host, port, user=self.user, password=self.password, ssl_ctx=self.ssl_ctx,
+            host, hport = self.sni_proxy
+        return CqlConnection(host, port or hport, user=self.user, password=self.password, ssl_ctx=self.ssl_ctx,
                              server_hostname=server_hostname, request_timeout=self.request_timeout,
-                             connect_timeout=self.connect_timeout)
+                             connect_timeout=self.connect_timeout, local_port=local_port)
 
     async def _open_host(self, h: Host) -> None:
-        conns = [self._new_conn(h) for _ in range(self.per_host)]
-        await asyncio.gather(*(c.connect(self.keyspace) for c in conns))
+        first = self._new_conn(h)
+        await first.connect(self.keyspace)
+        nr = int(first.scylla("SCYLLA_NR_SHARDS") or 0) if self.shard_aware else 0
+        if nr > 1 and first.scylla("SCYLLA_SHARDING_ALGORITHM") in (None, "biased-token-round-robin"):
+            conns, by_shard = await self._open_shards(h, first, nr)
+            h.nr_shards, h.ignore_msb = nr, int(first.scylla("SCYLLA_SHARDING_IGNORE_MSB") or 0)
+            self._sharded = True
+        else:
+            rest = [self._new_conn(h) for _ in range(self.per_host - 1)]
+            await asyncio.gather(*(c.connect(self.keyspace) for c in rest))
+            conns, by_shard = [first] + rest, []
+            h.nr_shards = 0
         for c in h.conns:
             c.close()
         h.conns = conns
+        h.shard_conns = by_shard
         h.up = True
         h.failures = 0
+
+    async def _open_shards(self, h: Host, first: CqlConnection, nr: int):
+        """``per_shard`` connections to every shard of a Scylla node.  With a shard-aware
+        port the local port picks the shard (``port % nr == shard``); without one, keep
+        reconnecting to the regular port until each shard has been handed out."""
+        by_shard: List[List[CqlConnection]] = [[] for _ in range(nr)]
+        by_shard[int(first.scylla("SCYLLA_SHARD") or 0) % nr].append(first)
+        aware = int(first.scylla("SCYLLA_SHARD_AWARE_PORT") or 0)
+
+        async def one(shard: int) -> None:
+            for attempt in range(32):
+                lp = 0
+                if aware:
+                    base = random.randrange(32768, 60000)
+                    lp = base - base % nr + shard
+                c = self._new_conn(h, port=aware or None, local_port=lp)
+                try:
+                    await c.connect(self.keyspace)
+                except OSError as exc:
+                    if aware and getattr(exc, "errno", None) in (98, 99):  # EADDRINUSE / EADDRNOTAVAIL
+                        continue
+                    raise
+                got = int(c.scylla("SCYLLA_SHARD") or 0) % nr
+                by_shard[got].append(c)  # a stray shard's connection still serves that shard
+                if len(by_shard[shard]) >= self.per_shard:
+                    return
+            log.warning("CQL host %s:%s: no connection to shard %d", h.address[0], h.address[1], shard)
+
+        for shard in range(nr):
+            while len(by_shard[shard]) < self.per_shard:
+                before = len(by_shard[shard])
+                await one(shard)
+                if len(by_shard[shard]) == before:
+                    break
+        conns = [c for lst in by_shard for c in lst]
+        return conns, by_shard
 
     async def connect(self) -> None:
         last: Optional[BaseException] = None
@@ -520,7 +613,7 @@ class CqlSession:
             self._plan_owner = {}
             self._plan_key = key
         up = self._plan_up
-        if routing_token is not None and self.token_aware:
+        if routing_token is not None and self.token_aware and self._ring:
             o = self.owner(routing_token)
             if o is not None and o.up:
                 self.stats["token_routed"] += 1
@@ -590,7 +683,7 @@ class CqlSession:
             self._preparing.pop(query, None)
 
     def routing_token(self, ps: PreparedStatement, values: Sequence[Any]) -> Optional[int]:
-        if not ps.pk_indexes or not self._ring:
+        if not ps.pk_indexes or not (self._ring or self._sharded):
             return None
         parts = []
         for i in ps.pk_indexes:
@@ -604,7 +697,7 @@ class CqlSession:
                       serial: Optional[int] = None, idempotent: bool = True, timeout: Optional[float] = None):
         ps = ps_or_query if isinstance(ps_or_query, PreparedStatement) else await self.prepare(ps_or_query)
         cl = self.consistency if consistency is None else consistency
-        token = self.routing_token(ps, values) if self.token_aware else None
+        token = self.routing_token(ps, values) if self.token_aware or self.shard_aware else None
         vals = list(values)
         hint = ps.result_types
         skip = hint is not None
@@ -618,13 +711,16 @@ class CqlSession:
             if not cands:
                 raise StoreError(f"no CQL host available: {last}")
             h = cands[0]
-            conn = h.pick()
+            shard = h.shard_of(token) if h.nr_shards else None
+            conn = h.pick(shard)
             if conn is None:
                 self._mark_down(h, ConnectionClosed("no live connection"))
                 tried.add(h.address)
                 attempts += 1
                 continue
             self.stats["requests"] += 1
+            if shard is not None:
+                self.stats["shard_routed"] += 1
             try:
                 qid = ps.query_id
                 r = await conn.request(lambda s: N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None),
@@ -827,7 +923,8 @@ class CqlCheckpointStore(CheckpointStore):
             hosts.append((host, int(port) if port else s.port))
         sess = CqlSession(hosts, user=s.user, password=s.password, local_dc=s.local_dc,
                           connections_per_host=s.connections_per_host, request_timeout=s.request_timeout,
-                          connect_timeout=s.connect_timeout, token_aware=s.token_aware, consistency=s.consistency)
+                          connect_timeout=s.connect_timeout, token_aware=s.token_aware, consistency=s.consistency,
+                          shard_aware=s.shard_aware, connections_per_shard=s.connections_per_shard)
         return cls(sess, keyspace=s.keyspace, table=s.table, consistency=s.consistency)
 
     async def connect(self) -> None:

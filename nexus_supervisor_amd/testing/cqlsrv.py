@@ -18,7 +18,8 @@ from typing import List, Optional, Sequence
 class CqlServer:
     def __init__(self, *, user: str = "", password: str = "", latency_us: int = 0, error_rate: float = 0.0,
                  persist: bool = False, tokens: Sequence[int] = (), peers: Sequence[str] = (), exec_statements: Sequence[str] = (),
-                 dc: str = "datacenter1", host: str = "127.0.0.1", port: int = 0, extra_args: Sequence[str] = ()):
+                 dc: str = "datacenter1", host: str = "127.0.0.1", port: int = 0, extra_args: Sequence[str] = (),
+                 shards: int = 0, shard_aware_port: int = 0):
         from .._build import binary
 
         # NEXUS_CQLSRV_BINARY selects e.g. a sanitizer build (bin/nexus-cqlsrv-address)
@@ -33,6 +34,9 @@ class CqlServer:
         self.peers = list(peers)
         self.dc = dc
         self.extra = list(extra_args)
+        # Scylla shard emulation: shard threads + SCYLLA_* SUPPORTED keys + shard-aware port
+        self.shards = shards
+        self.shard_aware_port = shard_aware_port
         self.exec_file = ""
         if exec_statements:
             self.exec_file = os.path.join(self.dir, "init.cql")
@@ -59,6 +63,8 @@ class CqlServer:
             argv += ["--peer", p]
         if self.exec_file:
             argv += ["--exec", self.exec_file]
+        if self.shards:
+            argv += ["--shards", str(self.shards), "--shard-aware-port", str(self.shard_aware_port)]
         return argv + self.extra
 
     def start(self, timeout: float = 10.0) -> "CqlServer":
@@ -72,7 +78,10 @@ class CqlServer:
         while time.monotonic() < deadline:
             if os.path.exists(ready):
                 with open(ready) as f:
-                    self.port = int(f.read().strip())
+                    lines = f.read().split()
+                self.port = int(lines[0])
+                if len(lines) > 1 and int(lines[1]):
+                    self.shard_aware_port = int(lines[1])  # kept across restarts
                 # a restarted persistent server with --exec must not re-run the seed
                 if self.exec_file and self.data:
                     self.exec_file = ""

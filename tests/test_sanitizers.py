@@ -37,7 +37,7 @@ from nexus_supervisor_amd.testing.seed import ALGORITHM, seed_cql_statements, se
 pytestmark = pytest.mark.slow
 
 
-@pytest.fixture(scope="module", params=["address", "undefined"])
+@pytest.fixture(scope="module", params=["address", "undefined", "thread"])
 def sanitized_server(request):
     try:
         _build.build(sanitize=request.param)
@@ -81,13 +81,26 @@ def test_cqlsrv_under_sanitizer(sanitized_server, arun):
     from nexus_supervisor_amd.testing.cqlsrv import CqlServer
     import datetime as dt
 
-    srv = CqlServer(persist=True, exec_statements=seed_cql_statements(), user="u", password="p").start(timeout=30)
+    # TSan: the shard threads (Scylla emulation) serve concurrent clients on every shard
+    shards = 4 if sanitized_server == "thread" else 0
+    srv = CqlServer(persist=True, exec_statements=seed_cql_statements(), user="u", password="p",
+                    shards=shards).start(timeout=30)
     try:
         async def go():
             st = CqlCheckpointStore(CqlSession([srv.address], user="u", password="p", request_timeout=3.0))
             await st.connect()
             for row in seed_rows():
                 assert await st.read_checkpoint(ALGORITHM, row.id) == row
+            burst = [r.deep_copy() for r in seed_rows()]
+            for i, r in enumerate(burst):
+                r.id = f"burst-{i}"
+            many = [dict(r=r, i=k) for k in range(40) for r in burst]
+            for m in many:
+                m["r"] = m["r"].deep_copy()
+                m["r"].id = f"{m['r'].id}-{m['i']}"
+            await asyncio.gather(*(st.upsert_checkpoint(m["r"]) for m in many))
+            got = await asyncio.gather(*(st.read_status(ALGORITHM, m["r"].id) for m in many))
+            assert all(g is not None for g in got)
             now = dt.datetime.now(dt.timezone.utc)
             assert await st.update_status(ALGORITHM, seed_rows()[0].id, "FAILED", "c" * 5000, "d☃", now)
             assert not await st.update_status(ALGORITHM, seed_rows()[0].id, "RUNNING", None, None, now,
@@ -104,6 +117,7 @@ def test_cqlsrv_under_sanitizer(sanitized_server, arun):
         srv.stop()
     log = srv.log()
     assert "AddressSanitizer" not in log and "runtime error" not in log and "LeakSanitizer" not in log, log[-3000:]
+    assert "ThreadSanitizer" not in log, log[-3000:]
 
 
 def test_frame_reader_fuzz():
