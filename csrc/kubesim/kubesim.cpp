@@ -49,7 +49,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -136,6 +140,10 @@ struct Options {
   size_t history = 400000;
   int64_t bookmark_ms = 1000;
   std::string token;
+  // watch fan-out threads: the dirty watch streams of one loop iteration are written by
+  // this many threads (the apiserver's watch cache serves many watchers in parallel; a
+  // sharded supervisor deployment has every replica watching the whole namespace)
+  int flush_threads = 1;
 } g_opt;
 
 int64_t mono_ns() {
@@ -449,7 +457,8 @@ std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x0
 int64_t g_rv = 1000;
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0;
-  uint64_t loops = 0, sends = 0, send_bytes = 0, eagain = 0;
+  uint64_t loops = 0;
+  std::atomic<uint64_t> sends{0}, send_bytes{0}, eagain{0};  // also counted by fan-out threads
   // wall time spent per phase of the event loop (ns): where a saturated simulator goes
   int64_t apply_ns = 0, request_ns = 0, flush_ns = 0, recv_ns = 0, busy_ns = 0;
 } g_stats;
@@ -1061,7 +1070,7 @@ bool flush_watch(Conn& c) {
     return true;
   }
   static char crlf[] = "\r\n";
-  static std::vector<iovec> iov;  // single-threaded event loop: reused across flushes
+  thread_local std::vector<iovec> iov;  // reused across flushes (one per fan-out thread)
   iov.clear();
   iov.reserve(5 * w->lines.size() + 3);
   iov.push_back({hdr, static_cast<size_t>(hl)});
@@ -1086,9 +1095,9 @@ bool flush_watch(Conn& c) {
     m.msg_iov = &iov[i];
     m.msg_iovlen = std::min<size_t>(iov.size() - i, 1024);  // IOV_MAX
     ssize_t n = sendmsg(c.fd, &m, MSG_NOSIGNAL);
-    ++g_stats.sends;
+    g_stats.sends.fetch_add(1, std::memory_order_relaxed);
     if (n > 0) {
-      g_stats.send_bytes += static_cast<uint64_t>(n);
+      g_stats.send_bytes.fetch_add(static_cast<uint64_t>(n), std::memory_order_relaxed);
       size_t k = static_cast<size_t>(n);
       while (k > 0) {
         if (k >= iov[i].iov_len) {
@@ -1103,7 +1112,7 @@ bool flush_watch(Conn& c) {
       continue;
     }
     if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-      ++g_stats.eagain;
+      g_stats.eagain.fetch_add(1, std::memory_order_relaxed);
       break;
     }
     if (n < 0 && errno == EINTR) continue;
@@ -1121,14 +1130,14 @@ bool flush(Conn& c) {
   size_t off = 0;
   while (off < c.out.size()) {
     ssize_t n = send(c.fd, c.out.data() + off, c.out.size() - off, MSG_NOSIGNAL);
-    ++g_stats.sends;
+    g_stats.sends.fetch_add(1, std::memory_order_relaxed);
     if (n > 0) {
       off += static_cast<size_t>(n);
-      g_stats.send_bytes += static_cast<uint64_t>(n);
+      g_stats.send_bytes.fetch_add(static_cast<uint64_t>(n), std::memory_order_relaxed);
       continue;
     }
     if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-      ++g_stats.eagain;
+      g_stats.eagain.fetch_add(1, std::memory_order_relaxed);
       break;
     }
     if (n < 0 && errno == EINTR) continue;
@@ -1139,6 +1148,76 @@ bool flush(Conn& c) {
   interest(c);
   return true;
 }
+
+// Fan-out pool: flushes of distinct connections are independent (each touches only its
+// connection, its watch and the immutable shared line texts), so one loop iteration's
+// dirty connections are split across `flush_threads` threads; the event loop thread
+// takes part and waits for the rest before it touches any connection again.
+class FlushPool {
+ public:
+  void start(int threads) {
+    for (int i = 1; i < threads; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+    workers_.clear();
+  }
+  // ok[i] = flush(*dirty[i])
+  void run(const std::vector<Conn*>& dirty, std::vector<uint8_t>& ok) {
+    if (workers_.empty() || dirty.size() < 2) {
+      for (size_t i = 0; i < dirty.size(); ++i) ok[i] = flush(*dirty[i]);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &dirty;
+      ok_ = &ok;
+      next_.store(0);
+      pending_ = workers_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void work() {
+    const auto& d = *job_;
+    size_t i;
+    while ((i = next_.fetch_add(1)) < d.size()) (*ok_)[i] = flush(*d[i]) ? 1 : 0;
+  }
+  void loop() {
+    uint64_t seen = 0;
+    while (true) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::vector<Conn*>* job_ = nullptr;
+  std::vector<uint8_t>* ok_ = nullptr;
+  std::atomic<size_t> next_{0};
+  size_t pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+} g_flush_pool;
 
 // ============================================================ HTTP
 std::string status_text(int code) {
@@ -1589,7 +1668,8 @@ void on_signal(int) { g_stop = 1; }
 
 void usage() {
   fprintf(stderr,
-          "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n");
+          "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n"
+          "              [--flush-threads N]\n");
 }
 
 }  // namespace
@@ -1610,6 +1690,7 @@ int main(int argc, char** argv) {
     else if (a == "--history") g_opt.history = static_cast<size_t>(atol(next().c_str()));
     else if (a == "--bookmark-ms") g_opt.bookmark_ms = atol(next().c_str());
     else if (a == "--token") g_opt.token = next();
+    else if (a == "--flush-threads") g_opt.flush_threads = std::max(1, atoi(next().c_str()));
     else {
       usage();
       return 2;
@@ -1671,6 +1752,7 @@ int main(int argc, char** argv) {
   fputs(info, stdout);
   fflush(stdout);
 
+  g_flush_pool.start(g_opt.flush_threads);
   std::vector<epoll_event> evs(512);
   int64_t last_tick = mono_ms();
   char buf[1 << 16];
@@ -1750,12 +1832,15 @@ int main(int argc, char** argv) {
       int64_t tf = mono_ns();
       std::vector<Conn*> dirty(g_dirty.begin(), g_dirty.end());
       g_dirty.clear();
-      for (Conn* c : dirty)
-        if (!flush(*c)) close_conn(c->fd);
+      std::vector<uint8_t> ok(dirty.size(), 1);
+      g_flush_pool.run(dirty, ok);
+      for (size_t i = 0; i < dirty.size(); ++i)
+        if (!ok[i]) close_conn(dirty[i]->fd);
       g_stats.flush_ns += mono_ns() - tf;
     }
     g_stats.busy_ns += mono_ns() - t_loop;
   }
+  g_flush_pool.stop();
   for (auto& kv : g_conns) close(kv.first);
   close(lfd);
   prof::dump();

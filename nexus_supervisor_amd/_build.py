@@ -120,7 +120,7 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
             "out": os.path.join(BIN, "nexus-kubesim" + sfx),
             "srcs": [os.path.join(CSRC, "kubesim", "kubesim.cpp")],
             "deps": [os.path.join(CSRC, "kubesim", "json.hpp")],
-            "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, *srcs, "-o", out],
+            "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, "-pthread", *srcs, "-o", out],
             "exe": True,
         },
         "gpu_stress": {

@@ -46,7 +46,8 @@ async def amain(args) -> None:
         # native apiserver simulator: the generator below only produces traffic
         from ..testing.kubesim import KubeSim, SimControl, encode_events
 
-        sim = KubeSim(host=args.host, port=args.port, history=args.history, bookmark_ms=2000).start()
+        sim = KubeSim(host=args.host, port=args.port, history=args.history, bookmark_ms=2000,
+                      flush_threads=args.flush_threads).start()
         simctl = SimControl(sim.url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)
@@ -234,6 +235,7 @@ def main(argv=None) -> int:
     # backlog.  A bigger window only grows the simulator's heap line by line (each line a
     # fresh page-faulted allocation instead of a recycled one) and costs it throughput.
     ap.add_argument("--history", type=int, default=50_000)
+    ap.add_argument("--flush-threads", type=int, default=1, help="simulator watch fan-out threads")
     ap.add_argument("--api", choices=("kubesim", "python"), default="kubesim",
                     help="native apiserver simulator (default) or the Python fake")
     args = ap.parse_args(argv)

@@ -33,13 +33,14 @@ def encode_events(events: Iterable[Tuple[str, Dict[str, Any]]]) -> bytes:
 
 class KubeSim:
     def __init__(self, *, host: str = "127.0.0.1", port: int = 0, history: int = 400_000, bookmark_ms: int = 1000,
-                 token: str = ""):
+                 token: str = "", flush_threads: int = 1):
         from .._build import binary
 
         self.exe = os.environ.get("NEXUS_KUBESIM_BINARY") or binary("nexus-kubesim")
         self.dir = tempfile.mkdtemp(prefix="nexus-kubesim-")
         self.host, self.port = host, port
         self.history, self.bookmark_ms, self.token = history, bookmark_ms, token
+        self.flush_threads = flush_threads  # parallel watch fan-out (many watching replicas)
         self.proc: Optional[subprocess.Popen] = None
         self.log_path = os.path.join(self.dir, "server.log")
         self.url = ""
@@ -52,6 +53,8 @@ class KubeSim:
                 "--history", str(self.history), "--bookmark-ms", str(self.bookmark_ms)]
         if self.token:
             argv += ["--token", self.token]
+        if self.flush_threads > 1:
+            argv += ["--flush-threads", str(self.flush_threads)]
         logf = open(self.log_path, "ab")
         self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True)
         logf.close()

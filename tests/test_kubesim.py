@@ -216,3 +216,70 @@ def test_reference_parity_over_kubesim_and_cql(arun):
                 await ctl.close()
 
     arun(go(), timeout=60)
+
+
+async def _fanout(sim, watchers=8, pods=300):
+    """``watchers`` concurrent watches of one namespace, a burst of pod traffic: every
+    watcher must see every line, in resourceVersion order."""
+    labels = _cfg().labels
+    ctl = SimControl(sim.url)
+    out = await ctl.apply([("ADDED", make_pod(f"f{i}", labels)) for i in range(5)])
+    rv0 = str(out["rv"])
+    clients = [KubeClient(KubeConfig(sim.url)) for _ in range(watchers)]
+    seen = [[] for _ in range(watchers)]
+
+    async def watch(k):
+        async for et, o in clients[k].watch("Pod", "nexus", rv0, timeout_seconds=20):
+            if et == "BOOKMARK":
+                continue
+            seen[k].append(int(o["metadata"]["resourceVersion"]))
+            if len(seen[k]) == pods:
+                return
+
+    tasks = [asyncio.create_task(watch(k)) for k in range(watchers)]
+    await asyncio.sleep(0.2)
+    for i in range(0, pods, 50):
+        await ctl.apply([("ADDED", make_pod(f"g{j}", labels)) for j in range(i, i + 50)])
+    await asyncio.wait_for(asyncio.gather(*tasks), 30)
+    for s in seen:
+        assert len(s) == pods and s == sorted(s)
+    assert seen.count(seen[0]) == watchers
+    for c in clients:
+        await c.close()
+    await ctl.close()
+
+
+def test_parallel_watch_fanout(arun):
+    """``--flush-threads``: the dirty watch streams of one loop iteration are written by a
+    thread pool (a sharded deployment has every replica watching the whole namespace)."""
+    async def go():
+        with KubeSim(flush_threads=4) as sim:
+            await _fanout(sim)
+
+    arun(go())
+
+
+@pytest.mark.slow
+def test_parallel_watch_fanout_under_tsan(arun, monkeypatch):
+    import os
+
+    from nexus_supervisor_amd import _build
+
+    try:
+        _build.build(only=["kubesim"], sanitize="thread")
+    except RuntimeError as exc:  # pragma: no cover - toolchain without the runtime
+        pytest.skip(f"TSan build unavailable: {exc}")
+    monkeypatch.setenv("NEXUS_KUBESIM_BINARY", os.path.join(_build.BIN, "nexus-kubesim-thread"))
+    holder = {}
+
+    async def go():
+        sim = KubeSim(flush_threads=4).start(timeout=30)
+        holder["sim"] = sim
+        try:
+            await _fanout(sim, watchers=6, pods=200)
+        finally:
+            sim.stop()
+
+    arun(go(), timeout=120)
+    log = holder["sim"].log()
+    assert "ThreadSanitizer" not in log, log[-3000:]
