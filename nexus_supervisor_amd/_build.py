@@ -166,7 +166,7 @@ def build_one(name: str, t: Dict, force: bool = False, verbose: bool = False) ->
     if not force and not _stale(t):
         return f"{name}: up to date"
     os.makedirs(os.path.dirname(t["out"]), exist_ok=True)
-    tmp = t["out"] + ".tmp"
+    tmp = f"{t['out']}.tmp{os.getpid()}"  # concurrent builders (test workers) never share a temp file
     cmd = t["cmd"](tmp, t["srcs"])
     if verbose:
         print(" ".join(cmd), flush=True)
