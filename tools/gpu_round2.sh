@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cql-latency-us 500 > g
 HIP_VISIBLE_DEVICES= CUDA_VISIBLE_DEVICES= timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --no-real-oom \
     > gpurun_out/bench_shared2.log 2> gpurun_out/bench_shared2.err &&
-timeout -k 10 600 python bench.py --steps ${PROF_STEPS:-1100} --warmup 2 --probe-events 0 \
+timeout -k 10 600 python bench.py --steps ${PROF_STEPS:-2200} --warmup 2 --probe-events 0 \
     --pprof-out gpurun_out/prof/bench.pb.gz --pprof-hz 499 > gpurun_out/prof_bench.log 2> gpurun_out/prof_bench.err &&
 python tools/pprof_merge.py gpurun_out/prof/workers_merged.top.txt gpurun_out/prof/bench.pb.gz.w*.pb.gz > /dev/null
 rc=$?
