@@ -86,6 +86,11 @@ def auto_procs(local_world: int) -> int:
     return max(1, min(12, int(cpu_share() / max(local_world, 1)) - 4))
 
 
+def _harness_bound(cpu) -> dict:
+    util = {k[:-5]: v for k, v in cpu.items() if k in ("kubesim_util", "cqlsrv_util", "cluster_util")}
+    return {"bound": any(v >= 0.9 for v in util.values()), "util": util}
+
+
 def real_hbm_oom(local_rank: int, workdir: str):
     """Run the HIP stress workload to a real HBM OOM on this rank's GPU; returns its
     termination message (None when unavailable)."""
@@ -222,6 +227,9 @@ def main(argv=None) -> int:
             "readback": {"checked": int(rb_checked), "wrong": int(rb_wrong),
                          "examples_rank0": rb.get("examples", [])[:3] + res.get("wrong_examples", [])[:3]},
             "supervisor_cpu_us_per_event_rank0": (res.get("cpu") or {}).get("supervisor_cpu_us_per_event"),
+            # which side limited the run: a harness process (apiserver simulator / CQL server /
+            # traffic generator) near a full core means the value is the harness's ceiling
+            "harness_bound": _harness_bound(res.get("cpu") or {}),
             "config": {
                 "model": "nexus-supervisor (informer→classify→CQL write), 1 replica-shard per GPU-job slot",
                 "global_batch": args.events * world,

@@ -47,7 +47,15 @@ class JsonFormatter(logging.Formatter):
         if record.exc_info:
             doc["error"] = self.formatException(record.exc_info)
         doc.update(self.static)
-        return json.dumps(doc, default=str)
+        if _dumps is not None:  # one log line per decision (reference V(0)): native encoder
+            return _dumps(doc, default=str).decode()
+        return json.dumps(doc, default=str, separators=(",", ":"), ensure_ascii=False)
+
+
+try:
+    from .._kube_native import dumps as _dumps
+except ImportError:  # pragma: no cover - CPU hosts without the native build
+    _dumps = None
 
 
 class KLogger:
