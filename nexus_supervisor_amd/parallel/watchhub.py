@@ -62,7 +62,7 @@ class WatchHub:
     def __init__(self, cfg, kube, count: int, send: Callable[[int, int, int, bytes], None],
                  buffered: Callable[[int], int], drain: Callable[[int], Any], metrics=None):
         from .. import _kube_native
-        from .workers import _SEED
+        from .workers import _SEED, POD_FORGET_AFTER
 
         self.cfg = cfg
         self.kube = kube
@@ -71,7 +71,7 @@ class WatchHub:
         self.buffered = buffered
         self.drain = drain
         self.metrics = metrics
-        self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label)
+        self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label, POD_FORGET_AFTER)
         from .sharding import ShardSet
 
         self.set_shards(ShardSet.from_config(cfg))

@@ -54,6 +54,11 @@ from ..obs.metrics import Metrics
 
 _SEED = 0x2545F491  # decorrelates worker placement from replica sharding (sharding.SHARD_SEED)
 _FOREIGN = -2  # pod owner: another replica's run (native router OWNER_NONE)
+# how long a deleted pod's owner is remembered for Pod Events still in flight: at tens of
+# thousands of pod failures per second every second of window is ~100k map entries in the
+# router (profiles/r2_pprof_*: a 120 s window held millions in the hub parent); an Event
+# later than this is parked by every worker and dropped as unmatched — harmless
+POD_FORGET_AFTER = 30.0
 _LINE_LIMIT = 64 << 20
 
 
@@ -68,7 +73,7 @@ class WorkerShard:
     """Ingest filter of worker ``index`` of ``count`` (installed on the Event/Pod/Job informers),
     and of the replica's shard set (``shards``: runs of other replicas are dropped)."""
 
-    def __init__(self, index: int, count: int, job_name_label: str, forget_after: float = 120.0,
+    def __init__(self, index: int, count: int, job_name_label: str, forget_after: float = POD_FORGET_AFTER,
                  clock: Callable[[], float] = time.monotonic, shards=None):
         from .sharding import ShardSet
 
@@ -727,5 +732,6 @@ def worker_main() -> int:
         return asyncio.run(amain())
     finally:
         prof.disable()
+        prof.dump_stats(f"{prof_path}.{idx}.prof")  # raw, for callers/callees analysis
         with open(f"{prof_path}.{idx}.txt", "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
