@@ -207,6 +207,9 @@ def test_inprocess_extensions_under_sanitizer(sanitize):
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
                TSAN_OPTIONS="halt_on_error=0:report_signal_unsafe=0", PYTHONDONTWRITEBYTECODE="1")
     env.pop("PYTEST_XDIST_WORKER", None)
+    # the servers these tests start run uninstrumented (a module-scoped sanitized_server
+    # parametrisation may still have its TSan binary selected in this process)
+    env.pop("NEXUS_CQLSRV_BINARY", None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "san_inproc.py"), *tests], cwd=ROOT,
                        capture_output=True, text=True, timeout=600, env=env)
     out = p.stdout + p.stderr
