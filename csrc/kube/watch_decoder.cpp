@@ -101,6 +101,30 @@ std::unique_ptr<Proj> compile(PyObject* spec) {
   return nullptr;
 }
 
+// str from UTF-8 bytes.  Kubernetes objects are almost entirely ASCII: build those directly
+// (one allocation + memcpy) instead of going through the generic decoder with an error
+// handler looked up by name on every call.
+PyObject* make_str(const char* p, size_t n) {
+  const unsigned char* u = reinterpret_cast<const unsigned char*>(p);
+  unsigned char any = 0;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, u + i, 8);
+    if (w & 0x8080808080808080ULL) {
+      any = 0x80;
+      break;
+    }
+  }
+  for (; !any && i < n; ++i) any |= u[i];
+  if (!(any & 0x80)) {
+    PyObject* o = PyUnicode_New(static_cast<Py_ssize_t>(n), 127);
+    if (o) memcpy(PyUnicode_DATA(o), p, n);
+    return o;
+  }
+  return PyUnicode_DecodeUTF8(p, static_cast<Py_ssize_t>(n), "replace");
+}
+
 // Interned Python key strings, looked up by bytes without allocating (open addressing).
 class KeyCache {
  public:
@@ -116,7 +140,7 @@ class KeyCache {
     for (size_t probe = 0; probe < 16; ++probe, i = (i + 1) & (kCap - 1)) {
       Slot& sl = slots_[i];
       if (!sl.obj) {
-        PyObject* o = PyUnicode_DecodeUTF8(k.data(), static_cast<Py_ssize_t>(k.size()), "replace");
+        PyObject* o = make_str(k.data(), k.size());
         if (!o) return nullptr;
         if (used_ < kCap / 2) {
           sl.hash = h;
@@ -132,7 +156,7 @@ class KeyCache {
         return sl.obj;
       }
     }
-    return PyUnicode_DecodeUTF8(k.data(), static_cast<Py_ssize_t>(k.size()), "replace");
+    return make_str(k.data(), k.size());
   }
 
  private:
@@ -237,11 +261,17 @@ class Parser {
         break;
     }
     if (i_ == st) throw ParseError{"bad value", i_};
-    std::string tok(s_ + st, i_ - st);
-    if (!flt) {
-      if (tok.size() < 18) return PyLong_FromLongLong(std::stoll(tok));
-      return PyLong_FromString(tok.c_str(), nullptr, 10);
+    size_t len = i_ - st;
+    if (!flt && len < 18) {  // fits in int64: no temporary string
+      const char* q = s_ + st;
+      bool neg = *q == '-';
+      if (*q == '-' || *q == '+') ++q;
+      long long v = 0;
+      for (; q < s_ + i_; ++q) v = v * 10 + (*q - '0');
+      return PyLong_FromLongLong(neg ? -v : v);
     }
+    std::string tok(s_ + st, len);
+    if (!flt) return PyLong_FromString(tok.c_str(), nullptr, 10);
     return PyFloat_FromDouble(std::stod(tok));
   }
 
@@ -354,9 +384,14 @@ class Parser {
     size_t a, b;
     bool esc;
     string_span(a, b, esc);
-    if (!esc) return PyUnicode_DecodeUTF8(s_ + a, static_cast<Py_ssize_t>(b - a), "replace");
+    if (!esc) {
+      // short values repeat across objects ("Pending", "True", "Always", label values):
+      // interned like keys, so they cost a lookup instead of an allocation
+      if (b - a <= 24) return keys_->get(std::string_view(s_ + a, b - a));
+      return make_str(s_ + a, b - a);
+    }
     std::string u = unescape(a, b);
-    return PyUnicode_DecodeUTF8(u.data(), static_cast<Py_ssize_t>(u.size()), "replace");
+    return make_str(u.data(), u.size());
   }
 
   // Key text as a view into the buffer (or into scratch_ when it had escapes).
