@@ -41,11 +41,25 @@
 namespace {
 
 struct Proj {
-  enum Kind { KEEP, OBJECT, LIST, PREFIX, MAP } kind = KEEP;
+  enum Kind { KEEP, OBJECT, LIST, PREFIX, MAP, KV } kind = KEEP;
   std::vector<std::pair<std::string, std::unique_ptr<Proj>>> fields;  // OBJECT (small: linear scan)
   std::unique_ptr<Proj> elem;                                         // LIST / MAP
   std::unique_ptr<Proj> on_deleted;                                   // OBJECT: "object" of a DELETED envelope
-  std::vector<std::string> prefixes;                                  // PREFIX
+  std::vector<std::string> prefixes;                                  // PREFIX, KV
+  // KV: a list of {key_field: k, value_field: v} objects becomes one {k: v} dict, keeping
+  // only keys in `keep` or starting with one of `prefixes` (both empty: every key); the
+  // first definition of a key wins and entries without a string value are dropped
+  std::string key_field, value_field;
+  std::vector<std::string> keep;
+
+  bool kv_wanted(std::string_view k) const {
+    if (keep.empty() && prefixes.empty()) return true;
+    for (auto& w : keep)
+      if (w == k) return true;
+    for (auto& pre : prefixes)
+      if (k.substr(0, pre.size()) == pre) return true;
+    return false;
+  }
 
   const Proj* field(std::string_view k) const {
     for (auto& f : fields)
@@ -85,6 +99,33 @@ std::unique_ptr<Proj> compile(PyObject* spec) {
       p->elem = compile(sub);
       Py_XDECREF(sub);
       return p->elem ? std::move(p) : nullptr;
+    }
+    if (h && !strcmp(h, "kv") && PySequence_Size(spec) == 5) {
+      p->kind = Proj::KV;
+      auto text = [&](Py_ssize_t i, std::string& out) {
+        PyObject* o = PySequence_GetItem(spec, i);
+        const char* c = o && PyUnicode_Check(o) ? PyUnicode_AsUTF8(o) : nullptr;
+        if (c) out = c;
+        Py_XDECREF(o);
+        return c != nullptr;
+      };
+      auto texts = [&](Py_ssize_t i, std::vector<std::string>& out) {
+        PyObject* o = PySequence_GetItem(spec, i);
+        bool ok = o && (PyList_Check(o) || PyTuple_Check(o));
+        for (Py_ssize_t k = 0; ok && k < PySequence_Size(o); ++k) {
+          PyObject* e = PySequence_GetItem(o, k);
+          const char* c = e && PyUnicode_Check(e) ? PyUnicode_AsUTF8(e) : nullptr;
+          if (c) out.emplace_back(c);
+          else ok = false;
+          Py_XDECREF(e);
+        }
+        Py_XDECREF(o);
+        return ok;
+      };
+      if (text(1, p->key_field) && text(2, p->value_field) && texts(3, p->keep) && texts(4, p->prefixes)) return p;
+      PyErr_Clear();
+      PyErr_SetString(PyExc_ValueError, "kv projection: [\"kv\", key_field, value_field, [keep...], [prefix...]]");
+      return nullptr;
     }
     if (h && !strcmp(h, "prefix")) {
       p->kind = Proj::PREFIX;
@@ -199,6 +240,7 @@ class Parser {
     }
     if (c == '[') {
       if (p && p->kind == Proj::LIST) return array(p->elem.get());
+      if (p && p->kind == Proj::KV) return kv_array(p);
       return array(nullptr);
     }
     if (c == '"') return string_obj();
@@ -506,6 +548,89 @@ class Parser {
     return object_loop([&](PyObject* d, std::string_view k) {
       return set_item(d, k, value(elem && elem->kind != Proj::KEEP ? elem : nullptr));
     });
+  }
+
+  // Text of a string member value into `out` (unescaped); false when not a string.
+  bool string_value(std::string& out) {
+    ws();
+    if (i_ >= n_ || s_[i_] != '"') {
+      skip();
+      return false;
+    }
+    size_t a, b;
+    bool esc;
+    string_span(a, b, esc);
+    if (esc) out = unescape(a, b);
+    else out.assign(s_ + a, b - a);
+    return true;
+  }
+
+  PyObject* kv_array(const Proj* p) {
+    ++i_;  // '['
+    PyObject* d = PyDict_New();
+    if (!d) return nullptr;
+    try {
+      std::string k, v, tmp;
+      while (true) {
+        ws();
+        if (i_ >= n_) throw ParseError{"unterminated array", i_};
+        if (s_[i_] == ']') {
+          ++i_;
+          return d;
+        }
+        if (s_[i_] != '{') {
+          skip();
+        } else {
+          ++i_;
+          bool has_k = false, has_v = false;
+          ws();
+          if (i_ < n_ && s_[i_] == '}') ++i_;
+          else {
+            while (true) {
+              std::string_view name = key_text();
+              if (name == p->key_field) has_k = string_value(k);
+              else if (name == p->value_field) has_v = string_value(v);
+              else skip();
+              ws();
+              if (i_ >= n_) throw ParseError{"unterminated object", i_};
+              if (s_[i_] == ',') {
+                ++i_;
+                continue;
+              }
+              if (s_[i_] == '}') {
+                ++i_;
+                break;
+              }
+              throw ParseError{"expected ',' or '}'", i_};
+            }
+          }
+          if (has_k && has_v && p->kv_wanted(k)) {
+            PyObject* ko = keys_->get(k);
+            if (!ko) {
+              Py_DECREF(d);
+              return nullptr;
+            }
+            int have = PyDict_Contains(d, ko);
+            if (have == 0) {  // first definition wins (container env semantics)
+              PyObject* vo = v.size() <= 24 ? keys_->get(v) : make_str(v.data(), v.size());
+              int rc = vo ? PyDict_SetItem(d, ko, vo) : -1;
+              Py_XDECREF(vo);
+              if (rc != 0) have = -1;
+            }
+            Py_DECREF(ko);
+            if (have < 0) {
+              Py_DECREF(d);
+              return nullptr;
+            }
+          }
+        }
+        ws();
+        if (i_ < n_ && s_[i_] == ',') ++i_;
+      }
+    } catch (...) {
+      Py_DECREF(d);
+      throw;
+    }
   }
 
   PyObject* array(const Proj* elem) {

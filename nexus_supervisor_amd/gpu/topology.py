@@ -19,7 +19,7 @@ from ..models import kube
 RANK_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "NODE_RANK", "NNODES",
              "ROLE_RANK", "ROLE_WORLD_SIZE", "JOB_COMPLETION_INDEX", "MASTER_ADDR", "MASTER_PORT")
 DEVICE_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
-COLLECTIVE_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_", "MSCCL", "UCX_")
+COLLECTIVE_PREFIXES = kube.ENV_PREFIXES  # the decoder keeps exactly these env families
 # MI355X node: 8 OAM GPUs, every pair joined by xGMI (7 links per GPU)
 GPUS_PER_NODE = 8
 XGMI_LINKS_PER_GPU = 7

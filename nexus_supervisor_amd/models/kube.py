@@ -162,18 +162,30 @@ def waiting_states(pod) -> Iterable[Dict[str, Any]]:
 
 
 def pod_env(pod) -> Dict[str, str]:
-    """Merged literal env of all containers (first definition wins)."""
+    """Merged literal env of all containers (first definition wins).  A container's env is
+    a list of ``{"name", "value"}`` (API shape) or, decoded natively, already a ``{name:
+    value}`` dict of the variables in :data:`ENV_KEEP` / :data:`ENV_PREFIXES`."""
     spec = pod.get("spec")
     if not spec:
         return {}
     cached = spec.get("_env")
     if cached is not None:
         return cached
+    containers = spec.get("containers") or []
+    if len(containers) == 1 and isinstance(containers[0].get("env"), dict):
+        out = spec["_env"] = containers[0]["env"]  # the decoder's dict (one container: nothing to merge)
+        return out
     out: Dict[str, str] = {}
     # memoised on the (per-version) spec: computed only for pods a rule actually inspects
     spec["_env"] = out
-    for c in spec.get("containers") or []:
-        for e in c.get("env") or []:
+    for c in containers:
+        env = c.get("env") or ()
+        if isinstance(env, dict):
+            for n, v in env.items():
+                if n not in out:
+                    out[n] = v
+            continue
+        for e in env:
             n = e.get("name")
             if n and n not in out and e.get("value") is not None:
                 out[n] = e["value"]
@@ -209,12 +221,21 @@ _META = {"name": True, "namespace": True, "uid": True, "resourceVersion": True, 
          "deletionTimestamp": True, "labels": True, "annotations": ["prefix", *_KEEP_ANNOTATIONS_PREFIXES],
          "ownerReferences": ["list", {"kind": True, "name": True, "uid": True}]}
 _CONDITIONS = ["list", {"type": True, "status": True, "reason": True, "message": True}]
+# Container env variables anything in the supervisor reads (the rank / device / collective
+# fold of gpu/topology.py).  The native decoder turns each container's env list into a
+# {name: value} dict of just these while decoding: a torchrun pod's env was most of the
+# cost of decoding a pod line (10 dicts of 2 strings each), and no other variable is used.
+ENV_KEEP = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "NODE_RANK", "NNODES",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "JOB_COMPLETION_INDEX", "MASTER_ADDR", "MASTER_PORT",
+            "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+ENV_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_", "MSCCL", "UCX_")
 _CSTATUS = ["list", {"name": True, "state": True, "lastState": True, "restartCount": True, "ready": True, "started": True}]
 
 PROJECTIONS: Dict[str, Any] = {
     "Pod": dict(_STATUS_FIELDS, metadata=_META, spec={
         "nodeName": True,
-        "containers": ["list", {"name": True, "env": ["list", {"name": True, "value": True}], "resources": True}]},
+        "containers": ["list", {"name": True, "env": ["kv", "name", "value", list(ENV_KEEP), list(ENV_PREFIXES)],
+                                "resources": True}]},
         status={"phase": True, "reason": True, "message": True, "hostIP": True, "podIP": True, "startTime": True,
                 "containerStatuses": _CSTATUS, "initContainerStatuses": _CSTATUS, "conditions": _CONDITIONS}),
     "Job": dict(_STATUS_FIELDS, metadata=_META, spec={

@@ -73,3 +73,34 @@ def test_deleted_watch_events_decode_identity_only():
     (ge,) = K.ProjectedDecoder(kube.watch_projection("Event")).feed((_json.dumps({"type": "DELETED", "object": ev}) + "\n").encode())
     assert ge["object"]["involvedObject"] == {"kind": "Job", "name": "j"}
     assert "source" not in ge["object"] and "count" not in ge["object"]
+
+
+def test_kv_env_projection_keeps_what_topology_reads():
+    """Pods decode their container env into a filtered {name: value} dict; every variable
+    gpu/topology.py reads must survive it (models/kube.py ENV_KEEP / ENV_PREFIXES)."""
+    import json as _json
+
+    from nexus_supervisor_amd.gpu import topology as T
+    from nexus_supervisor_amd.models import kube as KM
+    from nexus_supervisor_amd.models.kube import watch_projection
+
+    read = {v for v, _k in T._INT_VARS} | set(T.RANK_VARS) | set(T.DEVICE_VARS) | {"MASTER_ADDR"}
+    assert read <= set(KM.ENV_KEEP)
+    assert T.COLLECTIVE_PREFIXES == KM.ENV_PREFIXES
+    env = [{"name": "RANK", "value": "3"}, {"name": "PATH", "value": "/bin"}, {"name": "NCCL_DEBUG", "value": "INFO"},
+           {"name": "RANK", "value": "9"}, {"name": "SECRET", "valueFrom": {"secretKeyRef": {"name": "s"}}},
+           {"name": "HIP_VISIBLE_DEVICES", "value": "4,5,6,7"}, {"name": "MASTER_ADDR", "value": "h\\u00e9st"}]
+    pod = {"kind": "Pod", "metadata": {"name": "p", "resourceVersion": "1"},
+           "spec": {"containers": [{"name": "a", "env": env}, {"name": "b", "env": [{"name": "LOCAL_RANK", "value": "1"},
+                                                                                    {"name": "RANK", "value": "7"}]}]}}
+    line = (_json.dumps({"type": "ADDED", "object": pod}) + "\n").encode()
+    out = K.ProjectedDecoder(watch_projection("Pod")).feed(line)[0]["object"]
+    c0 = out["spec"]["containers"][0]["env"]
+    assert c0 == {"RANK": "3", "NCCL_DEBUG": "INFO", "HIP_VISIBLE_DEVICES": "4,5,6,7", "MASTER_ADDR": "h\\u00e9st"}
+    merged = KM.pod_env(out)
+    assert merged["RANK"] == "3" and merged["LOCAL_RANK"] == "1" and "PATH" not in merged
+    # the same pod in API shape folds to the same topology
+    raw = _json.loads(line)["object"]
+    t1 = T.topology_from_env(KM.pod_env(out), 1, "")
+    t2 = T.topology_from_env({k: v for k, v in KM.pod_env(raw).items()}, 1, "")
+    assert t1 == t2 and t1["visible_devices"] == ["4", "5", "6", "7"] and t1["rank"] == 3
