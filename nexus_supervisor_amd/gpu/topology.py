@@ -207,12 +207,33 @@ def resolve_devices(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, Any]]
     return out
 
 
+_XGMI_MEMO: Dict[Tuple, Dict[str, Any]] = {}
+
+
 def xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, Any]]) -> Dict[str, Any]:
     """Replace the platform-default xGMI block with the measured fabric of the pod's GPUs
-    (link metrics the native monitor read from amd-smi: peers, rates, link status)."""
+    (link metrics the native monitor read from amd-smi: peers, rates, link status).  The
+    block depends only on the GPUs' link records, which one telemetry snapshot shares
+    between every pod's evidence: it is built once per snapshot and GPU set (shared,
+    never mutated)."""
     gpus = [g for g in (gpu_evidence or {}).get("gpus", []) if g.get("links") is not None]
     if not gpus:
         return topo
+    key = (gpu_evidence.get("source"),) + tuple((g.get("index"), id(g["links"]), g.get("xgmi_links_up"),
+                                                 g.get("xgmi_links_down"), g.get("xgmi_hive_id")) for g in gpus)
+    hit = _XGMI_MEMO.get(key)
+    if hit is not None and all(h is g["links"] for h, g in zip(hit["_links"], gpus)):
+        out = dict(topo)
+        out["xgmi"] = hit["rec"]
+        return out
+    out = _xgmi_from_evidence(topo, gpu_evidence, gpus)
+    if len(_XGMI_MEMO) > 256:
+        _XGMI_MEMO.clear()
+    _XGMI_MEMO[key] = {"rec": out["xgmi"], "_links": [g["links"] for g in gpus]}  # keeps the ids alive
+    return out
+
+
+def _xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Dict[str, Any], gpus: List[Dict[str, Any]]) -> Dict[str, Any]:
     idx = {g.get("index") for g in gpus}
     links, hive = [], set()
     for g in gpus:

@@ -408,6 +408,7 @@ class CqlSession:
         self.discover = discover
         self.shard_aware = shard_aware and sni_proxy is None
         self._sharded = False  # some node advertised Scylla shards
+        self._tokens: Dict[tuple, int] = {}  # partition key values → token (recent)
         self.per_shard = max(1, connections_per_shard)
         self.hosts: Dict[Tuple[str, int], Host] = {}
         self._ring: List[int] = []
@@ -685,13 +686,21 @@ class CqlSession:
     def routing_token(self, ps: PreparedStatement, values: Sequence[Any]) -> Optional[int]:
         if not ps.pk_indexes or not (self._ring or self._sharded):
             return None
+        key = tuple(values[i] for i in ps.pk_indexes)
+        tok = self._tokens.get(key)  # a decision reads then writes the same partition
+        if tok is not None:
+            return tok
         parts = []
         for i in ps.pk_indexes:
             v = values[i]
             if v is None:
                 return None
             parts.append(N.serialize(v, ps.bind_types[i]))
-        return N.token_for(parts)
+        tok = N.token_for(parts)
+        if len(self._tokens) > 8192:
+            self._tokens.clear()
+        self._tokens[key] = tok
+        return tok
 
     async def execute(self, ps_or_query, values: Sequence[Any] = (), *, consistency: Optional[int] = None,
                       serial: Optional[int] = None, idempotent: bool = True, timeout: Optional[float] = None):
