@@ -5,7 +5,9 @@
 // Compared with CPython's C encoder this skips the per-container circular-reference
 // markers dict (a depth limit guards runaway recursion instead), reuses UTF-8 caches of
 // compact strings without copying, and writes straight into one growing buffer.
-// Output is UTF-8 (ensure_ascii=False semantics) with compact separators.
+// Output is UTF-8 (ensure_ascii=False semantics) with compact separators.  A value of a
+// bytes *subclass* is pre-encoded JSON and is copied verbatim (classify.RawJSON: a
+// sub-document shared by many outputs is encoded once); plain bytes go to default=.
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
@@ -207,6 +209,10 @@ struct Enc {
     if (PyLong_Check(o)) return number_int(o);
     if (PyList_Check(o) || PyTuple_Check(o)) return seq(o, depth);
     if (PyFloat_Check(o)) return number_float(o);
+    if (PyBytes_Check(o) && Py_TYPE(o) != &PyBytes_Type) {  // bytes subclass = pre-encoded JSON (RawJSON)
+      out.append(PyBytes_AS_STRING(o), static_cast<size_t>(PyBytes_GET_SIZE(o)));
+      return true;
+    }
     if (dflt) {
       PyObject* r = PyObject_CallOneArg(dflt, o);
       if (!r) return false;

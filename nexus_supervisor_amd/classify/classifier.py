@@ -449,14 +449,43 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
            "source": res.evidence.get("source", "")}
     doc.update(extra)
     gpu, topo = doc.get("gpu"), doc.get("topology")
-    if gpu and topo and (topo.get("xgmi") or {}).get("links") is not None:
+    xgmi = (topo or {}).get("xgmi")
+    if gpu and xgmi and xgmi.get("links") is not None:
         # the measured links are listed once, under topology.xgmi (with their GPU index)
         doc["gpu"] = dict(gpu, gpus=[{k: v for k, v in g.items() if k != "links"} for g in gpu.get("gpus", ())])
+    if xgmi and _native_dumps is not None:
+        # the xGMI block is shared by every decision of one telemetry snapshot
+        # (topology.xgmi_from_evidence): encode it once, splice it into each trace
+        doc["topology"] = dict(topo, xgmi=_raw_json(xgmi))
     # key order is the (deterministic) construction order: sorting every object doubled the
     # cost of the largest per-decision serialisation (profiles/r2_*_pprof_*)
     if _native_dumps is not None:
         return _native_dumps(doc, default=str).decode()
-    return json.dumps(doc, separators=(",", ":"), default=str, ensure_ascii=False)
+    return json.dumps(doc, separators=(",", ":"), default=_json_default, ensure_ascii=False)
+
+
+class RawJSON(bytes):
+    """Pre-encoded JSON spliced verbatim by the native encoder."""
+
+
+_RAW_MEMO: Dict[int, Tuple[Any, RawJSON]] = {}
+
+
+def _raw_json(obj) -> RawJSON:
+    hit = _RAW_MEMO.get(id(obj))
+    if hit is not None and hit[0] is obj:
+        return hit[1]
+    raw = RawJSON(_native_dumps(obj, default=str))
+    if len(_RAW_MEMO) > 512:
+        _RAW_MEMO.clear()
+    _RAW_MEMO[id(obj)] = (obj, raw)  # holds obj: its id cannot be reused while cached
+    return raw
+
+
+def _json_default(o):
+    if isinstance(o, RawJSON):
+        return json.loads(o)
+    return str(o)
 
 
 try:  # compact UTF-8 JSON (csrc/kube/json_encode.cpp); same document as the json fallback

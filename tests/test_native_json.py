@@ -104,3 +104,15 @@ def test_kv_env_projection_keeps_what_topology_reads():
     t1 = T.topology_from_env(KM.pod_env(out), 1, "")
     t2 = T.topology_from_env({k: v for k, v in KM.pod_env(raw).items()}, 1, "")
     assert t1 == t2 and t1["visible_devices"] == ["4", "5", "6", "7"] and t1["rank"] == 3
+
+
+def test_raw_json_splice_and_trace_equivalence():
+    from nexus_supervisor_amd.classify.classifier import RawJSON, _json_default
+
+    inner = {"links": [{"gpu": 0, "peer": 1}], "fully_connected": True}
+    raw = RawJSON(K.dumps(inner))
+    doc = {"a": 1, "topology": {"xgmi": raw}, "b": b"plain"}
+    out = K.dumps(doc, default=str)
+    back = json.loads(out)
+    assert back["topology"]["xgmi"] == inner and back["b"] == "b'plain'"
+    assert json.loads(json.dumps(doc, default=_json_default)) == back
