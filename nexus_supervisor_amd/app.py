@@ -122,11 +122,13 @@ class Application:
                 lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
                 on_started_leading=lambda: self.supervisor.set_active(True),
                 on_stopped_leading=lambda: self.supervisor.set_active(False), metrics=self.metrics)
+        if self.shard_leases is not None:
+            # before the cache sync: with shard leases the informers cache only owned shards,
+            # so a replica that synced first would list nothing and reach the lease race last
+            self.shard_leases.start()
         await self.supervisor.start()
         if self.elector is not None:
             self.elector.start()
-        if self.shard_leases is not None:
-            self.shard_leases.start()
 
     def ready(self) -> bool:
         return self.factory is not None and all(i.has_synced() for i in self.factory.informers.values())

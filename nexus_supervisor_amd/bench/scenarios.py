@@ -91,8 +91,9 @@ class Cluster:
     """Fake apiserver (HTTP) + native CQL server + ``replicas`` supervisor applications."""
 
     def __init__(self, jobs: int, profile: str, replicas: int = 1, leader_election: bool = False, seed: int = 0,
-                 persist: bool = False, telemetry=None):
+                 persist: bool = False, telemetry=None, shards: int = 0):
         self.jobs, self.profile, self.replicas, self.le = jobs, profile, replicas, leader_election
+        self.shards = shards  # > 0: runs split over this many shards held through per-shard Leases
         self.wl = Workload(concurrent_jobs=jobs, seed=seed)
         self.clock = AckClock()
         self.persist = persist
@@ -104,9 +105,11 @@ class Cluster:
                 "failure-rate-max-delay": "500ms", "max-retries": 0,
                 "scylla-cql-store": {"hosts": [f"127.0.0.1:{self.srv.port}"], "request-timeout": "1s"}}
         over.update(PROFILES[self.profile])
-        if self.le:
-            over["leader-election"] = {"enabled": True, "identity": ident, "lease-duration": "2s",
-                                       "renew-deadline": "1500ms", "retry-period": "200ms"}
+        if self.le or self.shards:
+            over["leader-election"] = {"enabled": bool(self.le and not self.shards), "identity": ident,
+                                       "lease-duration": "2s", "renew-deadline": "1500ms", "retry-period": "200ms"}
+        if self.shards:
+            over["sharding"] = {"shards": self.shards, "mode": "lease", "replicas": self.replicas}
         return load_config(path=None, env={}, overrides=over)
 
     async def start(self) -> None:
@@ -128,7 +131,7 @@ class Cluster:
                           telemetry=self.telemetry)
         app.supervisor.decision_hooks.append(self.clock)
         await app.start()
-        if not self.le:
+        if not self.le and not self.shards:
             await app.supervisor.factory.wait_for_cache_sync(60)
         self.apps.append(app)
         return app
@@ -157,17 +160,25 @@ class Cluster:
             (self.api.create if etype == "ADDED" else self.api.update)(obj, copy_obj=False)
         return failed
 
-    async def final_stages(self, rids) -> Dict[str, int]:
-        bad = 0
+    async def final_stages(self, rids) -> Dict[str, Any]:
+        bad = []
         for rid in rids:
             row = await self.store.read_checkpoint(self.wl.algorithm, rid)
             if row is None or row.lifecycle_stage != self.wl.expected[rid]:
-                bad += 1
-        return {"checked": len(rids), "wrong_stage": bad}
+                bad.append([rid, row.lifecycle_stage if row else None, self.wl.expected[rid],
+                            self.wl.kind_of.get(rid)])
+        out: Dict[str, Any] = {"checked": len(rids), "wrong_stage": len(bad)}
+        if bad:
+            out["wrong_examples"] = bad[:5]
+        return out
 
     def leader(self) -> Optional[Application]:
         act = [a for a in self.apps if a.supervisor.active]
         return act[0] if act else None
+
+    def shard_owners(self) -> Dict[int, List[str]]:
+        return {k: [a.cfg.leader_election.identity for a in self.apps if a.shard_leases and k in a.shard_leases.owned]
+                for k in range(self.shards)}
 
     async def stop(self) -> None:
         for a in self.apps:
@@ -290,6 +301,56 @@ async def cfg5_chaos(profile: str, seconds: float = 30.0, rate: float = 1000.0, 
         await c.stop()
 
 
+async def cfg5s_sharded_chaos(profile: str, seconds: float = 30.0, rate: float = 1000.0, jobs: int = 10_000,
+                              replicas: int = 3, shards: int = 6) -> Dict[str, Any]:
+    """Config 5 with horizontal scale: ``replicas`` replicas split the runs over ``shards``
+    shard Leases (fair share ``ceil(shards / replicas)``); chaos = CQL node restart, an
+    eviction storm, and a replica dying holding its shard Leases — its shards must move to
+    the survivors and every run must still end in its expected stage."""
+    c = Cluster(jobs=jobs, profile=profile, replicas=replicas, persist=True, shards=shards)
+    await c.start()
+    marks: Dict[str, Any] = {}
+    try:
+        deadline = time.monotonic() + 30
+        while any(len(v) != 1 for v in c.shard_owners().values()) and time.monotonic() < deadline:
+            await asyncio.sleep(0.05)
+        marks["initial_owners"] = c.shard_owners()
+
+        async def chaos(t: float) -> None:
+            if t >= seconds * 0.2 and "cql_restart" not in marks:
+                marks["cql_restart"] = round(t, 2)
+                c.srv.restart()
+            if t >= seconds * 0.4 and "storm" not in marks:
+                marks["storm"] = round(t, 2)
+                await c.push(50, kinds=["evicted"])
+            if t >= seconds * 0.6 and "replica_crash" not in marks:
+                marks["replica_crash"] = round(t, 2)
+                victim = next(a for a in c.apps if a.shard_leases.owned)
+                lost = sorted(victim.shard_leases.owned)
+                marks["crashed"] = {"replica": victim.cfg.leader_election.identity, "shards": lost}
+                await victim.shard_leases.stop(release=False)  # dies holding its leases
+                c.apps.remove(victim)
+                await victim.stop(drain_timeout=0.2)
+                asyncio.ensure_future(_failover(time.monotonic(), lost))
+
+        async def _failover(t_crash: float, lost) -> None:
+            while any(not c.shard_owners()[k] for k in lost):
+                await asyncio.sleep(0.01)
+            marks["failover_s"] = round(time.monotonic() - t_crash, 3)
+            marks["final_owners"] = c.shard_owners()
+
+        t0 = time.monotonic()
+        await _open_loop(c, rate, seconds, chaos)
+        rids = list(c.clock.pushed)
+        ok = await c.clock.wait(rids, 180)
+        dt = time.monotonic() - t0
+        return _summary(f"5s: {replicas} replicas x {shards} shard leases, {jobs} jobs, chaos", profile,
+                        c.clock.latencies_ms(rids), len(rids), dt, drained=ok, chaos=marks,
+                        **(await c.final_stages(rids)))
+    finally:
+        await c.stop()
+
+
 async def cfg3_gpu(profile: str, holders: int = 7, hold_gib: float = 30.0) -> Dict[str, Any]:
     """Real MI355X: ``holders`` pods keep ``hold_gib`` each resident on the GPU while one
     more pod allocates until HIP reports out-of-memory; its failure is pushed with the
@@ -344,7 +405,7 @@ async def cfg3_gpu(profile: str, holders: int = 7, hold_gib: float = 30.0) -> Di
         tel.stop()
 
 
-CONFIGS = {"1": cfg1_single, "2": cfg2_burst, "3": cfg3_gpu, "4": cfg4_rate, "5": cfg5_chaos}
+CONFIGS = {"1": cfg1_single, "2": cfg2_burst, "3": cfg3_gpu, "4": cfg4_rate, "5": cfg5_chaos, "5s": cfg5s_sharded_chaos}
 
 
 async def run_all(only: List[str], profiles: List[str], seconds: float, jobs: int) -> List[Dict[str, Any]]:
@@ -352,7 +413,7 @@ async def run_all(only: List[str], profiles: List[str], seconds: float, jobs: in
     for k in only:
         for prof in profiles:
             fn = CONFIGS[k]
-            kw = {"seconds": seconds, "jobs": jobs} if k in ("4", "5") else {}
+            kw = {"seconds": seconds, "jobs": jobs} if k in ("4", "5", "5s") else {}
             t0 = time.monotonic()
             res = await fn(prof, **kw)
             res["wall_s"] = round(time.monotonic() - t0, 2)
@@ -363,7 +424,7 @@ async def run_all(only: List[str], profiles: List[str], seconds: float, jobs: in
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--only", default="1,2,4,5")
+    ap.add_argument("--only", default="1,2,4,5,5s")
     ap.add_argument("--gpu", action="store_true", help="include config 3 (needs an MI355X)")
     ap.add_argument("--profiles", default="reference,uncapped")
     ap.add_argument("--seconds", type=float, default=30.0, help="duration of the open-loop configs 4 and 5")

@@ -72,6 +72,7 @@ class Workload:
         self.pods: Dict[str, Dict[str, Any]] = {}
         self.jobs: Dict[str, Dict[str, Any]] = {}
         self.expected: Dict[str, str] = {}
+        self.kind_of: Dict[str, str] = {}  # failed run → failure kind (diagnostics)
         self._rv = 1000
         self._seq = 0
         self.concurrent_jobs = concurrent_jobs
@@ -187,6 +188,7 @@ class Workload:
             out.append(("ADDED", make_event("Job", rid, "DeadlineExceeded", ns=self.ns,
                                             message="Job was active longer than specified deadline")))
         self.expected[rid] = self._stage[kind]
+        self.kind_of[rid] = kind
         return out
 
     def step(self, events: int, kinds: Optional[List[str]] = None

@@ -12,8 +12,11 @@ makes that safe but leaves every replica but one idle.  Here the runs are split 
 * it competes for free shards (never created, released, or expired as observed
   locally) while it holds fewer than its fair share ``ceil(shards / replicas)``
   (``sharding.replicas``, the Helm replica count; 0 = take everything);
-* a shard left free for a further full ``lease-duration`` is orphaned — its fair-share
-  owner is gone — and any replica takes it, so N−1 survivors cover all shards;
+* a shard whose lease *expired* under a holder (that replica crashed) is taken by anyone
+  after a short grace (two retry periods, so replicas below their share win the race),
+  and a shard *never held or released* after a full ``lease-duration`` — so N−1 survivors
+  cover all shards, a crash costs about one lease duration, and a cold start or rolling
+  restart still spreads the shards before anyone exceeds its share;
 * candidates walk the shards in an order rotated by their identity hash, so replicas
   starting together rarely collide on the same lease (a collision is a 409 anyway);
 * on shutdown the held leases are released so survivors take over within a retry
@@ -137,7 +140,10 @@ class ShardLeaseManager:
                 self.free_since.pop(k, None)
                 continue
             since = self.free_since.setdefault(k, now)
-            orphaned = now - since >= self.lease_duration
+            # expired under a holder (crash): short grace; never held / released: a lease duration
+            grace = 2 * self.retry_period if e.observed_holder and e.observed_holder != self.identity \
+                else self.lease_duration
+            orphaned = now - since >= grace
             if len(self.held) >= self.target and not orphaned:
                 continue
             try:

@@ -132,6 +132,7 @@ class Supervisor:
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
         self._deletes: Dict[Any, str] = {}  # in-flight asynchronous Job DELETEs → request id
+        self._bg: set = set()  # housekeeping tasks (post-re-list replays)
         self._sweeper: Optional[asyncio.Task] = None
         self.decision_hooks: List[Callable[[Decision], None]] = []
         # leader gating flips this; with shard leases ownership is per shard (self.shards)
@@ -206,6 +207,8 @@ class Supervisor:
 
     async def stop(self, drain: bool = True, timeout: float = 10.0) -> None:
         self.gc_tuner.stop()
+        for t in list(self._bg):
+            t.cancel()
         if self._sweeper:
             self._sweeper.cancel()
             try:
@@ -274,14 +277,33 @@ class Supervisor:
         if gained:
             self.metrics.inc("shards_gained", len(gained))
             self.replay(lambda rid: self.shards.of(rid) in gained)
+            infs = (self.event_informer, self.pod_informer, self.job_informer)
+            before = [inf.relists for inf in infs]
             if self.worker_shard is not None and not self.hub_fed:
-                for inf in (self.event_informer, self.pod_informer, self.job_informer):
+                for inf in infs:
                     inf.relist()
+            # the three kinds re-list independently: an Event of a gained run can be applied
+            # before its Job and parked; replay the gained shards once more after every
+            # informer took its new list (or the hub's fresh snapshot), so no ordering of
+            # the re-lists can strand a decision
+            t = asyncio.ensure_future(self._replay_after_relist(infs, before, gained))
+            self._bg.add(t)
+            t.add_done_callback(self._bg.discard)
         self.metrics.set("shards_owned", float(len(self.shards.owned or ())))
         if gained or lost:
             self.log.info("replica shards changed", owned=sorted(self.shards.owned or ()), gained=sorted(gained),
                           lost=sorted(lost))
         return gained, lost
+
+    async def _replay_after_relist(self, infs, before, gained, timeout: float = 10.0) -> None:
+        deadline = time.monotonic() + timeout
+        while any(inf.relists == b for inf, b in zip(infs, before)) and time.monotonic() < deadline:
+            await asyncio.sleep(0.05)
+        owned = self.shards.owned or frozenset()
+        still = frozenset(gained) & owned
+        if still and self.active:
+            self.metrics.inc("shard_replays")
+            self.replay(lambda rid: self.shards.of(rid) in still)
 
     def fence_shards(self, lost) -> int:
         of = self.shards.of

@@ -124,3 +124,20 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
         srv.stop()
 
     arun(go(), timeout=120)
+
+
+def test_sharded_replicas_survive_cql_restart_storm_and_a_replica_crash(arun):
+    """BASELINE config 5 with horizontal scale: 3 replicas over 6 shard Leases; a CQL node
+    restart, an eviction storm and a replica dying with its leases mid-stream.  Its shards
+    move to the survivors and every failed run ends in its expected stage."""
+    from nexus_supervisor_amd.bench.scenarios import cfg5s_sharded_chaos
+
+    async def go():
+        r = await cfg5s_sharded_chaos("uncapped", seconds=8, rate=3000, jobs=600)
+        assert r["drained"] and r["acked"] == r["events"] and r["wrong_stage"] == 0, r
+        ch = r["chaos"]
+        lost = ch["crashed"]["shards"]
+        assert lost and all(ch["final_owners"][k] and ch["final_owners"][k] != [ch["crashed"]["replica"]] for k in lost)
+        assert ch["failover_s"] < 2.0 + 1.5  # lease duration + grace + observation
+
+    arun(go(), timeout=120)
