@@ -306,13 +306,20 @@ async def cfg5s_sharded_chaos(profile: str, seconds: float = 30.0, rate: float =
     """Config 5 with horizontal scale: ``replicas`` replicas split the runs over ``shards``
     shard Leases (fair share ``ceil(shards / replicas)``); chaos = CQL node restart, an
     eviction storm, and a replica dying holding its shard Leases — its shards must move to
-    the survivors and every run must still end in its expected stage."""
+    the survivors, the replica's return must win its share back (rebalancing), and every
+    run must still end in its expected stage."""
     c = Cluster(jobs=jobs, profile=profile, replicas=replicas, persist=True, shards=shards)
     await c.start()
     marks: Dict[str, Any] = {}
     try:
         deadline = time.monotonic() + 30
-        while any(len(v) != 1 for v in c.shard_owners().values()) and time.monotonic() < deadline:
+
+        def settled() -> bool:  # every shard owned once, and the shares balanced (rebalancing)
+            own = c.shard_owners()
+            per = [sum(1 for v in own.values() if a.cfg.leader_election.identity in v) for a in c.apps]
+            return all(len(v) == 1 for v in own.values()) and max(per) - min(per) <= 1
+
+        while not settled() and time.monotonic() < deadline:
             await asyncio.sleep(0.05)
         marks["initial_owners"] = c.shard_owners()
 
@@ -332,6 +339,14 @@ async def cfg5s_sharded_chaos(profile: str, seconds: float = 30.0, rate: float =
                 c.apps.remove(victim)
                 await victim.stop(drain_timeout=0.2)
                 asyncio.ensure_future(_failover(time.monotonic(), lost))
+            if t >= seconds * 0.8 and "failover_s" in marks and "replica_return" not in marks:
+                await _return(t)
+
+        async def _return(t: float) -> None:
+            # the crashed replica comes back (pod restarted): rebalancing hands it its share
+            marks["replica_return"] = round(t, 2)
+            marks["t_return"] = time.monotonic()
+            await c.add_replica(marks["crashed"]["replica"])
 
         async def _failover(t_crash: float, lost) -> None:
             while any(not c.shard_owners()[k] for k in lost):
@@ -341,9 +356,21 @@ async def cfg5s_sharded_chaos(profile: str, seconds: float = 30.0, rate: float =
 
         t0 = time.monotonic()
         await _open_loop(c, rate, seconds, chaos)
+        if "crashed" in marks and "replica_return" not in marks:
+            deadline = time.monotonic() + 30
+            while "failover_s" not in marks and time.monotonic() < deadline:
+                await asyncio.sleep(0.05)
+            await _return(round(time.monotonic() - t0, 2))
         rids = list(c.clock.pushed)
         ok = await c.clock.wait(rids, 180)
         dt = time.monotonic() - t0
+        if "t_return" in marks:
+            deadline = time.monotonic() + 30
+            while not settled() and time.monotonic() < deadline:
+                await asyncio.sleep(0.05)
+            marks["rebalanced"] = settled()
+            marks["rebalanced_owners"] = c.shard_owners()
+            marks["rebalance_s"] = round(time.monotonic() - marks.pop("t_return"), 3)
         return _summary(f"5s: {replicas} replicas x {shards} shard leases, {jobs} jobs, chaos", profile,
                         c.clock.latencies_ms(rids), len(rids), dt, drained=ok, chaos=marks,
                         **(await c.final_stages(rids)))

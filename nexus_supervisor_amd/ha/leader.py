@@ -39,11 +39,12 @@ def _micro(t: Optional[float] = None) -> str:
 class LeaseLock:
     """Read/create/update one Lease object through a :class:`KubeClient`-like API."""
 
-    def __init__(self, client, namespace: str, name: str, identity: str):
+    def __init__(self, client, namespace: str, name: str, identity: str, labels: Optional[dict] = None):
         self.client = client
         self.namespace = namespace
         self.name = name
         self.identity = identity
+        self.labels = dict(labels or {})
 
     async def get(self):
         try:
@@ -52,8 +53,10 @@ class LeaseLock:
             return None
 
     async def create(self, spec):
-        body = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
-                "metadata": {"name": self.name, "namespace": self.namespace}, "spec": spec}
+        md = {"name": self.name, "namespace": self.namespace}
+        if self.labels:
+            md["labels"] = dict(self.labels)
+        body = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease", "metadata": md, "spec": spec}
         return await self.client.create("Lease", self.namespace, body)
 
     async def update(self, lease, spec):

@@ -20,7 +20,14 @@ makes that safe but leaves every replica but one idle.  Here the runs are split 
 * candidates walk the shards in an order rotated by their identity hash, so replicas
   starting together rarely collide on the same lease (a collision is a 409 anyway);
 * on shutdown the held leases are released so survivors take over within a retry
-  period instead of a lease duration.
+  period instead of a lease duration;
+* every replica also renews a *membership* Lease (``<lease-name>-member-<identity>``,
+  labelled with the group) and lists the group each round: the fair share is computed
+  over ``max(sharding.replicas, live members)``, and when a live member holds fewer
+  than ``shards // members`` shards the richest replica (ties: highest identity) fences
+  and releases one shard per round — so a replica that starts late, or comes back after
+  its shards failed over, gets its share back instead of idling until the next restart
+  (the taker is below its share and acquires a released shard on its next round).
 
 Changes of the held set are reported through ``on_change(frozenset)``: the replica
 fences lost shards and replays gained ones (``Supervisor.set_shards``).
@@ -29,17 +36,30 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import re
 import time
 import zlib
-from typing import Callable, Dict, FrozenSet, List, Optional
+from typing import Callable, Dict, FrozenSet, List, Optional, Tuple
 
 from .leader import LeaderElector, LeaseLock
 
 log = logging.getLogger("nexus_supervisor_amd.shards")
 
 
+MEMBER_LABEL = "nexus.sneaksanddata.com/shard-lease-group"
+
+
 def shard_lease_name(base: str, k: int) -> str:
     return f"{base}-shard-{k}"
+
+
+def member_lease_name(base: str, identity: str) -> str:
+    """DNS-1123 subdomain name of a replica's membership Lease."""
+    ident = re.sub(r"[^a-z0-9.-]+", "-", identity.lower()).strip("-.") or "replica"
+    name = f"{base}-member-{ident}"
+    if len(name) > 253:
+        name = f"{name[:240]}-{zlib.crc32(identity.encode()):08x}"
+    return name
 
 
 class ShardLeaseManager:
@@ -49,6 +69,9 @@ class ShardLeaseManager:
                  metrics=None, clock: Callable[[], float] = time.monotonic):
         if shards < 1:
             raise ValueError("shards must be >= 1")
+        self.client = client
+        self.namespace = namespace
+        self.base_name = base_name
         self.identity = identity
         self.shards = shards
         self.lease_duration = lease_duration
@@ -57,7 +80,18 @@ class ShardLeaseManager:
         self.on_change = on_change
         self.metrics = metrics
         self.clock = clock
+        self.replicas = replicas
         self.target = -(-shards // replicas) if replicas > 0 else shards
+        self.member = LeaderElector(LeaseLock(client, namespace, member_lease_name(base_name, identity), identity,
+                                              labels={MEMBER_LABEL: base_name}),
+                                    lease_duration=lease_duration, renew_deadline=renew_deadline,
+                                    retry_period=retry_period, clock=clock)
+        self._seen: Dict[str, Tuple[str, float]] = {}  # member → (last renewTime seen, local clock it changed)
+        self.members: FrozenSet[str] = frozenset({identity})
+        self.counts: Dict[str, int] = {}  # live holder → shards it holds (as last observed)
+        self._last_release = float("-inf")
+        self._released: Dict[int, float] = {}  # shard → clock this replica handed it back
+        self.rebalances = 0
         self.electors: List[LeaderElector] = [
             LeaderElector(LeaseLock(client, namespace, shard_lease_name(base_name, k), identity),
                           lease_duration=lease_duration, renew_deadline=renew_deadline, retry_period=retry_period,
@@ -97,6 +131,10 @@ class ShardLeaseManager:
                     await self.electors[k]._release()  # noqa: SLF001 - same package
                 except Exception as exc:  # noqa: BLE001
                     log.warning("shard %d lease release failed: %s", k, exc)
+            try:
+                await self.member._release()  # noqa: SLF001
+            except Exception as exc:  # noqa: BLE001
+                log.warning("membership lease release failed: %s", exc)
 
     async def _run(self) -> None:
         while True:
@@ -108,9 +146,54 @@ class ShardLeaseManager:
                 log.warning("shard leases: %s", exc)
             await asyncio.sleep(self.retry_period)
 
+    async def _refresh_members(self) -> None:
+        """Renew this replica's membership Lease and list the group's: a member is live
+        while its ``renewTime`` keeps changing within a lease duration (observed locally,
+        as for the shard leases — no cross-node clock comparison)."""
+        try:
+            await self.member.try_acquire_or_renew()
+            items, _ = await self.client.list("Lease", self.namespace, label_selector=f"{MEMBER_LABEL}={self.base_name}")
+        except Exception as exc:  # noqa: BLE001 - keep the last view; the fair share falls back to `replicas`
+            log.warning("shard membership: %s", exc)
+            return
+        now = self.clock()
+        live = {self.identity}
+        for it in items:
+            spec = it.get("spec") or {}
+            holder = spec.get("holderIdentity") or ""
+            if not holder:
+                continue  # released on shutdown
+            renew = str(spec.get("renewTime") or "")
+            prev = self._seen.get(holder)
+            if prev is None or prev[0] != renew:
+                self._seen[holder] = (renew, now)
+            if now - self._seen[holder][1] < self.lease_duration:
+                live.add(holder)
+        self.members = frozenset(live)
+        denom = max(self.replicas, len(live))
+        self.target = -(-self.shards // denom) if (self.replicas > 0 or len(live) > 1) else self.shards
+
+    def _rebalance_pick(self) -> Optional[int]:
+        """A shard to hand back: only when some live member holds fewer than the floor of
+        the fair share and this replica is the richest (ties → highest identity), at most
+        one per two retry periods so observations catch up between moves."""
+        members = self.members
+        if len(members) < 2 or not self.held:
+            return None
+        floor = self.shards // max(self.replicas, len(members))
+        counts = {m: self.counts.get(m, 0) for m in members}
+        counts[self.identity] = len(self.held)
+        if len(self.held) <= floor or not any(c < floor for m, c in counts.items() if m != self.identity):
+            return None
+        richest = max(counts.items(), key=lambda kv: (kv[1], kv[0]))[0]
+        if richest != self.identity or self.clock() - self._last_release < 2 * self.retry_period:
+            return None
+        return max(self.held, key=self.order.index)  # the shard this replica would take last
+
     async def tick(self) -> None:
-        """One round: renew what is held, then compete for free shards."""
+        """One round: membership, renew what is held, compete for free shards, rebalance."""
         changed = False
+        await self._refresh_members()
         for k in sorted(self.held):
             try:
                 ok = await asyncio.wait_for(self.electors[k].try_acquire_or_renew(), self.renew_deadline)
@@ -126,6 +209,7 @@ class ShardLeaseManager:
                 del self.held[k]
                 changed = True
                 log.info("%s lost shard %d", self.identity, k)
+        counts: Dict[str, int] = {}
         for k in self.order:
             if k in self.held:
                 continue
@@ -138,13 +222,17 @@ class ShardLeaseManager:
             now = self.clock()
             if not free:
                 self.free_since.pop(k, None)
+                counts[e.observed_holder] = counts.get(e.observed_holder, 0) + 1
                 continue
             since = self.free_since.setdefault(k, now)
             # expired under a holder (crash): short grace; never held / released: a lease duration
             grace = 2 * self.retry_period if e.observed_holder and e.observed_holder != self.identity \
                 else self.lease_duration
             orphaned = now - since >= grace
-            if len(self.held) >= self.target and not orphaned:
+            # a shard this replica just handed back is for the member below its share (the
+            # releaser itself may dip below the ceiling share): retaken only once orphaned
+            given = now - self._released.get(k, float("-inf")) < self.lease_duration
+            if (len(self.held) >= self.target or given) and not orphaned:
                 continue
             try:
                 ok = await e.try_acquire_or_renew()
@@ -157,6 +245,23 @@ class ShardLeaseManager:
                 self.acquisitions += 1
                 changed = True
                 log.info("%s acquired shard %d%s", self.identity, k, " (orphaned)" if orphaned else "")
+        self.counts = counts
+        give = self._rebalance_pick()
+        if give is not None:
+            # fence first (the supervisor drops the shard's queued work), then hand the lease over
+            del self.held[give]
+            self._changed()
+            changed = False
+            self._last_release = self._released[give] = self.clock()
+            self.rebalances += 1
+            if self.metrics is not None:
+                self.metrics.inc("shard_rebalances")
+            log.info("%s released shard %d to rebalance (members=%d, share=%d)", self.identity, give,
+                     len(self.members), self.target)
+            try:
+                await self.electors[give]._release()  # noqa: SLF001 - same package
+            except Exception as exc:  # noqa: BLE001 - expires after a lease duration instead
+                log.warning("shard %d lease release failed: %s", give, exc)
         if changed:
             self._changed()
 

@@ -129,7 +129,8 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
 def test_sharded_replicas_survive_cql_restart_storm_and_a_replica_crash(arun):
     """BASELINE config 5 with horizontal scale: 3 replicas over 6 shard Leases; a CQL node
     restart, an eviction storm and a replica dying with its leases mid-stream.  Its shards
-    move to the survivors and every failed run ends in its expected stage."""
+    move to the survivors, its return wins its share back, and every failed run ends in
+    its expected stage."""
     from nexus_supervisor_amd.bench.scenarios import cfg5s_sharded_chaos
 
     async def go():
@@ -139,5 +140,9 @@ def test_sharded_replicas_survive_cql_restart_storm_and_a_replica_crash(arun):
         lost = ch["crashed"]["shards"]
         assert lost and all(ch["final_owners"][k] and ch["final_owners"][k] != [ch["crashed"]["replica"]] for k in lost)
         assert ch["failover_s"] < 2.0 + 1.5  # lease duration + grace + observation
+        # the crashed replica came back and got its fair share (2 of 6) handed back
+        assert ch["rebalanced"], ch
+        back = ch["crashed"]["replica"]
+        assert sum(1 for v in ch["rebalanced_owners"].values() if back in v) == 2, ch
 
     arun(go(), timeout=120)

@@ -274,6 +274,67 @@ def test_last_survivor_takes_orphaned_shards(arun):
     arun(go(), timeout=60)
 
 
+def test_late_replica_gets_its_share_back_by_rebalancing(arun):
+    """Six shards, three replicas configured, only two running: after a lease duration they
+    cover the orphaned shards (3 + 3 or 2 + 4).  When the third replica joins (its membership Lease
+    appears), the richest replica fences and hands back one shard per round until every
+    replica holds its share of 2 — failures pushed throughout are written exactly once."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        wl = Workload(concurrent_jobs=300, seed=23)
+        objs, rows = wl.initial()
+        store = MemoryStore(rows)
+        for o in objs:
+            api.create(o)
+        sharding = {"sharding": {"shards": 6, "mode": "lease", "replicas": 3}}
+        apps = {}
+
+        async def start(ident):
+            app = Application(_cfg(ident, sharding), kube=KubeClient(KubeConfig(url)), store=store)
+            await app.start()
+            apps[ident] = app
+
+        def counts():
+            return sorted(len(a.shard_leases.owned) for a in apps.values())
+
+        def covered():
+            held = [k for a in apps.values() for k in a.shard_leases.owned]
+            return sorted(held) == list(range(6))
+
+        await start("rep-a")
+        await start("rep-b")
+        assert await _wait(lambda: covered() and counts() in ([3, 3], [2, 4]), 6), counts()
+        expected = {}
+        _push(api, wl, store, 40, expected)
+        await start("rep-c")
+        _push(api, wl, store, 40, expected)  # during the hand-over
+        assert await _wait(lambda: covered() and counts() == [2, 2, 2], 10), counts()
+        _push(api, wl, store, 40, expected)
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 15)
+        await asyncio.sleep(0.3)
+        wrong, twice = _check_exactly_once(store, wl, expected)
+        assert not wrong and not twice, (wrong, twice)
+        assert sum(a.shard_leases.rebalances for a in apps.values()) == 2  # 3+3 → 2+2+2 or 4+2 → 2+2+2
+        assert all(a.shard_leases.members == frozenset(apps) for a in apps.values())
+        for a in apps.values():
+            await a.stop(drain_timeout=1)
+        for ident in apps:  # membership released on shutdown
+            m = api.get("Lease", "nexus", f"nexus-supervisor-leader-member-{ident}")
+            assert m is not None and m["spec"]["holderIdentity"] == ""
+        await api.stop()
+
+    arun(go(), timeout=90)
+
+
+def test_member_lease_names_are_dns_safe():
+    from nexus_supervisor_amd.ha.shards import member_lease_name
+
+    assert member_lease_name("nexus-supervisor-leader", "Pod_Name.x") == "nexus-supervisor-leader-member-pod-name.x"
+    long = member_lease_name("base", "x" * 400)
+    assert len(long) <= 253 and long.startswith("base-member-")
+
+
 def test_shard_leases_with_worker_processes_and_watch_hub(arun, tmp_path):
     """Lease mode on process-per-core replicas: the parent holds the shard leases, its
     watch hub drops the other replica's runs before decode, and when the other replica
