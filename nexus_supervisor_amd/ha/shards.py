@@ -90,6 +90,7 @@ class ShardLeaseManager:
         self.members: FrozenSet[str] = frozenset({identity})
         self.counts: Dict[str, int] = {}  # live holder → shards it holds (as last observed)
         self._last_release = float("-inf")
+        self._member_warned = float("-inf")
         self._released: Dict[int, float] = {}  # shard → clock this replica handed it back
         self.rebalances = 0
         self.electors: List[LeaderElector] = [
@@ -154,7 +155,14 @@ class ShardLeaseManager:
             await self.member.try_acquire_or_renew()
             items, _ = await self.client.list("Lease", self.namespace, label_selector=f"{MEMBER_LABEL}={self.base_name}")
         except Exception as exc:  # noqa: BLE001 - keep the last view; the fair share falls back to `replicas`
-            log.warning("shard membership: %s", exc)
+            # e.g. RBAC without `list` on leases after an upgrade: say so once per lease
+            # duration, not every retry period
+            now = self.clock()
+            if now - self._member_warned >= self.lease_duration:
+                self._member_warned = now
+                log.warning("shard membership unavailable (fair share from sharding.replicas): %s", exc)
+            if self.metrics is not None:
+                self.metrics.inc("shard_membership_errors")
             return
         now = self.clock()
         live = {self.identity}

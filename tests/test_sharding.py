@@ -443,3 +443,41 @@ def test_replica_shard_is_independent_of_worker_placement():
     outs, _rv, _e = split.feed(b"".join(_line("ADDED", {"metadata": {"name": r}}) for r in ids))
     kept = {json.loads(x)["object"]["metadata"]["name"] for x in outs[0].splitlines()}
     assert kept == {r for r in ids if shard_of(r, 3) == 1}
+
+
+def test_membership_list_failure_falls_back_to_configured_share(arun):
+    """Without `list` on leases (an upgraded deployment whose RBAC lags), the fair share
+    stays ``ceil(shards / sharding.replicas)`` and nothing is rebalanced away."""
+    from nexus_supervisor_amd.ha.shards import ShardLeaseManager
+    from nexus_supervisor_amd.kube.errors import ApiError
+
+    class NoList:
+        def __init__(self):
+            self.leases = {}
+
+        async def get(self, kind, ns, name):
+            from nexus_supervisor_amd.kube.errors import NotFound
+            if name not in self.leases:
+                raise NotFound(404, "NotFound", name)
+            return self.leases[name]
+
+        async def create(self, kind, ns, body):
+            self.leases[body["metadata"]["name"]] = dict(body, metadata=dict(body["metadata"], resourceVersion="1"))
+            return self.leases[body["metadata"]["name"]]
+
+        async def replace(self, kind, ns, name, body):
+            self.leases[name] = body
+            return body
+
+        async def list(self, *a, **kw):
+            raise ApiError(403, "Forbidden", "leases is forbidden: cannot list")
+
+    async def go():
+        m = ShardLeaseManager(NoList(), "nexus", "lease", "solo", 4, replicas=2, lease_duration=0.8,
+                              renew_deadline=0.5, retry_period=0.1)
+        await m.tick()
+        assert m.target == 2 and len(m.owned) == 2 and m.members == frozenset({"solo"})
+        await m.tick()
+        assert len(m.owned) == 2 and m.rebalances == 0
+
+    arun(go())
