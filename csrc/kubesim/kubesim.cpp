@@ -881,6 +881,7 @@ bool apply_raw(std::string_view line) {
   std::string_view type;
   size_t ob = 0, oe = 0;
   Raw r;
+  r.labels.reserve(8);  // one allocation instead of growing 1 → 2 → 4 per object
   if (!sc.envelope(type, ob, oe, r)) return false;
   if (!r.has_kind || !r.has_api || !r.has_md || r.md_keys == 0 || r.name.empty() || r.has_gen) return false;
   int kind = kind_by_name(r.kind);
@@ -975,8 +976,10 @@ bool remove(int kind, const std::string& ns, const std::string& name, const std:
   if (kind == K_JOB && (propagation == "Background" || propagation == "Foreground")) {
     auto pit = g_pods_by_job.find(okey(ns, name));
     if (pit != g_pods_by_job.end()) {
-      std::vector<std::string> pods(pit->second.begin(), pit->second.end());
-      for (auto& p : pods) remove(K_POD, ns, p, propagation);
+      // take the job's pod set out of the index (the pods' own unindexing then finds
+      // nothing to do) instead of copying every name
+      auto node = g_pods_by_job.extract(pit);
+      for (auto& p : node.mapped()) remove(K_POD, ns, p, propagation);
     }
   }
   return true;
@@ -1648,7 +1651,10 @@ bool on_input(Conn& c) {
       at = c.in.size();
       return true;
     }
-    if (c.in.size() < he + 4 + clen) return true;  // body incomplete
+    if (c.in.size() < he + 4 + clen) {  // body incomplete: grow once, not by doubling per recv
+      if (c.in.capacity() < he + 4 + clen) c.in.reserve(he + 4 + clen);
+      return true;
+    }
     r.body = std::string_view(c.in.data() + he + 4, clen);  // no copy: c.in is compacted after the loop
     at = he + 4 + clen;
     int64_t th = mono_ns();
