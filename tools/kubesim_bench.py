@@ -70,12 +70,14 @@ async def main(argv=None):
     ap.add_argument("--events", type=int, default=1000)
     ap.add_argument("--jobs", type=int, default=10_000)
     ap.add_argument("--watchers", type=int, default=1, help="watch streams per kind (replicas watching the namespace)")
+    ap.add_argument("--flush-threads", type=int, default=0, help="simulator fan-out threads (0 = one per watcher, ≤ 8)")
     args = ap.parse_args(argv)
     wl = Workload(concurrent_jobs=args.jobs)
     objs, _ = wl.initial()
     steps = [wl.step(args.events) for _ in range(args.steps + 2)]
     bodies = [(failed, encode_events(traffic)) for failed, traffic, _ in steps]
-    with KubeSim(history=50_000, flush_threads=max(1, min(8, args.watchers))) as sim:
+    ft = args.flush_threads or max(1, min(8, args.watchers))
+    with KubeSim(history=50_000, flush_threads=ft) as sim:
         host, port = sim.url.split("//")[1].split(":")
         port = int(port)
         ctl = SimControl(sim.url)
@@ -90,6 +92,7 @@ async def main(argv=None):
             await ctl.apply_raw(body)
             delete_all(host, port, failed)
         c0, t0 = cpu_s(sim.proc.pid), time.monotonic()
+        b0 = (await ctl.stats()).get("busy_ns", 0)
         for failed, body in bodies[2:]:
             await ctl.apply_raw(body)
             await asyncio.get_running_loop().run_in_executor(None, delete_all, host, port, failed)
@@ -100,6 +103,7 @@ async def main(argv=None):
         await ctl.close()
     n = args.steps * args.events
     print(json.dumps({"failures": n, "kubesim_cpu_us_per_failure": round(1e6 * (c1 - c0) / n, 2),
+                      "event_loop_busy_us_per_failure": round((st.get("busy_ns", 0) - b0) / 1e3 / n, 2), "flush_threads": ft,
                       "wall_s": round(t1 - t0, 2), "watch_bytes": counter[0], "watchers_per_kind": args.watchers,
                       "sim": {k: st.get(k) for k in ("requests", "deleted", "applied", "sends")}}))
 
