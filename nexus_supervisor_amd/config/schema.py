@@ -203,7 +203,7 @@ class RuntimeConfig:
     # after the initial cache sync: collect once, then move every surviving object to the
     # permanent generation so full collections stop re-traversing 10k cached runs
     gc_freeze: bool = field(default=True, metadata=_k("gc-freeze"))
-    gc_threshold0: int = field(default=20000, metadata=_k("gc-threshold0"))  # CPython default 700
+    gc_threshold0: int = field(default=200000, metadata=_k("gc-threshold0"))  # CPython default 700
     gc_threshold1: int = field(default=20, metadata=_k("gc-threshold1"))
     gc_threshold2: int = field(default=20, metadata=_k("gc-threshold2"))
     gc_refreeze_interval: float = field(default=600.0, metadata=_k("gc-refreeze-interval", "duration"))  # 0 = never

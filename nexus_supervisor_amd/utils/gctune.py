@@ -9,8 +9,11 @@ loop per collection, several times a second under churn — pure p99 latency.
 :class:`GcTuner` does what a long-lived server does with such a heap: after the
 initial LIST sync it runs one full collection (nothing collectable is left behind)
 and ``gc.freeze()``-s the survivors into the permanent generation, then raises the
-generation-0 threshold so short-lived decision objects are collected in fewer, larger
-batches.  A periodic re-freeze keeps the steady-state cache (runs added after the
+generation-0 threshold (200k allocations) so a collection only ever sees what is still
+alive: under churn a run's decoded objects are freed by reference counting within a
+fraction of a second, so at 20k a generation-0 pass re-traversed live cache entries every
+~0.15 s (4.6 % of worker CPU in the saturated bench) and at 200k it finds them gone (≈1 %);
+the steady state creates almost no cyclic garbage (≈1k objects per 100k decisions).  A periodic re-freeze keeps the steady-state cache (runs added after the
 sync) out of the scanned generations too.  Cycles created later are still
 collected: only objects alive at a freeze are exempt.
 """
@@ -23,7 +26,7 @@ from typing import Optional
 
 
 class GcTuner:
-    def __init__(self, freeze: bool = True, thresholds=(20000, 20, 20), refreeze_interval: float = 600.0,
+    def __init__(self, freeze: bool = True, thresholds=(200000, 20, 20), refreeze_interval: float = 600.0,
                  metrics=None):
         self.freeze_enabled = freeze
         self.thresholds = tuple(int(t) for t in thresholds)
