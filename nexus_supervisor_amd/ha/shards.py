@@ -47,6 +47,7 @@ log = logging.getLogger("nexus_supervisor_amd.shards")
 
 
 MEMBER_LABEL = "nexus.sneaksanddata.com/shard-lease-group"
+STALE_MEMBER_LEASES = 10  # lease durations without a renewal before a membership Lease is garbage
 
 
 def shard_lease_name(base: str, k: int) -> str:
@@ -93,6 +94,7 @@ class ShardLeaseManager:
         self._member_warned = float("-inf")
         self._released: Dict[int, float] = {}  # shard → clock this replica handed it back
         self.rebalances = 0
+        self.stale_members_deleted = 0
         self.electors: List[LeaderElector] = [
             LeaderElector(LeaseLock(client, namespace, shard_lease_name(base_name, k), identity),
                           lease_duration=lease_duration, renew_deadline=renew_deadline, retry_period=retry_period,
@@ -132,10 +134,14 @@ class ShardLeaseManager:
                     await self.electors[k]._release()  # noqa: SLF001 - same package
                 except Exception as exc:  # noqa: BLE001
                     log.warning("shard %d lease release failed: %s", k, exc)
-            try:
-                await self.member._release()  # noqa: SLF001
-            except Exception as exc:  # noqa: BLE001
-                log.warning("membership lease release failed: %s", exc)
+            try:  # a pod name is not reused: its membership Lease goes with it
+                await self.client.delete("Lease", self.namespace, self.member.lock.name)
+            except Exception as exc:  # noqa: BLE001 - e.g. no `delete` verb: leave it released
+                log.debug("membership lease delete failed (%s); releasing", exc)
+                try:
+                    await self.member._release()  # noqa: SLF001
+                except Exception as exc2:  # noqa: BLE001
+                    log.warning("membership lease release failed: %s", exc2)
 
     async def _run(self) -> None:
         while True:
@@ -166,18 +172,31 @@ class ShardLeaseManager:
             return
         now = self.clock()
         live = {self.identity}
+        stale = []
         for it in items:
             spec = it.get("spec") or {}
             holder = spec.get("holderIdentity") or ""
-            if not holder:
-                continue  # released on shutdown
             renew = str(spec.get("renewTime") or "")
-            prev = self._seen.get(holder)
+            key = holder or (it.get("metadata") or {}).get("name", "")
+            prev = self._seen.get(key)
             if prev is None or prev[0] != renew:
-                self._seen[holder] = (renew, now)
-            if now - self._seen[holder][1] < self.lease_duration:
+                self._seen[key] = (renew, now)
+            quiet = now - self._seen[key][1]
+            if holder and quiet < self.lease_duration:
                 live.add(holder)
+            elif holder != self.identity and quiet >= STALE_MEMBER_LEASES * self.lease_duration:
+                stale.append((it.get("metadata") or {}).get("name", ""))
         self.members = frozenset(live)
+        # a replica killed without a clean shutdown (or a release without delete) leaves its
+        # membership Lease behind; one per pod ever started would pile up across rollouts
+        for name in stale[:4]:
+            if not name or name == self.member.lock.name:
+                continue
+            try:
+                await self.client.delete("Lease", self.namespace, name)
+                self.stale_members_deleted += 1
+            except Exception as exc:  # noqa: BLE001 - another replica got it first, or no `delete` verb
+                log.debug("stale membership lease %s not deleted: %s", name, exc)
         denom = max(self.replicas, len(live))
         self.target = -(-self.shards // denom) if (self.replicas > 0 or len(live) > 1) else self.shards
 

@@ -319,9 +319,8 @@ def test_late_replica_gets_its_share_back_by_rebalancing(arun):
         assert all(a.shard_leases.members == frozenset(apps) for a in apps.values())
         for a in apps.values():
             await a.stop(drain_timeout=1)
-        for ident in apps:  # membership released on shutdown
-            m = api.get("Lease", "nexus", f"nexus-supervisor-leader-member-{ident}")
-            assert m is not None and m["spec"]["holderIdentity"] == ""
+        for ident in apps:  # membership Leases deleted on shutdown
+            assert api.get("Lease", "nexus", f"nexus-supervisor-leader-member-{ident}") is None
         await api.stop()
 
     arun(go(), timeout=90)
@@ -481,3 +480,32 @@ def test_membership_list_failure_falls_back_to_configured_share(arun):
         assert len(m.owned) == 2 and m.rebalances == 0
 
     arun(go())
+
+
+def test_stale_membership_leases_are_garbage_collected(arun):
+    """A replica killed without a clean shutdown leaves its membership Lease; after ten
+    lease durations without a renewal a live replica deletes it (one Lease per pod ever
+    started would otherwise pile up across rollouts), and never deletes a live one."""
+    from nexus_supervisor_amd.ha.shards import ShardLeaseManager
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        kw = dict(replicas=2, lease_duration=0.2, renew_deadline=0.15, retry_period=0.05)
+        dead = ShardLeaseManager(KubeClient(KubeConfig(url)), "nexus", "grp", "dead-pod", 2, **kw)
+        await dead.tick()  # registers, then dies without releasing anything
+        live = ShardLeaseManager(KubeClient(KubeConfig(url)), "nexus", "grp", "live-pod", 2, **kw)
+        other = ShardLeaseManager(KubeClient(KubeConfig(url)), "nexus", "grp", "other-pod", 2, **kw)
+        live.start()
+        other.start()
+        assert api.get("Lease", "nexus", "grp-member-dead-pod") is not None
+        assert await _wait(lambda: api.get("Lease", "nexus", "grp-member-dead-pod") is None, 6)
+        assert live.stale_members_deleted + other.stale_members_deleted == 1
+        assert api.get("Lease", "nexus", "grp-member-live-pod") is not None
+        assert live.members == frozenset({"live-pod", "other-pod"})
+        await live.stop()
+        await other.stop()
+        assert api.get("Lease", "nexus", "grp-member-live-pod") is None
+        await api.stop()
+
+    arun(go(), timeout=30)
