@@ -13,6 +13,7 @@ from __future__ import annotations
 import json
 import logging
 import sys
+import threading
 import time
 from typing import Any, Dict, Optional
 
@@ -103,6 +104,46 @@ class _V:
         return self.level <= self.parent.verbosity
 
 
+class BufferedStreamHandler(logging.StreamHandler):
+    """``StreamHandler`` that does not flush per record: ``StreamHandler.emit`` flushes the
+    stream after every line, one ``write`` syscall per decision logged at V(0).  Lines go
+    into the stream's buffer and are flushed at most ``interval`` seconds later (a timer
+    armed by the first unflushed line), at WARNING and above immediately, and on shutdown."""
+
+    def __init__(self, stream=None, interval: float = 0.2):
+        super().__init__(stream)
+        self.interval = interval
+        self._timer: Optional[threading.Timer] = None
+
+    def emit(self, record: logging.LogRecord) -> None:
+        try:
+            msg = self.format(record)
+            self.stream.write(msg + self.terminator)
+        except RecursionError:  # pragma: no cover - as logging.StreamHandler
+            raise
+        except Exception:  # pragma: no cover
+            self.handleError(record)
+            return
+        if record.levelno >= logging.WARNING or self.interval <= 0:
+            self.flush()
+        elif self._timer is None:
+            t = threading.Timer(self.interval, self._timed_flush)
+            t.daemon = True
+            self._timer = t
+            t.start()
+
+    def _timed_flush(self) -> None:
+        self._timer = None
+        self.flush()
+
+    def close(self) -> None:
+        t, self._timer = self._timer, None
+        if t is not None:
+            t.cancel()
+        self.flush()
+        super().close()
+
+
 def configure_logging(level: str = "INFO", stream=None, static: Optional[Dict[str, Any]] = None,
                       env: Optional[Dict[str, str]] = None) -> KLogger:
     """Configure the root ``nexus_supervisor_amd`` logger (telemetry.ConfigureLogger analog,
@@ -112,7 +153,7 @@ def configure_logging(level: str = "INFO", stream=None, static: Optional[Dict[st
     root = logging.getLogger("nexus_supervisor_amd")
     root.setLevel(pylevel)
     shutdown_logging()
-    h = logging.StreamHandler(stream or sys.stdout)
+    h = BufferedStreamHandler(stream or sys.stdout)
     h.setFormatter(JsonFormatter(static))
     root.addHandler(h)
     from .datadog import DatadogLogHandler
@@ -130,5 +171,7 @@ def shutdown_logging() -> None:
     root = logging.getLogger("nexus_supervisor_amd")
     for h in list(root.handlers):
         root.removeHandler(h)
-        if not isinstance(h, logging.StreamHandler):
+        if isinstance(h, BufferedStreamHandler):
+            h.close()  # flushes; the stream itself (stdout) stays open
+        elif not isinstance(h, logging.StreamHandler):
             h.close()

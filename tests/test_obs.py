@@ -213,3 +213,27 @@ def test_buildmeta_stamp(tmp_path):
     import nexus_supervisor_amd as pkg
 
     assert pkg.__version__ == buildmeta.APP_VERSION and pkg.__build__ == buildmeta.BUILD_NUMBER
+
+
+def test_buffered_log_handler_flushes_on_timer_warning_and_shutdown():
+    """V(0) decision lines are not flushed one syscall each: they reach the stream within
+    the flush interval, at once for WARNING and above, and on shutdown."""
+    import io
+    import time
+
+    from nexus_supervisor_amd.obs.logging import BufferedStreamHandler, configure_logging, shutdown_logging
+
+    raw = io.BytesIO()
+    stream = io.TextIOWrapper(io.BufferedWriter(raw, buffer_size=1 << 16), encoding="utf-8")
+    log = configure_logging("INFO", stream=stream)
+    log.info("Algorithm run failed", requestId="r1")
+    assert raw.getvalue() == b""  # buffered
+    time.sleep(0.5)
+    assert b'"requestId":"r1"' in raw.getvalue()  # timer flush
+    log.info("second")
+    log.warning("loud")
+    assert b"loud" in raw.getvalue() and b"second" in raw.getvalue()
+    log.info("last")
+    shutdown_logging()
+    assert b"last" in raw.getvalue()
+    assert isinstance(BufferedStreamHandler(io.StringIO()), BufferedStreamHandler)
