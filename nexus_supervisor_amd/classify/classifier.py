@@ -451,8 +451,10 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
     gpu, topo = doc.get("gpu"), doc.get("topology")
     xgmi = (topo or {}).get("xgmi")
     if gpu and xgmi and xgmi.get("links") is not None:
-        # the measured links are listed once, under topology.xgmi (with their GPU index)
-        doc["gpu"] = dict(gpu, gpus=[{k: v for k, v in g.items() if k != "links"} for g in gpu.get("gpus", ())])
+        # the measured links are listed once, under topology.xgmi (with their GPU index); the
+        # per-GPU records are shared by every decision of one telemetry snapshot
+        # (telemetry.pod_evidence_provider): strip + encode them once per record list
+        doc["gpu"] = dict(gpu, gpus=_gpus_without_links(gpu.get("gpus") or []))
     if xgmi and _native_dumps is not None:
         # the xGMI block is shared by every decision of one telemetry snapshot
         # (topology.xgmi_from_evidence): encode it once, splice it into each trace
@@ -480,6 +482,21 @@ def _raw_json(obj) -> RawJSON:
         _RAW_MEMO.clear()
     _RAW_MEMO[id(obj)] = (obj, raw)  # holds obj: its id cannot be reused while cached
     return raw
+
+
+_GPUS_MEMO: Dict[int, Tuple[Any, Any]] = {}
+
+
+def _gpus_without_links(gpus: List[Dict[str, Any]]):
+    hit = _GPUS_MEMO.get(id(gpus))
+    if hit is not None and hit[0] is gpus:
+        return hit[1]
+    stripped = [{k: v for k, v in g.items() if k != "links"} for g in gpus]
+    out = RawJSON(_native_dumps(stripped, default=str)) if _native_dumps is not None else stripped
+    if len(_GPUS_MEMO) > 512:
+        _GPUS_MEMO.clear()
+    _GPUS_MEMO[id(gpus)] = (gpus, out)  # holds the list: its id cannot be reused while cached
+    return out
 
 
 def _json_default(o):

@@ -494,7 +494,7 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
     from ..models import kube
     from .topology import topology_from_pod
 
-    cache: Dict[str, Any] = {"t": -1.0, "snap": None, "by_uid": {}, "by_index": {}}
+    cache: Dict[str, Any] = {"t": -1.0, "snap": None, "by_uid": {}, "by_index": {}, "memo": {}}
     ttl = max(0.005, telemetry.interval / 2)  # the native sampler cannot have anything newer
 
     def refresh(now: float) -> None:
@@ -505,8 +505,8 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
                 u = p.get("pod_uid")
                 if u:
                     by_uid.setdefault(u, set()).add(g["index"])
-        cache.update(t=now, snap=snap, by_uid=by_uid, by_index={g["index"]: g for g in snap},
-                     links={g["index"]: _links_of(g) for g in snap})
+        cache.update(t=now, wall=time.time(), snap=snap, by_uid=by_uid, by_index={g["index"]: g for g in snap},
+                     links={g["index"]: _links_of(g) for g in snap}, memo={})
 
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         topo = topology_from_pod(pod, gpu_resource)
@@ -515,12 +515,29 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
             refresh(now)
         gpus = _pod_gpus(topo, cache["snap"])
         uid = kube.uid_of(pod)
-        # only the GPUs this pod could have used: its expected devices + where its processes ran
-        relevant = set(gpus) | cache["by_uid"].get(uid, set())
+        pod_node = node or (pod.get("spec") or {}).get("nodeName", "")
+        mine = cache["by_uid"].get(uid)
         by_index = cache["by_index"]
+        if not mine:
+            # no process of this pod on any GPU: its evidence is the expected devices' records
+            # of this snapshot, the same for every such pod — built once per snapshot (a burst
+            # of failures on one node shares them; the per-GPU records are never mutated)
+            key = (tuple(gpus), pod_node)
+            hit = cache["memo"].get(key)
+            if hit is None:
+                sub = [by_index[i] for i in sorted(set(gpus)) if i in by_index]
+                hit = cache["memo"][key] = (evidence_for(telemetry, gpu_indices=gpus, lookback=lookback, node=pod_node,
+                                                         snapshot=sub, links=cache["links"], now=cache["wall"]),)
+            if hit[0] is None:
+                return None
+            out = dict(hit[0])
+            if uid:
+                out["pod_uid"] = uid
+            return out
+        # only the GPUs this pod could have used: its expected devices + where its processes ran
+        relevant = set(gpus) | mine
         sub = [by_index[i] for i in sorted(relevant) if i in by_index]
-        return evidence_for(telemetry, pod_uid=uid, gpu_indices=gpus, lookback=lookback,
-                            node=node or (pod.get("spec") or {}).get("nodeName", ""), snapshot=sub,
+        return evidence_for(telemetry, pod_uid=uid, gpu_indices=gpus, lookback=lookback, node=pod_node, snapshot=sub,
                             links=cache["links"])
 
     return provider

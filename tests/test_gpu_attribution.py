@@ -217,3 +217,24 @@ def test_peak_series_matches_a_scan():
     s.trim(t / 2)
     assert s.t[0] <= t / 2 and len(s) < len(data)
     assert s.peak(t / 2, t) == max(v for ts, v in data if t / 2 <= ts <= t)
+
+
+def test_unmatched_pods_share_one_snapshot_evidence_matched_pods_get_their_own():
+    """Pods with no process on any GPU get the expected devices' records of the current
+    snapshot — built once per snapshot and shared (each with its own pod UID); a pod whose
+    processes the monitor matched by cgroup UID gets its own records with them."""
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry, pod_evidence_provider
+    from nexus_supervisor_amd.testing.seed import make_pod
+
+    labels = LabelConfig()
+    tel = FakeTelemetry(n_gpus=8)
+    tel.set_vram(3, 200_000)
+    env = {"LOCAL_RANK": "3", "RANK": "3", "WORLD_SIZE": "8", "HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}
+    a, b, c = (make_pod(f"run-{x}", labels, env=env, gpus=1, node="n1") for x in "abc")
+    tel.add_process(4242, 3, vram_bytes=1 << 30, pod_uid=c["metadata"]["uid"])
+    prov = pod_evidence_provider(tel)
+    ea, eb, ec = prov(a), prov(b), prov(c)
+    assert ea["pod_uid"] == a["metadata"]["uid"] and eb["pod_uid"] == b["metadata"]["uid"]
+    assert ea["gpus"] is eb["gpus"] and ea["gpus"][0]["index"] == 3 and not ea["gpus"][0]["matched"]
+    assert ec["gpus"] is not ea["gpus"] and ec["gpus"][0]["matched"] and ec["gpus"][0]["procs"][0]["pid"] == 4242
