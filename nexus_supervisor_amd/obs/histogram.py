@@ -44,12 +44,18 @@ class LatencyHistogram:
 
     def record(self, value_us: float, count: int = 1) -> None:
         v = int(value_us)
-        if v < 0:
-            v = 0
-        self.counts[self._index(v)] += count
+        if v < self.sub:  # _index inlined: a handful of records per decision on the hot path
+            if v < 0:
+                v = 0
+            idx = v
+        else:
+            e = v.bit_length() - self.sub_bits - 1
+            idx = e * self.sub + (v >> e) if e < self.max_exp else len(self.counts) - 1
+        self.counts[idx] += count
         self.total += count
         self.sum += v * count
-        if self.min is None or v < self.min:
+        m = self.min
+        if m is None or v < m:
             self.min = v
         if v > self.max:
             self.max = v
