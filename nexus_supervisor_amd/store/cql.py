@@ -42,12 +42,13 @@ import datetime as _dt
 import io
 import json
 import logging
+import operator
 import random
 import ssl
 import time
 import zipfile
 from dataclasses import dataclass, field
-from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..models.checkpoint import COLUMN_NAMES, COLUMNS, KEYSPACE, TABLE, CheckpointedRequest
 from .base import CheckpointStore, StoreError
@@ -312,9 +313,19 @@ class PreparedStatement:
     result_names: Optional[Tuple[str, ...]]
     result_types: Optional[List[Any]]
     keyspace: str = ""
+    _pk_get: Optional[Callable[[Sequence[Any]], Tuple]] = field(default=None, repr=False, compare=False)
+
+
+def _pk_getter(indexes: Sequence[int]) -> Callable[[Sequence[Any]], Tuple]:
+    """values → partition-key tuple (a C-level itemgetter; always a tuple)."""
+    if len(indexes) == 1:
+        i = indexes[0]
+        return lambda values: (values[i],)
+    return operator.itemgetter(*indexes)
 
 
 _HOST_EPOCH = [0]  # bumped on every host up/down flip: invalidates routing caches
+_NO_HOSTS: frozenset = frozenset()
 
 
 @dataclass
@@ -354,9 +365,14 @@ class Host:
         one), scanning from a rotating start (ties spread)."""
         conns = self.conns
         if shard is not None and shard < len(self.shard_conns):
-            own = [c for c in self.shard_conns[shard] if not c.closed]
-            if own:
-                conns = own
+            own = self.shard_conns[shard]
+            if len(own) == 1:  # the usual case: one connection per shard
+                if not own[0].closed:
+                    return own[0]
+            else:
+                own = [c for c in own if not c.closed]
+                if own:
+                    conns = own
         n = len(conns)
         if n == 1:
             c = conns[0]
@@ -686,7 +702,10 @@ class CqlSession:
     def routing_token(self, ps: PreparedStatement, values: Sequence[Any]) -> Optional[int]:
         if not ps.pk_indexes or not (self._ring or self._sharded):
             return None
-        key = tuple(values[i] for i in ps.pk_indexes)
+        get = ps._pk_get
+        if get is None:
+            get = ps._pk_get = _pk_getter(ps.pk_indexes)
+        key = get(values)
         tok = self._tokens.get(key)  # a decision reads then writes the same partition
         if tok is not None:
             return tok
@@ -712,7 +731,7 @@ class CqlSession:
         skip = hint is not None
         attempts = 0
         last: Optional[BaseException] = None
-        tried: set = set()
+        tried: set = _NO_HOSTS  # replaced by a real set on the first failure
         while attempts <= self.max_retries:
             cands = self._candidates(token)
             if tried:
@@ -724,6 +743,7 @@ class CqlSession:
             conn = h.pick(shard)
             if conn is None:
                 self._mark_down(h, ConnectionClosed("no live connection"))
+                tried = tried or set()
                 tried.add(h.address)
                 attempts += 1
                 continue
@@ -732,11 +752,13 @@ class CqlSession:
                 self.stats["shard_routed"] += 1
             try:
                 qid = ps.query_id
-                r = await conn.request(lambda s: N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None),
-                                       hint if skip else None, timeout)
+                r = await conn.request_nowait(
+                    lambda s: N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None),
+                    hint if skip else None, timeout)
             except (ConnectionClosed, OSError) as exc:
                 last = exc
                 self._mark_down(h, exc)
+                tried = tried or set()
                 tried.add(h.address)
                 attempts += 1
                 self.stats["retries"] += 1
@@ -745,6 +767,7 @@ class CqlSession:
                 last = exc
                 if not idempotent:
                     raise
+                tried = tried or set()
                 tried.add(h.address)
                 attempts += 1
                 self.stats["retries"] += 1
