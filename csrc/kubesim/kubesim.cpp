@@ -705,23 +705,22 @@ class RawScan {
     ++i_;
     return true;
   }
+  // memchr to the closing quote (a quote preceded by an odd run of backslashes is escaped):
+  // most of a line's bytes are inside strings, and skip() goes through here too
   std::string_view str(bool& esc) {
     if (!eat('"')) throw kjson::ParseError("expected string");
     size_t st = i_;
-    esc = false;
     while (i_ < n_) {
-      char c = s_[i_];
-      if (c == '\\') {
-        esc = true;
-        i_ += 2;
-        continue;
+      const char* q = static_cast<const char*>(memchr(s_ + i_, '"', n_ - i_));
+      if (!q) break;
+      size_t j = static_cast<size_t>(q - s_);
+      size_t bs = 0;
+      while (j > st + bs && s_[j - 1 - bs] == '\\') ++bs;
+      i_ = j + 1;
+      if (bs % 2 == 0) {
+        esc = memchr(s_ + st, '\\', j - st) != nullptr;
+        return std::string_view(s_ + st, j - st);
       }
-      if (c == '"') {
-        std::string_view v(s_ + st, i_ - st);
-        ++i_;
-        return v;
-      }
-      ++i_;
     }
     throw kjson::ParseError("unterminated string");
   }
