@@ -70,6 +70,9 @@ def parse_args(argv=None):
     ap.add_argument("--pprof-out", default="", help="write a pprof profile of the timed steps (rank 0)")
     ap.add_argument("--pprof-hz", type=int, default=199, help="pprof sampling rate (CPU-time Hz)")
     ap.add_argument("--cql-latency-us", type=int, default=0, help="inject CQL server response latency")
+    ap.add_argument("--two-step-write", action="store_true",
+                    help="actuate with the reference's read + write instead of one conditional write "
+                         "(compat.fused-write: false; A/B of the actuation path)")
     ap.add_argument("--cluster", choices=("auto", "shared", "per-rank"), default="auto",
                     help="shared = one apiserver + one CQL server for all ranks, each replica watching the whole "
                          "namespace and owning its shard (default for N>1); per-rank = independent copies")
@@ -166,6 +169,7 @@ def main(argv=None) -> int:
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
+                      fused_write=not args.two_step_write,
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster,
@@ -249,6 +253,7 @@ def main(argv=None) -> int:
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
                 "cql_latency_us": args.cql_latency_us,
+                "actuation": "read+write" if args.two_step_write else "fused conditional write",
                 "stages_ms": res.get("stages"),
                 "cpu_util_rank0": res.get("cpu"),
                 "step_done_ms_rank0": res.get("step_done_ms"),

@@ -36,6 +36,7 @@ class BenchConfig:
     workdir: str = "/tmp"
     step_timeout: float = 300.0
     cql_latency_us: int = 0
+    fused_write: bool = True  # compat.fused-write (False: the reference's read + write)
     pprof_out: str = ""
     kube_connections: int = 256
     inflight: int = 2
@@ -61,6 +62,7 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
     sc.rules.stale_event_grace = 5.0
     sc.observability.stage_timestamps = True
     sc.scylla_cql_store.connections_per_host = 2
+    sc.compat.fused_write = cfg.fused_write
     return sc
 
 

@@ -89,6 +89,11 @@ class CompatConfig:
     #   always — every write conditional; never — none (reference behaviour)
     # true / false are accepted as always / never.
     conditional_update: str = field(default="auto", metadata=_k("conditional-update"))
+    # one store round trip per decision: the conditional write alone decides (its not-applied
+    # answer carries the row's stage: no row / finished / already RUNNING) instead of the
+    # reference's read followed by a write (supervisor.go:264-301).  Makes every write
+    # conditional; off with conditional-update: never or full-row-upsert.
+    fused_write: bool = field(default=True, metadata=_k("fused-write"))
 
 
 @dataclass

@@ -12,7 +12,7 @@ being unfinished (lightweight transaction).
 from __future__ import annotations
 
 import datetime as _dt
-from typing import Iterable, Optional
+from typing import Iterable, Optional, Tuple
 
 from ..models.checkpoint import CheckpointedRequest
 
@@ -48,6 +48,34 @@ class CheckpointStore:
         """Write the owned columns. With ``only_if_stages`` the write is a CAS
         (``IF lifecycle_stage IN (...)``); returns whether it was applied."""
         raise NotImplementedError
+
+    async def cas_update(
+        self,
+        algorithm: str,
+        request_id: str,
+        lifecycle_stage: str,
+        failure_cause: Optional[str],
+        failure_details: Optional[str],
+        last_modified: _dt.datetime,
+        only_if_stages: Iterable[str],
+        set_failure: bool = True,
+    ) -> Tuple[bool, Optional[str]]:
+        """Fused read-modify-write (``compat.fused-write``): the conditional write alone
+        decides, so the actuator needs no prior read.  Returns ``(applied, stage)`` where
+        ``stage`` is the row's current stage when the condition failed (None: no row).
+        Stores that cannot do it atomically fall back to read + conditional write."""
+        only_if_stages = tuple(only_if_stages)
+        cp = await self.read_status(algorithm, request_id)
+        if cp is None:
+            return False, None
+        if cp.lifecycle_stage not in only_if_stages:
+            return False, cp.lifecycle_stage
+        applied = await self.update_status(algorithm, request_id, lifecycle_stage, failure_cause, failure_details,
+                                           last_modified, only_if_stages=only_if_stages, set_failure=set_failure)
+        if applied:
+            return True, None
+        cp = await self.read_status(algorithm, request_id)
+        return False, cp.lifecycle_stage if cp is not None else None
 
     async def connect(self) -> None:
         return None

@@ -931,6 +931,7 @@ class CqlCheckpointStore(CheckpointStore):
                                  f"algorithm_failure_details = ?, last_modified = ? WHERE algorithm = ? AND id = ?")
         self.q_update_stage = f"UPDATE {ft} SET lifecycle_stage = ?, last_modified = ? WHERE algorithm = ? AND id = ?"
         self.reads = self.writes = 0
+        self._cas_q: Dict[Tuple[str, int], str] = {}
 
     @classmethod
     def from_config(cls, cfg) -> "CqlCheckpointStore":
@@ -1013,10 +1014,38 @@ class CqlCheckpointStore(CheckpointStore):
         if only_if_stages is None:
             await self.session.execute(q, vals, consistency=self.cl)
             return True
+        applied, _stage = await self._cas(q, vals, only_if_stages)
+        return applied
+
+    async def cas_update(self, algorithm, request_id, lifecycle_stage, failure_cause, failure_details, last_modified,
+                         only_if_stages, set_failure=True) -> Tuple[bool, Optional[str]]:
+        """One lightweight transaction in place of read + write: ``(applied, current stage)``;
+        the stage is the row's when the condition failed (None: no such row)."""
+        self.writes += 1
+        if set_failure:
+            return await self._cas(self.q_update_failure, [lifecycle_stage, failure_cause, failure_details,
+                                                           last_modified, algorithm, request_id], only_if_stages)
+        return await self._cas(self.q_update_stage, [lifecycle_stage, last_modified, algorithm, request_id],
+                               only_if_stages)
+
+    async def _cas(self, q: str, vals: List[Any], only_if_stages) -> Tuple[bool, Optional[str]]:
         stages = tuple(only_if_stages)
-        cq = q + " IF lifecycle_stage IN (" + ", ".join("?" for _ in stages) + ")"
+        cq = self._cas_q.get((q, len(stages)))
+        if cq is None:
+            cq = self._cas_q[(q, len(stages))] = q + " IF lifecycle_stage IN (" + ", ".join("?" for _ in stages) + ")"
         rows = await self.session.execute(cq, vals + list(stages), consistency=self.cl, serial=self.serial)
-        return bool(rows.rows and rows.rows[0][0])
+        if not rows.rows:
+            return False, None
+        row = rows.rows[0]
+        if row[0]:
+            return True, None
+        # not applied: Cassandra/Scylla return the current values of the condition's columns
+        # (or the whole row); a missing row returns [applied] alone
+        try:
+            i = rows.names.index("lifecycle_stage")
+        except ValueError:
+            return False, None
+        return False, row[i] if i < len(row) else None
 
     async def create_schema(self, replication: str = "{'class': 'SimpleStrategy', 'replication_factor': 1}") -> None:
         """Keyspace + table + indexes (what ``prepare-scylla.sh`` applies in the reference)."""

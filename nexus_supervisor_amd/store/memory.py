@@ -66,5 +66,30 @@ class MemoryStore(CheckpointStore):
         self.write_log.append((key, lifecycle_stage))
         return True
 
+    async def cas_update(self, algorithm, request_id, lifecycle_stage, failure_cause, failure_details,
+                         last_modified: _dt.datetime, only_if_stages, set_failure=True) -> Tuple[bool, Optional[str]]:
+        """Atomic in one step (no await between the check and the write), like the LWT."""
+        await self._io()
+        self.reads += 1
+        self.writes += 1
+        if self.fail_next_writes:
+            self.fail_next_writes -= 1
+            raise StoreError("injected write failure")
+        key = (algorithm, request_id)
+        row = self.rows.get(key)
+        if row is None:
+            return False, None
+        if row.lifecycle_stage not in set(only_if_stages):
+            return False, row.lifecycle_stage
+        row = row.deep_copy()
+        row.lifecycle_stage = lifecycle_stage
+        if set_failure:
+            row.algorithm_failure_cause = failure_cause
+            row.algorithm_failure_details = failure_details
+        row.last_modified = last_modified
+        self.rows[key] = row
+        self.write_log.append((key, lifecycle_stage))
+        return True, None
+
     def get(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
         return self.rows.get((algorithm, request_id))

@@ -129,6 +129,11 @@ class Supervisor:
         self.pipeline: Optional[PipelineStage] = None
         self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
         self._applied_cap = 200_000
+        # one conditional write per decision instead of read + write (compat.fused-write);
+        # conditional-update: never (the reference's unconditional writes) turns it off
+        self._fused = (cfg.compat.fused_write and not cfg.compat.full_row_upsert
+                       and cfg.compat.conditional_update != "never")
+        self._guards: Dict[Any, Any] = {}
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
         self._deletes: Dict[Any, str] = {}  # in-flight asynchronous Job DELETEs → request id
@@ -609,6 +614,10 @@ class Supervisor:
         if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)
+        if self._fused:
+            d = await self._fused_action(r, epoch, failing)
+            if d is not None:
+                return d
         try:
             # the owned-columns write needs only the stage; the full-row upsert (reference
             # UpsertCheckpoint of the deep copy) needs every column
@@ -627,26 +636,9 @@ class Supervisor:
         stamps["read"] = wall()
         key = (r.algorithm, r.request_id)
         if cp is None:
-            self.log.info("no checkpoint exists for the provided request, skipping", requestId=r.request_id, algorithm=r.algorithm)
-            deleted = False
-            if compat.delete_on_read_error and failing:
-                deleted = await self._delete_job(r.request_id)
-            self.metrics.inc("decisions_missing_checkpoint")
-            return Decision(r, "skipped-missing", None, deleted)
+            return await self._skip_missing(r, failing)
         if cp.is_finished():
-            self.log.info("algorithm run completed, skipping action", algorithm=r.algorithm, requestId=r.request_id)
-            deleted = False
-            # a failing decision on a run already in a failed stage: the Job may have survived
-            # a crash between write and delete (or a failed delete) — finish the delete
-            if r.pending_delete or (failing and cp.lifecycle_stage in _FAILED_STAGES()
-                                    and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is not None):
-                if self._fenced(epoch, rid):
-                    return Decision(r, "fenced", cp.lifecycle_stage, False)
-                deleted = await self._delete_job(r.request_id)
-                r.pending_delete = False
-            self._remember(key, cp.lifecycle_stage)
-            self.metrics.inc("decisions_skipped_finished")
-            return Decision(r, "skipped-finished", cp.lifecycle_stage, deleted)
+            return await self._skip_finished(r, epoch, failing, cp.lifecycle_stage)
         stage = STAGE_FOR_ACTION[r.action]()
         now_dt = _dt.datetime.fromtimestamp(wall(), _dt.timezone.utc)
         if r.action == A.TO_RUNNING:
@@ -700,6 +692,115 @@ class Supervisor:
             r.pending_delete = True  # the retry sees the finished row and only deletes
             raise
         return Decision(r, "applied", stage, deleted)
+
+    async def _skip_missing(self, r: RunStatusAnalysisResult, failing: bool) -> Decision:
+        self.log.info("no checkpoint exists for the provided request, skipping", requestId=r.request_id, algorithm=r.algorithm)
+        deleted = False
+        if self.cfg.compat.delete_on_read_error and failing:
+            deleted = await self._delete_job(r.request_id)
+        self.metrics.inc("decisions_missing_checkpoint")
+        return Decision(r, "skipped-missing", None, deleted)
+
+    async def _skip_finished(self, r: RunStatusAnalysisResult, epoch, failing: bool, current: str) -> Decision:
+        self.log.info("algorithm run completed, skipping action", algorithm=r.algorithm, requestId=r.request_id)
+        deleted = False
+        # a failing decision on a run already in a failed stage: the Job may have survived
+        # a crash between write and delete (or a failed delete) — finish the delete
+        if r.pending_delete or (failing and current in _FAILED_STAGES()
+                                and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is not None):
+            if self._fenced(epoch, r.request_id):
+                return Decision(r, "fenced", current, False)
+            deleted = await self._delete_job(r.request_id)
+            r.pending_delete = False
+        self._remember((r.algorithm, r.request_id), current)
+        self.metrics.inc("decisions_skipped_finished")
+        return Decision(r, "skipped-finished", current, deleted)
+
+    async def _fused_action(self, r: RunStatusAnalysisResult, epoch, failing: bool) -> Optional[Decision]:
+        """``compat.fused-write``: the decision is ONE conditional write
+        (``UPDATE … IF lifecycle_stage IN (<unfinished stages>)``) instead of the reference's
+        read followed by a write (``supervisor.go:264-301``).  The store checks the stage
+        atomically, so a row finished by anyone between a read and a write (a third party's
+        CANCELLED, a new leader's FAILED) can never be overwritten, and the actuator pays one
+        store round trip and one request instead of two.  A not-applied answer carries the
+        row's stage, which drives the reference's skip paths (no row / finished / ToRunning on
+        a RUNNING row).  Returns None for a stage outside the known set (custom stage
+        strings): the two-step path then decides with that stage in its guard."""
+        wall = self.wall
+        compat = self.cfg.compat
+        stamps = r.stamps
+        rid = r.request_id
+        stage = STAGE_FOR_ACTION[r.action]()
+        running = r.action == A.TO_RUNNING
+        only_if = self._unfinished_guard(running)
+        if running:
+            cause = details = None
+        else:
+            cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
+            self.classifier.late_enrich(r, self.lookup)
+            details = render_trace(r, self.cfg.rules.trace_format)
+        if self._fenced(epoch, rid):
+            self.metrics.inc("decisions_fenced")
+            return Decision(r, "fenced", None, False)
+        t = wall()
+        stamps["read"] = t  # no separate read: the stage decomposition books the round trip as the write
+        now_dt = _dt.datetime.fromtimestamp(t, _dt.timezone.utc)
+        try:
+            applied, current = await self.store.cas_update(r.algorithm, rid, stage, cause, details, now_dt,
+                                                           only_if, set_failure=not running)
+        except Exception as exc:
+            self.log.error(exc, "failed to update algorithm submission status", requestId=rid, algorithm=r.algorithm)
+            if compat.delete_on_read_error and failing:
+                try:
+                    await self._delete_job(rid)
+                except Exception as del_exc:  # noqa: BLE001 - the store error is what is retried
+                    self.log.error(del_exc, "failed to delete an algorithm submission after a checkpoint store error",
+                                   requestId=rid, algorithm=r.algorithm)
+            raise
+        key = (r.algorithm, rid)
+        if not applied:
+            if current is None:
+                return await self._skip_missing(r, failing)
+            if current in _cp.FINISHED_STAGES:
+                return await self._skip_finished(r, epoch, failing, current)
+            if running and current == LifecycleStage.RUNNING:
+                self._remember(key, current)
+                return Decision(r, "skipped-already-running", current, False)
+            self.metrics.inc("fused_write_fallbacks")
+            return None
+        stamps["ack"] = wall()
+        stamps["ack_mono"] = time.monotonic()
+        self._observe(r)
+        self._remember(key, stage)
+        if running:
+            return Decision(r, "applied", stage, False)
+        self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
+        if self._fenced(epoch, rid):
+            return Decision(r, "applied", stage, False)
+        if self.cfg.async_job_delete:
+            self._spawn_delete(r)
+            return Decision(r, "applied", stage, False)
+        try:
+            deleted = await self._delete_job(rid)
+        except Exception as exc:
+            self.log.error(exc, "failed to delete an algorithm submission", requestId=rid, algorithm=r.algorithm)
+            r.pending_delete = True  # the retry sees the finished row and only deletes
+            raise
+        return Decision(r, "applied", stage, deleted)
+
+    def _unfinished_guard(self, running: bool) -> Tuple[str, ...]:
+        """``IF lifecycle_stage IN (...)`` of a fused write, memoised per stage configuration
+        (stage strings are configurable: ``stages:``).  ToRunning leaves RUNNING out, so a
+        RUNNING row answers "not applied, RUNNING" (the reference's skip) without a write."""
+        fin = _cp.FINISHED_STAGES
+        hit = self._guards.get((running, id(fin)))
+        if hit is not None and hit[0] is fin:
+            return hit[1]
+        g = _cp.unfinished_stages()
+        if running:
+            g = tuple(x for x in g if x != LifecycleStage.RUNNING)
+        self._guards[(running, id(fin))] = (fin, g)
+        return g
 
     def _spawn_delete(self, r: RunStatusAnalysisResult) -> None:
         nowait = getattr(self.jobs, "delete_job_nowait", None)

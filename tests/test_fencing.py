@@ -47,9 +47,14 @@ class GatedStore(MemoryStore):
 
 
 def _cfg(**over):
+    """These tests pin the two-step (read, then write) actuation: the fused single-write path
+    is covered by tests/test_fused_write.py."""
     base = {"cql-store-type": "memory", "rate-limit-elements-per-second": 0, "resync-period": "0s",
             "failure-rate-base-delay": "10ms", "failure-rate-max-delay": "50ms",
-            "leader-election": {"enabled": True}}
+            "leader-election": {"enabled": True}, "compat": {"fused-write": False}}
+    over = dict(over)
+    if "compat" in over:
+        over["compat"] = dict(base["compat"], **over["compat"])
     base.update(over)
     return load_config(path=None, env={}, overrides=base)
 
