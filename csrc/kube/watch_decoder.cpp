@@ -1376,8 +1376,60 @@ PyObject* Decoder_decode(Decoder* self, PyObject* arg) {
   return r;
 }
 
+// Watch envelope -> (type, object) with object["kind"] defaulted to `kind` (the informer's
+// batched path; what watchhub.HubListWatch.watch_batches did per line in Python).  A missing
+// or empty object becomes a fresh {} like `ev.get("object") or {}`.
+PyObject* envelope_pair(PyObject* ev, PyObject* kind) {
+  static PyObject* k_type = PyUnicode_InternFromString("type");
+  static PyObject* k_object = PyUnicode_InternFromString("object");
+  static PyObject* k_kind = PyUnicode_InternFromString("kind");
+  static PyObject* empty = PyUnicode_InternFromString("");
+  if (!PyDict_Check(ev)) {
+    PyErr_SetString(PyExc_ValueError, "watch line is not a JSON object");
+    return nullptr;
+  }
+  PyObject* t = PyDict_GetItemWithError(ev, k_type);
+  if (!t && PyErr_Occurred()) return nullptr;
+  PyObject* o = PyDict_GetItemWithError(ev, k_object);
+  if (!o && PyErr_Occurred()) return nullptr;
+  PyObject* obj;
+  if (o && PyObject_IsTrue(o) == 1) {
+    Py_INCREF(o);
+    obj = o;
+  } else {
+    obj = PyDict_New();
+    if (!obj) return nullptr;
+  }
+  if (PyDict_Check(obj)) {
+    PyObject* k = PyDict_GetItemWithError(obj, k_kind);
+    if (!k && PyErr_Occurred()) {
+      Py_DECREF(obj);
+      return nullptr;
+    }
+    if ((!k || k == Py_None) && PyDict_SetItem(obj, k_kind, kind) != 0) {
+      Py_DECREF(obj);
+      return nullptr;
+    }
+  }
+  PyObject* pair = PyTuple_Pack(2, t ? t : empty, obj);
+  Py_DECREF(obj);
+  return pair;
+}
+
+PyObject* feed_impl(Decoder* self, PyObject* arg, PyObject* kind);
+
 // feed(bytes) -> [projected documents] for every complete '\n'-terminated line
-PyObject* Decoder_feed(Decoder* self, PyObject* arg) {
+PyObject* Decoder_feed(Decoder* self, PyObject* arg) { return feed_impl(self, arg, nullptr); }
+
+// feed_events(bytes, kind) -> [(type, object)] for every complete line (object kind defaulted)
+PyObject* Decoder_feed_events(Decoder* self, PyObject* args) {
+  PyObject* data;
+  PyObject* kind;
+  if (!PyArg_ParseTuple(args, "OU", &data, &kind)) return nullptr;
+  return feed_impl(self, data, kind);
+}
+
+PyObject* feed_impl(Decoder* self, PyObject* arg, PyObject* kind) {
   Py_buffer view;
   if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) != 0) return nullptr;
   std::string& buf = *self->buf;
@@ -1401,6 +1453,11 @@ PyObject* Decoder_feed(Decoder* self, PyObject* arg) {
     if (b > a) {
       if (self->router) ++self->router->passed;
       PyObject* v = decode_one(self, buf.data() + a, b - a);
+      if (v && kind) {
+        PyObject* pair = envelope_pair(v, kind);
+        Py_DECREF(v);
+        v = pair;
+      }
       if (!v || PyList_Append(out, v) != 0) {
         Py_XDECREF(v);
         Py_DECREF(out);
@@ -1452,6 +1509,8 @@ PyObject* Decoder_stats(Decoder* self, void*) {
 PyMethodDef Decoder_methods[] = {
     {"decode", reinterpret_cast<PyCFunction>(Decoder_decode), METH_O, "Decode one JSON document with projection"},
     {"feed", reinterpret_cast<PyCFunction>(Decoder_feed), METH_O, "Feed stream bytes; decode complete lines"},
+    {"feed_events", reinterpret_cast<PyCFunction>(Decoder_feed_events), METH_VARARGS,
+     "Feed watch stream bytes; [(type, object)] per complete line, object kind defaulted"},
     {"reset", reinterpret_cast<PyCFunction>(Decoder_reset), METH_NOARGS, "Drop a partial line"},
     {"set_router", reinterpret_cast<PyCFunction>(Decoder_set_router), METH_VARARGS,
      "Drop watch lines another shard worker owns (router, role)"},

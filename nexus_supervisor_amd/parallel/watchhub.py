@@ -270,12 +270,8 @@ class HubListWatch(ListWatch):
                 return
             if ftype == 0:
                 raise ConnectionError("watch hub closed")
-            batch = []
-            for ev in decoder.feed(payload):
-                obj = ev.get("object") or {}
-                if obj.get("kind") is None:
-                    obj["kind"] = kind
-                batch.append((ev.get("type", ""), obj))
+            # (type, object) pairs with the object's kind defaulted, built by the decoder itself
+            batch = decoder.feed_events(payload, kind)
             if batch:
                 yield batch
 

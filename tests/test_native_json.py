@@ -116,3 +116,34 @@ def test_raw_json_splice_and_trace_equivalence():
     back = json.loads(out)
     assert back["topology"]["xgmi"] == inner and back["b"] == "b'plain'"
     assert json.loads(json.dumps(doc, default=_json_default)) == back
+
+
+def test_feed_events_matches_python_envelope_unpacking():
+    """``feed_events(bytes, kind)`` = ``[(ev.get("type", ""), ev.get("object") or {})]`` with the
+    object's missing / null kind set to ``kind`` (the hub feed's batched informer path)."""
+    import json as _json
+
+    from nexus_supervisor_amd import _kube_native as K
+    from nexus_supervisor_amd.models import kube
+
+    lines = [{"type": "ADDED", "object": {"metadata": {"name": "a", "namespace": "ns"}}},
+             {"type": "MODIFIED", "object": {"kind": "Pod", "metadata": {"name": "b"}}},
+             {"type": "DELETED", "object": {"kind": None, "metadata": {"name": "c"}}},
+             {"type": "BOOKMARK", "object": {}},
+             {"object": {"metadata": {"name": "d"}}},
+             {"type": "ERROR"}]
+    data = b"".join((_json.dumps(x) + "\n").encode() for x in lines)
+    proj = kube.watch_projection("Pod")
+    want = []
+    for ev in K.ProjectedDecoder(proj).feed(data):
+        obj = ev.get("object") or {}
+        if obj.get("kind") is None:
+            obj["kind"] = "Pod"
+        want.append((ev.get("type", ""), obj))
+    d = K.ProjectedDecoder(proj)
+    got = d.feed_events(data[:37], "Pod") + d.feed_events(data[37:], "Pod")  # split mid-line
+    assert got == want
+    assert [t for t, _ in got] == ["ADDED", "MODIFIED", "DELETED", "BOOKMARK", "", "ERROR"]
+    assert all(o["kind"] == "Pod" for _, o in got)
+    with pytest.raises(ValueError):
+        K.ProjectedDecoder(True).feed_events(b"[1, 2]\n", "Pod")

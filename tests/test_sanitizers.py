@@ -154,11 +154,17 @@ def test_projected_decoder_fuzz():
             else:
                 b.insert(i, rng.choice(b'{}[]",:\\u0'))
         d.reset()
+        line = bytes(b).replace(b"\n", b" ") + b"\n"
         try:
-            d.feed(bytes(b).replace(b"\n", b" ") + b"\n")
+            d.feed(line)
             ok += 1
         except ValueError:
             bad += 1
+        d.reset()
+        try:
+            d.feed_events(line, "Pod")  # same bytes through the (type, object) pair builder
+        except ValueError:
+            pass
     assert ok + bad == 5000 and bad > 0 and ok > 0
 
 
