@@ -435,6 +435,9 @@ class Classifier:
         self._apply_history(res)
 
 
+_PLAIN_CLASSES = frozenset((F.NONE, F.SCHEDULING, F.DEADLINE, F.FATAL, F.BACKOFF_LIMIT))
+
+
 def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
     """Trace column (``algorithm_failure_details``) for a decision.
 
@@ -442,12 +445,15 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
     ``json`` — message + reason + failure class + evidence; ``auto`` — json only
     when there is evidence beyond the message.
     """
-    extra = {k: v for k, v in res.evidence.items() if k != "source"}
-    if fmt == "raw" or (fmt == "auto" and not extra and res.failure_class in (F.NONE, F.SCHEDULING, F.DEADLINE, F.FATAL, F.BACKOFF_LIMIT)):
+    ev = res.evidence
+    if fmt == "raw" or (fmt == "auto" and res.failure_class in _PLAIN_CLASSES
+                        and (not ev or (len(ev) == 1 and "source" in ev))):
         return res.run_status_trace
     doc = {"message": res.run_status_trace, "reason": res.reason, "class": res.failure_class,
-           "source": res.evidence.get("source", "")}
-    doc.update(extra)
+           "source": ev.get("source", "")}
+    for k, v in ev.items():
+        if k != "source":
+            doc[k] = v
     gpu, topo = doc.get("gpu"), doc.get("topology")
     xgmi = (topo or {}).get("xgmi")
     if gpu and xgmi and xgmi.get("links") is not None:
