@@ -233,3 +233,36 @@ def test_cql_cas_update_against_native_server(arun):
                 await st.close()
 
     arun(go())
+
+
+def test_base_store_fallback_cas_is_read_then_conditional_write(arun):
+    """A store without an atomic ``cas_update`` gets the protocol's read + conditional write."""
+    from nexus_supervisor_amd.store.base import CheckpointStore
+
+    class TwoStep(CheckpointStore):
+        def __init__(self, rows):
+            self.inner = MemoryStore(rows)
+            self.race = None  # stage another writer sets between the read and the write
+
+        async def read_checkpoint(self, algorithm, request_id):
+            return await self.inner.read_checkpoint(algorithm, request_id)
+
+        async def update_status(self, algorithm, request_id, *a, **kw):
+            if self.race is not None:
+                self.inner.rows[(algorithm, request_id)].lifecycle_stage = self.race
+                self.race = None
+            return await self.inner.update_status(algorithm, request_id, *a, **kw)
+
+    async def go():
+        st = TwoStep([RUNNING_ROW, CANCELLED_ROW])
+        now = dt.datetime.now(UTC)
+        guard = cp_mod.unfinished_stages()
+        assert await st.cas_update(ALGORITHM, "missing", "FAILED", "c", "d", now, guard) == (False, None)
+        assert await st.cas_update(ALGORITHM, CANCELLED_ROW.id, "FAILED", "c", "d", now, guard) == (False, "CANCELLED")
+        st.race = "CANCELLED"  # lost the race after the read: the conditional write refuses, re-read reports it
+        assert await st.cas_update(ALGORITHM, RUNNING_ROW.id, "FAILED", "c", "d", now, guard) == (False, "CANCELLED")
+        st.inner.rows[(ALGORITHM, RUNNING_ROW.id)].lifecycle_stage = "RUNNING"
+        assert await st.cas_update(ALGORITHM, RUNNING_ROW.id, "FAILED", "c", "d", now, guard) == (True, None)
+        assert st.inner.get(ALGORITHM, RUNNING_ROW.id).lifecycle_stage == "FAILED"
+
+    arun(go())
