@@ -13,6 +13,9 @@ from typing import Dict, Iterable, List, Tuple
 
 
 class LatencyHistogram:
+    # slots: record() reads and writes six attributes, a handful of times per decision
+    __slots__ = ("sub_bits", "sub", "max_exp", "counts", "total", "sum", "min", "max")
+
     def __init__(self, sub_bits: int = 7, max_exp: int = 40):
         self.sub_bits = sub_bits
         self.sub = 1 << sub_bits
