@@ -419,7 +419,8 @@ class Supervisor:
         self._on_event_add(new)
 
     def _on_pod_add(self, pod):
-        self._unpark("Pod", kube.name_of(pod))
+        if self._parked:
+            self._unpark("Pod", kube.name_of(pod))
         self._on_pod_update(None, pod)
 
     def _on_pod_update(self, old, pod, waited: bool = False):
@@ -428,6 +429,8 @@ class Supervisor:
         recv = self.wall()
         wait = self.cfg.gpu.evidence_wait
         results = self.classifier.classify_pod(pod, old, allow_wait=wait > 0 and not waited)
+        if not results and not self._gpu_wait and not self.classifier.deferred:
+            return  # the common case (a new or unchanged pod): nothing to submit or un-defer
         key = kube.object_key(pod)
         if self.classifier.deferred:
             # failed GPU pod without node-agent evidence yet: give the annotation time to land
@@ -451,7 +454,8 @@ class Supervisor:
                 self._on_pod_update(None, pod, waited=True)
 
     def _on_job_add(self, job):
-        self._unpark("Job", kube.name_of(job))
+        if self._parked:
+            self._unpark("Job", kube.name_of(job))
         self._on_job_update(None, job)
 
     def _on_job_update(self, old, job):
