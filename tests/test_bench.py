@@ -48,11 +48,26 @@ def test_bench_wire_in_process(tmp_path, capsys):
     _check(out, 1, 2, 1, 60)
     cfg = out["config"]
     assert cfg["transport"] == "wire" and cfg["store"].startswith("cql")
+    assert cfg["actuation"] == "fused conditional write"
     st = cfg["stages_ms"]
     assert st["receive_to_checkpoint"]["count"] >= 120
     for k in ("stage_classify", "stage_queue", "stage_read", "stage_write"):
         assert st[k]["count"] == st["receive_to_checkpoint"]["count"]
     assert out["latency_at_rate"]["events"] == 3
+
+
+@pytest.mark.slow
+def test_bench_two_step_write_ab(capsys):
+    """``--two-step-write`` (the reference's read + write actuation) passes the same checks, and
+    the line says which actuation it measured."""
+    import bench
+
+    rc = bench.main(["--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "60", "--probe-events", "0",
+                     "--two-step-write"])
+    assert rc == 0
+    out = json.loads([x for x in capsys.readouterr().out.splitlines() if x.startswith("{")][-1])
+    _check(out, 1, 2, 1, 60)
+    assert out["config"]["actuation"] == "read+write"
 
 
 @pytest.mark.slow
