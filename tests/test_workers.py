@@ -478,3 +478,49 @@ def test_worker_gpu_evidence_from_parent_monitor(arun, tmp_path):
                 await ctl.close()
 
     arun(go(), timeout=90)
+
+
+def test_hub_feed_protocol_split_reads_join_lines_and_keep_order():
+    """Frames cut at every byte boundary parse the same; one kind's LINES frames of a read are
+    joined into one queue item, a SNAPSHOT stays behind that kind's earlier lines, and frames
+    of other kinds keep their own queues."""
+    from nexus_supervisor_amd.parallel.watchhub import HEADER, LINES, SNAPSHOT, HubFeed, _FeedProtocol
+
+    def frame(ftype, ki, payload):
+        return HEADER.pack(ftype, ki, len(payload)) + payload
+
+    stream = (frame(LINES, 1, b'{"a":1}\n') + frame(LINES, 2, b'{"j":1}\n') + frame(LINES, 1, b'{"a":2}\n')
+              + frame(SNAPSHOT, 1, b"9\n[]") + frame(LINES, 1, b'{"a":3}\n') + frame(LINES, 9, b"x\n"))
+
+    def drain(feed):
+        out = {}
+        for ki, q in feed.queues.items():
+            items = []
+            while not q.empty():
+                items.append(q.get_nowait())
+            out[ki] = items
+        return out
+
+    async def run(chunks):
+        feed = HubFeed()
+        proto = _FeedProtocol(feed)
+        for c in chunks:
+            proto.data_received(c)
+        assert not proto.buf  # everything consumed
+        return feed, drain(feed)
+
+    async def go():
+        feed, whole = await run([stream])
+        assert whole[1] == [(LINES, b'{"a":1}\n{"a":2}\n'), (SNAPSHOT, b"9\n[]"), (LINES, b'{"a":3}\n')]
+        assert whole[2] == [(LINES, b'{"j":1}\n')] and whole[0] == []
+        assert feed.frames == 6
+        _, bytewise = await run([stream[i:i + 1] for i in range(len(stream))])
+        joined = {ki: [(t, p) for t, p in items] for ki, items in bytewise.items()}
+        # one byte per read: nothing to join, same bytes in the same order per kind
+        assert b"".join(p for t, p in joined[1] if t == LINES) == b'{"a":1}\n{"a":2}\n{"a":3}\n'
+        assert [t for t, _ in joined[1]] == [LINES, LINES, SNAPSHOT, LINES]
+        proto_feed = HubFeed()
+        _FeedProtocol(proto_feed).connection_lost(None)
+        assert all(q.get_nowait() == (0, b"") for q in proto_feed.queues.values())
+
+    asyncio.run(go())
