@@ -505,7 +505,7 @@ class GpuMonitor {
       uint32_t n = static_cast<uint32_t>(buf.size());
       amdsmi_status_t st = amdsmi_get_gpu_process_list(gs[i].h, &n, buf.data());
       if (st == AMDSMI_STATUS_OUT_OF_RESOURCES || n > buf.size()) {
-        buf.resize(n + 16);
+        buf.resize(std::min<uint32_t>(n, 4096) + 16);  // a count read while processes exit: bounded
         n = static_cast<uint32_t>(buf.size());
         st = amdsmi_get_gpu_process_list(gs[i].h, &n, buf.data());
       }
@@ -519,8 +519,8 @@ class GpuMonitor {
           continue;
         }
         smi_listed = true;
-        seen.push_back(Obs{gs[i].index, static_cast<uint32_t>(pi.pid), pi.name, "amdsmi", v, pi.memory_usage.gtt_mem,
-                           pi.cu_occupancy});
+        seen.push_back(Obs{gs[i].index, static_cast<uint32_t>(pi.pid), std::string(pi.name, strnlen(pi.name, sizeof pi.name)),
+                           "amdsmi", v, pi.memory_usage.gtt_mem, pi.cu_occupancy});
       }
     }
     if (mode == "drm") {
@@ -644,7 +644,13 @@ class GpuMonitor {
     std::unique_lock<std::mutex> lk(wake_mu_);
     while (running_) {
       lk.unlock();
-      sample_once();
+      // a sampler thread must never take the process down: an exception escaping a
+      // std::thread is std::terminate (abort) — count it and sample again next tick
+      try {
+        sample_once();
+      } catch (...) {
+        sample_errors_.fetch_add(1);
+      }
       lk.lock();
       // system_clock deadline → pthread_cond_timedwait: a steady_clock wait_for compiles to
       // pthread_cond_clockwait, which GCC 11's TSan runtime does not intercept (it then
@@ -666,12 +672,17 @@ class GpuMonitor {
       amdsmi_status_t st = amdsmi_get_gpu_event_notification(200, &n, buf.data());
       if (st != AMDSMI_STATUS_SUCCESS || n == 0) continue;
       double t = now_s();
-      std::lock_guard<std::mutex> lk(mu_);
-      for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
-        int gpu = -1;
-        for (auto& h : handles)
-          if (h.first == buf[i].processor_handle) gpu = h.second;
-        record_event_locked(EventRec{gpu, event_name(buf[i].event), buf[i].message, t});
+      try {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (uint32_t i = 0; i < n && i < buf.size(); ++i) {
+          int gpu = -1;
+          for (auto& h : handles)
+            if (h.first == buf[i].processor_handle) gpu = h.second;
+          record_event_locked(EventRec{gpu, event_name(buf[i].event),
+                                       std::string(buf[i].message, strnlen(buf[i].message, sizeof buf[i].message)), t});
+        }
+      } catch (...) {  // as in the sampler: never std::terminate from a monitor thread
+        sample_errors_.fetch_add(1);
       }
     }
   }
@@ -692,6 +703,7 @@ class GpuMonitor {
   std::unordered_map<uint64_t, ProcRec> procs_;
   std::deque<EventRec> events_, pending_events_;
   std::atomic<uint64_t> samples_{0};
+  std::atomic<uint64_t> sample_errors_{0};  // exceptions caught in the monitor threads
   std::atomic<double> last_sample_s_{0};
 };
 
