@@ -8,11 +8,17 @@
 //        allocate + touch C-GiB chunks until hipMalloc reports hipErrorOutOfMemory,
 //        hold the peak for S s (so the node monitor samples it), write the HIP error
 //        to PATH (the pod's terminationMessagePath) and exit 1.
+//   gpu_stress hbm-oom --chunk-gib C --no-termination-log --linger 0
+//        what a default PyTorch pod does: the OOM goes to stderr only, in torch's own
+//        "torch.OutOfMemoryError: HIP out of memory. Tried to allocate … GPU N has a
+//        total capacity of …" wording, and the process exits 1 at once (its VRAM is
+//        freed by the exit, nothing lingers for a sampler to see).
 //
 // Kernels are sized for CDNA4: 256-thread workgroups (4 × 64-wide wavefronts),
 // grid = 8 workgroups per CU over the 256 CUs, grid-stride loops, 16-byte stores.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -72,16 +78,27 @@ static void write_termination(const std::string& path, const std::string& msg) {
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: gpu_stress hold|hbm-oom [--gib G] [--seconds S] [--chunk-gib C] [--linger S] "
-                    "[--termination-log PATH] [--device D]\n");
+                    "[--termination-log PATH | --no-termination-log] [--max-gib M] [--device D]\n");
     return 2;
   }
   std::string mode = argv[1];
   double gib = 1.0, seconds = 2.0, chunk_gib = 32.0, linger = 1.0, max_gib = 1e9;
   int device = 0;
   std::string term_log;
-  for (int i = 2; i + 1 < argc; i += 2) {
+  bool no_term_log = false;
+  for (int i = 2; i < argc;) {
     std::string k = argv[i];
+    if (k == "--no-termination-log") {
+      no_term_log = true;
+      i += 1;
+      continue;
+    }
+    if (i + 1 >= argc) {
+      fprintf(stderr, "option %s needs a value\n", k.c_str());
+      return 2;
+    }
     const char* v = argv[i + 1];
+    i += 2;
     if (k == "--gib") gib = atof(v);
     else if (k == "--seconds") seconds = atof(v);
     else if (k == "--chunk-gib") chunk_gib = atof(v);
@@ -94,6 +111,7 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
+  if (no_term_log) term_log.clear();
   CHECK(hipSetDevice(device));
   const int grid = grid_for(device);
   printf("gpu_stress %s device=%d rank=%s local_rank=%s world=%s visible=%s\n", mode.c_str(), device,
@@ -110,7 +128,10 @@ int main(int argc, char** argv) {
     auto t0 = std::chrono::steady_clock::now();
     int rounds = 0;
     while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < seconds) {
-      hipLaunchKernelGGL(fma_kernel, dim3(grid), dim3(256), 0, 0, static_cast<float*>(p), bytes / 4, 256);
+      // the whole allocation is filled once (resident); the busy loop runs over its first
+      // GiB only, so a multi-hundred-GiB hold still checks the clock every few ms
+      hipLaunchKernelGGL(fma_kernel, dim3(grid), dim3(256), 0, 0, static_cast<float*>(p),
+                         std::min(bytes / 4, static_cast<size_t>(1) << 28), 256);
       CHECK(hipGetLastError());
       CHECK(hipDeviceSynchronize());
       ++rounds;
@@ -135,16 +156,29 @@ int main(int argc, char** argv) {
       hipError_t e = hipMalloc(&p, chunk);
       if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
         (void)hipGetLastError();  // clear the sticky-free error state
-        char msg[512];
-        snprintf(msg, sizeof msg,
-                 "%s: HIP out of memory. Tried to allocate %.2f GiB. GPU %d has a total capacity of %.2f GiB; "
-                 "%.2f GiB already allocated by this process (rank=%s local_rank=%s)",
-                 hipGetErrorName(e), chunk / double(1ull << 30), device, total_b / double(1ull << 30),
-                 total / double(1ull << 30), env_or("RANK", "-"), env_or("LOCAL_RANK", "-"));
-        fprintf(stderr, "%s\n", msg);
+        char msg[768];
+        size_t free_now = 0, total_now = 0;
+        (void)hipMemGetInfo(&free_now, &total_now);
+        if (no_term_log) {
+          // torch's caching-allocator wording (what a default pod leaves in its log only)
+          snprintf(msg, sizeof msg,
+                   "torch.OutOfMemoryError: HIP out of memory. Tried to allocate %.2f GiB. GPU %d has a total "
+                   "capacity of %.2f GiB of which %.2f GiB is free. Of the allocated memory %.2f GiB is allocated "
+                   "by PyTorch, and 0 bytes is reserved by PyTorch but unallocated.",
+                   chunk / double(1ull << 30), device, total_b / double(1ull << 30), free_now / double(1ull << 30),
+                   total / double(1ull << 30));
+          fprintf(stderr, "Traceback (most recent call last):\n  File \"train.py\", line 42, in <module>\n%s\n", msg);
+        } else {
+          snprintf(msg, sizeof msg,
+                   "%s: HIP out of memory. Tried to allocate %.2f GiB. GPU %d has a total capacity of %.2f GiB; "
+                   "%.2f GiB already allocated by this process (rank=%s local_rank=%s)",
+                   hipGetErrorName(e), chunk / double(1ull << 30), device, total_b / double(1ull << 30),
+                   total / double(1ull << 30), env_or("RANK", "-"), env_or("LOCAL_RANK", "-"));
+          fprintf(stderr, "%s\n", msg);
+        }
         fflush(stderr);
         write_termination(term_log, msg);
-        std::this_thread::sleep_for(std::chrono::duration<double>(linger));
+        if (linger > 0) std::this_thread::sleep_for(std::chrono::duration<double>(linger));
         for (void* q : chunks) (void)hipFree(q);
         return 1;
       }

@@ -25,6 +25,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..config.schema import GpuConfig, LabelConfig, RulesConfig
+from ..gpu import logtail
 from ..gpu import oom as oom_mod
 from ..gpu.telemetry import FAULT_EVENTS
 from ..gpu.topology import merge_process_ranks, resolve_devices, topology_from_pod, xgmi_from_evidence
@@ -109,6 +110,11 @@ class Classifier:
         # with the GPUs, or a node agent in-process): pod -> evidence record or None.
         self.evidence_provider: Optional[Callable[[Dict[str, Any]], Optional[Dict[str, Any]]]] = None
         self.deferred = False
+        # failed GPU pod whose OOM signature may only be in its container log: the
+        # (container, previous) instances to fetch (set by classify_pod, see log_cache)
+        self.deferred_log: List[Dict[str, Any]] = []
+        # pod uid -> log-tail records fetched by the supervisor (pods/log API; logtail.py)
+        self.log_cache: "OrderedDict[str, List[Dict[str, Any]]]" = OrderedDict()
         self._ctx_cache: Dict[Tuple[str, str, bool], Tuple[Dict[str, Any], Optional[Dict[str, Any]]]] = {}
 
     # ------------------------------------------------------------ helpers
@@ -189,11 +195,17 @@ class Classifier:
         return self.evidence_provider is not None or bool(kube.annotations_of(pod).get(self.gpu.evidence_annotation))
 
     def classify_pod(self, pod: Dict[str, Any], old: Optional[Dict[str, Any]] = None,
-                     allow_wait: bool = False) -> List[RunStatusAnalysisResult]:
+                     allow_wait: bool = False, allow_log_fetch: bool = False) -> List[RunStatusAnalysisResult]:
         """Pod-status rules.  With ``allow_wait`` a failed GPU pod whose node agent has not
         annotated it yet is *deferred* (``self.deferred`` set, no result) so the caller can
-        give the evidence ``gpu.evidence-wait`` to arrive."""
+        give the evidence ``gpu.evidence-wait`` to arrive.  With ``allow_log_fetch`` a failed
+        GPU container with an empty termination message and no OOM verdict yet is deferred
+        too (``self.deferred_log`` names the container instances) until the caller stored
+        its log tail in :attr:`log_cache` (``gpu.log-tail``; a default pod's termination
+        message is empty, its OOM text is in the log)."""
         self.deferred = False
+        if self.deferred_log:
+            self.deferred_log = []
         if not self.rules.pod_status_rules or not self.is_nexus(pod):
             return []
         if old is not None and kube.resource_version(old) == kube.resource_version(pod) and kube.resource_version(pod):
@@ -216,7 +228,13 @@ class Classifier:
             if allow_wait and not self.has_gpu_evidence(pod) and kube.gpu_request(pod, self.gpu.gpu_resource_name) > 0:
                 self.deferred = True
                 return []
-            verdict = self._oom(pod, [t.get("message", "") for t in failed_terms], failed_terms)
+            verdict = self._oom(pod, [], failed_terms)
+            if not verdict.kind and allow_log_fetch:
+                want = self._log_fetch_needed(pod)
+                if want:
+                    self.deferred_log = want
+                    self.deferred = True
+                    return []
             if verdict.kind:
                 hbm = verdict.kind == "hbm"
                 t0 = failed_terms[0]
@@ -257,6 +275,12 @@ class Classifier:
                 self._enrich(res, pods=[pod])
                 return [res]
             if wr == "CrashLoopBackOff":
+                if allow_log_fetch:
+                    want = self._log_fetch_needed(pod)
+                    if want:  # the last instance's OOM text may be in its log only
+                        self.deferred_log = want
+                        self.deferred = True
+                        return []
                 texts = [t.get("message", "") for t in kube.terminated_states(pod)]
                 res = self._result(A.TO_FAIL_FATAL_ERROR, MSG_CRASH_LOOP, w.get("message", ""), inv, request_id, algorithm, wr, F.CRASH_LOOP, "pod-status")
                 self._enrich(res, pods=[pod], texts=texts)
@@ -369,8 +393,46 @@ class Classifier:
 
     def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
         topo, gev = self._pod_ctx(pod)
-        return oom_mod.analyze(texts, terms, gev, topo.get("expected_gpu"),
+        return oom_mod.analyze(list(texts) + self._log_texts(pod, gev), terms, gev, topo.get("expected_gpu"),
                                self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction, topo=topo)
+
+    # ------------------------------------------------------------ container log tails
+    def _log_records(self, pod, gev) -> List[Dict[str, Any]]:
+        if self.gpu.log_tail == "off":
+            return []
+        recs = list((gev or {}).get("logs") or ())
+        got = self.log_cache.get(kube.uid_of(pod) or kube.name_of(pod))
+        if got:
+            recs.extend(got)
+        return recs
+
+    def _log_texts(self, pod, gev) -> List[Tuple[str, str]]:
+        return logtail.log_texts(self._log_records(pod, gev))
+
+    def _log_fetch_needed(self, pod) -> List[Dict[str, Any]]:
+        """Container instances whose log tail the supervisor should fetch (``pods/log``):
+        a GPU pod's failed containers with an empty termination message that neither the
+        node agent (``auto``) nor an earlier fetch has read."""
+        mode = self.gpu.log_tail
+        if mode not in ("auto", "api") or kube.gpu_request(pod, self.gpu.gpu_resource_name) <= 0:
+            return []
+        if (kube.uid_of(pod) or kube.name_of(pod)) in self.log_cache:
+            return []
+        want = logtail.failed_containers(pod)
+        if want and mode == "auto":
+            _topo, gev = self._pod_ctx(pod)
+            read = {r.get("container") for r in (gev or {}).get("logs") or () if not r.get("error")}
+            want = [w for w in want if w["container"] not in read]
+        return want
+
+    def store_logs(self, pod, records: List[Dict[str, Any]]) -> None:
+        """Log-tail records fetched for ``pod`` (kept even when empty or failed: one fetch
+        per pod); bounded LRU."""
+        key = kube.uid_of(pod) or kube.name_of(pod)
+        self.log_cache[key] = records
+        self.log_cache.move_to_end(key)
+        while len(self.log_cache) > 4096:
+            self.log_cache.popitem(last=False)
 
     def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
         if not self.gpu.attribution_enabled:
@@ -387,9 +449,13 @@ class Classifier:
                 res.evidence["topology"] = topo
             if gev:
                 res.evidence["gpu"] = gev
+            logs = [r for p in pods for r in (self.log_cache.get(kube.uid_of(p) or kube.name_of(p)) or ())]
+            if logs and want_gpu:
+                res.evidence["logs"] = logs
             if verdict is None and res.action != A.TO_RUNNING:
                 terms = [t for p in pods for t in kube.terminated_states(p)]
-                verdict = oom_mod.analyze(list(texts) + [t.get("message", "") for t in terms], terms, gev,
+                ltexts = [x for p in pods for x in self._log_texts(p, gev if p is pod else self._pod_ctx(p)[1])]
+                verdict = oom_mod.analyze(list(texts) + ltexts, terms, gev,
                                           topo.get("expected_gpu"), self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction,
                                           topo=topo)
         elif verdict is None and res.action != A.TO_RUNNING and any(texts):
@@ -427,11 +493,17 @@ class Classifier:
                 terms = [t for p in pods for t in kube.terminated_states(p)]
                 if terms:
                     topo, gev = self._pod_ctx(pods[-1])
-                    v = oom_mod.analyze([t.get("message", "") for t in terms], terms, gev, topo.get("expected_gpu"),
+                    ltexts = [x for p in pods for x in self._log_texts(p, self._pod_ctx(p)[1])]
+                    v = oom_mod.analyze(ltexts, terms, gev, topo.get("expected_gpu"),
                                         self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction, topo=topo)
                     if v.kind:
                         res.evidence["oom"] = v.as_dict()
                         res.failure_class = F.HBM_OOM if v.kind == "hbm" else F.HOST_OOM
+                        if res.action == A.TO_FAIL_DEADLINE_EXCEEDED:
+                            # BackoffLimitExceeded of a run whose pods died of an OOM: the run
+                            # failed, it did not time out (what the pod-status rule writes)
+                            res.action = A.TO_FAIL_FATAL_ERROR
+                            res.run_status_message = MSG_HBM_OOM if v.kind == "hbm" else MSG_HOST_OOM
         self._apply_history(res)
 
 

@@ -143,6 +143,14 @@ class GpuConfig:
     # hold a failed GPU pod's decision this long for the node agent's evidence annotation
     # (0 = decide immediately on whatever is there)
     evidence_wait: float = field(default=0.0, metadata=_k("evidence-wait", "duration"))
+    # container log tails for the OOM signature of a failed GPU container whose termination
+    # message is empty (the default terminationMessagePolicy: File; torch prints its OOM to
+    # stderr): auto — the node agent's /var/log/pods reading when its annotation has one,
+    # else the supervisor GETs pods/<pod>/log (RBAC pods/log get); api — always the API;
+    # node — the agent's reading only; off — never look at logs
+    log_tail: str = field(default="auto", metadata=_k("log-tail"))
+    log_tail_timeout: float = field(default=2.0, metadata=_k("log-tail-timeout", "duration"))
+    log_tail_bytes: int = field(default=65536, metadata=_k("log-tail-bytes"))
 
 
 @dataclass
@@ -318,6 +326,10 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("runtime.worker-processes must be >= 0 (0 = auto) and runtime.worker-index in [0, worker-processes)")
     if not 0 < cfg.gpu.hbm_oom_fraction <= 1:
         raise ConfigError("gpu.hbm-oom-fraction must be in (0, 1]")
+    if cfg.gpu.log_tail not in ("auto", "api", "node", "off"):
+        raise ConfigError("gpu.log-tail must be auto|api|node|off")
+    if cfg.gpu.log_tail_bytes < 1024 or cfg.gpu.log_tail_timeout <= 0:
+        raise ConfigError("gpu.log-tail-bytes must be >= 1024 and gpu.log-tail-timeout > 0")
     if cfg.leader_election.enabled or cfg.sharding.mode == "lease":
         le = cfg.leader_election
         if not le.lease_duration > le.renew_deadline > le.retry_period > 0:

@@ -13,18 +13,31 @@ GPU ↔ pod mapping, strongest first: cgroup pod UID of the processes amd-smi sa
 on each GPU (needs hostPID); the kubelet pod-resources allocation (device BDFs,
 :mod:`.podresources`); the pod's ``HIP_VISIBLE_DEVICES``/``LOCAL_RANK`` env.
 
+Container logs: for every failed container whose termination message is empty (the
+default ``terminationMessagePolicy: File`` — PyTorch prints its HBM-OOM to stderr and
+exits 1) the agent reads the tail of ``/var/log/pods/<ns>_<pod>_<uid>/<container>/<n>.log``
+(read-only hostPath) and publishes the allocation-failure lines it finds (``logs``,
+:mod:`.logtail`).
+
+Delivery: an annotation PATCH that fails is retried with capped exponential backoff for
+as long as the pod exists; the per-pod bookkeeping is dropped when the pod is deleted
+(and by TTL), fault history is bounded, and every publish task is tracked and cancelled
+on stop.
+
 No counterpart in the reference (it has no node component).
 """
 from __future__ import annotations
 
 import asyncio
+import collections
 import json
 import logging
 import time
-from typing import Any, Dict, List, Optional, Set, Tuple
+from typing import Any, Deque, Dict, List, Optional, Set, Tuple
 
 from ..informer import InformerFactory
 from ..models import kube
+from . import logtail
 from .podresources import PodResourcesClient, gpu_allocations, normalize_bdf
 from .telemetry import ATTRIBUTION_EVENTS, FAULT_EVENTS, GpuTelemetry, _pod_gpus, evidence_for
 from .topology import topology_from_pod
@@ -47,7 +60,10 @@ class NodeAgent:
     def __init__(self, kube_client, telemetry: GpuTelemetry, node_name: str, namespace: str, *,
                  label_selector: str = "", annotation: str = "nexus.amd.com/gpu-evidence",
                  gpu_resource: str = "amd.com/gpu", pod_resources: Optional[PodResourcesClient] = None,
-                 event_poll: float = 0.1, lookback: float = 600.0, factory: Optional[InformerFactory] = None):
+                 event_poll: float = 0.1, lookback: float = 600.0, factory: Optional[InformerFactory] = None,
+                 log_root: Optional[str] = logtail.LOG_ROOT, log_tail_bytes: int = logtail.TAIL_BYTES,
+                 retry_base: float = 0.2, retry_max: float = 10.0, published_ttl: float = 3600.0,
+                 max_faults: int = 1024):
         self.kube = kube_client
         self.tel = telemetry
         self.node = node_name
@@ -64,24 +80,35 @@ class NodeAgent:
                                                                  field_selector=f"spec.nodeName={node_name}"), resync_period=0)
         self.factory = factory
         self.pods = factory.informer("Pod")
-        self.published: Dict[str, str] = {}  # pod uid -> reason published
-        self.faults: List[Dict[str, Any]] = []
+        self.log_root = log_root
+        self.log_tail_bytes = log_tail_bytes
+        self.retry_base, self.retry_max = retry_base, retry_max
+        self.published_ttl = published_ttl
+        # pod uid -> (state, monotonic time): "pending" while a publish task runs, then the
+        # reason published ("present": an annotation was already there)
+        self.published: Dict[str, Tuple[str, float]] = {}
+        self.faults: Deque[Dict[str, Any]] = collections.deque(maxlen=max_faults)
         self._tasks: List[asyncio.Task] = []
+        self._publishing: Dict[str, asyncio.Task] = {}  # pod uid -> publish-with-retry task
         self._bdf_index: Dict[str, int] = {}
         self.patches = 0
+        self.patch_failures = 0
 
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> None:
         self.tel.start()
         self._bdf_index = {normalize_bdf(d.get("bdf", "")): d["index"] for d in self.tel.devices() if d.get("bdf")}
-        self.pods.add_event_handler(on_add=lambda p: self._on_pod(None, p), on_update=self._on_pod)
+        self.pods.add_event_handler(on_add=lambda p: self._on_pod(None, p), on_update=self._on_pod,
+                                    on_delete=self._on_pod_delete)
         self.factory.start()
         self._tasks.append(asyncio.create_task(self._event_loop(), name="agent-gpu-events"))
 
     async def stop(self) -> None:
-        for t in self._tasks:
+        tasks = self._tasks + list(self._publishing.values())
+        for t in tasks:
             t.cancel()
-        await asyncio.gather(*self._tasks, return_exceptions=True)
+        await asyncio.gather(*tasks, return_exceptions=True)
+        self._publishing.clear()
         await self.factory.stop()
         self.tel.stop()
         if self.podres is not None:
@@ -113,38 +140,110 @@ class NodeAgent:
 
     def evidence(self, pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         alloc = self.allocation(pod)
-        return evidence_for(self.tel, pod_uid=kube.uid_of(pod), gpu_indices=self.gpus_for(pod, alloc),
-                            lookback=self.lookback, node=self.node, allocated=alloc)
+        ev = evidence_for(self.tel, pod_uid=kube.uid_of(pod), gpu_indices=self.gpus_for(pod, alloc),
+                          lookback=self.lookback, node=self.node, allocated=alloc)
+        logs = self.log_evidence(pod)
+        if logs:
+            if ev is None:
+                ev = {"source": self.tel.name, "t": round(time.time(), 3), "gpus": [], "node": self.node,
+                      "pod_uid": kube.uid_of(pod)}
+            ev["logs"] = logs
+        return ev
+
+    def log_evidence(self, pod: Dict[str, Any]) -> List[Dict[str, Any]]:
+        """Allocation-failure lines from the tails of the pod's failed containers' logs."""
+        if not self.log_root:
+            return []
+        try:
+            return logtail.node_log_evidence(self.log_root, pod, self.log_tail_bytes)
+        except Exception as exc:  # noqa: BLE001 - logs are evidence, never a reason to skip the GPU record
+            log.debug("log tail of %s failed: %s", kube.name_of(pod), exc)
+            return []
 
     # ------------------------------------------------------------ publishing
-    async def publish(self, pod: Dict[str, Any], reason: str) -> bool:
+    async def publish(self, pod: Dict[str, Any], reason: str) -> Optional[bool]:
+        """One annotation PATCH; True when it landed, False when it failed, None when there
+        is no evidence to publish (no GPU matched, no log read)."""
         ev = self.evidence(pod)
         if ev is None:
-            return False
+            return None
         ev["reason"] = reason
         body = {"metadata": {"annotations": {self.annotation: json.dumps(ev, separators=(",", ":"), sort_keys=True)}}}
         try:
             await self.kube.patch_merge("Pod", kube.namespace_of(pod), kube.name_of(pod), body)
         except Exception as exc:  # noqa: BLE001
+            self.patch_failures += 1
             log.warning("annotating pod %s failed: %s", kube.name_of(pod), exc)
             return False
-        self.published[kube.uid_of(pod)] = reason
+        self.published[kube.uid_of(pod)] = (reason, time.monotonic())
         self.patches += 1
         return True
+
+    async def _publish_with_retry(self, uid: str, key: str, pod: Dict[str, Any], reason: str) -> None:
+        """Retry the PATCH with capped exponential backoff while the pod still exists (the
+        evidence is rebuilt from the latest cached pod each attempt); the pod's entry is
+        dropped when it goes away, so nothing is lost for good to one apiserver 5xx."""
+        delay = self.retry_base
+        try:
+            while True:
+                cur = self.pods.indexer.get(key) if key else pod
+                if cur is None or kube.uid_of(cur) != uid:
+                    self.published.pop(uid, None)
+                    return
+                ok = await self.publish(cur, reason)
+                if ok is None:
+                    self.published[uid] = ("no-evidence", time.monotonic())
+                    return
+                if ok:
+                    return
+                await asyncio.sleep(delay)
+                delay = min(self.retry_max, delay * 2)
+        finally:
+            self._publishing.pop(uid, None)
+            if self.published.get(uid, ("",))[0] == "pending":
+                self.published.pop(uid, None)  # cancelled (stop) or gone: nothing is claimed
+
+    def _spawn_publish(self, pod: Dict[str, Any], reason: str) -> None:
+        uid = kube.uid_of(pod)
+        if uid in self._publishing:
+            return
+        self.published[uid] = ("pending", time.monotonic())
+        self._publishing[uid] = asyncio.ensure_future(
+            self._publish_with_retry(uid, kube.object_key(pod), pod, reason))
 
     def _on_pod(self, old, pod) -> None:
         uid = kube.uid_of(pod)
         if uid in self.published or not pod_failed(pod):
             return
         if kube.annotations_of(pod).get(self.annotation):
-            self.published[uid] = "present"
+            self.published[uid] = ("present", time.monotonic())
             return
-        self.published[uid] = "pending"
-        asyncio.ensure_future(self.publish(pod, "pod-failed"))
+        self._spawn_publish(pod, "pod-failed")
+
+    def _on_pod_delete(self, pod) -> None:
+        uid = kube.uid_of(pod)
+        self.published.pop(uid, None)
+        t = self._publishing.pop(uid, None)
+        if t is not None:
+            t.cancel()
+
+    def _prune(self, now: float) -> None:
+        """TTL for published entries whose pod deletion was missed (e.g. across a re-list)."""
+        if not self.published:
+            return
+        cutoff = now - self.published_ttl
+        for uid, (state, t) in list(self.published.items()):
+            if t < cutoff and state != "pending":
+                del self.published[uid]
 
     async def _event_loop(self) -> None:
+        next_prune = time.monotonic() + 60.0
         while True:
             await asyncio.sleep(self.event_poll)
+            now = time.monotonic()
+            if now >= next_prune:
+                self._prune(now)
+                next_prune = now + 60.0
             try:
                 events = self.tel.drain_events()
             except Exception:  # noqa: BLE001
@@ -158,7 +257,9 @@ class NodeAgent:
                 if (pod.get("status") or {}).get("phase") not in ("Running", "Pending"):
                     continue
                 if hit & set(self.gpus_for(pod)):
-                    await self.publish(pod, "gpu-fault:" + ",".join(sorted({e["type"] for e in faults})))
+                    ok = await self.publish(pod, "gpu-fault:" + ",".join(sorted({e["type"] for e in faults})))
+                    if ok is False and kube.uid_of(pod) not in self._publishing:
+                        self._spawn_publish(pod, "gpu-fault:" + ",".join(sorted({e["type"] for e in faults})))
 
 
 async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process entry
@@ -173,8 +274,11 @@ async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process 
         raise RuntimeError("no GPU telemetry backend on this node")
     pr = PodResourcesClient() if os.path.exists(SOCKET) else None
     sel = f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
+    log_root = os.environ.get("NEXUS_AGENT_LOG_ROOT", logtail.LOG_ROOT)
     agent = NodeAgent(kc, tel, node_name, cfg.resource_namespace, label_selector=sel,
-                      annotation=cfg.gpu.evidence_annotation, gpu_resource=cfg.gpu.gpu_resource_name, pod_resources=pr)
+                      annotation=cfg.gpu.evidence_annotation, gpu_resource=cfg.gpu.gpu_resource_name, pod_resources=pr,
+                      log_root=log_root if cfg.gpu.log_tail != "off" and os.path.isdir(log_root) else None,
+                      log_tail_bytes=cfg.gpu.log_tail_bytes)
     await agent.start()
     stop = asyncio.Event()
     import signal

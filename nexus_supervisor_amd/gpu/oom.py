@@ -9,18 +9,24 @@ host-OOM
   * in-process host allocation failure (``MemoryError``, ``std::bad_alloc``,
     ``Cannot allocate memory``)                                             +0.6
 HBM-OOM (288 GB HBM3E per MI355X)
-  * HIP OOM signature in the termination / event message
-    (``hipErrorOutOfMemory``, ``HIP out of memory``, torch
-    ``OutOfMemoryError``, RCCL/hipMalloc allocation failures)              +1.0
-  * agent-sampled VRAM peak ≥ ``hbm_oom_fraction`` × capacity on the rank's GPU +0.5
+  * HIP OOM signature in the termination / event message or in the container's log
+    tail (``hipErrorOutOfMemory``, ``HIP out of memory``, torch ``OutOfMemoryError``,
+    RCCL/hipMalloc allocation failures; :mod:`.logtail` reads the tail from the node's
+    ``/var/log/pods`` or the ``pods/log`` API, because a default pod's termination
+    message is empty — PyTorch prints its OOM to stderr and exits 1)           +1.0
+  * the pod's OWN processes (cgroup pod UID / PID match) peaked at
+    ≥ ``hbm_oom_fraction`` × capacity and the container exited non-zero       +0.75
+  * agent-sampled device-wide VRAM peak ≥ ``hbm_oom_fraction`` × capacity    +0.5
   * VM-fault / queue-eviction event on that GPU                             +0.25
 
-A verdict needs ≥0.5 **and** at least one OOM *signature* (a HIP/host allocation
-failure message, OOMKilled, or exit 137): VRAM peaks and GPU events corroborate and
-attribute, they never make a plain crash an OOM on their own (a GPU left full by a
-previous tenant must not turn an exit-1 into an HBM-OOM that bypasses the Job's
-retry policy).  The larger score wins, with a cgroup OOMKill (a hard kernel fact about
-*host* memory) winning ties.
+A verdict needs ≥0.5 **and** at least one OOM *signature* (an allocation-failure message
+or log line, OOMKilled, exit 137, or the own-process peak): the device-wide peak and GPU
+events corroborate and attribute, they never make a plain crash an OOM on their own (a
+GPU left full by a previous tenant must not turn an exit-1 into an HBM-OOM that bypasses
+the Job's retry policy).  The larger score wins; a cgroup OOMKill (a hard kernel fact
+about *host* memory) is beaten only by HIP's own words, never by VRAM numbers.  Every
+signal names its source (termination message, node-log / pods/log tail, own-process
+peak, device peak).
 
 GPU index.  torch's ``GPU N`` is the *logical* HIP ordinal inside the process, after
 ROCR/HIP_VISIBLE_DEVICES and the device plugin's allocation narrowed the node's GPUs.
@@ -33,7 +39,7 @@ from __future__ import annotations
 
 import re
 from dataclasses import dataclass, field
-from typing import Any, Dict, Iterable, List, Optional
+from typing import Any, Dict, Iterable, List, Optional, Tuple
 
 HBM_PATTERNS = [
     re.compile(r"hipErrorOutOfMemory", re.I),
@@ -87,6 +93,8 @@ class OomVerdict:
     peak_vram_bytes: Optional[int] = None
     device_peak_vram_bytes: Optional[int] = None
     signature: bool = False
+    oomkilled: bool = False
+    hbm_text: bool = False
 
     def as_dict(self) -> Dict[str, Any]:
         d: Dict[str, Any] = {"kind": self.kind, "hbm_score": round(self.hbm_score, 3),
@@ -120,7 +128,7 @@ def host_signature(text: str) -> Optional[str]:
 
 
 def analyze(
-    texts: Iterable[str] = (),
+    texts: Iterable[Any] = (),
     terminated: Iterable[Dict[str, Any]] = (),
     gpu_evidence: Optional[Dict[str, Any]] = None,
     expected_gpu: Optional[str] = None,
@@ -128,38 +136,51 @@ def analyze(
     hbm_oom_fraction: float = 0.97,
     topo: Optional[Dict[str, Any]] = None,
 ) -> OomVerdict:
+    """``texts``: strings (a termination / event / condition message) or ``(source, text)``
+    pairs (container log tails, :mod:`.logtail`) — every signal names where it was found."""
     from .topology import physical_gpu
 
     v = OomVerdict()
-    texts = [t for t in texts if t]
+    sourced: List[Tuple[str, str]] = []
+    for t in texts:
+        if isinstance(t, tuple):
+            if t[1]:
+                sourced.append((t[0], t[1]))
+        elif t:
+            sourced.append(("message", t))
+    failed_exit = False
     for t in terminated:
         reason = t.get("reason") or ""
         code = t.get("exitCode")
+        if code not in (None, 0) or reason == "OOMKilled":
+            failed_exit = True
         if reason == "OOMKilled":
             v.host_score += 1.0
             v.signature = True
+            v.oomkilled = True
             v.signals.append(f"container {t.get('container', '')!s} OOMKilled (cgroup, exit {code})")
         elif code == 137:
             v.host_score += 0.35
             v.signature = True
             v.signals.append(f"container {t.get('container', '')!s} exit 137 (SIGKILL)")
         if t.get("message"):
-            texts.append(t["message"])
+            sourced.append((f"termination message of container {t.get('container', '')}", t["message"]))
     hbm_hit = host_hit = False
     logical = None
-    for text in texts:
+    for source, text in sourced:
         s = hbm_signature(text)
         if s and not hbm_hit:
             hbm_hit = True
             v.signature = True
+            v.hbm_text = True
             v.hbm_score += 1.0
-            v.signals.append(f"HIP OOM signature: {s!r}")
+            v.signals.append(f"HIP OOM signature in {source}: {s!r}")
         h = host_signature(text)
         if h and not host_hit and h != "OOMKilled":
             host_hit = True
             v.signature = True
             v.host_score += 0.6
-            v.signals.append(f"host allocation failure: {h!r}")
+            v.signals.append(f"host allocation failure in {source}: {h!r}")
         if not _mentions(text, _TORCH_KEYS):
             continue
         m = _TORCH_GPU.search(text)
@@ -178,15 +199,29 @@ def analyze(
             v.gpu_index = logical  # no topology: the process saw the node's numbering
     if gpu_evidence:
         cap = int(hbm_capacity_gb * (1 << 30))
+        own_sig = False
         for g in _candidate_gpus(gpu_evidence, expected_gpu, v.gpu_index):
             total = int(g.get("vram_total_mb") or 0) * (1 << 20) or cap
             peak = int(g.get("vram_peak_mb") or g.get("vram_used_mb") or 0) * (1 << 20)
             own = int(g.get("proc_peak_vram_bytes") or 0)
+            if own and own >= hbm_oom_fraction * total and failed_exit and not own_sig:
+                # the pod's OWN processes (matched by cgroup pod UID / PID) filled the GPU and
+                # the container then failed: an OOM signature in its own right — unlike the
+                # device-wide peak, which a previous tenant or a neighbour can produce
+                own_sig = True
+                v.signature = True
+                v.hbm_score += 0.75
+                v.signals.append(f"own-process VRAM peak: the pod's processes on GPU {g.get('index')} peaked at "
+                                 f"{own / (1 << 30):.1f} GiB of {total / (1 << 30):.1f} GiB, then the container "
+                                 f"exited non-zero")
+                v.peak_vram_bytes = own
+                if v.gpu_index is None:
+                    v.gpu_index = g.get("index")
             if peak and peak >= hbm_oom_fraction * total:
                 v.hbm_score += 0.5
                 share = f"; the pod's own processes peaked at {own / (1 << 30):.1f} GiB" if own else ""
                 v.signals.append(f"GPU {g.get('index')} VRAM peak {peak / (1 << 30):.1f} GiB of "
-                                 f"{total / (1 << 30):.1f} GiB{share}")
+                                 f"{total / (1 << 30):.1f} GiB{share} (device-wide: corroboration only)")
                 v.device_peak_vram_bytes = peak
                 v.peak_vram_bytes = own or peak
                 if v.gpu_index is None:
@@ -200,14 +235,17 @@ def analyze(
             if v.capacity_bytes is None and g.get("vram_total_mb"):
                 v.capacity_bytes = int(g["vram_total_mb"]) * (1 << 20)
     if v.signature and (v.hbm_score >= 0.5 or v.host_score >= 0.5):
-        if v.host_score >= 1.0 and v.host_score >= v.hbm_score:
+        if v.oomkilled and not v.hbm_text:
+            v.kind = "host"  # a cgroup OOMKill is a kernel fact about host memory: only HIP's own words beat it
+        elif v.host_score >= 1.0 and v.host_score >= v.hbm_score:
             v.kind = "host"
         elif v.hbm_score >= v.host_score:
             v.kind = "hbm"
         else:
             v.kind = "host"
     elif v.hbm_score >= 0.5:
-        v.signals.append("no OOM signature (allocation-failure message, OOMKilled or exit 137): not an OOM verdict")
+        v.signals.append("no OOM signature (allocation-failure message or log line, OOMKilled, exit 137, or the pod's "
+                         "own processes filling the GPU): not an OOM verdict")
     return v
 
 

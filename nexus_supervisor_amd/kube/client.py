@@ -437,6 +437,15 @@ class KubeClient:
             raise from_status(status, doc)
         return doc
 
+    async def pod_log(self, namespace: str, name: str, container: str, *, previous: bool = False,
+                      tail_lines: int = 200, limit_bytes: int = 65536, timeout: float = 2.0) -> Tuple[int, bytes]:
+        """``GET …/pods/<name>/log`` tail of one container instance: ``(status, raw text)``
+        (``previous``: the instance before the last restart)."""
+        params = {"container": container, "tailLines": str(int(tail_lines)), "limitBytes": str(int(limit_bytes))}
+        if previous:
+            params["previous"] = "true"
+        return await self.get_raw(resource_path("Pod", namespace, name) + "/log", params, timeout=timeout)
+
     # JobClient protocol (Supervisor actuator)
     async def delete_job(self, namespace: str, name: str, propagation_policy: str = "Background") -> None:
         await self.delete("Job", namespace, name, propagation_policy, want_body=False)

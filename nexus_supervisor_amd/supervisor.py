@@ -136,6 +136,10 @@ class Supervisor:
         self._guards: Dict[Any, Any] = {}
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
+        self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
+        g = cfg.gpu
+        self._log_fetch = (g.attribution_enabled and g.log_tail in ("auto", "api")
+                           and callable(getattr(jobs, "pod_log", None)))
         self._deletes: Dict[Any, str] = {}  # in-flight asynchronous Job DELETEs → request id
         self._bg: set = set()  # housekeeping tasks (post-re-list replays)
         self._sweeper: Optional[asyncio.Task] = None
@@ -212,7 +216,7 @@ class Supervisor:
 
     async def stop(self, drain: bool = True, timeout: float = 10.0) -> None:
         self.gc_tuner.stop()
-        for t in list(self._bg):
+        for t in list(self._bg) + list(self._log_fetches.values()):
             t.cancel()
         if self._sweeper:
             self._sweeper.cancel()
@@ -428,10 +432,17 @@ class Supervisor:
             return
         recv = self.wall()
         wait = self.cfg.gpu.evidence_wait
-        results = self.classifier.classify_pod(pod, old, allow_wait=wait > 0 and not waited)
+        results = self.classifier.classify_pod(pod, old, allow_wait=wait > 0 and not waited,
+                                               allow_log_fetch=self._log_fetch)
         if not results and not self._gpu_wait and not self.classifier.deferred:
             return  # the common case (a new or unchanged pod): nothing to submit or un-defer
         key = kube.object_key(pod)
+        if self.classifier.deferred_log:
+            # failed GPU container, empty termination message: its OOM text (if any) is in
+            # the container log — fetch the tail, then decide (gpu.log-tail)
+            self._gpu_wait.pop(key, None)
+            self._start_log_fetch(key, pod, self.classifier.deferred_log, waited)
+            return
         if self.classifier.deferred:
             # failed GPU pod without node-agent evidence yet: give the annotation time to land
             if key not in self._gpu_wait:
@@ -441,6 +452,35 @@ class Supervisor:
         self._gpu_wait.pop(key, None)
         for r in results:
             self._submit(r, recv, recv)
+
+    def _start_log_fetch(self, key: str, pod: Dict[str, Any], want: List[Dict[str, Any]], waited: bool) -> None:
+        if key in self._log_fetches:
+            return
+        self.metrics.inc("decisions_deferred_for_log_tail")
+        t = asyncio.ensure_future(self._fetch_log_tail(key, pod, want, waited))
+        self._log_fetches[key] = t
+
+    async def _fetch_log_tail(self, key: str, pod: Dict[str, Any], want: List[Dict[str, Any]], waited: bool) -> None:
+        from .gpu.logtail import fetch_api_tail
+
+        g = self.cfg.gpu
+        try:
+            recs = await asyncio.gather(*(fetch_api_tail(self.jobs, self.namespace, kube.name_of(pod), w["container"],
+                                                         previous=w["previous"], limit_bytes=g.log_tail_bytes,
+                                                         timeout=g.log_tail_timeout) for w in want))
+            for r, w in zip(recs, want):
+                r["restart"] = w["restart"]
+                if r.get("error"):
+                    self.metrics.inc("log_tail_errors")
+                elif r.get("match"):
+                    self.metrics.inc("log_tail_hits", labels={"match": r["match"]})
+            self.metrics.inc("log_tail_fetches", len(recs))
+            self.classifier.store_logs(pod, list(recs))
+        finally:
+            self._log_fetches.pop(key, None)
+        latest = self.pod_informer.indexer.get(key)
+        if latest is not None and self.active:
+            self._on_pod_update(None, latest, waited=waited)
 
     def _expire_gpu_waits(self) -> None:
         now = time.monotonic()
@@ -618,6 +658,13 @@ class Supervisor:
         if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)
+        if failing:
+            # a Job-level failure can overtake its pod's (deferred) log-tail read: wait for it,
+            # then re-enrich — an OOM found now also fixes the action (BackoffLimitExceeded of
+            # an OOM-killed run is FAILED, not DEADLINE_EXCEEDED), so it must precede the stage
+            if self._log_fetches and r.object_kind == "Job":
+                await self._await_pod_logs(r)
+            self.classifier.late_enrich(r, self.lookup)
         if self._fused:
             d = await self._fused_action(r, epoch, failing)
             if d is not None:
@@ -660,7 +707,6 @@ class Supervisor:
             self._remember(key, stage)
             return Decision(r, "applied", stage, False)
         cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
-        self.classifier.late_enrich(r, self.lookup)
         details = render_trace(r, self.cfg.rules.trace_format)
         # The reference deletes the Job, then upserts the row (supervisor.go:289-301).  This
         # build writes first: deleting first (or concurrently) lets a crash between the two
@@ -696,6 +742,13 @@ class Supervisor:
             r.pending_delete = True  # the retry sees the finished row and only deletes
             raise
         return Decision(r, "applied", stage, deleted)
+
+    async def _await_pod_logs(self, r: RunStatusAnalysisResult) -> None:
+        keys = [kube.object_key(p) for p in self.lookup.pods_of_job(r.request_id)]
+        tasks = [self._log_fetches[k] for k in keys if k in self._log_fetches]
+        if tasks:
+            self.metrics.inc("decisions_awaited_log_tail")
+            await asyncio.wait(tasks, timeout=self.cfg.gpu.log_tail_timeout + 0.5)
 
     async def _skip_missing(self, r: RunStatusAnalysisResult, failing: bool) -> Decision:
         self.log.info("no checkpoint exists for the provided request, skipping", requestId=r.request_id, algorithm=r.algorithm)
@@ -741,7 +794,6 @@ class Supervisor:
             cause = details = None
         else:
             cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
-            self.classifier.late_enrich(r, self.lookup)
             details = render_trace(r, self.cfg.rules.trace_format)
         if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")

@@ -183,6 +183,10 @@ class FakeApiServer:
         self.fail_next: Dict[Tuple[str, str], int] = {}  # (method, kind) -> count of 500s to inject
         self._snapshots: Dict[str, Tuple[int, List[Dict[str, Any]]]] = {}  # paginated LIST snapshots
         self.latency = 0.0
+        # container logs served by GET …/pods/{name}/log: (ns, pod, container, previous) -> text
+        self.pod_logs: Dict[Tuple[str, str, str, bool], str] = {}
+        self.log_requests: List[Dict[str, str]] = []
+        self.log_latency = 0.0  # extra delay of pods/log answers only
         self.coalesce = 0.0005  # watch write coalescing window (seconds)
         self.requests = 0
         self.watch_requests = 0
@@ -201,6 +205,7 @@ class FakeApiServer:
             srv.add_route("PATCH", base + "/{name}", self._h_patch)
             srv.add_route("DELETE", base + "/{name}", self._h_delete)
             srv.add_route("GET", f"{prefix}/{plural}", self._h_collection)
+        srv.add_route("GET", "/api/v1/namespaces/{ns}/pods/{name}/log", self._h_pod_log)
         port = await srv.start(host, port)
         self._server = srv
         self.url = f"http://{host}:{port}"
@@ -461,6 +466,40 @@ class FakeApiServer:
         finally:
             self.watchers[kind].discard(w)
         return resp
+
+    def set_pod_log(self, ns: str, pod: str, container: str, text: str, previous: bool = False) -> None:
+        self.pod_logs[(ns, pod, container, previous)] = text
+
+    async def _h_pod_log(self, req: web.Request):
+        """``pods/{name}/log`` (text/plain): ``container``, ``previous``, ``tailLines`` and
+        ``limitBytes`` as the apiserver applies them (limitBytes cuts the tail's end)."""
+        self.requests += 1
+        bad = self._auth(req)
+        if bad is not None:
+            return bad
+        if self.latency or self.log_latency:
+            await asyncio.sleep(self.latency + self.log_latency)
+        q = req.query
+        self.log_requests.append(dict(q, pod=req.match_info["name"]))
+        n = self.fail_next.get(("GET", "PodLog"), 0)
+        if n:
+            self.fail_next[("GET", "PodLog")] = n - 1
+            return self._status(500, "InternalError", "injected failure")
+        ns, name = req.match_info["ns"], req.match_info["name"]
+        if (ns, name) not in self.objects["Pod"]:
+            return self._status(404, "NotFound", f'pods "{name}" not found')
+        prev = q.get("previous") in ("true", "1")
+        text = self.pod_logs.get((ns, name, q.get("container", ""), prev))
+        if text is None:
+            return self._status(400, "BadRequest", f'previous terminated container "{q.get("container")}" not found'
+                                if prev else f'container "{q.get("container")}" has no log')
+        lines = text.splitlines(keepends=True)
+        if q.get("tailLines"):
+            lines = lines[-int(q["tailLines"]):]
+        body = "".join(lines).encode()
+        if q.get("limitBytes"):
+            body = body[:int(q["limitBytes"])]
+        return web.Response(body=body, content_type="text/plain")
 
     async def _h_get(self, req: web.Request):
         bad = await self._pre(req, "GET")
