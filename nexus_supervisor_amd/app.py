@@ -43,14 +43,14 @@ def _identity(cfg: SupervisorConfig) -> str:
     return le.identity or os.environ.get("POD_NAME") or f"{socket.gethostname()}-{os.getpid()}"
 
 
-def make_shard_leases(cfg: SupervisorConfig, kube, on_change, metrics):
+def make_shard_leases(cfg: SupervisorConfig, kube, on_change, metrics, on_renewed=None):
     """``sharding.mode: lease``: the replica's :class:`~.ha.shards.ShardLeaseManager`."""
     from .ha.shards import ShardLeaseManager
 
     le, sh = cfg.leader_election, cfg.sharding
     return ShardLeaseManager(kube, cfg.resource_namespace, le.lease_name, _identity(cfg), sh.shards,
                              replicas=sh.replicas, lease_duration=le.lease_duration, renew_deadline=le.renew_deadline,
-                             retry_period=le.retry_period, on_change=on_change, metrics=metrics)
+                             retry_period=le.retry_period, on_change=on_change, metrics=metrics, on_renewed=on_renewed)
 
 
 def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
@@ -111,7 +111,8 @@ class Application:
             await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
         if cfg.sharding.mode == "lease":
             # one Lease per shard replaces the single leader lease (ha/shards.py)
-            self.shard_leases = make_shard_leases(cfg, self.kube, self.supervisor.set_shards, self.metrics)
+            self.shard_leases = make_shard_leases(cfg, self.kube, self.supervisor.set_shards, self.metrics,
+                                                  on_renewed=self.supervisor.shards.set_deadlines)
         elif cfg.leader_election.enabled:
             from .ha.leader import LeaderElector, LeaseLock
 
@@ -121,7 +122,9 @@ class Application:
                 LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, _identity(cfg)),
                 lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
                 on_started_leading=lambda: self.supervisor.set_active(True),
-                on_stopped_leading=lambda: self.supervisor.set_active(False), metrics=self.metrics)
+                on_stopped_leading=lambda: self.supervisor.set_active(False), metrics=self.metrics,
+                on_renewed=self.supervisor.set_lease_deadline)
+            self.supervisor.active_until = float("-inf")  # nothing until the first hold
         if self.shard_leases is not None:
             # before the cache sync: with shard leases the informers cache only owned shards,
             # so a replica that synced first would list nothing and reach the lease race last
@@ -263,7 +266,8 @@ class ShardedApplication:
 
                 self.kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
         if lease_mode:
-            self.shard_leases = make_shard_leases(cfg, self.kube, self.set_shards, self.metrics)
+            self.shard_leases = make_shard_leases(cfg, self.kube, self.set_shards, self.metrics,
+                                                  on_renewed=self._shard_holds)
             self.shard_leases.start()
         elif le.enabled:
             from .ha.leader import LeaderElector, LeaseLock
@@ -271,15 +275,21 @@ class ShardedApplication:
             self.elector = LeaderElector(
                 LeaseLock(self.kube, cfg.resource_namespace, le.lease_name, _identity(cfg)),
                 lease_duration=le.lease_duration, renew_deadline=le.renew_deadline, retry_period=le.retry_period,
-                on_started_leading=lambda: self.pool.set_active(True),
-                on_stopped_leading=lambda: self.pool.set_active(False), metrics=self.metrics)
+                on_started_leading=lambda: self.pool.set_active(True, until=self.elector.valid_until),
+                on_stopped_leading=lambda: self.pool.set_active(False), metrics=self.metrics,
+                on_renewed=self.pool.set_lease_deadline)
             self.elector.start()
+
+    def _shard_holds(self, until) -> None:
+        """Shard hold deadlines renewed: the workers self-fence on them (no parent round trip)."""
+        self.shards.set_deadlines(until)
+        self.pool.set_shard_deadlines(until)
 
     def set_shards(self, owned) -> None:
         """Shard leases won / lost: the workers fence and replay, the hub re-routes and
         re-lists so the workers receive the runs of gained shards."""
         gained, lost = self.shards.update(owned)
-        self.pool.set_shards(owned)
+        self.pool.set_shards(owned, self.shard_leases.deadlines() if self.shard_leases is not None else None)
         if self.hub is not None:
             self.hub.set_shards(self.shards)
             if gained or lost:

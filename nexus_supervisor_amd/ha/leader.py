@@ -17,6 +17,16 @@ client-go ``leaderelection`` contract:
 Time comparisons use the local clock on *observed* record changes (as client-go
 does): a candidate measures expiry from when it last saw the record change,
 so skew between nodes does not matter.
+
+Ownership is time-bounded at write time, not only by renewal progress: a renewal that
+*started* at ``t0`` (before its GET) and succeeded makes this replica the holder until
+``t0 + renew_deadline`` (:attr:`LeaderElector.valid_until`, reported through
+``on_renewed``).  Any other candidate can only take over ``lease_duration`` after it
+*observed* that renewal, i.e. after ``t0 + lease_duration`` > ``valid_until``.  Every
+renewal attempt is bounded by the time left to ``valid_until`` and the holder steps down
+the moment it passes, so a stalled or partitioned apiserver can never leave a deposed
+leader acting after its successor started (the supervisor also checks ``valid_until``
+before each write and Job DELETE).
 """
 from __future__ import annotations
 
@@ -24,7 +34,7 @@ import asyncio
 import datetime as _dt
 import logging
 import time
-from typing import Callable, Optional
+from typing import Callable, Optional, Tuple
 
 from ..kube.errors import ApiError, Conflict, NotFound
 
@@ -69,7 +79,8 @@ class LeaderElector:
     def __init__(self, lock: LeaseLock, *, lease_duration: float = 15.0, renew_deadline: float = 10.0,
                  retry_period: float = 2.0, on_started_leading: Optional[Callable[[], None]] = None,
                  on_stopped_leading: Optional[Callable[[], None]] = None, metrics=None,
-                 clock: Callable[[], float] = time.monotonic):
+                 clock: Callable[[], float] = time.monotonic,
+                 on_renewed: Optional[Callable[[float], None]] = None):
         if not lease_duration > renew_deadline > retry_period > 0:
             raise ValueError("lease_duration > renew_deadline > retry_period > 0 required")
         self.lock = lock
@@ -78,9 +89,11 @@ class LeaderElector:
         self.retry_period = retry_period
         self.on_started = on_started_leading
         self.on_stopped = on_stopped_leading
+        self.on_renewed = on_renewed
         self.metrics = metrics
         self.clock = clock
         self.leader = False
+        self.valid_until = float("-inf")  # clock time this replica's hold expires locally
         self.observed_holder = ""
         self._observed_record = None
         self._observed_at = 0.0
@@ -110,6 +123,23 @@ class LeaderElector:
             except Exception as exc:  # noqa: BLE001
                 log.warning("lease release failed: %s", exc)
         self._set_leader(False)
+
+    def _renewed(self, t0: float) -> None:
+        self.valid_until = t0 + self.renew_deadline
+        if self.on_renewed is not None:
+            try:
+                self.on_renewed(self.valid_until)
+            except Exception:  # pragma: no cover
+                log.exception("lease renewal callback failed")
+
+    async def acquire_or_renew_bounded(self, budget: float) -> Tuple[bool, float]:
+        """:meth:`try_acquire_or_renew` bounded by ``budget`` seconds; returns (ok, t0) with
+        ``t0`` the clock before the request went out — the start of the new hold."""
+        t0 = self.clock()
+        if budget <= 0:
+            return False, t0
+        ok = await asyncio.wait_for(self.try_acquire_or_renew(), budget)
+        return ok, t0
 
     def _set_leader(self, v: bool) -> None:
         if v == self.leader:
@@ -206,25 +236,31 @@ class LeaderElector:
         while True:
             if not self.leader:
                 try:
-                    ok = await self.try_acquire_or_renew()
-                except Exception as exc:  # noqa: BLE001 - API errors: keep trying
-                    log.warning("leader election: acquire failed: %s", exc)
+                    ok, t0 = await self.acquire_or_renew_bounded(self.renew_deadline)
+                except Exception as exc:  # noqa: BLE001 - API errors / timeouts: keep trying
+                    log.warning("leader election: acquire failed: %r", exc)
                     ok = False
                 if ok:
-                    self._set_leader(True)
-                    last_renew = self.clock()
-                else:
-                    await asyncio.sleep(self.retry_period)
-                    continue
-            # leading: renew every retry_period, step down after renew_deadline without success
-            await asyncio.sleep(self.retry_period)
+                    self._renewed(t0)
+                    if self.clock() < self.valid_until:
+                        self._set_leader(True)
+                        continue
+                await asyncio.sleep(self.retry_period)
+                continue
+            # leading: renew every retry_period; every attempt is bounded by the time left on
+            # the current hold, and the hold ends at valid_until whatever the API does
+            left = self.valid_until - self.clock()
+            await asyncio.sleep(max(0.0, min(self.retry_period, left)))
             try:
-                ok = await asyncio.wait_for(self.try_acquire_or_renew(), self.renew_deadline)
-            except Exception as exc:  # noqa: BLE001
-                log.warning("leader election: renew failed: %s", exc)
+                ok, t0 = await self.acquire_or_renew_bounded(self.valid_until - self.clock())
+            except Exception as exc:  # noqa: BLE001 - incl. the wait_for timeout at valid_until
+                log.warning("leader election: renew failed: %r", exc)
                 ok = False
-            now = self.clock()
             if ok:
-                last_renew = now
-            elif now - last_renew >= self.renew_deadline:
+                self._renewed(t0)
+            elif self.observed_holder and self.observed_holder != self.identity:
+                self.valid_until = float("-inf")  # somebody else holds it now: step down at once
+            if self.clock() >= self.valid_until:
+                if self.metrics is not None:
+                    self.metrics.inc("lease_expired_locally")
                 self._set_leader(False)

@@ -31,6 +31,16 @@ makes that safe but leaves every replica but one idle.  Here the runs are split 
 
 Changes of the held set are reported through ``on_change(frozenset)``: the replica
 fences lost shards and replays gained ones (``Supervisor.set_shards``).
+
+Ownership is time-bounded (ADVICE r2 ha/shards.py:224): a shard
+renewal that *started* at ``t0`` and succeeded is good until ``t0 + renew-deadline``;
+every API call (membership, renewals, observations, acquisitions) runs under a
+``wait_for`` bounded by the time it may take, held shards are renewed concurrently, and
+a watchdog task drops a shard the moment its hold lapses — whatever the apiserver is
+doing — so a partitioned replica stops acting on a shard strictly before any other
+replica can take it (``lease-duration`` after observing the last renewal).  The hold
+deadlines are published through ``on_renewed({shard: valid_until})`` so the supervisor
+(and its worker processes) check them before every write and Job DELETE.
 """
 from __future__ import annotations
 
@@ -67,7 +77,8 @@ class ShardLeaseManager:
     def __init__(self, client, namespace: str, base_name: str, identity: str, shards: int, *,
                  replicas: int = 0, lease_duration: float = 15.0, renew_deadline: float = 10.0,
                  retry_period: float = 2.0, on_change: Optional[Callable[[FrozenSet[int]], None]] = None,
-                 metrics=None, clock: Callable[[], float] = time.monotonic):
+                 metrics=None, clock: Callable[[], float] = time.monotonic,
+                 on_renewed: Optional[Callable[[Dict[int, float]], None]] = None):
         if shards < 1:
             raise ValueError("shards must be >= 1")
         self.client = client
@@ -79,6 +90,7 @@ class ShardLeaseManager:
         self.renew_deadline = renew_deadline
         self.retry_period = retry_period
         self.on_change = on_change
+        self.on_renewed = on_renewed
         self.metrics = metrics
         self.clock = clock
         self.replicas = replicas
@@ -102,10 +114,27 @@ class ShardLeaseManager:
             for k in range(shards)]
         start = zlib.crc32(identity.encode()) % shards
         self.order = [(start + i) % shards for i in range(shards)]
-        self.held: Dict[int, float] = {}       # shard → clock of the last successful renewal
+        self.held: Dict[int, float] = {}       # shard → clock the last successful renewal STARTED
         self.free_since: Dict[int, float] = {}  # shard → clock it was first seen free
         self._task: Optional[asyncio.Task] = None
+        self._watchdog: Optional[asyncio.Task] = None
+        self._wake: Optional[asyncio.Event] = None
         self.acquisitions = 0
+        self.expired_locally = 0
+
+    def valid_until(self, k: int) -> float:
+        t = self.held.get(k)
+        return float("-inf") if t is None else t + self.renew_deadline
+
+    def deadlines(self) -> Dict[int, float]:
+        return {k: t + self.renew_deadline for k, t in self.held.items()}
+
+    def _publish_deadlines(self) -> None:
+        if self.on_renewed is not None and self.held:
+            try:
+                self.on_renewed(self.deadlines())
+            except Exception:  # pragma: no cover
+                log.exception("shard renewal callback failed")
 
     @property
     def owned(self) -> FrozenSet[int]:
@@ -113,17 +142,21 @@ class ShardLeaseManager:
 
     def start(self) -> asyncio.Task:
         if self._task is None:
+            self._wake = asyncio.Event()
             self._task = asyncio.create_task(self._run(), name=f"shard-leases-{self.identity}")
+            self._watchdog = asyncio.create_task(self._expire_loop(), name=f"shard-expiry-{self.identity}")
         return self._task
 
     async def stop(self, release: bool = True) -> None:
-        if self._task is not None:
-            self._task.cancel()
-            try:
-                await self._task
-            except (asyncio.CancelledError, Exception):
-                pass
-            self._task = None
+        for attr in ("_task", "_watchdog"):
+            t = getattr(self, attr)
+            if t is not None:
+                t.cancel()
+                try:
+                    await t
+                except (asyncio.CancelledError, Exception):
+                    pass
+                setattr(self, attr, None)
         held = sorted(self.held)
         self.held.clear()
         if held:
@@ -131,15 +164,16 @@ class ShardLeaseManager:
         if release:
             for k in held:
                 try:
-                    await self.electors[k]._release()  # noqa: SLF001 - same package
+                    await asyncio.wait_for(self.electors[k]._release(), self.renew_deadline)  # noqa: SLF001
                 except Exception as exc:  # noqa: BLE001
                     log.warning("shard %d lease release failed: %s", k, exc)
             try:  # a pod name is not reused: its membership Lease goes with it
-                await self.client.delete("Lease", self.namespace, self.member.lock.name)
+                await asyncio.wait_for(self.client.delete("Lease", self.namespace, self.member.lock.name),
+                                       self.renew_deadline)
             except Exception as exc:  # noqa: BLE001 - e.g. no `delete` verb: leave it released
                 log.debug("membership lease delete failed (%s); releasing", exc)
                 try:
-                    await self.member._release()  # noqa: SLF001
+                    await asyncio.wait_for(self.member._release(), self.renew_deadline)  # noqa: SLF001
                 except Exception as exc2:  # noqa: BLE001
                     log.warning("membership lease release failed: %s", exc2)
 
@@ -153,13 +187,39 @@ class ShardLeaseManager:
                 log.warning("shard leases: %s", exc)
             await asyncio.sleep(self.retry_period)
 
+    async def _expire_loop(self) -> None:
+        """Watchdog: drop every shard whose hold lapsed, at the moment it lapses — it does
+        not wait for a renewal round (which may be stuck on a slow apiserver)."""
+        while True:
+            now = self.clock()
+            expired = [k for k, t in self.held.items() if now >= t + self.renew_deadline]
+            if expired:
+                for k in expired:
+                    del self.held[k]
+                    log.warning("%s: hold on shard %d lapsed (no renewal within renew-deadline): fenced", self.identity, k)
+                self.expired_locally += len(expired)
+                if self.metrics is not None:
+                    self.metrics.inc("shard_leases_expired_locally", len(expired))
+                self._changed()
+            nxt = min((t + self.renew_deadline for t in self.held.values()), default=now + self.retry_period)
+            self._wake.clear()
+            try:
+                await asyncio.wait_for(self._wake.wait(), max(0.001, min(nxt - now, self.retry_period)))
+            except asyncio.TimeoutError:
+                pass
+
+    async def _bounded(self, coro, budget: Optional[float] = None):
+        return await asyncio.wait_for(coro, self.renew_deadline if budget is None else max(0.001, budget))
+
     async def _refresh_members(self) -> None:
         """Renew this replica's membership Lease and list the group's: a member is live
         while its ``renewTime`` keeps changing within a lease duration (observed locally,
-        as for the shard leases — no cross-node clock comparison)."""
+        as for the shard leases — no cross-node clock comparison).  Each call is bounded by
+        ``renew-deadline`` and runs next to (never in front of) the shard renewals."""
         try:
-            await self.member.try_acquire_or_renew()
-            items, _ = await self.client.list("Lease", self.namespace, label_selector=f"{MEMBER_LABEL}={self.base_name}")
+            await self._bounded(self.member.try_acquire_or_renew())
+            items, _ = await self._bounded(self.client.list("Lease", self.namespace,
+                                                            label_selector=f"{MEMBER_LABEL}={self.base_name}"))
         except Exception as exc:  # noqa: BLE001 - keep the last view; the fair share falls back to `replicas`
             # e.g. RBAC without `list` on leases after an upgrade: say so once per lease
             # duration, not every retry period
@@ -193,7 +253,7 @@ class ShardLeaseManager:
             if not name or name == self.member.lock.name:
                 continue
             try:
-                await self.client.delete("Lease", self.namespace, name)
+                await self._bounded(self.client.delete("Lease", self.namespace, name))
                 self.stale_members_deleted += 1
             except Exception as exc:  # noqa: BLE001 - another replica got it first, or no `delete` verb
                 log.debug("stale membership lease %s not deleted: %s", name, exc)
@@ -217,34 +277,55 @@ class ShardLeaseManager:
             return None
         return max(self.held, key=self.order.index)  # the shard this replica would take last
 
+    async def _renew(self, k: int) -> Optional[bool]:
+        """Renew one held shard within the time left on its hold.  True: renewed (the hold
+        now runs from this attempt's start); False: failed; None: dropped meanwhile."""
+        t0 = self.clock()
+        left = self.valid_until(k) - t0
+        try:
+            ok = await self._bounded(self.electors[k].try_acquire_or_renew(), left) if left > 0 else False
+        except asyncio.CancelledError:
+            raise
+        except Exception as exc:  # noqa: BLE001 - incl. the wait_for timeout at the hold's end
+            log.warning("shard %d lease renew failed: %r", k, exc)
+            ok = False
+        if k not in self.held:
+            return None  # the watchdog fenced it while the call was out: regained by acquisition
+        if ok:
+            self.held[k] = t0
+            return True
+        return False
+
     async def tick(self) -> None:
-        """One round: membership, renew what is held, compete for free shards, rebalance."""
+        """One round: membership (concurrently), renew every held shard (concurrently,
+        each bounded by its hold), compete for free shards, rebalance."""
         changed = False
-        await self._refresh_members()
-        for k in sorted(self.held):
-            try:
-                ok = await asyncio.wait_for(self.electors[k].try_acquire_or_renew(), self.renew_deadline)
-            except asyncio.CancelledError:
-                raise
-            except Exception as exc:  # noqa: BLE001
-                log.warning("shard %d lease renew failed: %s", k, exc)
-                ok = False
-            now = self.clock()
-            if ok:
-                self.held[k] = now
-            elif now - self.held[k] >= self.renew_deadline:
-                del self.held[k]
-                changed = True
-                log.info("%s lost shard %d", self.identity, k)
+        members = asyncio.ensure_future(self._refresh_members())
+        try:
+            held = sorted(self.held)
+            if held:
+                await asyncio.gather(*(self._renew(k) for k in held))
+                self._publish_deadlines()
+                now = self.clock()
+                for k in held:
+                    if k in self.held and now >= self.held[k] + self.renew_deadline:
+                        del self.held[k]
+                        changed = True
+                        log.info("%s lost shard %d", self.identity, k)
+            await members
+        finally:
+            if not members.done():
+                members.cancel()
         counts: Dict[str, int] = {}
-        for k in self.order:
-            if k in self.held:
-                continue
+        free_keys = [k for k in self.order if k not in self.held]
+        observed = await asyncio.gather(*(self._bounded(self.electors[k].observe()) for k in free_keys),
+                                        return_exceptions=True)
+        for k, free in zip(free_keys, observed):
             e = self.electors[k]
-            try:
-                free = await e.observe()
-            except Exception as exc:  # noqa: BLE001
-                log.warning("shard %d lease read failed: %s", k, exc)
+            if isinstance(free, BaseException):
+                if isinstance(free, asyncio.CancelledError):
+                    raise free
+                log.warning("shard %d lease read failed: %r", k, free)
                 continue
             now = self.clock()
             if not free:
@@ -261,13 +342,16 @@ class ShardLeaseManager:
             given = now - self._released.get(k, float("-inf")) < self.lease_duration
             if (len(self.held) >= self.target or given) and not orphaned:
                 continue
+            t0 = self.clock()
             try:
-                ok = await e.try_acquire_or_renew()
+                ok = await self._bounded(e.try_acquire_or_renew())
+            except asyncio.CancelledError:
+                raise
             except Exception as exc:  # noqa: BLE001
-                log.warning("shard %d lease acquire failed: %s", k, exc)
+                log.warning("shard %d lease acquire failed: %r", k, exc)
                 ok = False
-            if ok:
-                self.held[k] = self.clock()
+            if ok and self.clock() < t0 + self.renew_deadline:
+                self.held[k] = t0
                 self.free_since.pop(k, None)
                 self.acquisitions += 1
                 changed = True
@@ -286,16 +370,19 @@ class ShardLeaseManager:
             log.info("%s released shard %d to rebalance (members=%d, share=%d)", self.identity, give,
                      len(self.members), self.target)
             try:
-                await self.electors[give]._release()  # noqa: SLF001 - same package
+                await self._bounded(self.electors[give]._release())  # noqa: SLF001 - same package
             except Exception as exc:  # noqa: BLE001 - expires after a lease duration instead
-                log.warning("shard %d lease release failed: %s", give, exc)
+                log.warning("shard %d lease release failed: %r", give, exc)
         if changed:
             self._changed()
+        if self._wake is not None:
+            self._wake.set()  # holds moved: let the watchdog re-arm on the new deadlines
 
     def _changed(self) -> None:
         if self.metrics is not None:
             self.metrics.set("shard_leases_held", float(len(self.held)))
             self.metrics.inc("shard_lease_changes")
+        self._publish_deadlines()  # gained shards' holds before the ownership change lands
         if self.on_change is not None:
             try:
                 self.on_change(self.owned)

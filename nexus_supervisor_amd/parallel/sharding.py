@@ -18,8 +18,9 @@ replica (:data:`.workers._SEED`).
 """
 from __future__ import annotations
 
+import time
 import zlib
-from typing import FrozenSet, Iterable, Optional, Tuple
+from typing import Dict, FrozenSet, Iterable, Optional, Tuple
 
 SHARD_SEED = 0x5BD1E995
 
@@ -48,20 +49,33 @@ class ShardSet:
     """The shards this replica currently owns, with a fencing epoch per shard.
 
     ``owned`` None means "every shard" (sharding off).  An epoch is bumped whenever the
-    shard is lost, so a decision dequeued before the loss never writes after it."""
+    shard is lost, so a decision dequeued before the loss never writes after it.
 
-    def __init__(self, shards: int = 1, owned: Optional[Iterable[int]] = None):
+    ``leased`` sets (``sharding.mode: lease``) also carry a per-shard hold deadline
+    (``CLOCK_MONOTONIC`` seconds — one clock for every process of the host, so a shard
+    worker compares its parent's deadlines directly): a shard whose hold lapsed is not
+    owned any more, even before the lease manager's fencing reaches this process."""
+
+    def __init__(self, shards: int = 1, owned: Optional[Iterable[int]] = None, leased: bool = False,
+                 clock=time.monotonic):
         self.shards = max(1, int(shards))
-        self.owned: Optional[FrozenSet[int]] = None if owned is None or self.shards <= 1 else frozenset(owned)
+        # one shard is "everything" unless it is leased: then the lease is the ownership
+        self.owned: Optional[FrozenSet[int]] = (None if owned is None or (self.shards <= 1 and not leased)
+                                                else frozenset(owned))
         self.epochs = [0] * self.shards
+        self.leased = leased and self.owned is not None
+        self.valid_until = [float("-inf") if self.leased else float("inf")] * self.shards
+        self.clock = clock
 
     @classmethod
     def from_config(cls, cfg) -> "ShardSet":
         s = cfg.sharding
+        if s.mode == "lease":
+            # nothing until a shard lease is won (also with one shard: the lease then is the
+            # replica's only ownership, ADVICE r2 parallel/sharding.py:61)
+            return cls(max(1, s.shards), (), leased=True)
         if s.shards <= 1:
             return cls(1)
-        if s.mode == "lease":
-            return cls(s.shards, ())  # nothing until a shard lease is won
         return cls(s.shards, (s.shard_index,))
 
     @property
@@ -72,7 +86,17 @@ class ShardSet:
         return shard_of(request_id, self.shards)
 
     def owns(self, request_id: str) -> bool:
-        return self.owned is None or shard_of(request_id, self.shards) in self.owned
+        if self.owned is None:
+            return True
+        k = shard_of(request_id, self.shards)
+        return k in self.owned and (not self.leased or self.clock() < self.valid_until[k])
+
+    def set_deadlines(self, until: Dict[int, float]) -> None:
+        """Hold deadlines of leased shards (monotonic seconds), from the lease manager."""
+        for k, t in until.items():
+            k = int(k)
+            if 0 <= k < self.shards:
+                self.valid_until[k] = float(t)
 
     def token(self, request_id: str) -> int:
         return self.epochs[shard_of(request_id, self.shards)] if self.owned is not None else 0
@@ -88,3 +112,4 @@ class ShardSet:
         for k in lost:
             self.epochs[k] += 1
         return new - old, lost
+

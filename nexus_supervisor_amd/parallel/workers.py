@@ -309,6 +309,10 @@ class WorkerPool:
         self.remote_gpu = bool(cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry)
         self.on_restart: Optional[Callable[[int], Any]] = None  # async callback (watch hub resync)
         self.owned_shards: Optional[List[int]] = None  # lease mode: shards held right now
+        # lease hold deadlines (CLOCK_MONOTONIC, one clock for the host's processes): the
+        # workers fence themselves on them without waiting for the parent
+        self.shard_until: Dict[str, float] = {}
+        self.active_until: Optional[float] = None  # leader lease
         self._stopping = False
         self._watchdog: Optional[asyncio.Task] = None
 
@@ -402,7 +406,9 @@ class WorkerPool:
         w.exited.clear()
         w.reader = asyncio.create_task(self._read(w), name=f"worker-{w.index}-ctl")
         if self.owned_shards is not None:  # lease mode: the shards this replica holds right now
-            w.chan.send({"op": "shards", "owned": self.owned_shards})
+            w.chan.send({"op": "shards", "owned": self.owned_shards, "until": self.shard_until})
+        if self.active_until is not None:
+            w.chan.send({"op": "lease", "active_until": self.active_until})
 
     async def _read(self, w: _Worker) -> None:
         while True:
@@ -464,18 +470,33 @@ class WorkerPool:
             if w.chan is not None and not w.exited.is_set():
                 w.chan.send(msg)
 
-    def set_active(self, active: bool) -> None:
+    def set_active(self, active: bool, until: Optional[float] = None) -> None:
         self.active = active
+        msg: Dict[str, Any] = {"op": "active", "v": active}
+        if until is not None:
+            self.active_until = msg["until"] = until
         for w in self.workers:
             if w.chan is not None:
-                w.chan.send({"op": "active", "v": active})
+                w.chan.send(msg)
 
-    def set_shards(self, owned) -> None:
-        """Relay the replica's owned shard set; a worker restarted later gets it at spawn."""
+    def set_lease_deadline(self, until: float) -> None:
+        """Leader lease renewed: the workers' hold deadline moves with it."""
+        self.active_until = until
+        self.broadcast({"op": "lease", "active_until": until})
+
+    def set_shard_deadlines(self, until: Dict[int, float]) -> None:
+        self.shard_until = {str(k): t for k, t in until.items()}
+        self.broadcast({"op": "lease", "until": self.shard_until})
+
+    def set_shards(self, owned, until: Optional[Dict[int, float]] = None) -> None:
+        """Relay the replica's owned shard set (with the holds' deadlines); a worker
+        restarted later gets it at spawn."""
         self.owned_shards = sorted(owned)
+        if until is not None:
+            self.shard_until = {str(k): t for k, t in until.items()}
         for w in self.workers:
             if w.chan is not None:
-                w.chan.send({"op": "shards", "owned": self.owned_shards})
+                w.chan.send({"op": "shards", "owned": self.owned_shards, "until": self.shard_until})
 
     def all_synced(self) -> bool:
         return all(w.synced.is_set() for w in self.workers)
@@ -645,11 +666,19 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
                 break
             op = msg.get("op")
             if op == "active":
+                if msg.get("until") is not None:
+                    sup.set_lease_deadline(float(msg["until"]))
                 sup.set_active(bool(msg.get("v")))
             elif op == "metrics":
                 send_metrics(int(msg.get("seq", 0)))
             elif op == "shards":
+                sup.shards.set_deadlines(msg.get("until") or {})
                 sup.set_shards(msg.get("owned") or ())
+            elif op == "lease":
+                if msg.get("until"):
+                    sup.shards.set_deadlines(msg["until"])
+                if msg.get("active_until") is not None:
+                    sup.set_lease_deadline(float(msg["active_until"]))
             elif op == "gpu" and remote_tel is not None:
                 remote_tel.update(msg)
             elif op == "pprof":

@@ -149,6 +149,9 @@ class Supervisor:
         # fencing epoch: bumped on every loss of leadership; a decision dequeued under an
         # older epoch never writes or deletes (see set_active)
         self.epoch = 0
+        # leader lease hold deadline (CLOCK_MONOTONIC seconds, LeaderElector.valid_until):
+        # past it this replica acts on nothing, even before the elector's step-down lands
+        self.active_until = float("inf")
         self._label_check_at = 0.0
         self.label_mismatch = False
         self._unfinished_cache: Optional[Tuple[str, ...]] = None
@@ -269,7 +272,14 @@ class Supervisor:
         return self.epoch, self.shards.token(request_id)
 
     def _fenced(self, token: Tuple[int, int], request_id: str) -> bool:
-        return not self.active or token != self._token(request_id) or not self.shards.owns(request_id)
+        """True when this replica must not write or delete for ``request_id``: leadership or
+        the run's shard lost since the decision was dequeued (epoch), not held now, or the
+        lease's hold lapsed (time-bounded: a stalled apiserver cannot extend it)."""
+        return (not self.active or token != self._token(request_id) or not self.shards.owns(request_id)
+                or time.monotonic() >= self.active_until)
+
+    def set_lease_deadline(self, until: float) -> None:
+        self.active_until = until
 
     def set_shards(self, owned) -> Tuple[frozenset, frozenset]:
         """New owned replica-shard set (lease mode: a shard lease won or lost).  Lost shards

@@ -212,3 +212,63 @@ def test_profile_decode_and_merge_roundtrip():
     assert q.stacks == p.stacks and q.period_ns == p.period_ns
     m = merge_profiles([q, load_profile(p.encode())])
     assert sum(m.stacks.values()) == 20 and "leaf (a.py)" in m.top(5)
+
+
+def test_partitioned_leader_steps_down_at_its_hold_deadline(arun):
+    """The leader is cut off from the apiserver (requests stall): it steps down no later
+    than ``renew-deadline`` after its last renewal *started* — before the standby can take
+    the lease (a lease duration after it last saw a renewal) — and reports each hold's
+    deadline (``on_renewed``) so the supervisor fences writes on the clock."""
+    from nexus_supervisor_amd.testing.netproxy import PausableProxy
+
+    async def go():
+        api = FakeApiServer()
+        url = await api.start()
+        host, port = url.rsplit(":", 1)
+        proxy = PausableProxy(host.split("//")[1], int(port))
+        purl = await proxy.start()
+        kw = dict(lease_duration=0.8, renew_deadline=0.5, retry_period=0.1)
+        holds = []
+        a, ca = _elector(purl, "a", on_renewed=holds.append, **kw)
+        b, cb = _elector(url, "b", **kw)
+        a.start()
+        await asyncio.sleep(0.3)
+        b.start()
+        await asyncio.sleep(0.3)
+        assert a.leader and not b.leader and holds and holds[-1] == a.valid_until
+        t_cut = time.monotonic()
+        proxy.pause()
+        end = a.valid_until
+        assert end <= t_cut + 0.5 + 0.01
+        while a.leader and time.monotonic() - t_cut < 5:
+            await asyncio.sleep(0.005)
+        t_down = time.monotonic()
+        while not b.leader and time.monotonic() - t_cut < 5:
+            await asyncio.sleep(0.005)
+        t_b = time.monotonic()
+        assert not a.leader and t_down <= end + 0.05, (t_down - end)
+        assert b.leader and t_b > end, (t_b - end)
+        proxy.resume()
+        await a.stop(release=False)
+        await b.stop()
+        for x in (ca, cb):
+            await x.close()
+        await proxy.stop()
+        await api.stop()
+
+    arun(go(), timeout=30)
+
+
+def test_supervisor_fences_on_the_hold_deadline():
+    from nexus_supervisor_amd.supervisor import Supervisor
+    from nexus_supervisor_amd.testing.inproc import InProcCluster
+
+    cfg = load_config(path=None, env={}, overrides={"cql-store-type": "memory", "leader-election": {"enabled": True}})
+    c = InProcCluster(cfg, MemoryStore(), [])
+    sup: Supervisor = c.supervisor
+    sup.active = True
+    tok = sup._token("r1")
+    sup.set_lease_deadline(time.monotonic() + 60)
+    assert not sup._fenced(tok, "r1")
+    sup.set_lease_deadline(time.monotonic() - 0.001)  # the hold lapsed: nothing is written any more
+    assert sup._fenced(tok, "r1")

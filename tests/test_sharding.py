@@ -509,3 +509,129 @@ def test_stale_membership_leases_are_garbage_collected(arun):
         await api.stop()
 
     arun(go(), timeout=30)
+
+
+class _Tagged:
+    """Per-replica view of the shared store / Job client recording when each write and
+    DELETE was *issued* (monotonic) and by whom."""
+
+    def __init__(self, inner, ident, log):
+        self.inner, self.ident, self.log = inner, ident, log
+
+    def __getattr__(self, name):
+        return getattr(self.inner, name)
+
+    async def cas_update(self, algorithm, request_id, *a, **kw):
+        self.log.append((time.monotonic(), self.ident, "write", request_id))
+        return await self.inner.cas_update(algorithm, request_id, *a, **kw)
+
+    async def update_status(self, algorithm, request_id, *a, **kw):
+        self.log.append((time.monotonic(), self.ident, "write", request_id))
+        return await self.inner.update_status(algorithm, request_id, *a, **kw)
+
+    async def delete_job(self, namespace, name, propagation_policy="Background"):
+        self.log.append((time.monotonic(), self.ident, "delete", name))
+        return await self.inner.delete_job(namespace, name, propagation_policy)
+
+
+def test_partitioned_shard_owner_stops_acting_before_anyone_takes_over(arun):
+    """replica A is cut off from the apiserver (every request
+    stalls) while it still has a backlog of decisions for its shard.  Its hold lapses
+    ``renew-deadline`` after its last renewal started: A issues no write and no Job DELETE
+    after that, B acquires the shard only later (a lease duration after it last saw A
+    renew), finishes the runs, and no run is written twice."""
+    from nexus_supervisor_amd.testing.netproxy import PausableProxy
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        host, port = url.rsplit(":", 1)
+        proxy = PausableProxy(host.split("//")[1], int(port))
+        purl = await proxy.start()
+        wl = Workload(concurrent_jobs=400, seed=31)
+        objs, rows = wl.initial()
+        store = MemoryStore(rows, latency=0.015)  # a slow store: A keeps a backlog
+        for o in objs:
+            api.create(o)
+        events = []
+        apps = {}
+        lease = {"lease-duration": "1200ms", "renew-deadline": "800ms", "retry-period": "150ms"}
+        for ident, u in (("rep-a", purl), ("rep-b", url)):
+            cfg = _cfg(ident, {"workers": 2, "sharding": {"shards": 2, "mode": "lease", "replicas": 2},
+                               "leader-election": dict(lease, identity=ident)})
+            kc = KubeClient(KubeConfig(u))
+            app = Application(cfg, kube=kc, store=_Tagged(store, ident, events), jobs=_Tagged(kc, ident, events))
+            await app.start()
+            apps[ident] = app
+        a, b = apps["rep-a"], apps["rep-b"]
+        assert await _wait(lambda: len(a.shard_leases.owned) == 1 and len(b.shard_leases.owned) == 1, 6)
+        ka = next(iter(a.shard_leases.owned))
+        expected = {}
+        failed, traffic, new_rows = wl.step(300)
+        for r in new_rows:
+            store.rows[r.key] = r.deep_copy()
+        for etype, obj in traffic:
+            (api.create if etype == "ADDED" else api.update)(obj)
+        for rid in failed:
+            expected[rid] = wl.expected[rid]
+        mine = [rid for rid in failed if shard_of(rid, 2) == ka]
+        # A has received (most of) its shard's failures and is working through them
+        assert await _wait(lambda: a.supervisor.pipeline.depth() >= 20, 5), a.supervisor.pipeline.depth()
+        t_cut = time.monotonic()
+        proxy.pause()
+        hold_end = a.shard_leases.valid_until(ka)
+        assert hold_end <= t_cut + 0.8 + 0.01
+        assert await _wait(lambda: ka in b.shard_leases.owned, 6), "B never took A's shard"
+        t_b = time.monotonic()
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 20)
+        a_acts = [t for t, who, _kind, rid in events if who == "rep-a" and shard_of(rid, 2) == ka]
+        assert a_acts and max(a_acts) < hold_end, (max(a_acts) - hold_end)
+        assert max(a_acts) < t_b
+        b_acts = [t for t, who, _kind, rid in events if who == "rep-b" and shard_of(rid, 2) == ka]
+        assert b_acts and min(b_acts) > hold_end
+        assert a.shard_leases.expired_locally >= 1 and ka not in a.supervisor.shards.owned
+        wrong, twice = _check_exactly_once(store, wl, expected)
+        assert not wrong and not twice, (wrong, twice)
+        assert len(mine) > 20
+        proxy.resume()
+        for x in apps.values():
+            await x.stop(drain_timeout=1)
+        await proxy.stop()
+        await api.stop()
+
+    arun(go(), timeout=90)
+
+
+def test_single_shard_lease_mode_gates_the_whole_namespace(arun):
+    """ADVICE r2 parallel/sharding.py:61: ``mode: lease`` with one shard is one Lease for the
+    namespace — a replica that loses the race for it acts on nothing (it used to own
+    "every shard" and run with leader election silently off)."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        wl = Workload(concurrent_jobs=60, seed=9)
+        objs, rows = wl.initial()
+        store = MemoryStore(rows)
+        for o in objs:
+            api.create(o)
+        events = []
+        apps = []
+        for ident in ("solo-a", "solo-b"):
+            cfg = _cfg(ident, {"sharding": {"shards": 1, "mode": "lease"}})
+            kc = KubeClient(KubeConfig(url))
+            app = Application(cfg, kube=kc, store=_Tagged(store, ident, events))
+            await app.start()
+            apps.append(app)
+        assert await _wait(lambda: sum(len(x.shard_leases.owned) for x in apps) == 1, 5)
+        assert not any(not x.supervisor.shards.owned and x.supervisor.shards.owns("anything") for x in apps)
+        holder = next(x for x in apps if x.shard_leases.owned)
+        expected = {}
+        _push(api, wl, store, 30, expected)
+        assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 10)
+        writers = {who for _t, who, _k, _r in events}
+        assert writers == {holder.cfg.leader_election.identity}, writers
+        for x in apps:
+            await x.stop(drain_timeout=1)
+        await api.stop()
+
+    arun(go(), timeout=60)
