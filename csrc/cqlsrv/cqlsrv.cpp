@@ -77,6 +77,7 @@ struct Options {
   bool verbose = false;
   int shards = 0;        // Scylla shard emulation: 0 = off (one shard, no extensions)
   int shard_port = 0;    // shard-aware port (0 = ephemeral) when --shards is given
+  int advertise_shard_port = -1;  // test hook: advertise this port (e.g. a closed one) instead
   int ignore_msb = 12;   // SCYLLA_SHARDING_IGNORE_MSB
 };
 
@@ -1476,6 +1477,12 @@ Prepared prepare(const std::string& q, const std::string& cur_ks) {
     }
     if (pr.pk_idx.size() != t->pk.size()) pr.pk_idx.clear();
     if (st.kind == S_SELECT && !st.count) pr.result = specs_of(*t, select_cols(*t, st));
+    // a conditional (LWT) write prepares with result metadata [applied] alone, as Cassandra
+    // does: the not-applied answer carries more columns, so a client that executes it with
+    // skip_metadata would decode that row with the wrong shape
+    bool conditional = (st.kind == S_UPDATE || st.kind == S_DELETE || st.kind == S_INSERT) &&
+                       (st.if_exists || !st.ifs.empty() || (st.kind == S_INSERT && st.if_not_exists));
+    if (conditional) pr.result = {applied_spec(*t)};
   } else if (st.kind == S_SELECT || st.kind == S_INSERT || st.kind == S_UPDATE || st.kind == S_DELETE) {
     if (!(ks == "system" || ks.rfind("system", 0) == 0)) throw CqlError(ERR_INVALID, "unconfigured table " + st.table);
   }
@@ -1560,7 +1567,7 @@ void handle_frame(Shard& sh, Conn& c, const FrameHeader& h, const uint8_t* body)
           w.string("SCYLLA_SHARDING_IGNORE_MSB");
           w.string_list({std::to_string(g_opt.ignore_msb)});
           w.string("SCYLLA_SHARD_AWARE_PORT");
-          w.string_list({std::to_string(g_shard_port)});
+          w.string_list({std::to_string(g_opt.advertise_shard_port >= 0 ? g_opt.advertise_shard_port : g_shard_port)});
         }
         respond(sh, c, h.stream, OP_SUPPORTED, w.buf);
         return;
@@ -1868,7 +1875,7 @@ void usage() {
           "nexus-cqlsrv [--host H] [--port P (0 = ephemeral)] [--user U --password P] [--latency-us N]\n"
           "             [--error-rate F] [--seed N] [--data WAL] [--ready-file PATH] [--dc DC] [--rack R]\n"
           "             [--tokens t1,t2] [--peer host:port:tok1;tok2]... [--exec FILE.cql] [-v]\n"
-          "             [--shards N [--shard-aware-port P] [--ignore-msb B]]\n");
+          "             [--shards N [--shard-aware-port P] [--ignore-msb B] [--advertise-shard-aware-port P]]\n");
 }
 
 void exec_file(const std::string& path) {
@@ -1944,6 +1951,7 @@ int main(int argc, char** argv) {
     } else if (a == "--peer") g_opt.peers.push_back(val());
     else if (a == "--shards") g_opt.shards = std::stoi(val());
     else if (a == "--shard-aware-port") g_opt.shard_port = std::stoi(val());
+    else if (a == "--advertise-shard-aware-port") g_opt.advertise_shard_port = std::stoi(val());
     else if (a == "--ignore-msb") g_opt.ignore_msb = std::stoi(val());
     else if (a == "-v") g_opt.verbose = true;
     else {

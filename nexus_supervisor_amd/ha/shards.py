@@ -121,6 +121,7 @@ class ShardLeaseManager:
         self._wake: Optional[asyncio.Event] = None
         self.acquisitions = 0
         self.expired_locally = 0
+        self._gc: Dict[str, asyncio.Future] = {}  # stale membership Lease deletes in flight
 
     def valid_until(self, k: int) -> float:
         t = self.held.get(k)
@@ -148,6 +149,8 @@ class ShardLeaseManager:
         return self._task
 
     async def stop(self, release: bool = True) -> None:
+        for t in list(self._gc.values()):
+            t.cancel()
         for attr in ("_task", "_watchdog"):
             t = getattr(self, attr)
             if t is not None:
@@ -208,6 +211,13 @@ class ShardLeaseManager:
             except asyncio.TimeoutError:
                 pass
 
+    async def _delete_stale(self, name: str) -> None:
+        try:
+            await self._bounded(self.client.delete("Lease", self.namespace, name), self.lease_duration)
+            self.stale_members_deleted += 1
+        except Exception as exc:  # noqa: BLE001 - another replica got it first, or no `delete` verb
+            log.debug("stale membership lease %s not deleted: %r", name, exc)
+
     async def _bounded(self, coro, budget: Optional[float] = None):
         return await asyncio.wait_for(coro, self.renew_deadline if budget is None else max(0.001, budget))
 
@@ -250,13 +260,12 @@ class ShardLeaseManager:
         # a replica killed without a clean shutdown (or a release without delete) leaves its
         # membership Lease behind; one per pod ever started would pile up across rollouts
         for name in stale[:4]:
-            if not name or name == self.member.lock.name:
+            if not name or name == self.member.lock.name or name in self._gc:
                 continue
-            try:
-                await self._bounded(self.client.delete("Lease", self.namespace, name))
-                self.stale_members_deleted += 1
-            except Exception as exc:  # noqa: BLE001 - another replica got it first, or no `delete` verb
-                log.debug("stale membership lease %s not deleted: %s", name, exc)
+            # housekeeping, not ownership: off the renewal path, bounded by a lease duration
+            t = asyncio.ensure_future(self._delete_stale(name))
+            self._gc[name] = t
+            t.add_done_callback(lambda _t, n=name: self._gc.pop(n, None))
         denom = max(self.replicas, len(live))
         self.target = -(-self.shards // denom) if (self.replicas > 0 or len(live) > 1) else self.shards
 

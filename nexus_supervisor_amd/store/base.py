@@ -21,6 +21,11 @@ class StoreError(Exception):
     """Transient or permanent store failure (the pipeline retries it)."""
 
 
+class NotSent(StoreError):
+    """The request never reached any replica (no live host / connection): the write
+    certainly did not land."""
+
+
 class CheckpointStore:
     async def read_checkpoint(self, algorithm: str, request_id: str) -> Optional[CheckpointedRequest]:
         raise NotImplementedError

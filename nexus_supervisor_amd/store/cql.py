@@ -44,6 +44,7 @@ import json
 import logging
 import operator
 import random
+import re
 import ssl
 import time
 import zipfile
@@ -51,7 +52,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..models.checkpoint import COLUMN_NAMES, COLUMNS, KEYSPACE, TABLE, CheckpointedRequest
-from .base import CheckpointStore, StoreError
+from .base import CheckpointStore, NotSent, StoreError
 
 log = logging.getLogger("nexus_supervisor_amd.cql")
 
@@ -314,6 +315,17 @@ class PreparedStatement:
     result_types: Optional[List[Any]]
     keyspace: str = ""
     _pk_get: Optional[Callable[[Sequence[Any]], Tuple]] = field(default=None, repr=False, compare=False)
+    # a conditional (LWT) statement: never executed with skip_metadata — its not-applied
+    # answer carries the condition's columns, a different shape from the prepared one
+    conditional: bool = False
+
+
+_CONDITIONAL = re.compile(r"^\s*(?:UPDATE|INSERT|DELETE)\b.*\bIF\b", re.I | re.S)
+
+
+def is_conditional(query: str) -> bool:
+    """An LWT write (``UPDATE … IF …``, ``INSERT … IF NOT EXISTS``, ``DELETE … IF EXISTS``)."""
+    return bool(_CONDITIONAL.match(query))
 
 
 def _pk_getter(indexes: Sequence[int]) -> Callable[[Sequence[Any]], Tuple]:
@@ -423,6 +435,7 @@ class CqlSession:
         self.max_retries = max_retries
         self.discover = discover
         self.shard_aware = shard_aware and sni_proxy is None
+        self.shard_aware_port = True  # use SCYLLA_SHARD_AWARE_PORT when advertised (falls back per host)
         self._sharded = False  # some node advertised Scylla shards
         self._tokens: Dict[tuple, int] = {}  # partition key values → token (recent)
         self.per_shard = max(1, connections_per_shard)
@@ -451,17 +464,25 @@ class CqlSession:
 
     async def _open_host(self, h: Host) -> None:
         first = self._new_conn(h)
-        await first.connect(self.keyspace)
-        nr = int(first.scylla("SCYLLA_NR_SHARDS") or 0) if self.shard_aware else 0
-        if nr > 1 and first.scylla("SCYLLA_SHARDING_ALGORITHM") in (None, "biased-token-round-robin"):
-            conns, by_shard = await self._open_shards(h, first, nr)
-            h.nr_shards, h.ignore_msb = nr, int(first.scylla("SCYLLA_SHARDING_IGNORE_MSB") or 0)
-            self._sharded = True
-        else:
-            rest = [self._new_conn(h) for _ in range(self.per_host - 1)]
-            await asyncio.gather(*(c.connect(self.keyspace) for c in rest))
-            conns, by_shard = [first] + rest, []
-            h.nr_shards = 0
+        opened: List[CqlConnection] = [first]
+        try:
+            await first.connect(self.keyspace)
+            nr = int(first.scylla("SCYLLA_NR_SHARDS") or 0) if self.shard_aware else 0
+            if nr > 1 and first.scylla("SCYLLA_SHARDING_ALGORITHM") in (None, "biased-token-round-robin"):
+                conns, by_shard = await self._open_shards(h, first, nr, opened)
+                h.nr_shards, h.ignore_msb = nr, int(first.scylla("SCYLLA_SHARDING_IGNORE_MSB") or 0)
+                self._sharded = True
+            else:
+                rest = [self._new_conn(h) for _ in range(self.per_host - 1)]
+                opened.extend(rest)
+                await asyncio.gather(*(c.connect(self.keyspace) for c in rest))
+                conns, by_shard = [first] + rest, []
+                h.nr_shards = 0
+        except BaseException:
+            # a failed open never leaks what it already opened (each reconnect would pile up)
+            for c in opened:
+                c.close()
+            raise
         for c in h.conns:
             c.close()
         h.conns = conns
@@ -469,29 +490,46 @@ class CqlSession:
         h.up = True
         h.failures = 0
 
-    async def _open_shards(self, h: Host, first: CqlConnection, nr: int):
+    async def _open_shards(self, h: Host, first: CqlConnection, nr: int, opened: List[CqlConnection]):
         """``per_shard`` connections to every shard of a Scylla node.  With a shard-aware
-        port the local port picks the shard (``port % nr == shard``); without one, keep
-        reconnecting to the regular port until each shard has been handed out."""
+        port the local port picks the shard (``port % nr == shard``); without one — or when
+        the advertised aware port is refused, filtered or times out (e.g. a Service that
+        only exposes 9042), as the scylladb gocql fork does — keep reconnecting to the
+        regular port until each shard has been handed out.  Connections that land on a
+        shard that already has its ``per_shard`` are closed, not kept (NAT-rewritten source
+        ports would otherwise pile up ~nr_shards×32 of them); every connection opened is
+        recorded in ``opened`` so the caller can close them all if the open fails."""
         by_shard: List[List[CqlConnection]] = [[] for _ in range(nr)]
         by_shard[int(first.scylla("SCYLLA_SHARD") or 0) % nr].append(first)
-        aware = int(first.scylla("SCYLLA_SHARD_AWARE_PORT") or 0)
+        aware = [int(first.scylla("SCYLLA_SHARD_AWARE_PORT") or 0)] if self.shard_aware_port else [0]
 
         async def one(shard: int) -> None:
             for attempt in range(32):
                 lp = 0
-                if aware:
+                port = aware[0]
+                if port:
                     base = random.randrange(32768, 60000)
                     lp = base - base % nr + shard
-                c = self._new_conn(h, port=aware or None, local_port=lp)
+                c = self._new_conn(h, port=port or None, local_port=lp)
+                opened.append(c)
                 try:
                     await c.connect(self.keyspace)
-                except OSError as exc:
-                    if aware and getattr(exc, "errno", None) in (98, 99):  # EADDRINUSE / EADDRNOTAVAIL
+                except (OSError, asyncio.TimeoutError) as exc:
+                    c.close()
+                    if port and getattr(exc, "errno", None) in (98, 99):  # EADDRINUSE / EADDRNOTAVAIL
+                        continue
+                    if port:
+                        log.warning("CQL host %s:%s: shard-aware port %d unusable (%r); falling back to the "
+                                    "regular port", h.address[0], h.address[1], port, exc)
+                        aware[0] = 0
+                        self.stats["shard_port_fallbacks"] = self.stats.get("shard_port_fallbacks", 0) + 1
                         continue
                     raise
                 got = int(c.scylla("SCYLLA_SHARD") or 0) % nr
-                by_shard[got].append(c)  # a stray shard's connection still serves that shard
+                if len(by_shard[got]) >= self.per_shard:
+                    c.close()  # a stray connection to a shard that is already served
+                else:
+                    by_shard[got].append(c)
                 if len(by_shard[shard]) >= self.per_shard:
                     return
             log.warning("CQL host %s:%s: no connection to shard %d", h.address[0], h.address[1], shard)
@@ -685,7 +723,8 @@ class CqlSession:
                 _, qid, bind, pk, result = r
                 ps = PreparedStatement(query, qid, [b[3] for b in bind], list(pk),
                                        tuple(n for n, _ in result) if result is not None else None,
-                                       [t for _, t in result] if result is not None else None)
+                                       [t for _, t in result] if result is not None else None,
+                                       conditional=is_conditional(query))
                 conn.prepared_here.add(qid)
                 self._prepared[query] = ps
                 fut.set_result(ps)
@@ -728,8 +767,9 @@ class CqlSession:
         token = self.routing_token(ps, values) if self.token_aware or self.shard_aware else None
         vals = list(values)
         hint = ps.result_types
-        skip = hint is not None
+        skip = hint is not None and not ps.conditional
         attempts = 0
+        sent = False  # a request went onto a connection (it may have landed)
         last: Optional[BaseException] = None
         tried: set = _NO_HOSTS  # replaced by a real set on the first failure
         while attempts <= self.max_retries:
@@ -737,7 +777,7 @@ class CqlSession:
             if tried:
                 cands = [h for h in cands if h.address not in tried] or cands
             if not cands:
-                raise StoreError(f"no CQL host available: {last}")
+                raise NotSent(f"no CQL host available: {last}")
             h = cands[0]
             shard = h.shard_of(token) if h.nr_shards else None
             conn = h.pick(shard)
@@ -750,6 +790,7 @@ class CqlSession:
             self.stats["requests"] += 1
             if shard is not None:
                 self.stats["shard_routed"] += 1
+            sent = True
             try:
                 qid = ps.query_id
                 r = await conn.request_nowait(
@@ -795,7 +836,7 @@ class CqlSession:
                 names = ps.result_names if skip else tuple(r[1])
                 return Rows(names, r[2], r[3])
             return r
-        raise StoreError(f"CQL request failed after {attempts} attempts: {last}")
+        raise (StoreError if sent else NotSent)(f"CQL request failed after {attempts} attempts: {last}")
 
     async def execute_batch(self, ps: PreparedStatement, rows: Sequence[Sequence[Any]], *,
                             consistency: Optional[int] = None, logged: bool = False,

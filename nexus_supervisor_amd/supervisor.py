@@ -41,7 +41,7 @@ from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
 from .parallel.sharding import ShardSet
-from .store.base import CheckpointStore
+from .store.base import CheckpointStore, NotSent
 from .utils.gctune import GcTuner
 
 STAGE_FOR_ACTION = {
@@ -816,7 +816,11 @@ class Supervisor:
                                                            only_if, set_failure=not running)
         except Exception as exc:
             self.log.error(exc, "failed to update algorithm submission status", requestId=rid, algorithm=r.algorithm)
-            if compat.delete_on_read_error and failing:
+            # the reference deletes on a failed checkpoint *read* (supervisor.go:265-273); here
+            # the one store call is the write itself, so delete only when it provably never
+            # reached the store — a timed-out write may have landed, and deleting then could
+            # leave an unfinished row with nothing left to replay from
+            if compat.delete_on_read_error and failing and isinstance(exc, NotSent):
                 try:
                     await self._delete_job(rid)
                 except Exception as del_exc:  # noqa: BLE001 - the store error is what is retried

@@ -266,3 +266,47 @@ def test_base_store_fallback_cas_is_read_then_conditional_write(arun):
         assert st.inner.get(ALGORITHM, RUNNING_ROW.id).lifecycle_stage == "FAILED"
 
     arun(go())
+
+
+class FailingCas(MemoryStore):
+    """Fused write that fails once with ``exc`` (then works)."""
+
+    def __init__(self, rows, exc):
+        super().__init__(rows)
+        self.exc = exc
+
+    async def cas_update(self, *a, **kw):
+        if self.exc is not None:
+            exc, self.exc = self.exc, None
+            raise exc
+        return await super().cas_update(*a, **kw)
+
+
+def test_fused_delete_on_store_error_only_when_the_write_never_left(arun):
+    """ADVICE r2 supervisor.py:757: with ``compat.delete-on-read-error`` the fused path used
+    to delete the Job whenever its conditional write failed — also on a timeout after which
+    the write may have landed.  Now only a write that provably never reached the store
+    (:class:`NotSent`) deletes; otherwise the retry (which sees the finished row) does."""
+    from nexus_supervisor_amd.store.base import NotSent, StoreError
+
+    async def case(exc):
+        cfg = _cfg(compat={"delete-on-read-error": True})
+        jobs = RecordingJobs([RUNNING_ROW.id])
+        store = FailingCas([RUNNING_ROW], exc)
+        c = InProcCluster(cfg, store, [make_job(RUNNING_ROW.id, cfg.labels)], jobs=jobs)
+        await c.start()
+        c.push(make_event("Job", RUNNING_ROW.id, "DeadlineExceeded", "deadline"))
+        assert await c.settle(5)
+        deleted_first = list(jobs.deleted)
+        await c.stop()
+        return deleted_first, store.get(ALGORITHM, RUNNING_ROW.id).lifecycle_stage
+
+    async def go():
+        # a timed-out write: no delete on the error; the retry writes, then deletes once
+        deleted, stage = await case(StoreError("request timed out"))
+        assert stage == LifecycleStage.DEADLINE_EXCEEDED and deleted == [RUNNING_ROW.id]
+        # never sent: the reference's delete-on-error happens (and the retry's delete is NotFound-tolerant)
+        deleted, stage = await case(NotSent("no CQL host available"))
+        assert stage == LifecycleStage.DEADLINE_EXCEEDED and deleted[0] == RUNNING_ROW.id
+
+    arun(go())

@@ -90,3 +90,115 @@ def test_shard_unaware_client_pays_cross_shard_hops(arun):
         arun(go())
     finally:
         srv.stop()
+
+
+def _closed_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_unreachable_shard_aware_port_falls_back_without_leaks(arun):
+    """ADVICE r2 store/cql.py:478: a node advertises SCYLLA_SHARD_AWARE_PORT but the port is
+    refused (e.g. a Service exposing only 9042).  The host still comes up — every shard
+    reached by reconnecting to the regular port — and nothing is left open but the
+    per-shard connections."""
+    srv = CqlServer(exec_statements=schema_statements(), shards=4, shard_aware_port=-1,
+                    extra_args=["--advertise-shard-aware-port", str(_closed_port())]).start()
+
+    async def go():
+        store = CqlCheckpointStore(CqlSession([srv.address], connections_per_host=1))
+        await store.connect()
+        h = next(iter(store.session.hosts.values()))
+        assert h.up and h.nr_shards == 4
+        assert store.session.stats.get("shard_port_fallbacks", 0) >= 1
+        assert all(len(c) == 1 for c in h.shard_conns), [len(c) for c in h.shard_conns]
+        assert len(h.conns) == 4
+        rows = _rows(50)
+        await asyncio.gather(*(store.upsert_checkpoint(r) for r in rows))
+        stats = await _stats(store)
+        assert stats["shard_misses"] == 0
+        # connections accepted in total: the regular port hands each new connection the
+        # least-loaded shard, so the fallback needs exactly one per shard (the refused
+        # aware-port attempts never reach the server)
+        assert stats["connections"] == 4, stats
+        await store.close()
+
+    try:
+        arun(go())
+    finally:
+        srv.stop()
+
+
+def test_failed_host_open_closes_what_it_opened(arun, monkeypatch):
+    """A host whose open fails half-way (here: the 3rd shard connection raises) leaves no
+    connection behind — every reconnect attempt used to leak the ones already opened."""
+    from nexus_supervisor_amd.store import cql as cql_mod
+
+    srv = CqlServer(exec_statements=schema_statements(), shards=4).start()
+    made = []
+    real = cql_mod.CqlConnection.connect
+
+    async def flaky(self, keyspace=None):
+        made.append(self)
+        if len(made) == 3:
+            raise OSError(111, "injected refusal")
+        return await real(self, keyspace)
+
+    async def go():
+        sess = CqlSession([srv.address], connections_per_host=1, discover=False)
+        h = cql_mod.Host(address=srv.address)
+        sess.shard_aware_port = False  # regular-port mode: an OSError is fatal for this open
+        monkeypatch.setattr(cql_mod.CqlConnection, "connect", flaky)
+        try:
+            await sess._open_host(h)
+        except OSError:
+            pass
+        else:
+            raise AssertionError("open should have failed")
+        assert made and all(c.closed for c in made)
+        assert not h.up and h.conns == []
+
+    try:
+        arun(go())
+    finally:
+        srv.stop()
+
+
+def test_conditional_writes_never_skip_metadata(arun):
+    """ADVICE r2 store/cql.py:1040: a conditional write prepares with result metadata
+    ``[applied]`` alone (as Cassandra), while its not-applied answer carries the row's
+    stage.  The client must not execute it with skip_metadata, or the finished-row skip
+    and the unknown-stage fallback would silently stop working."""
+    from nexus_supervisor_amd.store.cql import is_conditional
+
+    assert is_conditional("UPDATE t SET a=? WHERE k=? IF a IN (?)")
+    assert is_conditional("insert into t (k) values (?) if not exists")
+    assert not is_conditional("SELECT lifecycle_stage FROM t WHERE k=?")
+    assert not is_conditional("UPDATE t SET a=? WHERE k=?")
+    srv = CqlServer(exec_statements=schema_statements()).start()
+
+    async def go():
+        store = CqlCheckpointStore(CqlSession([srv.address], connections_per_host=1))
+        await store.connect()
+        row = _rows(1)[0]
+        row.lifecycle_stage = LifecycleStage.CANCELLED
+        await store.upsert_checkpoint(row)
+        unfinished = ("NEW", "BUFFERED", "RUNNING")
+        applied, current = await store.cas_update(row.algorithm, row.id, LifecycleStage.FAILED, "c", "d", None,
+                                                  unfinished)
+        assert (applied, current) == (False, LifecycleStage.CANCELLED)
+        ps = next(p for q, p in store.session._prepared.items() if " IF " in q)
+        assert ps.conditional and ps.result_names == ("[applied]",)  # the prepared shape is [applied] only
+        missing = await store.cas_update(row.algorithm, "no-such-run", LifecycleStage.FAILED, "c", "d", None, unfinished)
+        assert missing == (False, None)
+        await store.close()
+
+    try:
+        arun(go())
+    finally:
+        srv.stop()

@@ -500,6 +500,7 @@ def test_stale_membership_leases_are_garbage_collected(arun):
         other.start()
         assert api.get("Lease", "nexus", "grp-member-dead-pod") is not None
         assert await _wait(lambda: api.get("Lease", "nexus", "grp-member-dead-pod") is None, 6)
+        assert await _wait(lambda: live.stale_members_deleted + other.stale_members_deleted >= 1, 2)
         assert live.stale_members_deleted + other.stale_members_deleted == 1
         assert api.get("Lease", "nexus", "grp-member-live-pod") is not None
         assert live.members == frozenset({"live-pod", "other-pod"})
