@@ -40,7 +40,7 @@ class BenchConfig:
     pprof_out: str = ""
     kube_connections: int = 256
     inflight: int = 2
-    probe_events: int = 60
+    probe_events: int = 600
     probe_rate_per_min: float = 1000.0
     procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
     pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
@@ -270,6 +270,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             for k in ("busy", "apply", "request", "recv", "flush"):
                 if f"{k}_ns" in s1:
                     cpu[f"kubesim_{k}_us_per_event"] = round((s1[f"{k}_ns"] - s0.get(f"{k}_ns", 0)) / 1000.0 / n_ev, 2)
+        if getattr(harness, "cql_shards", None):
+            cpu["cqlsrv_shards"] = harness.cql_shards
         workers = [v for k, v in cpu.items() if k.startswith("worker")]
         if workers:
             cpu["workers_util_sum"] = round(sum(workers), 3)
@@ -321,16 +323,22 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
 
 
 async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dict[str, Any]:
-    """Open-loop latency at a fixed pod-failure rate (BASELINE config 4: 1000 pod-fail
-    events/min): single failures pushed on a fixed schedule, each timed from push to
-    checkpoint ack — the latency a run sees when the supervisor is not saturated."""
+    """Open-loop latency at a pod-failure rate (BASELINE config 4: 1000 pod-fail events/min):
+    single failures arriving as a Poisson process of that mean rate (seeded: the same
+    schedule every run), each timed from push to checkpoint ack — the latency a run sees
+    when the supervisor is not saturated, including the occasional near-simultaneous pair."""
+    import random
+
     saved, tracker.latencies = tracker.latencies, []
-    interval = 60.0 / cfg.probe_rate_per_min
+    rate = cfg.probe_rate_per_min / 60.0
+    rng = random.Random(0x5EED + cfg.seed + cfg.rank)
     loop = asyncio.get_running_loop()
     start = loop.time()
     states = []
+    at = 0.0
     for i in range(cfg.probe_events):
-        delay = start + i * interval - loop.time()
+        at += rng.expovariate(rate)
+        delay = start + at - loop.time()
         if delay > 0:
             await asyncio.sleep(delay)
         failed, t_push, expected = await harness.step(1)
@@ -345,8 +353,9 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     if not lat:
         return {"events": 0}
     q = lambda p: lat[min(len(lat) - 1, int(round(p * (len(lat) - 1))))]  # noqa: E731
-    return {"rate_per_min": cfg.probe_rate_per_min, "events": len(lat), "p50_ms": round(q(0.5), 3),
-            "p99_ms": round(q(0.99), 3), "max_ms": round(lat[-1], 3)}
+    return {"rate_per_min": cfg.probe_rate_per_min, "arrivals": "poisson", "events": len(lat),
+            "p50_ms": round(q(0.5), 3), "p90_ms": round(q(0.9), 3), "p99_ms": round(q(0.99), 3),
+            "max_ms": round(lat[-1], 3)}
 
 
 async def _read_back(harness, tracker: "Tracker") -> Dict[str, Any]:

@@ -103,7 +103,8 @@ def test_bench_two_ranks_wire_worker_processes():
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
                         "--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "50", "--procs", "2",
-                        "--probe-events", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+                        "--probe-events", "0", "--cluster", "shared"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, p.stdout
@@ -131,3 +132,47 @@ def test_baseline_scenarios_small(arun):
     assert r5["drained"] and r5["wrong_stage"] == 0
     assert {"cql_restart", "storm", "leader_crash", "failover_s"} <= set(r5["chaos"])
     assert r5["chaos"]["failover_s"] < 10
+
+
+def _torchrun(nproc, *args, timeout=400):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(nproc),
+                        *args], cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+def test_bench_four_ranks_shared_cluster_not_harness_bound():
+    """4 gloo ranks on the shared cluster (one apiserver simulator
+    + one CQL server, four replicas each owning a shard of the namespace): no harness
+    process saturated, every decision in its expected stage, every timed row read back,
+    and the replica CPU per failure reported for every rank."""
+    out = _torchrun(4, "--steps", "2", "--warmup", "1", "--jobs", "200", "--events", "30", "--procs", "1",
+                    "--probe-events", "0", "--cluster", "shared")
+    _check(out, 4, 2, 1, 30)
+    assert out["config"]["cluster"] == "shared" and out["config"]["parallelism"] == "shard4x1proc"
+    assert out["harness_bound"]["bound"] is False and out["harness_bound"]["bound_ranks"] == [], out["harness_bound"]
+    assert out["wrong_stage"] == 0 and out["readback"]["wrong"] == 0 and out["readback"]["checked"] == 4 * 2 * 30
+    assert len(out["supervisor_cpu_us_per_event_by_rank"]) == 4
+    assert all(v and v > 0 for v in out["supervisor_cpu_us_per_event_by_rank"])
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_per_rank_clusters_and_poisson_probe():
+    """The default N>1 layout: every GPU-job slot's replica with its own apiserver simulator
+    and CQL server (weak scaling with nothing shared), plus the open-loop probe: Poisson
+    arrivals, every probe event acknowledged."""
+    out = _torchrun(2, "--steps", "2", "--warmup", "1", "--jobs", "200", "--events", "30", "--procs", "1",
+                    "--probe-events", "40", "--probe-rate", "6000")
+    _check(out, 2, 2, 1, 30)
+    assert out["config"]["cluster"] == "per-rank"
+    probe = out["latency_at_rate"]
+    assert probe["events"] == 40 and probe["arrivals"] == "poisson" and probe["p99_ms"] >= probe["p50_ms"] > 0

@@ -43,7 +43,7 @@ def test_exactly_one_leader_and_failover(arun):
         while not b.leader and time.monotonic() - t0 < 5:
             await asyncio.sleep(0.02)
         took = time.monotonic() - t0
-        assert b.leader and took < 0.6 + 0.5, took
+        assert b.leader and took < 0.6 + 0.9, took  # lease duration + observation (CPU-loaded CI slack)
         lease = api.get("Lease", "nexus", "nexus-supervisor-leader")
         assert lease["spec"]["holderIdentity"] == "b" and lease["spec"]["leaseTransitions"] >= 1
         # graceful release: a fresh candidate gets it within ~one retry period

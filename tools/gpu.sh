@@ -12,6 +12,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[=ARGS]          python bench.py --steps ${BENCH_STEPS:-30} --warmup 2 ARGS
 #                         (ARGS: commas become spaces, e.g. bench=--procs,6)
+#   variant=NAME:ARGS     one bench logged as gpurun_out/var_NAME.log (A/B runs)
 #   repeat=N[:ARGS]       N benches in a row (median spread)
 #   sweep=P1,P2,..        one bench per --procs value
 #   profile[=ARGS]        long pprof bench (${PROF_STEPS:-1200} steps) + merged worker profile
@@ -54,6 +55,9 @@ for step in "$@"; do
       rc=$?; summary+=("smoke: $(tail -1 gpurun_out/smoke.log | cut -c1-160)"); [ $rc -eq 0 ] ;;
     bench)
       run_bench bench 600 ${val//,/ } ;;
+    variant)
+      name=${val%%:*}; args=""; [[ "$val" == *:* ]] && args=${val#*:}
+      run_bench "var_$name" 300 ${args//,/ } ;;
     repeat)
       n=${val%%:*}; args=""; [[ "$val" == *:* ]] && args=${val#*:}
       mkdir -p gpurun_out/rep

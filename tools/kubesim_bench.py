@@ -92,7 +92,8 @@ async def main(argv=None):
             await ctl.apply_raw(body)
             delete_all(host, port, failed)
         c0, t0 = cpu_s(sim.proc.pid), time.monotonic()
-        b0 = (await ctl.stats()).get("busy_ns", 0)
+        st0 = await ctl.stats()
+        b0, l0 = st0.get("busy_ns", 0), st0.get("lock_ns", 0)
         for failed, body in bodies[2:]:
             await ctl.apply_raw(body)
             await asyncio.get_running_loop().run_in_executor(None, delete_all, host, port, failed)
@@ -104,6 +105,9 @@ async def main(argv=None):
     n = args.steps * args.events
     print(json.dumps({"failures": n, "kubesim_cpu_us_per_failure": round(1e6 * (c1 - c0) / n, 2),
                       "event_loop_busy_us_per_failure": round((st.get("busy_ns", 0) - b0) / 1e3 / n, 2), "flush_threads": ft,
+                      # time holding the store mutex: the serial part, the simulator's ceiling
+                      "store_lock_us_per_failure": round((st.get("lock_ns", 0) - l0) / 1e3 / n, 2),
+                      "threads": st.get("threads"),
                       "wall_s": round(t1 - t0, 2), "watch_bytes": counter[0], "watchers_per_kind": args.watchers,
                       "sim": {k: st.get(k) for k in ("requests", "deleted", "applied", "sends")}}))
 
