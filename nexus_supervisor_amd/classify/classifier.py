@@ -510,13 +510,22 @@ class Classifier:
 _PLAIN_CLASSES = frozenset((F.NONE, F.SCHEDULING, F.DEADLINE, F.FATAL, F.BACKOFF_LIMIT))
 
 
-def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
+TRACE_TOP_PROCS = 4   # per GPU, by VRAM peak
+TRACE_MAX_EVENTS = 8  # per GPU, newest
+
+
+def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto", max_bytes: int = 8192) -> str:
     """Trace column (``algorithm_failure_details``) for a decision.
 
     ``raw`` — the event/status message, as the reference (``supervisor.go:299``);
     ``json`` — message + reason + failure class + evidence; ``auto`` — json only
     when there is evidence beyond the message.
-    """
+
+    Bounded (``rules.trace-max-bytes``): per GPU the top
+    ``TRACE_TOP_PROCS`` processes by VRAM peak and the newest ``TRACE_MAX_EVENTS`` events,
+    the xGMI fabric as a per-GPU summary (:func:`..gpu.topology.xgmi_from_evidence`), and a
+    deterministic trimming ladder (:func:`_trim_trace`) when the document still exceeds
+    the cap — a real 8-GPU job's row stays small and the most telling facts survive."""
     ev = res.evidence
     if fmt == "raw" or (fmt == "auto" and res.failure_class in _PLAIN_CLASSES
                         and (not ev or (len(ev) == 1 and "source" in ev))):
@@ -528,20 +537,84 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto") -> str:
             doc[k] = v
     gpu, topo = doc.get("gpu"), doc.get("topology")
     xgmi = (topo or {}).get("xgmi")
-    if gpu and xgmi and xgmi.get("links") is not None:
-        # the measured links are listed once, under topology.xgmi (with their GPU index); the
-        # per-GPU records are shared by every decision of one telemetry snapshot
-        # (telemetry.pod_evidence_provider): strip + encode them once per record list
-        doc["gpu"] = dict(gpu, gpus=_gpus_without_links(gpu.get("gpus") or []))
+    if gpu and gpu.get("gpus"):
+        # the per-GPU records are shared by every decision of one telemetry snapshot
+        # (telemetry.pod_evidence_provider): bound + encode them once per record list
+        doc["gpu"] = dict(gpu, gpus=_trace_gpus(gpu.get("gpus") or []))
     if xgmi and _native_dumps is not None:
         # the xGMI block is shared by every decision of one telemetry snapshot
         # (topology.xgmi_from_evidence): encode it once, splice it into each trace
         doc["topology"] = dict(topo, xgmi=_raw_json(xgmi))
     # key order is the (deterministic) construction order: sorting every object doubled the
     # cost of the largest per-decision serialisation (profiles/r2_*_pprof_*)
+    out = _dumps(doc)
+    if max_bytes and len(out.encode()) > max_bytes:
+        out = _trim_trace(doc, max_bytes)
+    return out
+
+
+def _dumps(doc) -> str:
     if _native_dumps is not None:
         return _native_dumps(doc, default=str).decode()
     return json.dumps(doc, separators=(",", ":"), default=_json_default, ensure_ascii=False)
+
+
+def _plain(obj):
+    """A document with every spliced RawJSON decoded (for trimming)."""
+    return json.loads(json.dumps(obj, separators=(",", ":"), default=_json_default, ensure_ascii=False))
+
+
+def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
+    """Deterministic trimming ladder: each step drops less telling detail than the next,
+    and the document is re-measured after each; ``trimmed`` lists the steps applied."""
+    d = _plain(doc)
+    steps: List[str] = []
+
+    def size() -> int:
+        return len(json.dumps(dict(d, trimmed=steps), separators=(",", ":"), ensure_ascii=False).encode())
+
+    def gpus():
+        return ((d.get("gpu") or {}).get("gpus")) or []
+
+    def slim(g):
+        for k in [k for k in g if k not in ("index", "vram_total_mb", "vram_peak_mb", "matched", "proc_peak_vram_bytes")]:
+            del g[k]
+
+    topo = d.get("topology") or {}
+    xg = topo.get("xgmi") or {}
+    ladder = [
+        ("gpu.procs:1", lambda: [g.__setitem__("procs", (g.get("procs") or [])[:1]) for g in gpus()]),
+        ("gpu.events:2", lambda: [g.__setitem__("events", (g.get("events") or [])[-2:]) for g in gpus() if "events" in g]),
+        ("history:4", lambda: d.__setitem__("history", (d.get("history") or [])[-4:]) if "history" in d else None),
+        ("topology.collective_env", lambda: topo.pop("collective_env", None)),
+        ("logs.lines:1", lambda: [r.__setitem__("lines", [x[-300:] for x in (r.get("lines") or [])[-1:]])
+                                  for r in (d.get("logs") or []) + ((d.get("gpu") or {}).get("logs") or [])]),
+        ("oom.signals:4", lambda: (d.get("oom") or {}).__setitem__("signals", (d.get("oom") or {}).get("signals", [])[:4])
+         if d.get("oom") else None),
+        ("topology.rank_map", lambda: topo.pop("rank_map", None)),
+        ("gpu.procs", lambda: [g.pop("procs", None) for g in gpus()]),
+        ("gpu.events", lambda: [g.pop("events", None) for g in gpus()]),
+        ("gpu.gpus:slim", lambda: [slim(g) for g in gpus()]),
+        ("topology.xgmi.peers", lambda: [r.pop("peers", None) for r in xg.get("per_gpu", [])]),
+        ("topology.xgmi.per_gpu", lambda: xg.pop("per_gpu", None)),
+        ("message:1024", lambda: d.__setitem__("message", (d.get("message") or "")[-1024:])),
+        ("topology.xgmi", lambda: topo.pop("xgmi", None)),
+    ]
+    for name, step in ladder:
+        if size() <= max_bytes:
+            break
+        step()
+        steps.append(name)
+    if size() > max_bytes:
+        # last resort: the decision's essentials only
+        keep = {k: d[k] for k in ("message", "reason", "class", "source") if k in d}
+        if d.get("oom"):
+            keep["oom"] = {k: v for k, v in d["oom"].items() if k != "signals"}
+        keep["message"] = (keep.get("message") or "")[-min(1024, max_bytes // 4):]
+        d = keep
+        steps.append("essentials")
+    d["trimmed"] = steps
+    return json.dumps(d, separators=(",", ":"), ensure_ascii=False)
 
 
 class RawJSON(bytes):
@@ -563,14 +636,34 @@ def _raw_json(obj) -> RawJSON:
 
 
 _GPUS_MEMO: Dict[int, Tuple[Any, Any]] = {}
+# fields a trace states once elsewhere: the link list and port counts (topology.xgmi), and
+# each process's world sizes / visible devices (topology)
+_GPU_DUP = frozenset(("links", "xgmi_links_up", "xgmi_links_down", "xgmi_links_total", "xgmi_hive_id"))
+_PROC_DUP = frozenset(("world_size", "local_world_size", "visible_devices"))
 
 
-def _gpus_without_links(gpus: List[Dict[str, Any]]):
+def _trace_gpus(gpus: List[Dict[str, Any]]):
+    """Per-GPU records as they go into a trace: without the link list (the fabric is in
+    topology.xgmi), the top processes by VRAM peak (``procs_total`` says how many there
+    were) and the newest events; memoised per (shared, immutable) record list."""
     hit = _GPUS_MEMO.get(id(gpus))
     if hit is not None and hit[0] is gpus:
         return hit[1]
-    stripped = [{k: v for k, v in g.items() if k != "links"} for g in gpus]
-    out = RawJSON(_native_dumps(stripped, default=str)) if _native_dumps is not None else stripped
+    out_l = []
+    for g in gpus:
+        r = {k: v for k, v in g.items() if k not in _GPU_DUP}
+        procs = g.get("procs")
+        if procs:
+            top = sorted(procs, key=lambda p: (-(p.get("peak_vram_bytes") or 0), p.get("pid") or 0))[:TRACE_TOP_PROCS]
+            r["procs"] = [{k: v for k, v in p.items() if k not in _PROC_DUP} for p in top]
+            if len(procs) > TRACE_TOP_PROCS:
+                r["procs_total"] = len(procs)
+        evs = g.get("events")
+        if evs and len(evs) > TRACE_MAX_EVENTS:
+            r["events"] = evs[-TRACE_MAX_EVENTS:]
+            r["events_total"] = len(evs)
+        out_l.append(r)
+    out = RawJSON(_native_dumps(out_l, default=str)) if _native_dumps is not None else out_l
     if len(_GPUS_MEMO) > 512:
         _GPUS_MEMO.clear()
     _GPUS_MEMO[id(gpus)] = (gpus, out)  # holds the list: its id cannot be reused while cached

@@ -122,6 +122,9 @@ class RulesConfig:
     stale_event_grace: float = field(default=2.0, metadata=_k("stale-event-grace", "duration"))
     # trace column format: raw (reference: event message), json, or auto (json when extra evidence exists)
     trace_format: str = field(default="auto", metadata=_k("trace-format"))
+    # cap on the trace column's size (bytes of JSON); larger documents are trimmed
+    # deterministically (least telling detail first); 0 = no cap
+    trace_max_bytes: int = field(default=8192, metadata=_k("trace-max-bytes"))
 
 
 @dataclass
@@ -311,6 +314,8 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("rules.evicted-policy must be fail|observe")
     if cfg.rules.trace_format not in ("raw", "json", "auto"):
         raise ConfigError("rules.trace-format must be raw|json|auto")
+    if cfg.rules.trace_max_bytes and cfg.rules.trace_max_bytes < 1024:
+        raise ConfigError("rules.trace-max-bytes must be 0 (no cap) or >= 1024")
     if cfg.sharding.shards < 1 or not 0 <= cfg.sharding.shard_index < cfg.sharding.shards:
         raise ConfigError("sharding.shard-index must be in [0, shards)")
     if cfg.sharding.mode not in ("static", "lease"):

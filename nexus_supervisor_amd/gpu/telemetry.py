@@ -405,11 +405,10 @@ def _links_of(g: Dict[str, Any]) -> Optional[List[Dict[str, Any]]]:
         peer = l.get("peer_bdf") or ""
         if not peer or peer.startswith("ffff") or l.get("type") not in ("xgmi", None):
             continue
-        rec = {"peer_bdf": peer, "peer": l.get("peer_index") if (l.get("peer_index") or 0) >= 0 else None,
-               "gbps": l.get("bit_rate_gbps"), "max_gbps": l.get("max_bandwidth_gbps")}
-        if l.get("read_kb") or l.get("write_kb"):
-            rec["read_kb"], rec["write_kb"] = l.get("read_kb", 0), l.get("write_kb", 0)
-        out.append(rec)
+        # no cumulative read/write counters: they grow without bound and say nothing about
+        # a failure
+        out.append({"peer_bdf": peer, "peer": l.get("peer_index") if (l.get("peer_index") or 0) >= 0 else None,
+                    "gbps": l.get("bit_rate_gbps"), "max_gbps": l.get("max_bandwidth_gbps")})
     return out
 
 

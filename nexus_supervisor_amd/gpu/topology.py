@@ -234,28 +234,59 @@ def xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, An
 
 
 def _xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Dict[str, Any], gpus: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """The measured fabric as a compact, bounded block: per GPU the
+    peers its xGMI ports reach — resolved to the peer's index when the peer is one of the
+    node's enumerated GPUs (matched by PCI BDF in the native monitor), else its BDF — the
+    link rate, and the port counts.  ``links_listed`` / ``links_up`` count those peer links
+    (so they agree with the peers listed), ``ports_total`` / ``ports_up`` are amd-smi's
+    link-status view of every port (it includes ports without a peer).  No cumulative
+    traffic counters: they grow without bound and say nothing about the failure.
+    ``fully_connected`` is None for fewer than two GPUs (nothing to connect)."""
     idx = {g.get("index") for g in gpus}
-    links, hive = [], set()
+    hive = set()
+    per_gpu = []
+    pairs = set()
     for g in gpus:
         if g.get("xgmi_hive_id"):
             hive.add(g["xgmi_hive_id"])
+        peers, rates, maxes = [], set(), set()
+        up = 0
         for l in g["links"]:
-            links.append(dict(l, gpu=g.get("index")))
-    within = sorted({tuple(sorted((l["gpu"], l["peer"]))) for l in links if l.get("peer") in idx})
+            peer = l.get("peer")
+            peers.append(peer if peer is not None else l.get("peer_bdf"))
+            if l.get("gbps"):
+                up += 1
+                rates.add(l["gbps"])
+            if l.get("max_gbps"):
+                maxes.add(l["max_gbps"])
+            if peer in idx and peer != g.get("index"):
+                pairs.add(tuple(sorted((g.get("index"), peer))))
+        rec_g: Dict[str, Any] = {"gpu": g.get("index"), "peers": peers, "links_listed": len(peers), "links_up": up}
+        if rates:
+            rec_g["gbps"] = rates.pop() if len(rates) == 1 else sorted(rates)
+        if maxes:
+            rec_g["max_gbps"] = maxes.pop() if len(maxes) == 1 else sorted(maxes)
+        if g.get("xgmi_links_total") is not None:
+            rec_g["ports_total"] = g.get("xgmi_links_total")
+            rec_g["ports_up"] = g.get("xgmi_links_up")
+            rec_g["ports_down"] = g.get("xgmi_links_down") or 0
+        per_gpu.append(rec_g)
     n = len(idx)
     rec: Dict[str, Any] = {
         "source": gpu_evidence.get("source", "telemetry"),
         "gpus": sorted(idx),
-        "links": links,
-        "pairs_connected": [list(p) for p in within],
-        "fully_connected": len(within) == n * (n - 1) // 2,
+        "per_gpu": per_gpu,
+        "pairs_connected": [list(p) for p in sorted(pairs)],
+        "fully_connected": (len(pairs) == n * (n - 1) // 2) if n >= 2 else None,
+        "links_listed": sum(r["links_listed"] for r in per_gpu),
+        "links_up": sum(r["links_up"] for r in per_gpu),
     }
     if hive:
         rec["hive_ids"] = sorted(hive)
-    up = [g.get("xgmi_links_up") for g in gpus if g.get("xgmi_links_up") is not None]
-    if up:
-        rec["links_up"] = sum(up)
-        rec["links_down"] = sum(g.get("xgmi_links_down") or 0 for g in gpus)
+    if any("ports_total" in r for r in per_gpu):
+        rec["ports_total"] = sum(r.get("ports_total") or 0 for r in per_gpu)
+        rec["ports_up"] = sum(r.get("ports_up") or 0 for r in per_gpu)
+        rec["ports_down"] = sum(r.get("ports_down") or 0 for r in per_gpu)
     out = dict(topo)
     out["xgmi"] = rec
     return out
@@ -294,18 +325,30 @@ def _topology_from_pod(pod: Dict[str, Any], gpu_resource: str) -> Dict[str, Any]
 
 
 def merge_process_ranks(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, Any]]) -> Dict[str, Any]:
-    """Attach the agent's per-GPU rank map (``{"gpu": idx, "rank": r, "pid": p}``) to ``topo``."""
+    """Attach the agent's per-GPU rank map to ``topo``: one entry per (rank, GPU) —
+    ``{"rank", "local_rank", "gpu", "pid", "procs"}`` with ``pid`` the rank's process with
+    the largest VRAM peak and ``procs`` how many of its processes used that GPU (a
+    dataloader's helpers must not multiply the trace)."""
     if not gpu_evidence:
         return topo
-    ranks = []
+    groups: Dict[Tuple, Dict[str, Any]] = {}
     for g in gpu_evidence.get("gpus", []):
         for p in g.get("procs", []):
-            entry = {"gpu": g.get("index"), "pid": p.get("pid")}
-            for k in ("rank", "local_rank", "world_size"):
-                if p.get(k) is not None:
-                    entry[k] = p[k]
-            ranks.append(entry)
-    if ranks:
+            key = (p.get("rank"), g.get("index"))
+            e = groups.get(key)
+            if e is None:
+                e = groups[key] = {"gpu": g.get("index"), "pid": p.get("pid"), "procs": 0, "_peak": -1}
+                for k in ("rank", "local_rank"):
+                    if p.get(k) is not None:
+                        e[k] = p[k]
+                if p.get("world_size") is not None and "world_size" not in topo:
+                    e["world_size"] = p["world_size"]
+            e["procs"] += 1
+            peak = p.get("peak_vram_bytes") or 0
+            if peak > e["_peak"]:
+                e["_peak"], e["pid"] = peak, p.get("pid")
+    if groups:
+        ranks = [{k: v for k, v in e.items() if k != "_peak"} for e in groups.values()]
         topo = dict(topo, rank_map=sorted(ranks, key=lambda e: (e.get("rank", 1 << 30), e.get("gpu") or 0)))
     return topo
 

@@ -717,7 +717,7 @@ class Supervisor:
             self._remember(key, stage)
             return Decision(r, "applied", stage, False)
         cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
-        details = render_trace(r, self.cfg.rules.trace_format)
+        details = render_trace(r, self.cfg.rules.trace_format, self.cfg.rules.trace_max_bytes)
         # The reference deletes the Job, then upserts the row (supervisor.go:289-301).  This
         # build writes first: deleting first (or concurrently) lets a crash between the two
         # lose the decision for good — the Job's pods are garbage-collected, so the replay
@@ -804,7 +804,7 @@ class Supervisor:
             cause = details = None
         else:
             cause = R.failure_cause(r.action, r.run_status_message, compat.doubled_fatal_cause)
-            details = render_trace(r, self.cfg.rules.trace_format)
+            details = render_trace(r, self.cfg.rules.trace_format, self.cfg.rules.trace_max_bytes)
         if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)

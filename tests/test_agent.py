@@ -163,7 +163,9 @@ def test_supervisor_waits_for_agent_evidence_then_attributes(arun):
         assert trace["topology"]["rank"] == 10 and trace["topology"]["expected_gpu"] == "6"
         assert [g["index"] for g in trace["gpu"]["gpus"]] == [6]
         assert any("VRAM peak" in sig for sig in trace["oom"]["signals"])
-        assert trace["topology"]["xgmi"]["source"] == "fake" and len(trace["topology"]["xgmi"]["links"]) == 7
+        xg = trace["topology"]["xgmi"]
+        assert xg["source"] == "fake" and xg["per_gpu"][0]["links_listed"] == 7 and xg["fully_connected"] is None
+        assert sorted(xg["per_gpu"][0]["peers"]) == [0, 1, 2, 3, 4, 5, 7]
         assert app.metrics.counter("decisions_deferred_for_gpu_evidence") == 1
         await agent.stop()
         await kc.close()

@@ -164,8 +164,9 @@ def test_xgmi_link_down_and_ecc_are_gpu_faults():
         trace = json.loads(render_trace(res[0]))
         g = trace["gpu"]["gpus"][0]
         assert g["index"] == gpu and any(e["type"] == expect for e in g["events"])
-        if expect == "XGMI_LINK_DOWN":
-            assert g["xgmi_links_down"] == 2 and g["xgmi_links_total"] == 7
+        if expect == "XGMI_LINK_DOWN":  # the link state is stated once, in the fabric summary
+            xg = trace["topology"]["xgmi"]["per_gpu"][0]
+            assert xg["gpu"] == 5 and xg["ports_down"] == 2 and xg["ports_total"] == 7 and xg["ports_up"] == 5
         assert not [e for e in tel.snapshot()[0]["events"]]
 
 

@@ -125,7 +125,9 @@ def test_real_hbm_oom_attributed_to_gpu(telemetry, stress_exe, tmp_path):
     assert trace["class"] == "hbm-oom" and trace["gpu"]["gpus"][0]["index"] == 0
     xg = trace["topology"]["xgmi"]
     if g.get("links"):  # amd-smi link metrics: the GPU's real xGMI ports and peers
-        assert xg["source"] == "amdsmi" and all(l["max_gbps"] for l in xg["links"]), xg
+        assert xg["source"] == "amdsmi" and all(r.get("max_gbps") for r in xg["per_gpu"]), xg
+        r0 = xg["per_gpu"][0]
+        assert r0["links_listed"] == len(g["links"]) and xg["fully_connected"] is None  # one GPU: nothing to connect
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/hbm_oom_attribution.json", "w") as f:
         json.dump({"pid_matched": pid_matched, "proc_source": telemetry.proc_mode, "pid": pid,

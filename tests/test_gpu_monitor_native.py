@@ -93,6 +93,7 @@ def test_monitor_attributes_pod_processes_without_amdsmi_pids(tmp_path, source):
         assert rec["procs"][0]["rank"] == 3 and rec["procs"][0]["source"] == p["source"]
         # measured xGMI: the stub node's peer link plus six unconnected ports filtered out
         assert [l["peer"] for l in rec["links"]] == [0] and rec["links"][0]["max_gbps"] == 608
+        assert "read_kb" not in rec["links"][0]  # no cumulative counters in the evidence
         assert rec["xgmi_links_up"] == 7 and rec["xgmi_hive_id"]
     finally:
         tel.stop()
@@ -155,3 +156,57 @@ def test_classifier_attributes_through_native_monitor(tmp_path):
     finally:
         tel.stop()
         M.stub_set_vram(1, 283)
+
+
+def test_eight_gpu_trace_is_bounded_and_resolves_every_peer(tmp_path):
+    """an 8-GPU job (48 processes, 40 GPU events) on the stub node: the
+    trace stays under ``rules.trace-max-bytes``, every xGMI peer resolves to a GPU index,
+    the fabric is fully connected by real pairs, the port counts agree with the listed
+    links, no cumulative traffic counters are carried — and the OOM verdict survives."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, NEXUS_STUB_GPUS="8")
+    p = subprocess.run([sys.executable, "-m", "nexus_supervisor_amd.testing.trace8", str(tmp_path), "8192"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    t = out["trace"]
+    assert out["bytes"] <= 8192, out["bytes"]
+    assert t["class"] == "hbm-oom" and t["oom"]["gpu_index"] == 3
+    xg = t["topology"]["xgmi"]
+    assert xg["gpus"] == list(range(8)) and xg["fully_connected"] is True
+    assert len(xg["pairs_connected"]) == 28
+    for r in xg.get("per_gpu", []):
+        assert sorted(r["peers"]) == [i for i in range(8) if i != r["gpu"]]  # every peer resolved
+        assert r["links_listed"] == r["links_up"] == 7 and r["ports_total"] == 8 and r["ports_up"] == 7
+    assert xg["links_up"] == 56 and xg["links_listed"] == 56
+    text = json.dumps(t)
+    assert "read_kb" not in text and "write_kb" not in text
+    for g in t["gpu"]["gpus"]:
+        assert len(g.get("procs", [])) <= 4 and "links" not in g
+        assert len(g.get("events", [])) <= 8
+
+
+def test_trim_ladder_is_deterministic():
+    """A trace over the cap is trimmed by the same steps every time, least telling detail
+    first, and keeps the verdict."""
+    import json
+
+    from nexus_supervisor_amd.classify import render_trace
+    from nexus_supervisor_amd.models.decisions import RunStatusAnalysisResult
+
+    r = RunStatusAnalysisResult("ToFailFatalError", "m", "boom " * 2000, request_id="x", algorithm="a",
+                                reason="Error", failure_class="hbm-oom")
+    r.evidence = {"source": "pod-status", "oom": {"kind": "hbm", "signals": [f"s{i}" for i in range(10)], "gpu_index": 2},
+                  "history": [{"kind": "exit", "message": "y" * 300} for _ in range(16)],
+                  "gpu": {"source": "fake", "gpus": [{"index": i, "procs": [{"pid": j, "peak_vram_bytes": j} for j in range(9)],
+                                                       "events": [{"type": "VMFAULT", "message": "z" * 150}] * 20}
+                                                      for i in range(8)]}}
+    a, b = render_trace(r, max_bytes=4096), render_trace(r, max_bytes=4096)
+    assert a == b and len(a.encode()) <= 4096
+    t = json.loads(a)
+    assert t["trimmed"][0] == "gpu.procs:1" and t["oom"]["kind"] == "hbm" and t["class"] == "hbm-oom"
+    one = json.loads(render_trace(r, max_bytes=0))
+    assert "trimmed" not in one and len(one["gpu"]["gpus"][0]["procs"]) == 4 and one["gpu"]["gpus"][0]["procs_total"] == 9
