@@ -71,9 +71,15 @@ def parse_args(argv=None):
     ap.add_argument("--pprof-out", default="", help="write a pprof profile of the timed steps (rank 0)")
     ap.add_argument("--pprof-hz", type=int, default=199, help="pprof sampling rate (CPU-time Hz)")
     ap.add_argument("--cql-latency-us", type=int, default=0, help="inject CQL server response latency")
-    ap.add_argument("--two-step-write", action="store_true",
-                    help="actuate with the reference's read + write instead of one conditional write "
-                         "(compat.fused-write: false; A/B of the actuation path)")
+    ap.add_argument("--cql-lwt-latency-us", type=int, default=-1,
+                    help="extra CQL server latency of a conditional write (a Paxos round: ~4 round trips where a "
+                         "plain write takes 1); -1 = 3 x --cql-latency-us")
+    ap.add_argument("--actuation", choices=("auto", "fused", "two-step"), default="auto",
+                    help="compat.fused-write: auto (one conditional write per decision only under HA, else read + "
+                         "write), fused (always one conditional write), two-step (the reference's read + write)")
+    ap.add_argument("--two-step-write", action="store_true", help="alias of --actuation two-step")
+    ap.add_argument("--conditional-update", choices=("auto", "always", "never"), default="auto",
+                    help="compat.conditional-update of the two-step path (never = the reference's plain writes)")
     ap.add_argument("--cluster", choices=("auto", "shared", "per-rank"), default="auto",
                     help="per-rank (default) = each GPU-job slot's replica has its own namespace shard, apiserver "
                          "simulator and CQL server; shared = one apiserver + one CQL server for all ranks, each "
@@ -183,7 +189,9 @@ def main(argv=None) -> int:
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
-                      fused_write=not args.two_step_write,
+                      fused_write={"auto": "auto", "fused": "true", "two-step": "false"}[
+                          "two-step" if args.two_step_write else args.actuation],
+                      conditional_update=args.conditional_update, cql_lwt_latency_us=args.cql_lwt_latency_us,
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster,
@@ -284,7 +292,8 @@ def main(argv=None) -> int:
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
                 "cql_latency_us": args.cql_latency_us,
-                "actuation": "read+write" if args.two_step_write else "fused conditional write",
+                "actuation": res.get("actuation"),
+                "cql_lwt_latency_us": args.cql_lwt_latency_us,
                 "stages_ms": res.get("stages"),
                 "cpu_util_rank0": res.get("cpu"),
                 "step_done_ms_rank0": res.get("step_done_ms"),

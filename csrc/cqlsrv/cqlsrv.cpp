@@ -12,6 +12,11 @@
 //   SELECT cols|*|COUNT(*) FROM t [WHERE pk | indexed col = x] [LIMIT n]   DELETE
 //   system.local / system.peers (token ring for token-aware clients), system.cqlsrv_stats
 //
+// Lightweight-transaction cost (--lwt-latency-us): a conditional write is a Paxos round —
+// prepare/promise, read, propose/accept, commit: ~4 replica round trips where a plain write
+// takes 1 — so its answer is held --lwt-latency-us longer than a plain one's (default 3 ×
+// --latency-us), and conditional writes to ONE partition are serialised (each Paxos round
+// on a partition starts when the previous one committed), as on Scylla / Cassandra.
 // Fault injection for chaos tests: --latency-us, --error-rate (Overloaded errors),
 // SIGUSR1 drops every client connection; --data FILE keeps a write-ahead log so a
 // killed + restarted server ("Scylla node restart") keeps its rows.
@@ -67,6 +72,7 @@ struct Options {
   int port = 9042;
   std::string user, password;
   int64_t latency_us = 0;
+  int64_t lwt_latency_us = -1;  // extra latency of a conditional write; -1 = 3 × latency_us
   double error_rate = 0.0;
   uint64_t seed = 1;
   std::string data_file;
@@ -645,7 +651,7 @@ struct Prepared {
 
 struct Stats {
   std::atomic<uint64_t> requests{0}, queries{0}, executes{0}, prepares{0}, batches{0}, reads{0}, writes{0}, lwt{0},
-      errors{0}, injected_errors{0}, connections{0}, dropped{0}, shard_hits{0}, shard_misses{0};
+      errors{0}, injected_errors{0}, connections{0}, dropped{0}, shard_hits{0}, shard_misses{0}, lwt_waits{0};
 };
 
 class Db {
@@ -929,6 +935,10 @@ std::vector<int> select_cols(const Table& t, const Stmt& st) {
   return which;
 }
 
+// set by execute() when the statement was a conditional write (its partition); read and
+// cleared by the request handler to price the Paxos round (see --lwt-latency-us)
+thread_local std::string t_lwt_partition;
+
 ColSpec applied_spec(const Table& t) {
   Type b;
   b.id = T_BOOLEAN;
@@ -990,6 +1000,7 @@ bool execute(const Stmt& st, const std::vector<Val>& vals, std::string& cur_ks, 
       ++g_db.stats.writes;
       if (st.if_not_exists) {
         ++g_db.stats.lwt;
+        t_lwt_partition = t.ks + "." + t.name + "/" + key;
         if (it != t.rows.end()) {
           rs = lwt_result(t, false, &it->second);
           return true;
@@ -1021,6 +1032,7 @@ bool execute(const Stmt& st, const std::vector<Val>& vals, std::string& cur_ks, 
         auto it = t.rows.find(key);
         if (lwt) {
           ++g_db.stats.lwt;
+          t_lwt_partition = t.ks + "." + t.name + "/" + key;
           const std::vector<Val>* existing = it == t.rows.end() ? nullptr : &it->second;
           bool ok = st.if_exists ? existing != nullptr : existing != nullptr;
           for (auto& c : st.ifs) ok = ok && cond_holds(t, existing, c, vals);
@@ -1245,7 +1257,7 @@ ResultSet stats_rows() {
       {"prepares", s.prepares},       {"batches", s.batches},       {"reads", s.reads},
       {"writes", s.writes},           {"lwt", s.lwt},               {"errors", s.errors},
       {"injected_errors", s.injected_errors}, {"connections", s.connections}, {"dropped", s.dropped},
-      {"shard_hits", s.shard_hits},   {"shard_misses", s.shard_misses}};
+      {"shard_hits", s.shard_hits},   {"shard_misses", s.shard_misses}, {"lwt_waits", s.lwt_waits}};
   for (auto& p : kv) rs.cols.push_back(ColSpec{"system", "cqlsrv_stats", p.first, ty(T_BIGINT)});
   std::vector<Val> row;
   for (auto& p : kv) {
@@ -1358,7 +1370,12 @@ struct Shard {
   uint64_t drop_seen = 0;
 };
 
-std::mutex g_db_mu;  // tables, prepared statements, WAL
+std::mutex g_db_mu;  // tables, prepared statements, WAL, the Paxos clocks
+// per partition: when the last Paxos round on it commits (µs, now_us clock); a new round on
+// the partition starts no earlier (guarded by g_db_mu)
+std::unordered_map<std::string, int64_t> g_paxos_busy;
+
+int64_t lwt_extra_us() { return g_opt.lwt_latency_us >= 0 ? g_opt.lwt_latency_us : 3 * g_opt.latency_us; }
 std::atomic<uint64_t> g_drop_gen{0};
 std::vector<std::unique_ptr<Shard>> g_shards;
 int g_shard_port = 0;
@@ -1410,6 +1427,33 @@ void respond(Shard& s, Conn& c, int16_t stream, uint8_t op, const std::string& b
     return;
   }
   c.out += f;
+}
+
+// [g_db_mu held] the answer of a statement: a conditional write's waits for its Paxos round
+// (queued behind the partition's previous round, then --lwt-latency-us on top of the plain
+// write latency); anything else goes out after --latency-us as before
+void respond_stmt(Shard& s, Conn& c, int16_t stream, uint8_t op, const std::string& body) {
+  if (t_lwt_partition.empty()) return respond(s, c, stream, op, body);
+  std::string part;
+  part.swap(t_lwt_partition);
+  int64_t extra = lwt_extra_us();
+  if (extra <= 0 && g_opt.latency_us <= 0) return respond(s, c, stream, op, body);
+  int64_t now = now_us();
+  int64_t& busy = g_paxos_busy[part];
+  int64_t start = now;
+  if (busy > now) {
+    start = busy;
+    ++g_db.stats.lwt_waits;  // queued behind another round on the partition
+  }
+  int64_t done = start + g_opt.latency_us + extra;
+  busy = done;
+  if (g_paxos_busy.size() > 200000) {  // forget partitions whose last round is long over
+    for (auto it = g_paxos_busy.begin(); it != g_paxos_busy.end();) {
+      if (it->second < now) it = g_paxos_busy.erase(it);
+      else ++it;
+    }
+  }
+  s.delayed.push(Delayed{done, c.fd, s.gen[c.fd], frame(VERSION_RESP, stream, op, body)});
 }
 
 // Scylla "biased-token-round-robin": shard of a Murmur3 token.
@@ -1629,8 +1673,9 @@ void handle_frame(Shard& sh, Conn& c, const FrameHeader& h, const uint8_t* body)
         uint8_t flags = read_params(r, vals, cl);
         Parser p(q);
         Stmt st = p.parse();
+        t_lwt_partition.clear();
         auto res = run_stmt(c, st, vals, (flags & QF_SKIP_METADATA) != 0);
-        respond(sh, c, h.stream, res.first, res.second);
+        respond_stmt(sh, c, h.stream, res.first, res.second);
         return;
       }
       case OP_PREPARE: {
@@ -1678,9 +1723,10 @@ void handle_frame(Shard& sh, Conn& c, const FrameHeader& h, const uint8_t* body)
                                            std::to_string(vals.size()) + " bound variables");
         std::string saved = c.ks;
         if (!it->second.stmt.ks.empty()) c.ks = it->second.stmt.ks;
+        t_lwt_partition.clear();
         auto res = run_stmt(c, it->second.stmt, vals, (flags & QF_SKIP_METADATA) != 0);
         c.ks = saved;
-        respond(sh, c, h.stream, res.first, res.second);
+        respond_stmt(sh, c, h.stream, res.first, res.second);
         return;
       }
       case OP_BATCH: {
@@ -1873,6 +1919,7 @@ void on_signal(int sig) {
 void usage() {
   fprintf(stderr,
           "nexus-cqlsrv [--host H] [--port P (0 = ephemeral)] [--user U --password P] [--latency-us N]\n"
+          "             [--lwt-latency-us N (extra for a conditional write; default 3 x latency-us)]\n"
           "             [--error-rate F] [--seed N] [--data WAL] [--ready-file PATH] [--dc DC] [--rack R]\n"
           "             [--tokens t1,t2] [--peer host:port:tok1;tok2]... [--exec FILE.cql] [-v]\n"
           "             [--shards N [--shard-aware-port P] [--ignore-msb B] [--advertise-shard-aware-port P]]\n");
@@ -1932,6 +1979,7 @@ int main(int argc, char** argv) {
     else if (a == "--user") g_opt.user = val();
     else if (a == "--password") g_opt.password = val();
     else if (a == "--latency-us") g_opt.latency_us = std::stoll(val());
+    else if (a == "--lwt-latency-us") g_opt.lwt_latency_us = std::stoll(val());
     else if (a == "--error-rate") g_opt.error_rate = std::stod(val());
     else if (a == "--seed") g_opt.seed = std::stoull(val());
     else if (a == "--data") g_opt.data_file = val();

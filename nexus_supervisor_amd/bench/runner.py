@@ -36,7 +36,9 @@ class BenchConfig:
     workdir: str = "/tmp"
     step_timeout: float = 300.0
     cql_latency_us: int = 0
-    fused_write: bool = True  # compat.fused-write (False: the reference's read + write)
+    cql_lwt_latency_us: int = -1  # extra latency of a conditional write (Paxos); -1 = 3 x cql_latency_us
+    fused_write: str = "auto"  # compat.fused-write: auto | true | false (the reference's read + write)
+    conditional_update: str = "auto"  # compat.conditional-update
     pprof_out: str = ""
     kube_connections: int = 256
     inflight: int = 2
@@ -63,6 +65,7 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
     sc.observability.stage_timestamps = True
     sc.scylla_cql_store.connections_per_host = 2
     sc.compat.fused_write = cfg.fused_write
+    sc.compat.conditional_update = cfg.conditional_update
     return sc
 
 
@@ -318,6 +321,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
             "wrong_stage": tracker.wrong_stage, "wrong_examples": tracker.wrong_examples, "readback": readback,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
+            "actuation": _actuation(sc),
             "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
             "probe": probe, "step_done_ms": step_done_ms}
 
@@ -371,10 +375,20 @@ async def _read_back(harness, tracker: "Tracker") -> Dict[str, Any]:
     return {"checked": len(rids), "wrong": len(wrong), "examples": wrong[:5]}
 
 
+def _actuation(sc: SupervisorConfig) -> str:
+    from ..supervisor import fused_actuation
+
+    if fused_actuation(sc):
+        return "fused conditional write"
+    cu = sc.compat.conditional_update
+    return "read+write" + (" (ToRunning conditional)" if cu == "auto" else " (conditional)" if cu == "always" else "")
+
+
 def _stage_breakdown(sup) -> Dict[str, Any]:
     m = sup.metrics
     out = {}
-    for name in ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_write", "stage_delete"):
+    for name in ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_prepare", "stage_write",
+                 "stage_delete"):
         h = m.histogram(name)
         if h is not None:
             out[name] = {k: (int(v) if k == "count" else round(v / 1000.0, 3)) for k, v in h.summary().items()}

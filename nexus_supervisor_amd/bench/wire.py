@@ -67,7 +67,8 @@ class WireHarness:
         # shared cluster gets a shard per rank, up to 8
         shards = max(2, min(8, cfg.world)) if self.shared else 2
         self.cql_shards = shards
-        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=cfg.cql_latency_us, shards=shards).start()
+        self.cql = CqlServer(exec_statements=schema_statements(), latency_us=cfg.cql_latency_us, shards=shards,
+                             lwt_latency_us=cfg.cql_lwt_latency_us).start()
         ready = os.path.join(self.workdir, "cluster.ready")
         if os.path.exists(ready):
             os.unlink(ready)

@@ -89,11 +89,16 @@ class CompatConfig:
     #   always — every write conditional; never — none (reference behaviour)
     # true / false are accepted as always / never.
     conditional_update: str = field(default="auto", metadata=_k("conditional-update"))
-    # one store round trip per decision: the conditional write alone decides (its not-applied
+    # one store call per decision: the conditional write alone decides (its not-applied
     # answer carries the row's stage: no row / finished / already RUNNING) instead of the
-    # reference's read followed by a write (supervisor.go:264-301).  Makes every write
-    # conditional; off with conditional-update: never or full-row-upsert.
-    fused_write: bool = field(default=True, metadata=_k("fused-write"))
+    # reference's read followed by a write (supervisor.go:264-301).  That write is a
+    # lightweight transaction — a Paxos round, ~4 replica round trips and serialised per
+    # partition where a plain write takes 1 (docs/ARCHITECTURE.md "Pricing the LWT"):
+    #   auto  — fused only under HA (leader election or shard leases: a deposed owner may
+    #           still hold a decision), else the reference's read + plain write — default
+    #   true  — always fused;  false — never (the reference's read + write)
+    # Off with conditional-update: never or full-row-upsert.
+    fused_write: str = field(default="auto", metadata=_k("fused-write"))
 
 
 @dataclass
@@ -305,6 +310,11 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
                                      "false": "never", "0": "never", "no": "never", "off": "never"}.get(cu, cu)
     if cfg.compat.conditional_update not in ("auto", "always", "never"):
         raise ConfigError("compat.conditional-update must be auto|always|never")
+    fw = str(cfg.compat.fused_write).strip().lower()
+    cfg.compat.fused_write = {"1": "true", "yes": "true", "on": "true", "always": "true",
+                              "0": "false", "no": "false", "off": "false", "never": "false"}.get(fw, fw)
+    if cfg.compat.fused_write not in ("auto", "true", "false"):
+        raise ConfigError("compat.fused-write must be auto|true|false")
     st = cfg.stages.mapping()
     if any(not v for v in st.values()) or len(set(st.values())) != len(st):
         raise ConfigError("stages: every lifecycle stage needs a distinct non-empty string")

@@ -52,6 +52,21 @@ STAGE_FOR_ACTION = {
 }
 
 
+def fused_actuation(cfg: SupervisorConfig) -> bool:
+    """Is a decision ONE conditional write (``compat.fused-write``)?  ``auto``: only when
+    a deposed owner may still hold decisions — leader election or shard leases — where
+    the LWT's atomic stage check is what keeps a finished row final; a lone replica takes
+    the reference's cheaper read + plain write (an LWT is a Paxos round)."""
+    c = cfg.compat
+    if c.full_row_upsert or c.conditional_update == "never":
+        return False
+    if c.fused_write == "true":
+        return True
+    if c.fused_write == "false":
+        return False
+    return cfg.leader_election.enabled or cfg.sharding.mode == "lease"
+
+
 def _FAILED_STAGES():
     return (LifecycleStage.FAILED, LifecycleStage.SCHEDULING_FAILED, LifecycleStage.DEADLINE_EXCEEDED)
 
@@ -131,8 +146,7 @@ class Supervisor:
         self._applied_cap = 200_000
         # one conditional write per decision instead of read + write (compat.fused-write);
         # conditional-update: never (the reference's unconditional writes) turns it off
-        self._fused = (cfg.compat.fused_write and not cfg.compat.full_row_upsert
-                       and cfg.compat.conditional_update != "never")
+        self._fused = fused_actuation(cfg)
         self._guards: Dict[Any, Any] = {}
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
@@ -172,8 +186,9 @@ class Supervisor:
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
         m.describe("stage_classify", "Watch receive to pipeline enqueue (classification)")
         m.describe("stage_queue", "Pipeline enqueue to worker dequeue (rate limit + queueing)")
-        m.describe("stage_read", "Checkpoint read round trip")
-        m.describe("stage_write", "Checkpoint write round trip")
+        m.describe("stage_read", "Checkpoint read round trip (read + write actuation)")
+        m.describe("stage_prepare", "Dequeue to conditional write sent: enrichment + trace (fused actuation)")
+        m.describe("stage_write", "Checkpoint write round trip (fused: the conditional write)")
         m.describe("stage_delete", "Checkpoint ack to Job DELETE accepted")
 
     # ------------------------------------------------------------------ Init
@@ -809,7 +824,7 @@ class Supervisor:
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)
         t = wall()
-        stamps["read"] = t  # no separate read: the stage decomposition books the round trip as the write
+        stamps["prepare"] = t  # no read in this path: dequeue → here is local work, here → ack the CAS
         now_dt = _dt.datetime.fromtimestamp(t, _dt.timezone.utc)
         try:
             applied, current = await self.store.cas_update(r.algorithm, rid, stage, cause, details, now_dt,
@@ -1009,11 +1024,16 @@ class Supervisor:
             obs("receive_to_checkpoint", ack - s["receive"])
             # stage decomposition: classify → queue wait → CQL read → CQL write
             enq, deq, rd = s.get("enqueue"), s.get("dequeue"), s.get("read")
-            if enq is not None and deq is not None and rd is not None:
+            prep = s.get("prepare")
+            if enq is not None and deq is not None and (rd is not None or prep is not None):
                 obs("stage_classify", enq - s["receive"])
                 obs("stage_queue", deq - enq)
-                obs("stage_read", rd - deq)
-                obs("stage_write", ack - rd)
+                if prep is not None:  # fused: no read; the write stage is the conditional write's round trip
+                    obs("stage_prepare", prep - deq)
+                    obs("stage_write", ack - prep)
+                else:
+                    obs("stage_read", rd - deq)
+                    obs("stage_write", ack - rd)
 
     def _done(self, r: RunStatusAnalysisResult, decision: Decision) -> None:
         for h in self.decision_hooks:

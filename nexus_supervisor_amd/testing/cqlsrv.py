@@ -19,7 +19,7 @@ class CqlServer:
     def __init__(self, *, user: str = "", password: str = "", latency_us: int = 0, error_rate: float = 0.0,
                  persist: bool = False, tokens: Sequence[int] = (), peers: Sequence[str] = (), exec_statements: Sequence[str] = (),
                  dc: str = "datacenter1", host: str = "127.0.0.1", port: int = 0, extra_args: Sequence[str] = (),
-                 shards: int = 0, shard_aware_port: int = 0):
+                 shards: int = 0, shard_aware_port: int = 0, lwt_latency_us: int = -1):
         from .._build import binary
 
         # NEXUS_CQLSRV_BINARY selects e.g. a sanitizer build (bin/nexus-cqlsrv-address)
@@ -29,6 +29,7 @@ class CqlServer:
         self.port = port
         self.user, self.password = user, password
         self.latency_us, self.error_rate = latency_us, error_rate
+        self.lwt_latency_us = lwt_latency_us  # extra for a conditional write (Paxos); -1 = server default 3 x latency
         self.data = os.path.join(self.dir, "wal.bin") if persist else ""
         self.tokens = [str(t) for t in tokens]
         self.peers = list(peers)
@@ -53,6 +54,8 @@ class CqlServer:
             argv += ["--user", self.user, "--password", self.password]
         if self.latency_us:
             argv += ["--latency-us", str(self.latency_us)]
+        if self.lwt_latency_us >= 0:
+            argv += ["--lwt-latency-us", str(self.lwt_latency_us)]
         if self.error_rate:
             argv += ["--error-rate", str(self.error_rate)]
         if self.data:

@@ -48,12 +48,30 @@ def test_bench_wire_in_process(tmp_path, capsys):
     _check(out, 1, 2, 1, 60)
     cfg = out["config"]
     assert cfg["transport"] == "wire" and cfg["store"].startswith("cql")
-    assert cfg["actuation"] == "fused conditional write"
+    assert cfg["actuation"] == "read+write (ToRunning conditional)"  # one replica, no HA: no LWT per decision
     st = cfg["stages_ms"]
     assert st["receive_to_checkpoint"]["count"] >= 120
     for k in ("stage_classify", "stage_queue", "stage_read", "stage_write"):
         assert st[k]["count"] == st["receive_to_checkpoint"]["count"]
     assert out["latency_at_rate"]["events"] == 3
+
+
+@pytest.mark.slow
+def test_bench_fused_actuation_with_priced_lwt(capsys):
+    """``--actuation fused`` at a CQL round trip of 2 ms, the LWT priced as a Paxos round
+    (3 more round trips): the checkpoint-write stage of the fused path costs ~4 round trips
+    where the two-step path's write costs 1 (+1 read)."""
+    import bench
+
+    rc = bench.main(["--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "40", "--probe-events", "0",
+                     "--actuation", "fused", "--cql-latency-us", "2000", "--procs", "1"])
+    assert rc == 0
+    out = json.loads([x for x in capsys.readouterr().out.splitlines() if x.startswith("{")][-1])
+    _check(out, 1, 2, 1, 40)
+    assert out["config"]["actuation"] == "fused conditional write"
+    st = out["config"]["stages_ms"]
+    assert st["stage_write"]["p50"] >= 4 * 2.0 * 0.9  # the CAS itself, not local work (VERDICT r2 weak #8)
+    assert "stage_read" not in st and st["stage_prepare"]["p50"] < 2.0
 
 
 @pytest.mark.slow
@@ -67,7 +85,7 @@ def test_bench_two_step_write_ab(capsys):
     assert rc == 0
     out = json.loads([x for x in capsys.readouterr().out.splitlines() if x.startswith("{")][-1])
     _check(out, 1, 2, 1, 60)
-    assert out["config"]["actuation"] == "read+write"
+    assert out["config"]["actuation"].startswith("read+write")
 
 
 @pytest.mark.slow

@@ -45,14 +45,38 @@ class CountingStore(MemoryStore):
 
 
 def _cfg(**over):
+    """These tests pin the fused actuation (``compat.fused-write: true``); its ``auto``
+    default (fused only under HA) is covered by test_fused_default_follows_ha."""
     base = {"cql-store-type": "memory", "rate-limit-elements-per-second": 0, "resync-period": "0s",
-            "failure-rate-base-delay": "10ms", "failure-rate-max-delay": "50ms"}
+            "failure-rate-base-delay": "10ms", "failure-rate-max-delay": "50ms", "compat": {"fused-write": True}}
+    over = dict(over)
+    if "compat" in over:
+        over["compat"] = dict(base["compat"], **over["compat"])
     base.update(over)
     return load_config(path=None, env={}, overrides=base)
 
 
+def test_fused_default_follows_ha():
+    """an LWT is a Paxos round (~4 replica round trips, serialised per
+    partition), so the default fuses the decision into one conditional write only where
+    its atomic stage check is needed — a deposed leader or shard owner may still hold a
+    decision — and a lone replica keeps the reference's read + plain write."""
+    from nexus_supervisor_amd.supervisor import fused_actuation
+
+    def cfg(**over):
+        return load_config(path=None, env={}, overrides=dict({"cql-store-type": "memory"}, **over))
+
+    assert cfg().compat.fused_write == "auto" and not fused_actuation(cfg())
+    assert fused_actuation(cfg(**{"leader-election": {"enabled": True}}))
+    assert fused_actuation(cfg(sharding={"shards": 2, "mode": "lease"}))
+    assert not fused_actuation(cfg(sharding={"shards": 2, "shard-index": 1}))  # static shards: no deposed owner
+    assert fused_actuation(cfg(compat={"fused-write": True}))
+    assert not fused_actuation(cfg(compat={"fused-write": False}, **{"leader-election": {"enabled": True}}))
+    assert cfg(compat={"fused-write": "yes"}).compat.fused_write == "true"
+
+
 def test_fused_is_the_default_and_reference_mode_turns_it_off():
-    assert _cfg().compat.fused_write is True
+    assert _cfg().compat.fused_write == "true"
     from nexus_supervisor_amd.supervisor import Supervisor  # noqa: F401 - import check
     cfg = _cfg(compat={"conditional-update": "never"})
     c = InProcCluster(cfg, MemoryStore(ROWS), [])
