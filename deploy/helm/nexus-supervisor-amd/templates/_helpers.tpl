@@ -43,6 +43,19 @@ app.kubernetes.io/instance: {{ .Release.Name }}
 {{- printf "%s:%s" .Values.agent.image.repository (default (printf "v%s" .Chart.AppVersion) .Values.agent.image.tag) -}}
 {{- end -}}
 
+{{- /* reference: rbac.clusterRole.supervisor.nameOverride (/root/reference/.helm/templates/_helpers.tpl:77-83) */ -}}
 {{- define "nexus.roleName" -}}
+{{- $override := .Values.rbac.nameOverride -}}
+{{- if .Values.rbac.clusterRole -}}
+{{- if .Values.rbac.clusterRole.supervisor -}}
+{{- if .Values.rbac.clusterRole.supervisor.nameOverride -}}
+{{- $override = .Values.rbac.clusterRole.supervisor.nameOverride -}}
+{{- end -}}
+{{- end -}}
+{{- end -}}
+{{- if $override -}}
+{{- $override -}}
+{{- else -}}
 {{- printf "%s-api-access" (include "nexus.fullname" .) -}}
+{{- end -}}
 {{- end -}}
