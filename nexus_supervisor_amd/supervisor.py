@@ -802,12 +802,18 @@ class Supervisor:
         """``compat.fused-write``: the decision is ONE conditional write
         (``UPDATE … IF lifecycle_stage IN (<unfinished stages>)``) instead of the reference's
         read followed by a write (``supervisor.go:264-301``).  The store checks the stage
-        atomically, so a row finished by anyone between a read and a write (a third party's
-        CANCELLED, a new leader's FAILED) can never be overwritten, and the actuator pays one
-        store round trip and one request instead of two.  A not-applied answer carries the
-        row's stage, which drives the reference's skip paths (no row / finished / ToRunning on
-        a RUNNING row).  Returns None for a stage outside the known set (custom stage
-        strings): the two-step path then decides with that stage in its guard."""
+        inside a Paxos round, so a row finished by another *conditional* writer (a new
+        leader's or shard owner's FAILED) is never overwritten, nor is one whose plain write
+        was committed before the round's read phase.  A plain (non-LWT) write racing with the
+        round — other Nexus components write the row without conditions — is not ordered
+        against it: Cassandra / Scylla only linearise LWTs among themselves, so that window
+        stays as narrow as, not narrower than, the reference's read→write window.  A
+        not-applied answer carries the row's stage, which drives the reference's skip paths
+        (no row / finished / ToRunning on a RUNNING row).  The price is a Paxos round (~4
+        replica round trips, serialised per partition; ``compat.fused-write: auto`` uses it
+        only under HA — docs/ARCHITECTURE.md "Pricing the LWT").  Returns None for a stage
+        outside the known set (custom stage strings): the two-step path then decides with
+        that stage in its guard."""
         wall = self.wall
         compat = self.cfg.compat
         stamps = r.stamps
