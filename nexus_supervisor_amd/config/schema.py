@@ -34,37 +34,42 @@ CQL_STORE_TYPES = (CQL_STORE_ASTRA, CQL_STORE_SCYLLA, CQL_STORE_MEMORY)
 class AstraBundleConfig:
     """``request.AstraBundleConfig`` (``/root/reference/appconfig.local.yaml:1-4``)."""
 
+    # Astra secure-connect zip, base64
     secure_connection_bundle_base64: str = field(default="", metadata=_k("secure-connection-bundle-base64", secret=True))
-    gateway_user: str = field(default="", metadata=_k("gateway-user"))
-    gateway_password: str = field(default="", metadata=_k("gateway-password", secret=True))
+    gateway_user: str = field(default="", metadata=_k("gateway-user"))  # Astra token client id
+    gateway_password: str = field(default="", metadata=_k("gateway-password", secret=True))  # Astra token secret
     # extensions
-    keyspace: str = field(default="nexus", metadata=_k("keyspace"))
-    table: str = field(default="checkpoints", metadata=_k("table"))
+    keyspace: str = field(default="nexus", metadata=_k("keyspace"))  # keyspace of the checkpoints table
+    table: str = field(default="checkpoints", metadata=_k("table"))  # checkpoints table (nexus-core schema)
+    # consistency of reads and writes; conditional writes use the matching SERIAL level
     consistency: str = field(default="LOCAL_QUORUM", metadata=_k("consistency"))
-    request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))
+    request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))  # per CQL request
 
 
 @dataclass
 class ScyllaCqlStoreConfig:
     """``request.ScyllaCqlStoreConfig`` (``/root/reference/appconfig.local.yaml:5-10``)."""
 
-    hosts: List[str] = field(default_factory=list, metadata=_k("hosts", "list"))
-    port: int = field(default=9042, metadata=_k("port"))
-    user: str = field(default="", metadata=_k("user"))
-    password: str = field(default="", metadata=_k("password", secret=True))
-    local_dc: str = field(default="", metadata=_k("local-dc"))
+    hosts: List[str] = field(default_factory=list, metadata=_k("hosts", "list"))  # contact points
+    port: int = field(default=9042, metadata=_k("port"))  # native protocol port
+    user: str = field(default="", metadata=_k("user"))  # PasswordAuthenticator user; empty = no auth
+    password: str = field(default="", metadata=_k("password", secret=True))  # PasswordAuthenticator password
+    local_dc: str = field(default="", metadata=_k("local-dc"))  # DC-aware routing: prefer this DC's nodes
     # extensions
-    keyspace: str = field(default="nexus", metadata=_k("keyspace"))
-    table: str = field(default="checkpoints", metadata=_k("table"))
+    keyspace: str = field(default="nexus", metadata=_k("keyspace"))  # keyspace of the checkpoints table
+    table: str = field(default="checkpoints", metadata=_k("table"))  # checkpoints table (nexus-core schema)
+    # consistency of reads and writes; conditional writes use the matching SERIAL level
     consistency: str = field(default="LOCAL_QUORUM", metadata=_k("consistency"))
+    # connections per node when the node is not sharded (or shard-aware is off)
     connections_per_host: int = field(default=2, metadata=_k("connections-per-host"))
-    request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))
-    connect_timeout: float = field(default=5.0, metadata=_k("connect-timeout", "duration"))
+    request_timeout: float = field(default=5.0, metadata=_k("request-timeout", "duration"))  # per CQL request
+    connect_timeout: float = field(default=5.0, metadata=_k("connect-timeout", "duration"))  # TCP + STARTUP
+    # send each statement to a replica owning its partition token (ring from system.peers)
     token_aware: bool = field(default=True, metadata=_k("token-aware"))
     # Scylla shard-aware routing (scylladb/gocql fork, /root/reference/go.mod:93): one
     # connection per shard through the shard-aware port, requests to the owning shard
     shard_aware: bool = field(default=True, metadata=_k("shard-aware"))
-    connections_per_shard: int = field(default=1, metadata=_k("connections-per-shard"))
+    connections_per_shard: int = field(default=1, metadata=_k("connections-per-shard"))  # with shard-aware
 
 
 @dataclass
@@ -116,7 +121,10 @@ class LabelConfig:
 class RulesConfig:
     """Classifier extensions beyond the reference decision table (SURVEY §2.9.1 gaps)."""
 
+    # also classify Event *updates* (repeat counts), not only adds (the reference: adds only)
     handle_event_updates: bool = field(default=True, metadata=_k("handle-event-updates"))
+    # classify pod status (OOMKilled, HIP OOM, image pull, config errors, crash loops) beyond
+    # the reference's event table
     pod_status_rules: bool = field(default=True, metadata=_k("pod-status-rules"))
     # Evicted pods: "fail" the run immediately, or "observe" (record evidence, let the
     # Job controller retry and enrich the terminal Job event)
@@ -136,13 +144,17 @@ class RulesConfig:
 class GpuConfig:
     """MI355X attribution (north star in BASELINE.json)."""
 
+    # enrich failing GPU decisions with GPU evidence, RCCL/xGMI topology and the OOM verdict
     attribution_enabled: bool = field(default=True, metadata=_k("attribution-enabled"))
-    hbm_capacity_gb: float = field(default=288.0, metadata=_k("hbm-capacity-gb"))
+    hbm_capacity_gb: float = field(default=288.0, metadata=_k("hbm-capacity-gb"))  # per GPU (MI355X: 288)
+    # a pod's own VRAM peak at or above this share of capacity, with a failed exit, is HBM OOM
     hbm_oom_fraction: float = field(default=0.97, metadata=_k("hbm-oom-fraction"))
+    # pod annotation the node agent writes its GPU evidence to
     evidence_annotation: str = field(default="nexus.amd.com/gpu-evidence", metadata=_k("evidence-annotation"))
+    # extended resource that marks a GPU pod
     gpu_resource_name: str = field(default="amd.com/gpu", metadata=_k("gpu-resource-name"))
     backend: str = field(default="auto", metadata=_k("backend"))  # auto | amdsmi | fake | none
-    sample_interval: float = field(default=0.5, metadata=_k("sample-interval", "duration"))
+    sample_interval: float = field(default=0.5, metadata=_k("sample-interval", "duration"))  # amd-smi VRAM sampling
     # read GPUs of the node this process runs on (in-node supervisor / bench); the cluster
     # deployment instead reads the node agents' pod annotations
     local_telemetry: bool = field(default=False, metadata=_k("local-telemetry"))
@@ -157,8 +169,9 @@ class GpuConfig:
     # else the supervisor GETs pods/<pod>/log (RBAC pods/log get); api — always the API;
     # node — the agent's reading only; off — never look at logs
     log_tail: str = field(default="auto", metadata=_k("log-tail"))
+    # longest a decision waits for an outstanding log-tail fetch
     log_tail_timeout: float = field(default=2.0, metadata=_k("log-tail-timeout", "duration"))
-    log_tail_bytes: int = field(default=65536, metadata=_k("log-tail-bytes"))
+    log_tail_bytes: int = field(default=65536, metadata=_k("log-tail-bytes"))  # limitBytes of a tail
 
 
 @dataclass
@@ -193,12 +206,18 @@ class StagesConfig:
 
 @dataclass
 class LeaderElectionConfig:
+    """Lease-based active/standby (``ha/leader.py``); the timings also drive shard leases."""
+
+    # one active replica holds a coordination.k8s.io Lease; standbys keep warm caches
     enabled: bool = field(default=False, metadata=_k("enabled"))
-    lease_name: str = field(default="nexus-supervisor-leader", metadata=_k("lease-name"))
+    lease_name: str = field(default="nexus-supervisor-leader", metadata=_k("lease-name"))  # Lease object name
+    # how long a Lease stays held without renewal before another replica may take it
     lease_duration: float = field(default=15.0, metadata=_k("lease-duration", "duration"))
+    # the holder stops acting this long after its last successful renewal *started* (bounded
+    # renewals + a watchdog), so a partitioned holder stops before anyone can take over
     renew_deadline: float = field(default=10.0, metadata=_k("renew-deadline", "duration"))
-    retry_period: float = field(default=2.0, metadata=_k("retry-period", "duration"))
-    identity: str = field(default="", metadata=_k("identity"))
+    retry_period: float = field(default=2.0, metadata=_k("retry-period", "duration"))  # renew / acquire interval
+    identity: str = field(default="", metadata=_k("identity"))  # holder identity; empty = pod name
 
 
 @dataclass
@@ -210,8 +229,8 @@ class ShardingConfig:
     each replica holds up to its fair share ``ceil(shards / replicas)`` and takes over any
     shard left unheld for a full lease duration, so shards fail over individually."""
 
-    shards: int = field(default=1, metadata=_k("shards"))
-    shard_index: int = field(default=0, metadata=_k("shard-index"))
+    shards: int = field(default=1, metadata=_k("shards"))  # runs split into this many shards; 1 = off
+    shard_index: int = field(default=0, metadata=_k("shard-index"))  # static mode: the shard this replica owns
     mode: str = field(default="static", metadata=_k("mode"))  # static | lease
     # expected replica count (Helm replicaCount) for the lease-mode fair share; 0 = greedy
     replicas: int = field(default=0, metadata=_k("replicas"))
@@ -225,8 +244,8 @@ class RuntimeConfig:
     # permanent generation so full collections stop re-traversing 10k cached runs
     gc_freeze: bool = field(default=True, metadata=_k("gc-freeze"))
     gc_threshold0: int = field(default=200000, metadata=_k("gc-threshold0"))  # CPython default 700
-    gc_threshold1: int = field(default=20, metadata=_k("gc-threshold1"))
-    gc_threshold2: int = field(default=20, metadata=_k("gc-threshold2"))
+    gc_threshold1: int = field(default=20, metadata=_k("gc-threshold1"))  # CPython default 10
+    gc_threshold2: int = field(default=20, metadata=_k("gc-threshold2"))  # CPython default 10
     gc_refreeze_interval: float = field(default=600.0, metadata=_k("gc-refreeze-interval", "duration"))  # 0 = never
     # process-per-core runtime: this many shard-worker processes, each owning the runs whose
     # job name hashes to it (informers filter at ingest), under one coordinating parent that
@@ -242,10 +261,12 @@ class RuntimeConfig:
 
 @dataclass
 class ObservabilityConfig:
+    # DogStatsD metric namespace (the reference: nexus_receiver)
     statsd_name: str = field(default="nexus_supervisor", metadata=_k("statsd-name"))
     http_port: int = field(default=0, metadata=_k("http-port"))  # /metrics /healthz /readyz /debug/pprof; 0 = off
-    http_host: str = field(default="0.0.0.0", metadata=_k("http-host"))
-    profiler_hz: int = field(default=97, metadata=_k("profiler-hz"))
+    http_host: str = field(default="0.0.0.0", metadata=_k("http-host"))  # bind address of the HTTP endpoints
+    profiler_hz: int = field(default=97, metadata=_k("profiler-hz"))  # /debug/pprof sampling rate
+    # per-decision stage timestamps -> stage_classify/queue/read/write/delete histograms
     stage_timestamps: bool = field(default=True, metadata=_k("stage-timestamps"))
 
 
@@ -255,20 +276,22 @@ class SupervisorConfig:
 
     astra_cql_store: AstraBundleConfig = field(default_factory=AstraBundleConfig, metadata=_k("astra-cql-store"))
     scylla_cql_store: ScyllaCqlStoreConfig = field(default_factory=ScyllaCqlStoreConfig, metadata=_k("scylla-cql-store"))
-    cql_store_type: str = field(default=CQL_STORE_ASTRA, metadata=_k("cql-store-type"))
-    kube_config_path: str = field(default="", metadata=_k("kube-config-path"))
-    resource_namespace: str = field(default="nexus", metadata=_k("resource-namespace"))
-    log_level: str = field(default="INFO", metadata=_k("log-level"))
+    cql_store_type: str = field(default=CQL_STORE_ASTRA, metadata=_k("cql-store-type"))  # astra | scylla | memory
+    kube_config_path: str = field(default="", metadata=_k("kube-config-path"))  # empty = in-cluster service account
+    resource_namespace: str = field(default="nexus", metadata=_k("resource-namespace"))  # namespace of the runs' Jobs
+    log_level: str = field(default="INFO", metadata=_k("log-level"))  # DEBUG | INFO | WARN | ERROR
+    # first retry backoff of a run
     failure_rate_base_delay: float = field(default=0.1, metadata=_k("failure-rate-base-delay", "duration"))
-    failure_rate_max_delay: float = field(default=1.0, metadata=_k("failure-rate-max-delay", "duration"))
+    failure_rate_max_delay: float = field(default=1.0, metadata=_k("failure-rate-max-delay", "duration"))  # backoff cap
+    # token bucket; 0 = uncapped
     rate_limit_elements_per_second: float = field(default=10, metadata=_k("rate-limit-elements-per-second", "number"))
-    rate_limit_elements_burst: int = field(default=100, metadata=_k("rate-limit-elements-burst"))
-    workers: int = field(default=2, metadata=_k("workers"))
+    rate_limit_elements_burst: int = field(default=100, metadata=_k("rate-limit-elements-burst"))  # bucket size
+    workers: int = field(default=2, metadata=_k("workers"))  # concurrent decisions per replica
     # ---- extensions ----
-    resync_period: float = field(default=30.0, metadata=_k("resync-period", "duration"))
+    resync_period: float = field(default=30.0, metadata=_k("resync-period", "duration"))  # informer resync
     # server-side label selector on the Pod/Job informers (only Nexus runs are cached)
     informer_label_selector: bool = field(default=True, metadata=_k("informer-label-selector"))
-    watch_timeout: float = field(default=300.0, metadata=_k("watch-timeout", "duration"))
+    watch_timeout: float = field(default=300.0, metadata=_k("watch-timeout", "duration"))  # server-side watch timeout
     max_retries: int = field(default=16, metadata=_k("max-retries"))  # 0 = retry forever
     # issue the Job DELETE after the checkpoint write without holding a worker (retried
     # in the background with the failure backoff); false = delete inside the worker
