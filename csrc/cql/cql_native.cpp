@@ -360,6 +360,185 @@ py::bytes encode_execute(int16_t stream, const std::string& qid, const py::objec
   return to_frame(stream, OP_EXECUTE, w.buf);
 }
 
+// ---------------------------------------------------------------- EXECUTE fast path
+// encode_execute_fast(stream, query_id: bytes, values: list|tuple, codes: bytes, consistency,
+//                     skip_metadata, serial) -> bytes | NotImplemented
+// The two statements of every decision (status read, owned-columns write) bind only scalar
+// columns.  ``codes`` holds one CQL type id per bind marker (precomputed at prepare time);
+// strings are written from CPython's cached UTF-8 buffer and the frame is built in one
+// buffer (pybind's 10-argument dispatch, per-call type vector and three copies of the
+// ~2 KB trace were ~2/3 of encode_execute's cost).  Anything outside the scalar set, or a
+// value of an unexpected Python type, answers NotImplemented: the caller uses encode_execute.
+namespace {
+
+struct Buf {
+  std::string s;
+  void u8(uint8_t v) { s.push_back(static_cast<char>(v)); }
+  void u16(uint16_t v) {
+    char b[2] = {static_cast<char>(v >> 8), static_cast<char>(v)};
+    s.append(b, 2);
+  }
+  void i32(int32_t v) {
+    uint32_t u = static_cast<uint32_t>(v);
+    char b[4] = {static_cast<char>(u >> 24), static_cast<char>(u >> 16), static_cast<char>(u >> 8), static_cast<char>(u)};
+    s.append(b, 4);
+  }
+  void i64(int64_t v) {
+    uint64_t u = static_cast<uint64_t>(v);
+    char b[8];
+    for (int i = 7; i >= 0; --i) {
+      b[i] = static_cast<char>(u);
+      u >>= 8;
+    }
+    s.append(b, 8);
+  }
+};
+
+// 1 = written, 0 = not handled (caller falls back), -1 = Python error set
+int fast_value(Buf& w, PyObject* v, uint8_t code) {
+  if (v == Py_None) {
+    w.i32(-1);
+    return 1;
+  }
+  switch (code) {
+    case T_VARCHAR:
+    case T_ASCII: {
+      Py_ssize_t n;
+      const char* p;
+      if (PyUnicode_Check(v)) {
+        p = PyUnicode_AsUTF8AndSize(v, &n);
+        if (!p) return -1;
+      } else if (PyBytes_Check(v)) {
+        p = PyBytes_AS_STRING(v);
+        n = PyBytes_GET_SIZE(v);
+      } else {
+        return 0;
+      }
+      w.i32(static_cast<int32_t>(n));
+      w.s.append(p, static_cast<size_t>(n));
+      return 1;
+    }
+    case T_BLOB:
+      if (!PyBytes_Check(v)) return 0;
+      w.i32(static_cast<int32_t>(PyBytes_GET_SIZE(v)));
+      w.s.append(PyBytes_AS_STRING(v), static_cast<size_t>(PyBytes_GET_SIZE(v)));
+      return 1;
+    case T_BIGINT:
+    case T_COUNTER:
+    case T_TIME:
+    case T_INT:
+    case T_TIMESTAMP: {
+      int64_t x;
+      if (PyLong_Check(v) && !PyBool_Check(v)) {
+        x = PyLong_AsLongLong(v);
+        if (x == -1 && PyErr_Occurred()) return -1;
+      } else if (code == T_TIMESTAMP && PyFloat_Check(v)) {
+        x = static_cast<int64_t>(std::llround(PyFloat_AS_DOUBLE(v) * 1000.0));
+      } else if (code == T_TIMESTAMP) {
+        PyObject* r = PyObject_CallMethod(v, "timestamp", nullptr);  // datetime
+        if (!r) {
+          PyErr_Clear();
+          return 0;
+        }
+        double s = PyFloat_AsDouble(r);
+        Py_DECREF(r);
+        if (s == -1.0 && PyErr_Occurred()) return -1;
+        x = static_cast<int64_t>(std::llround(s * 1000.0));
+      } else {
+        return 0;
+      }
+      if (code == T_INT) {
+        if (x < INT32_MIN || x > INT32_MAX) return 0;
+        w.i32(4);
+        w.i32(static_cast<int32_t>(x));
+      } else {
+        w.i32(8);
+        w.i64(x);
+      }
+      return 1;
+    }
+    case T_BOOLEAN: {
+      if (!PyBool_Check(v)) return 0;
+      w.i32(1);
+      w.u8(v == Py_True ? 1 : 0);
+      return 1;
+    }
+    case T_DOUBLE: {
+      if (!PyFloat_Check(v) && !PyLong_Check(v)) return 0;
+      double d = PyFloat_AsDouble(v);
+      if (d == -1.0 && PyErr_Occurred()) return -1;
+      int64_t bits;
+      memcpy(&bits, &d, 8);
+      w.i32(8);
+      w.i64(bits);
+      return 1;
+    }
+    default: return 0;
+  }
+}
+
+PyObject* encode_execute_fast(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 7) {
+    PyErr_SetString(PyExc_TypeError, "encode_execute_fast(stream, query_id, values, codes, consistency, skip, serial)");
+    return nullptr;
+  }
+  long stream = PyLong_AsLong(args[0]);
+  if (stream == -1 && PyErr_Occurred()) return nullptr;
+  PyObject* qid = args[1];
+  PyObject* values = args[2];
+  PyObject* codes = args[3];
+  long consistency = PyLong_AsLong(args[4]);
+  if (consistency == -1 && PyErr_Occurred()) return nullptr;
+  int skip = PyObject_IsTrue(args[5]);
+  if (skip < 0) return nullptr;
+  PyObject* serial = args[6];
+  if (!PyBytes_Check(qid) || !PyBytes_Check(codes) || !(PyList_Check(values) || PyTuple_Check(values))) Py_RETURN_NOTIMPLEMENTED;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(values);
+  if (n != PyBytes_GET_SIZE(codes) || n > 0xFFFF) Py_RETURN_NOTIMPLEMENTED;
+  long serial_cl = 0;
+  if (serial != Py_None) {
+    serial_cl = PyLong_AsLong(serial);
+    if (serial_cl == -1 && PyErr_Occurred()) return nullptr;
+  }
+  PyObject** items = PySequence_Fast_ITEMS(values);
+  const uint8_t* cd = reinterpret_cast<const uint8_t*>(PyBytes_AS_STRING(codes));
+  Buf w;
+  size_t guess = HEADER_LEN + 2 + static_cast<size_t>(PyBytes_GET_SIZE(qid)) + 8 + 16 * static_cast<size_t>(n);
+  for (Py_ssize_t i = 0; i < n; ++i)
+    if (PyUnicode_Check(items[i])) guess += static_cast<size_t>(PyUnicode_GET_LENGTH(items[i]));
+  w.s.reserve(guess + 64);
+  w.s.append(HEADER_LEN, '\0');  // patched below
+  w.u16(static_cast<uint16_t>(PyBytes_GET_SIZE(qid)));
+  w.s.append(PyBytes_AS_STRING(qid), static_cast<size_t>(PyBytes_GET_SIZE(qid)));
+  w.u16(static_cast<uint16_t>(consistency));
+  uint8_t flags = 0;
+  if (n > 0) flags |= QF_VALUES;
+  if (skip) flags |= QF_SKIP_METADATA;
+  if (serial != Py_None) flags |= QF_SERIAL_CONSISTENCY;
+  w.u8(flags);
+  if (n > 0) {
+    w.u16(static_cast<uint16_t>(n));
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      int rc = fast_value(w, items[i], cd[i]);
+      if (rc < 0) return nullptr;
+      if (rc == 0) Py_RETURN_NOTIMPLEMENTED;
+    }
+  }
+  if (serial != Py_None) w.u16(static_cast<uint16_t>(serial_cl));
+  std::string head;
+  write_header(head, VERSION_REQ, 0, static_cast<int16_t>(stream), OP_EXECUTE,
+               static_cast<uint32_t>(w.s.size() - HEADER_LEN));
+  memcpy(&w.s[0], head.data(), HEADER_LEN);
+  return PyBytes_FromStringAndSize(w.s.data(), static_cast<Py_ssize_t>(w.s.size()));
+}
+
+PyMethodDef g_fast_defs[] = {
+    {"encode_execute_fast", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(encode_execute_fast)),
+     METH_FASTCALL, "EXECUTE frame for scalar bind values (NotImplemented: use encode_execute)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+}  // namespace
+
 // statements: iterable of (kind, query_or_id, values, types) with kind 0 = query string, 1 = prepared id.
 py::bytes encode_batch(int16_t stream, uint8_t batch_type, const py::object& statements, uint16_t consistency,
                        const py::object& serial, const py::object& timestamp) {
@@ -668,6 +847,11 @@ PYBIND11_MODULE(_cql_native, m) {
   m.doc() = "CQL native protocol v4 codec + Cassandra Murmur3 tokens (native core of the checkpoint store client)";
   m.attr("HEADER_LEN") = HEADER_LEN;
   m.def("set_timestamp_factory", [](py::object f) { g_ts_factory = std::move(f); });
+  {
+    PyObject* f = PyCFunction_NewEx(&g_fast_defs[0], nullptr, m.attr("__name__").ptr());
+    if (!f) throw py::error_already_set();
+    m.add_object("encode_execute_fast", py::reinterpret_steal<py::object>(f));
+  }
   m.def("murmur3_token", &token_of, "Murmur3Partitioner token of a routing key");
   m.def("murmur3_h1", &h1_of, "Raw MurmurHash3_x64_128 h1 (Cassandra variant, no normalisation)");
   m.def("routing_key", &routing_key, "Composite routing key of partition-key components");

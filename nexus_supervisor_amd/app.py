@@ -168,6 +168,9 @@ class _SupervisorFacade:
         self._app = app
         self.namespace = app.cfg.resource_namespace
         self.decision_hooks = app.pool.decision_hooks
+        # (request_id, outcome, ack_mono, stage) per reported decision, without building the
+        # result/decision objects (the bench tracker: harness work stays out of the parent's CPU)
+        self.report_hooks = app.pool.report_hooks
         self.classifier = type("RemoteClassifier", (), {"evidence_provider": None})()
 
     @property

@@ -89,14 +89,16 @@ class Tracker:
         self.record = False
 
     def __call__(self, d: Decision):
-        rid = d.result.request_id
+        self.report(d.result.request_id, d.outcome, d.result.stamps.get("ack_mono"), d.new_stage)
+
+    def report(self, rid: str, outcome: str, ack: Optional[float], stage: Optional[str]) -> None:
         # the metric is pod-fail → checkpoint *write ack* (the Job DELETE follows the write)
-        t = d.result.stamps.get("ack_mono") or time.monotonic()
+        t = ack or time.monotonic()
         st = self.owner.pop(rid, None)
         if st is None:
-            self.acks[rid] = (t, d.outcome, d.new_stage)  # ack raced ahead of the step response
+            self.acks[rid] = (t, outcome, stage)  # ack raced ahead of the step response
             return
-        st.settle(self, rid, t, d.outcome, d.new_stage)
+        st.settle(self, rid, t, outcome, stage)
 
     def arm(self, rids: List[str], t_push: float, expected: Optional[Dict[str, str]] = None) -> "StepState":
         st = StepState(set(rids), t_push, self.record, expected or {})
@@ -211,7 +213,10 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         await harness.start()
         sup = harness.supervisor
         sup.classifier.evidence_provider = pod_evidence_provider(telemetry)
-        sup.decision_hooks.append(tracker)
+        if hasattr(sup, "report_hooks"):  # worker processes: their decision reports as plain tuples
+            sup.report_hooks.append(tracker.report)
+        else:
+            sup.decision_hooks.append(tracker)
 
         done_at: List[float] = []  # completion time of each timed step (diagnostics)
 

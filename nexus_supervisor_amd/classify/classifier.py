@@ -547,6 +547,11 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto", max_bytes: int
         doc["topology"] = dict(topo, xgmi=_raw_json(xgmi))
     # key order is the (deterministic) construction order: sorting every object doubled the
     # cost of the largest per-decision serialisation (profiles/r2_*_pprof_*)
+    if _native_dumps is not None:
+        raw = _native_dumps(doc, default=str)  # UTF-8 bytes: the cap is measured without re-encoding
+        if max_bytes and len(raw) > max_bytes:
+            return _trim_trace(doc, max_bytes)
+        return raw.decode()
     out = _dumps(doc)
     if max_bytes and len(out.encode()) > max_bytes:
         out = _trim_trace(doc, max_bytes)

@@ -29,6 +29,8 @@ import os
 import re
 from typing import Any, Dict, List, Optional, Tuple
 
+from ..models import kube
+
 from . import oom
 
 LOG_ROOT = "/var/log/pods"
@@ -133,8 +135,6 @@ def failed_containers(pod: Dict[str, Any]) -> List[Dict[str, Any]]:
     message *is* the log's last words).  ``restart`` is the instance's log file number
     (``state`` → restartCount, ``lastState`` → restartCount − 1); ``previous`` is what
     the pods/log API needs to reach that instance."""
-    from ..models import kube
-
     out = []
     for cs in kube.container_statuses(pod):
         rc = int(cs.get("restartCount") or 0)
@@ -154,8 +154,6 @@ def failed_containers(pod: Dict[str, Any]) -> List[Dict[str, Any]]:
 def node_log_evidence(root: str, pod: Dict[str, Any], max_bytes: int = TAIL_BYTES) -> List[Dict[str, Any]]:
     """Node-agent reader: one record per failed container (``match`` None when the tail
     was read and carries no signature — the supervisor then need not fetch it again)."""
-    from ..models import kube
-
     ns, name, uid = kube.namespace_of(pod), kube.name_of(pod), kube.uid_of(pod)
     out = []
     for fc in failed_containers(pod):

@@ -41,6 +41,8 @@ import re
 from dataclasses import dataclass, field
 from typing import Any, Dict, Iterable, List, Optional, Tuple
 
+from .topology import physical_gpu
+
 HBM_PATTERNS = [
     re.compile(r"hipErrorOutOfMemory", re.I),
     re.compile(r"\bHIP out of memory", re.I),
@@ -138,7 +140,6 @@ def analyze(
 ) -> OomVerdict:
     """``texts``: strings (a termination / event / condition message) or ``(source, text)``
     pairs (container log tails, :mod:`.logtail`) — every signal names where it was found."""
-    from .topology import physical_gpu
 
     v = OomVerdict()
     sourced: List[Tuple[str, str]] = []

@@ -23,7 +23,8 @@ import threading
 import time
 from typing import Any, Dict, Iterable, List, Optional
 
-from .topology import _int
+from ..models import kube
+from .topology import _int, physical_gpu, topology_from_pod
 
 ATTRIBUTION_EVENTS = ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET", "GPU_POST_RESET", "THERMAL_THROTTLE",
                       "ECC_UNCORRECTABLE", "XGMI_LINK_DOWN", "XGMI_ERROR")
@@ -490,9 +491,6 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
     """Classifier hook (``Classifier.evidence_provider``): live evidence for a pod from a
     co-located telemetry backend, matched by pod UID (cgroup) or the pod's expected GPU
     (``visible_devices[local_rank]`` from its env)."""
-    from ..models import kube
-    from .topology import topology_from_pod
-
     cache: Dict[str, Any] = {"t": -1.0, "snap": None, "by_uid": {}, "by_index": {}, "memo": {}}
     ttl = max(0.005, telemetry.interval / 2)  # the native sampler cannot have anything newer
 
@@ -542,13 +540,32 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
     return provider
 
 
+_POD_GPUS_MEMO: Dict[Any, List[int]] = {}
+
+
 def _pod_gpus(topo: Dict[str, Any], snap: Iterable[Dict[str, Any]] = ()) -> List[int]:
     """Physical GPUs a pod's env points at: the rank's expected device, else every visible
-    device; UUID entries resolved against the telemetry snapshot."""
-    from .topology import physical_gpu
-
+    device; UUID entries resolved against the telemetry snapshot.  Memoised when the device
+    chain is plain indices (then the snapshot plays no part): every rank of a template on
+    a node asks the same question."""
     lr = topo.get("local_rank")
     devs = topo.get("visible_devices") or []
+    chain = topo.get("device_chain")
+    key = None
+    if chain is not None and all(x.isdigit() for _v, sel in chain for x in sel):
+        key = (lr, tuple(tuple(sel) for _v, sel in chain))
+        hit = _POD_GPUS_MEMO.get(key)
+        if hit is not None:
+            return hit
+    out = _pod_gpus_of(topo, lr, devs, snap)
+    if key is not None:
+        if len(_POD_GPUS_MEMO) > 1024:
+            _POD_GPUS_MEMO.clear()
+        _POD_GPUS_MEMO[key] = out
+    return out
+
+
+def _pod_gpus_of(topo, lr, devs, snap) -> List[int]:
     out = []
     if devs and lr is not None and 0 <= lr < len(devs):
         p = physical_gpu(topo, lr, snap)

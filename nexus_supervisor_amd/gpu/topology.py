@@ -59,18 +59,24 @@ def topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str = 
     """:func:`_topology_from_env`, memoised on the variables it reads except ``MASTER_ADDR``
     (unique per run; re-attached to a shallow copy).  Every run of a job template on a
     node folds the same rank/device/collective env: the fold is done once.  The result
-    is shared and must not be mutated (callers build new dicts, as everywhere here)."""
-    key = (tuple(sorted((k, v) for k, v in env.items()
-                        if k != "MASTER_ADDR" and (k in _READ_VARS or k.startswith(COLLECTIVE_PREFIXES)))),
-           gpus_requested, node)
+    is shared and must not be mutated (callers build new dicts, as everywhere here).
+
+    The memo key is the env's items in document order (C-level copy, no sort or filter:
+    one job template always lists its variables in the same order, and a variable the
+    fold does not read only splits the memo, it cannot change a result)."""
+    addr = env.get("MASTER_ADDR")
+    if addr is not None:
+        env = env.copy()
+        del env["MASTER_ADDR"]
+    key = (tuple(env.items()), gpus_requested, node)
     topo = _ENV_MEMO.get(key)
     if topo is None:
         if len(_ENV_MEMO) > 4096:
             _ENV_MEMO.clear()
-        topo = _ENV_MEMO[key] = _topology_from_env({k: v for k, v in key[0]}, gpus_requested, node)
-    addr = env.get("MASTER_ADDR")
+        topo = _ENV_MEMO[key] = _topology_from_env(
+            {k: v for k, v in key[0] if k in _READ_VARS or k.startswith(COLLECTIVE_PREFIXES)}, gpus_requested, node)
     if addr:
-        return dict(topo, master_addr=addr) if topo else _topology_from_env(env, gpus_requested, node)
+        return dict(topo, master_addr=addr) if topo else _topology_from_env({"MASTER_ADDR": addr}, gpus_requested, node)
     return topo
 
 

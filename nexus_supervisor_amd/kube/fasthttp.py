@@ -47,6 +47,9 @@ class _Conn(asyncio.Protocol):
         self.pool = pool
         self.transport: Optional[asyncio.Transport] = None
         self.waiting: Deque[asyncio.Future] = collections.deque()
+        # (deadline, method, path) of each request_nowait in ``waiting`` order (None for a
+        # request() with its own timer): FIFO on one connection, so the head expires first
+        self.deadlines: Deque[Optional[Tuple[float, str, str]]] = collections.deque()
         self.buf = bytearray()
         self.out: List[bytes] = []
         self.flush_scheduled = False
@@ -66,6 +69,7 @@ class _Conn(asyncio.Protocol):
     def connection_lost(self, exc):
         self.closed = True
         err = HttpError(f"connection lost: {exc}")
+        self.deadlines.clear()
         while self.waiting:
             f = self.waiting.popleft()
             if not f.done():
@@ -123,6 +127,7 @@ class _Conn(asyncio.Protocol):
             del buf[: self._need]
         self._in_body = False
         fut = self.waiting.popleft()
+        self.deadlines.popleft()
         if not fut.done():
             fut.set_result((self._status, bytes(self._body)))
         if self._headers.get("connection", "").lower() == "close":
@@ -130,6 +135,7 @@ class _Conn(asyncio.Protocol):
         return True
 
     def _fail(self, exc: Exception) -> None:
+        self.deadlines.clear()
         while self.waiting:
             f = self.waiting.popleft()
             if not f.done():
@@ -138,8 +144,9 @@ class _Conn(asyncio.Protocol):
             self.transport.close()
 
     # ----------------------------------------------------------- sending
-    def send(self, data: bytes, fut: asyncio.Future) -> None:
+    def send(self, data: bytes, fut: asyncio.Future, deadline: Optional[Tuple[float, str, str]] = None) -> None:
         self.waiting.append(fut)
+        self.deadlines.append(deadline)
         self.out.append(data)
         if not self.flush_scheduled:
             self.flush_scheduled = True
@@ -169,6 +176,8 @@ class PipelinedHttp:
         self._conns: List[_Conn] = []
         self._connecting: Optional[asyncio.Future] = None
         self.requests = 0
+        self._head_cache: Dict[Tuple, bytes] = {}
+        self._sweeper: Optional[asyncio.TimerHandle] = None
 
     def _drop(self, c: _Conn) -> None:
         if c in self._conns:
@@ -226,20 +235,51 @@ class PipelinedHttp:
             return None
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
-        best.send(self._encode(method, path, body, headers), fut)
+        # no timer per request: the deadline rides with the request and one sweep per pool
+        # fails an expired head of line (a TimerHandle + done-callback per DELETE was ~1 %
+        # of a shard worker's CPU)
+        best.send(self._encode(method, path, body, headers), fut, (loop.time() + self.timeout, method, path))
         self.requests += 1
-        timer = loop.call_later(self.timeout, _expire_and_reset, fut, best, f"{method} {path}")
-        fut.add_done_callback(lambda _f, t=timer: t.cancel())
+        if self._sweeper is None:
+            self._arm_sweep(loop)
         return fut
 
+    def _arm_sweep(self, loop) -> None:
+        self._sweeper = loop.call_later(min(1.0, max(self.timeout / 4, 0.005)), self._sweep)
+
+    def _sweep(self) -> None:
+        """Fail the connections whose oldest pipelined request is past its deadline (the
+        response order on them is unknown from then on), re-arm while any is pending."""
+        self._sweeper = None
+        loop = asyncio.get_running_loop()
+        now = loop.time()
+        pending = False
+        for c in list(self._conns):
+            dl = c.deadlines
+            if dl and dl[0] is not None and dl[0][0] <= now:  # None: a request() with its own timer
+                _, method, path = dl[0]
+                _expire_and_reset(c.waiting[0], c, f"{method} {path}")
+            if c.waiting:
+                pending = True
+        if pending:
+            self._arm_sweep(loop)
+
     def _encode(self, method: str, path: str, body: Optional[bytes], headers: Optional[Dict[str, str]]) -> bytes:
-        h = dict(self.default_headers)
-        if headers:
-            h.update(headers)
-        lines = [f"{method} {path} HTTP/1.1", f"Host: {self.hostport}"]
-        lines += [f"{k}: {v}" for k, v in h.items()]
-        lines.append(f"Content-Length: {len(body) if body else 0}")
-        return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1") + (body or b"")
+        """Request bytes; the header block (Host, default and per-call headers) is encoded
+        once per distinct header set."""
+        key = tuple(headers.items()) if headers else ()
+        head = self._head_cache.get(key)
+        if head is None:
+            h = dict(self.default_headers)
+            if headers:
+                h.update(headers)
+            lines = [f"Host: {self.hostport}"] + [f"{k}: {v}" for k, v in h.items()]
+            head = ("\r\n".join(lines) + "\r\nContent-Length: ").encode("latin-1")
+            if len(self._head_cache) > 64:
+                self._head_cache.clear()
+            self._head_cache[key] = head
+        return b"%s %s HTTP/1.1\r\n%s%d\r\n\r\n%s" % (method.encode(), path.encode("latin-1"), head,
+                                                              len(body) if body else 0, body or b"")
 
     async def request(self, method: str, path: str, body: Optional[bytes] = None,
                       headers: Optional[Dict[str, str]] = None) -> Tuple[int, bytes]:
@@ -260,6 +300,9 @@ class PipelinedHttp:
             timer.cancel()
 
     async def close(self) -> None:
+        if self._sweeper is not None:
+            self._sweeper.cancel()
+            self._sweeper = None
         for c in list(self._conns):
             if c.transport is not None:
                 c.transport.close()

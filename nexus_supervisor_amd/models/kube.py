@@ -193,8 +193,16 @@ def pod_env(pod) -> Dict[str, str]:
 
 
 def gpu_request(pod, resource: str = "amd.com/gpu") -> int:
+    """GPUs the pod's containers ask for (limits, else requests); memoised on the
+    (per-version) spec like :func:`pod_env`."""
+    spec = pod.get("spec")
+    if not spec:
+        return 0
+    memo = spec.get("_gpureq")
+    if memo is not None and memo[0] == resource:
+        return memo[1]
     total = 0
-    for c in (pod.get("spec") or {}).get("containers") or []:
+    for c in spec.get("containers") or []:
         res = c.get("resources") or {}
         v = (res.get("limits") or {}).get(resource) or (res.get("requests") or {}).get(resource)
         if v is not None:
@@ -202,6 +210,7 @@ def gpu_request(pod, resource: str = "amd.com/gpu") -> int:
                 total += int(str(v))
             except ValueError:
                 pass
+    spec["_gpureq"] = (resource, total)
     return total
 
 

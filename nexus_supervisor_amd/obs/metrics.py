@@ -79,6 +79,15 @@ class Metrics:
         if self.statsd is not None:
             self.statsd.timing(name, seconds * 1e3, labels)
 
+    def hist0(self, name: str) -> LatencyHistogram:
+        """The unlabelled series of ``name`` (created when missing), for a caller that records
+        into it directly — only while no DogStatsD sink is attached (``statsd is None``)."""
+        h = self._h0.get(name)
+        if h is None:
+            h = self.hists.setdefault(name, {}).setdefault((), LatencyHistogram())
+            self._h0[name] = h
+        return h
+
     def histogram(self, name: str, labels: Optional[Dict[str, str]] = None) -> Optional[LatencyHistogram]:
         return self.hists.get(name, {}).get(_lk(labels))
 

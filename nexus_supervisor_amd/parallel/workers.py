@@ -297,6 +297,7 @@ class WorkerPool:
         self.log_dir = log_dir
         self.workers: List[_Worker] = [_Worker(i) for i in range(self.count)]
         self.decision_hooks: List[Callable[[Decision], None]] = []
+        self.report_hooks: List[Callable[[str, str, Optional[float], Optional[str]], None]] = []
         self.active = True
         self._mapping = to_mapping(cfg)
         self._metrics_seq = 0
@@ -417,6 +418,9 @@ class WorkerPool:
                 break
             op = msg.get("op")
             if op == "dec":
+                for h in self.report_hooks:
+                    for rid, _alg, outcome, ack, stage in msg["d"]:
+                        h(rid, outcome, ack, stage)
                 if self.decision_hooks:
                     for rid, alg, outcome, ack, stage in msg["d"]:
                         r = RunStatusAnalysisResult("", "", "", request_id=rid, algorithm=alg)

@@ -319,6 +319,19 @@ class PreparedStatement:
     # answer carries the condition's columns, a different shape from the prepared one
     conditional: bool = False
 
+    @property
+    def codes(self) -> Optional[bytes]:
+        """One type-id byte per bind marker when every bind type is a scalar the native fast
+        encoder writes (``encode_execute_fast``), else None (computed once)."""
+        c = self.__dict__.get("_codes", False)
+        if c is False:
+            ok = all(isinstance(t, int) and t in _FAST_CODES for t in self.bind_types)
+            c = self.__dict__["_codes"] = bytes(self.bind_types) if ok else None
+        return c
+
+
+# ascii bigint blob boolean counter double int timestamp varchar time
+_FAST_CODES = frozenset((0x01, 0x02, 0x03, 0x04, 0x05, 0x07, 0x09, 0x0B, 0x0D, 0x12))
 
 _CONDITIONAL = re.compile(r"^\s*(?:UPDATE|INSERT|DELETE)\b.*\bIF\b", re.I | re.S)
 
@@ -438,6 +451,9 @@ class CqlSession:
         self.shard_aware_port = True  # use SCYLLA_SHARD_AWARE_PORT when advertised (falls back per host)
         self._sharded = False  # some node advertised Scylla shards
         self._tokens: Dict[tuple, int] = {}  # partition key values → token (recent)
+        # partition key values → (routing epoch, token, owner host, shard): a decision reads
+        # then writes one partition; the second statement skips ring lookup and shard math
+        self._routes: Dict[tuple, Tuple[Any, int, Host, Optional[int]]] = {}
         self.per_shard = max(1, connections_per_shard)
         self.hosts: Dict[Tuple[str, int], Host] = {}
         self._ring: List[int] = []
@@ -760,11 +776,41 @@ class CqlSession:
         self._tokens[key] = tok
         return tok
 
+    def _route(self, ps: PreparedStatement, values: Sequence[Any]):
+        """(token, owner host, owner shard) of a statement's partition when token-aware
+        routing applies and the owner is up, cached per partition key until a host flips or
+        joins; else ``(token, None, None)`` and :meth:`_candidates` plans as usual."""
+        if not (self.token_aware or self.shard_aware):
+            return None, None, None
+        get = ps._pk_get
+        if get is None:
+            if not ps.pk_indexes:
+                return None, None, None
+            get = ps._pk_get = _pk_getter(ps.pk_indexes)
+        key = get(values)
+        epoch = (_HOST_EPOCH[0], len(self.hosts))
+        hit = self._routes.get(key)
+        if hit is not None and hit[0] == epoch:
+            self.stats["token_routed"] += 1
+            return hit[1], hit[2], hit[3]
+        tok = self.routing_token(ps, values)
+        if tok is None or not (self.token_aware and self._ring):
+            return tok, None, None
+        o = self.owner(tok)
+        if o is None or not o.up:
+            return tok, None, None
+        shard = o.shard_of(tok) if o.nr_shards else None
+        if len(self._routes) > 8192:
+            self._routes.clear()
+        self._routes[key] = (epoch, tok, o, shard)
+        self.stats["token_routed"] += 1
+        return tok, o, shard
+
     async def execute(self, ps_or_query, values: Sequence[Any] = (), *, consistency: Optional[int] = None,
                       serial: Optional[int] = None, idempotent: bool = True, timeout: Optional[float] = None):
         ps = ps_or_query if isinstance(ps_or_query, PreparedStatement) else await self.prepare(ps_or_query)
         cl = self.consistency if consistency is None else consistency
-        token = self.routing_token(ps, values) if self.token_aware or self.shard_aware else None
+        token, owner, owner_shard = self._route(ps, values)
         vals = list(values)
         hint = ps.result_types
         skip = hint is not None and not ps.conditional
@@ -773,13 +819,16 @@ class CqlSession:
         last: Optional[BaseException] = None
         tried: set = _NO_HOSTS  # replaced by a real set on the first failure
         while attempts <= self.max_retries:
-            cands = self._candidates(token)
-            if tried:
-                cands = [h for h in cands if h.address not in tried] or cands
-            if not cands:
-                raise NotSent(f"no CQL host available: {last}")
-            h = cands[0]
-            shard = h.shard_of(token) if h.nr_shards else None
+            if owner is not None and not tried:
+                h, shard = owner, owner_shard  # cached token-aware route (first attempt)
+            else:
+                cands = self._candidates(token)
+                if tried:
+                    cands = [h for h in cands if h.address not in tried] or cands
+                if not cands:
+                    raise NotSent(f"no CQL host available: {last}")
+                h = cands[0]
+                shard = h.shard_of(token) if h.nr_shards else None
             conn = h.pick(shard)
             if conn is None:
                 self._mark_down(h, ConnectionClosed("no live connection"))
@@ -793,9 +842,17 @@ class CqlSession:
             sent = True
             try:
                 qid = ps.query_id
-                r = await conn.request_nowait(
-                    lambda s: N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None),
-                    hint if skip else None, timeout)
+                codes = ps.codes
+                if codes is not None:
+                    def build(s, qid=qid):
+                        out = N.encode_execute_fast(s, qid, vals, codes, cl, skip, serial)
+                        if out is NotImplemented:  # a value of an unexpected Python type
+                            out = N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None)
+                        return out
+                else:
+                    def build(s, qid=qid):
+                        return N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None)
+                r = await conn.request_nowait(build, hint if skip else None, timeout)
             except (ConnectionClosed, OSError) as exc:
                 last = exc
                 self._mark_down(h, exc)

@@ -144,6 +144,7 @@ class Supervisor:
         self.pipeline: Optional[PipelineStage] = None
         self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
         self._applied_cap = 200_000
+        self._hists: Optional[List[Any]] = None  # _observe: the stage histograms, once looked up
         # one conditional write per decision instead of read + write (compat.fused-write);
         # conditional-update: never (the reference's unconditional writes) turns it off
         self._fused = fused_actuation(cfg)
@@ -1018,10 +1019,42 @@ class Supervisor:
         if len(self._applied) > self._applied_cap:
             self._applied.popitem(last=False)
 
+    _STAGE_HISTS = ("event_to_checkpoint", "receive_to_checkpoint", "stage_classify", "stage_queue",
+                    "stage_prepare", "stage_write", "stage_read")
+
     def _observe(self, r: RunStatusAnalysisResult):
         s = r.stamps
         ack = s.get("ack")
         if ack is None:
+            return
+        if self.metrics.statsd is None:
+            # six records per decision straight into the histograms (no name lookups); a
+            # series exists once it has a sample (fused mode has no stage_read)
+            hs = self._hists
+            if hs is None:
+                hs = self._hists = [None] * len(self._STAGE_HISTS)
+            rec = []
+            origin = s.get("origin")
+            if origin is not None:
+                rec.append((0, ack - origin))
+            recv = s.get("receive")
+            if recv is not None:
+                rec.append((1, ack - recv))
+                enq, deq, rd, prep = s.get("enqueue"), s.get("dequeue"), s.get("read"), s.get("prepare")
+                if enq is not None and deq is not None and (rd is not None or prep is not None):
+                    rec.append((2, enq - recv))
+                    rec.append((3, deq - enq))
+                    if prep is not None:
+                        rec.append((4, prep - deq))
+                        rec.append((5, ack - prep))
+                    else:
+                        rec.append((6, rd - deq))
+                        rec.append((5, ack - rd))
+            for i, dt in rec:
+                h = hs[i]
+                if h is None:
+                    h = hs[i] = self.metrics.hist0(self._STAGE_HISTS[i])
+                h.record(dt * 1e6)
             return
         if "origin" in s:
             self.metrics.observe_seconds("event_to_checkpoint", ack - s["origin"])

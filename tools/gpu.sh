@@ -18,6 +18,9 @@
 #   profile[=ARGS]        long pprof bench (${PROF_STEPS:-1200} steps) + merged worker profile
 #   scenarios=IDS         python -m nexus_supervisor_amd.bench.scenarios --only IDS
 #   rocprof               rocprofv3 kernel stats of the HIP stress workload
+#   hotpath[=N]           tools/hotpath_bench.py (one shard worker's CPU per failure, no sockets)
+#                         N rounds, alternating with the _ab/base tree when it exists (A/B)
+#   basebench[=ARGS]      bench.py of the _ab/base tree (A/B against bench)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
@@ -79,6 +82,23 @@ for step in "$@"; do
       ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$GRAFT_REPO_ROOT/gpurun_out/rocprof" -o stress \
           -- "$GRAFT_REPO_ROOT/nexus_supervisor_amd/bin/gpu_stress" hold --gib 32 --seconds 3 ) > gpurun_out/rocprof.log 2>&1 ;;
+    hotpath)
+      mkdir -p gpurun_out/hotpath
+      rc=0
+      for i in $(seq 1 "${val:-3}"); do
+        if [ -d _ab/base ]; then
+          ( cd _ab/base && timeout -k 10 300 python tools/hotpath_bench.py --steps 10 --repeat 1 ) \
+            > "gpurun_out/hotpath/base_$i.json" 2> "gpurun_out/hotpath/base_$i.err" || { rc=$?; break; }
+        fi
+        timeout -k 10 300 python tools/hotpath_bench.py --steps 10 --repeat 1 \
+          > "gpurun_out/hotpath/new_$i.json" 2> "gpurun_out/hotpath/new_$i.err" || { rc=$?; break; }
+      done
+      summary+=("hotpath: $(cat gpurun_out/hotpath/*.json | python -c 'import sys,json; print([json.loads(l)["cpu_us_per_event_median"] for l in sys.stdin if l.strip()])')")
+      [ $rc -eq 0 ] ;;
+    basebench)
+      ( cd _ab/base && timeout -k 10 600 python bench.py --steps "$STEPS_N" --warmup 2 ${val//,/ } ) \
+        > gpurun_out/basebench.log 2> gpurun_out/basebench.err
+      rc=$?; summary+=("basebench: $(tail -1 gpurun_out/basebench.log | cut -c1-240)"); [ $rc -eq 0 ] ;;
     *)
       echo "unknown step $step"; false ;;
   esac
