@@ -90,14 +90,19 @@ def parse_args(argv=None):
 
 def auto_procs(local_world: int) -> int:
     """Shard-worker processes per replica: the rank's CPU share minus 4 (simulated
-    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 8].
-    MI355X (profiles/r3_kubesim_threads_ab, r2_sweep_procs_v16): 12 workers add ~20 %
-    throughput over 8 only by driving the single-threaded apiserver simulator to 0.98
-    (harness-bound: the number is then the simulator's), at +20 % CPU per failure; at 8
-    the supervisor is the bottleneck and the simulator has headroom."""
+    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 6].
+
+    Six is the efficient point: a saturated worker shares every watch
+    frame, socket wakeup and CQL flush among more decisions, so CPU per failure falls as
+    the per-worker load rises.  MI355X box, one box back to back
+    (profiles/r3_cpu_ab/sweep_procs*.json, prof_procs8.json): 6 workers 36.5k/s at
+    158 µs of replica CPU per failure, 7 workers 38.6k/s at 180 µs, 8 workers (profiled)
+    36.8k/s at 187 µs — the apiserver simulator at 0.84–0.94 is the ceiling either way;
+    round 2's sweep found the same (r2_sweep_procs_v16: 6 workers ≈ 12 in throughput at
+    ~40 % less CPU)."""
     from nexus_supervisor_amd.utils.cpus import cpu_share
 
-    return max(1, min(8, int(cpu_share() / max(local_world, 1)) - 4))
+    return max(1, min(6, int(cpu_share() / max(local_world, 1)) - 4))
 
 
 def _harness_bound(cpu) -> dict:

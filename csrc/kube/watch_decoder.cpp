@@ -166,33 +166,34 @@ PyObject* make_str(const char* p, size_t n) {
   return PyUnicode_DecodeUTF8(p, static_cast<Py_ssize_t>(n), "replace");
 }
 
-// Interned Python key strings, looked up by bytes without allocating (open addressing).
+// Interned Python strings (object keys and short repeated values), looked up by bytes
+// without allocating (open addressing).  ONE cache per process, shared by every decoder:
+// the three informers' decoders see the same keys, and a shard worker touches the cache
+// between long stretches of other work, so it must stay small enough to be cache-resident —
+// a slot is (hash, object) and the key bytes are compared against the str's own buffer
+// (8192 slots of hash + std::string + object per decoder were ~1.2 MB per worker).
 class KeyCache {
  public:
   KeyCache() : slots_(kCap) {}
-  ~KeyCache() {
-    for (auto& sl : slots_) Py_XDECREF(sl.obj);
-  }
   // New reference to the Python str for `k`.
   PyObject* get(std::string_view k) {
     uint64_t h = 1469598103934665603ULL;
     for (unsigned char c : k) h = (h ^ c) * 1099511628211ULL;
     size_t i = h & (kCap - 1);
-    for (size_t probe = 0; probe < 16; ++probe, i = (i + 1) & (kCap - 1)) {
+    for (size_t probe = 0; probe < kProbe; ++probe, i = (i + 1) & (kCap - 1)) {
       Slot& sl = slots_[i];
       if (!sl.obj) {
         PyObject* o = make_str(k.data(), k.size());
         if (!o) return nullptr;
-        if (used_ < kCap / 2) {
+        if (used_ < kCap * 3 / 4) {
           sl.hash = h;
-          sl.key.assign(k.data(), k.size());
           sl.obj = o;
           Py_INCREF(o);
           ++used_;
         }
         return o;
       }
-      if (sl.hash == h && sl.key.size() == k.size() && memcmp(sl.key.data(), k.data(), k.size()) == 0) {
+      if (sl.hash == h && same(sl.obj, k)) {
         Py_INCREF(sl.obj);
         return sl.obj;
       }
@@ -201,15 +202,43 @@ class KeyCache {
   }
 
  private:
-  static constexpr size_t kCap = 8192;
+  static bool same(PyObject* o, std::string_view k) {
+    if (PyUnicode_IS_COMPACT_ASCII(o))
+      return static_cast<size_t>(PyUnicode_GET_LENGTH(o)) == k.size() && memcmp(PyUnicode_DATA(o), k.data(), k.size()) == 0;
+    Py_ssize_t n;
+    const char* u = PyUnicode_AsUTF8AndSize(o, &n);
+    if (!u) {
+      PyErr_Clear();
+      return false;
+    }
+    return static_cast<size_t>(n) == k.size() && memcmp(u, k.data(), k.size()) == 0;
+  }
+  static constexpr size_t kCap = 4096;  // 64 KB of slots
+  static constexpr size_t kProbe = 8;
   struct Slot {
     uint64_t hash = 0;
-    std::string key;
     PyObject* obj = nullptr;
   };
   std::vector<Slot> slots_;
   size_t used_ = 0;
 };
+
+KeyCache* shared_keys() {
+  static KeyCache* k = new KeyCache();  // process lifetime (interned strs stay alive)
+  return k;
+}
+
+// Short values worth interning: they repeat across objects ("Pending", "True", label
+// values, env values).  Digit runs (resourceVersions, counts) and RFC 3339 timestamps are
+// unique per object: interning them would fill the shared cache with one-off entries.
+inline bool internable(const char* p, size_t n) {
+  if (n > 24) return false;
+  bool digits = n > 0;
+  for (size_t i = 0; i < n && digits; ++i) digits = p[i] >= '0' && p[i] <= '9';
+  if (digits && n > 2) return false;
+  if (n >= 20 && p[4] == '-' && p[10] == 'T') return false;
+  return true;
+}
 
 struct ParseError {
   const char* msg;
@@ -429,7 +458,7 @@ class Parser {
     if (!esc) {
       // short values repeat across objects ("Pending", "True", "Always", label values):
       // interned like keys, so they cost a lookup instead of an allocation
-      if (b - a <= 24) return keys_->get(std::string_view(s_ + a, b - a));
+      if (internable(s_ + a, b - a)) return keys_->get(std::string_view(s_ + a, b - a));
       return make_str(s_ + a, b - a);
     }
     std::string u = unescape(a, b);
@@ -612,7 +641,7 @@ class Parser {
             }
             int have = PyDict_Contains(d, ko);
             if (have == 0) {  // first definition wins (container env semantics)
-              PyObject* vo = v.size() <= 24 ? keys_->get(v) : make_str(v.data(), v.size());
+              PyObject* vo = internable(v.data(), v.size()) ? keys_->get(v) : make_str(v.data(), v.size());
               int rc = vo ? PyDict_SetItem(d, ko, vo) : -1;
               Py_XDECREF(vo);
               if (rc != 0) have = -1;
@@ -1313,7 +1342,6 @@ typedef struct {
 void Decoder_dealloc(Decoder* self) {
   delete self->proj;
   delete self->buf;
-  delete self->keys;
   Py_XDECREF(reinterpret_cast<PyObject*>(self->router));
   Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
 }
@@ -1327,7 +1355,7 @@ int Decoder_init(Decoder* self, PyObject* args, PyObject* kw) {
   delete self->proj;
   self->proj = p.release();
   if (!self->buf) self->buf = new std::string();
-  if (!self->keys) self->keys = new KeyCache();
+  self->keys = shared_keys();
   return 0;
 }
 

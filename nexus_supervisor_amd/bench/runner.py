@@ -253,6 +253,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             if pool is not None:  # shard workers profile themselves over the same window
                 pool.broadcast({"op": "pprof", "on": True, "hz": cfg.pprof_hz})
         barrier_sync()
+        pool = getattr(getattr(harness, "app", None), "pool", None)
+        r0 = getattr(pool, "report_cpu_s", 0.0)
         t0 = time.perf_counter()
         c0 = time.process_time()
         x0 = harness.external_cpu()
@@ -284,9 +286,13 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         if workers:
             cpu["workers_util_sum"] = round(sum(workers), 3)
         # supervisor CPU per pod failure: the replica's processes (coordinating parent — here
-        # also the bench driver — plus its shard workers), whole-run CPU seconds ÷ failures
+        # also the bench driver — plus its shard workers), whole-run CPU seconds ÷ failures.
+        # The decision-report channel (workers → parent → tracker; it exists only so the bench
+        # can time every decision) is measured in the parent and reported on its own line
         n_ev = max(cfg.events * cfg.steps, 1)
-        sup_cpu = cpu["supervisor_util"] * elapsed + sum(workers) * elapsed
+        report_s = getattr(pool, "report_cpu_s", 0.0) - r0
+        cpu["bench_report_cpu_us_per_event"] = round(report_s * 1e6 / n_ev, 1)
+        sup_cpu = cpu["supervisor_util"] * elapsed - report_s + sum(workers) * elapsed
         cpu["supervisor_cpu_us_per_event"] = round(sup_cpu * 1e6 / n_ev, 1)
         if workers:
             cpu["worker_cpu_us_per_event"] = round(sum(workers) * elapsed * 1e6 / n_ev, 1)

@@ -400,14 +400,18 @@ class Classifier:
     def _log_records(self, pod, gev) -> List[Dict[str, Any]]:
         if self.gpu.log_tail == "off":
             return []
-        recs = list((gev or {}).get("logs") or ())
-        got = self.log_cache.get(kube.uid_of(pod) or kube.name_of(pod))
+        agent = (gev or _NO_EV).get("logs")
+        got = self.log_cache.get(kube.uid_of(pod) or kube.name_of(pod)) if self.log_cache else None
+        if not agent:
+            return list(got) if got else []
+        recs = list(agent)
         if got:
             recs.extend(got)
         return recs
 
     def _log_texts(self, pod, gev) -> List[Tuple[str, str]]:
-        return logtail.log_texts(self._log_records(pod, gev))
+        recs = self._log_records(pod, gev)
+        return logtail.log_texts(recs) if recs else []
 
     def _log_fetch_needed(self, pod) -> List[Dict[str, Any]]:
         """Container instances whose log tail the supervisor should fetch (``pods/log``):
@@ -507,6 +511,7 @@ class Classifier:
         self._apply_history(res)
 
 
+_NO_EV: Dict[str, Any] = {}
 _PLAIN_CLASSES = frozenset((F.NONE, F.SCHEDULING, F.DEADLINE, F.FATAL, F.BACKOFF_LIMIT))
 
 

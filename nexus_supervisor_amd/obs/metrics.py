@@ -23,8 +23,24 @@ from .histogram import LatencyHistogram
 LabelKey = Tuple[Tuple[str, str], ...]
 
 
+_LK_MEMO: Dict[Tuple, LabelKey] = {}
+
+
 def _lk(labels: Optional[Dict[str, str]]) -> LabelKey:
-    return tuple(sorted((labels or {}).items()))
+    """Canonical (sorted) label key; memoised on the items in call order, since the hot
+    counters pass the same few label sets (action, stage × class) once per decision."""
+    if not labels:
+        return ()
+    raw = tuple(labels.items())
+    try:
+        k = _LK_MEMO.get(raw)
+    except TypeError:  # an unhashable label value
+        return tuple(sorted(raw))
+    if k is None:
+        if len(_LK_MEMO) > 4096:
+            _LK_MEMO.clear()
+        k = _LK_MEMO[raw] = tuple(sorted(raw))
+    return k
 
 
 class Metrics:

@@ -28,6 +28,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import struct
+from time import thread_time as _thread_time
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..informer.informer import ListWatch
@@ -279,6 +280,10 @@ class HubListWatch(ListWatch):
         self._watch_proj = watch_projection(kind)
         self._pending: Optional[bytes] = None
         self.transform = None
+        # native decode cost of the watch lines (thread CPU seconds, lines): the
+        # informer_decode_* gauges, so a profile's decode share can be checked directly
+        self.decode_seconds = 0.0
+        self.decoded_lines = 0
 
     async def list(self) -> Tuple[List[Dict[str, Any]], str]:
         while self._pending is None:
@@ -322,7 +327,10 @@ class HubListWatch(ListWatch):
             if parts is not None:
                 payload = b"".join(parts)
             # (type, object) pairs with the object's kind defaulted, built by the decoder itself
+            t0 = _thread_time()
             batch = decoder.feed_events(payload, kind)
+            self.decode_seconds += _thread_time() - t0
+            self.decoded_lines += len(batch)
             if batch:
                 yield batch
 

@@ -222,6 +222,10 @@ def collect_gauges(sup, m: Metrics) -> None:
     for kind, inf in sup.factory.informers.items():
         m.set("informer_objects", len(inf.indexer), {"kind": kind})
         m.set("informer_relists", inf.relists, {"kind": kind})
+        lw = inf.lw
+        if hasattr(lw, "decode_seconds"):
+            m.set("informer_decode_seconds", lw.decode_seconds, {"kind": kind})
+            m.set("informer_decoded_lines", lw.decoded_lines, {"kind": kind})
     m.set("active", 1.0 if sup.active else 0.0)
 
 
@@ -250,14 +254,16 @@ class Channel:
                 data = json.dumps(msg, separators=(",", ":")).encode()
             self.writer.write(data + b"\n")
 
-    async def recv(self) -> Optional[Dict[str, Any]]:
+    async def recv_line(self) -> Optional[bytes]:
         try:
             line = await self.reader.readline()
         except (ConnectionError, asyncio.IncompleteReadError, ValueError):
             return None
-        if not line:
-            return None
-        return json.loads(line)
+        return line or None
+
+    async def recv(self) -> Optional[Dict[str, Any]]:
+        line = await self.recv_line()
+        return json.loads(line) if line else None
 
     def close(self) -> None:
         try:
@@ -298,6 +304,9 @@ class WorkerPool:
         self.workers: List[_Worker] = [_Worker(i) for i in range(self.count)]
         self.decision_hooks: List[Callable[[Decision], None]] = []
         self.report_hooks: List[Callable[[str, str, Optional[float], Optional[str]], None]] = []
+        # parent CPU spent on the decision-report channel (benchmarks / tests only: decode +
+        # hooks); the bench reports it apart from the supervisor's own CPU
+        self.report_cpu_s = 0.0
         self.active = True
         self._mapping = to_mapping(cfg)
         self._metrics_seq = 0
@@ -413,9 +422,11 @@ class WorkerPool:
 
     async def _read(self, w: _Worker) -> None:
         while True:
-            msg = await w.chan.recv()
-            if msg is None:
+            line = await w.chan.recv_line()
+            if line is None:
                 break
+            t0 = time.thread_time()
+            msg = json.loads(line)
             op = msg.get("op")
             if op == "dec":
                 for h in self.report_hooks:
@@ -429,6 +440,7 @@ class WorkerPool:
                         d = Decision(r, outcome, stage)
                         for h in self.decision_hooks:
                             h(d)
+                self.report_cpu_s += time.thread_time() - t0
             elif op == "metrics":
                 w.state = msg.get("s") or {}
                 waiter = self._metrics_waiters.get(msg.get("seq", -1))

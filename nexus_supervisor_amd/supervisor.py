@@ -114,6 +114,24 @@ class _Lookup(ObjectLookup):
         return self.sup.pod_informer.indexer.by_index("job-name", job_name)
 
 
+class _StageHists:
+    """The unlabelled stage histograms of :meth:`Supervisor._observe`, each created on its
+    first sample (fused mode never has a ``stage_read``)."""
+
+    __slots__ = ("_m", "_names", "_h")
+
+    def __init__(self, metrics: Metrics, names: Tuple[str, ...]):
+        self._m = metrics
+        self._names = names
+        self._h: List[Any] = [None] * len(names)
+
+    def rec(self, i: int, seconds: float) -> None:
+        h = self._h[i]
+        if h is None:
+            h = self._h[i] = self._m.hist0(self._names[i])
+        h.record(seconds * 1e6)
+
+
 class Supervisor:
     def __init__(
         self,
@@ -144,7 +162,7 @@ class Supervisor:
         self.pipeline: Optional[PipelineStage] = None
         self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
         self._applied_cap = 200_000
-        self._hists: Optional[List[Any]] = None  # _observe: the stage histograms, once looked up
+        self._hists: Optional["_StageHists"] = None  # _observe: the stage histograms, once looked up
         # one conditional write per decision instead of read + write (compat.fused-write);
         # conditional-update: never (the reference's unconditional writes) turns it off
         self._fused = fused_actuation(cfg)
@@ -456,6 +474,10 @@ class Supervisor:
     def _on_pod_update(self, old, pod, waited: bool = False):
         if not self.active or old is pod:
             return
+        st = pod.get("status")
+        if (not self._gpu_wait and (not st or not (st.get("containerStatuses") or st.get("initContainerStatuses")
+                                                   or st.get("conditions") or st.get("reason") == "Evicted"))):
+            return  # a new (pending, unscheduled) pod: no pod-status rule can match it yet
         recv = self.wall()
         wait = self.cfg.gpu.evidence_wait
         results = self.classifier.classify_pod(pod, old, allow_wait=wait > 0 and not waited,
@@ -1032,29 +1054,23 @@ class Supervisor:
             # series exists once it has a sample (fused mode has no stage_read)
             hs = self._hists
             if hs is None:
-                hs = self._hists = [None] * len(self._STAGE_HISTS)
-            rec = []
+                hs = self._hists = _StageHists(self.metrics, self._STAGE_HISTS)
             origin = s.get("origin")
             if origin is not None:
-                rec.append((0, ack - origin))
+                hs.rec(0, ack - origin)
             recv = s.get("receive")
             if recv is not None:
-                rec.append((1, ack - recv))
+                hs.rec(1, ack - recv)
                 enq, deq, rd, prep = s.get("enqueue"), s.get("dequeue"), s.get("read"), s.get("prepare")
                 if enq is not None and deq is not None and (rd is not None or prep is not None):
-                    rec.append((2, enq - recv))
-                    rec.append((3, deq - enq))
+                    hs.rec(2, enq - recv)
+                    hs.rec(3, deq - enq)
                     if prep is not None:
-                        rec.append((4, prep - deq))
-                        rec.append((5, ack - prep))
+                        hs.rec(4, prep - deq)
+                        hs.rec(5, ack - prep)
                     else:
-                        rec.append((6, rd - deq))
-                        rec.append((5, ack - rd))
-            for i, dt in rec:
-                h = hs[i]
-                if h is None:
-                    h = hs[i] = self.metrics.hist0(self._STAGE_HISTS[i])
-                h.record(dt * 1e6)
+                        hs.rec(6, rd - deq)
+                        hs.rec(5, ack - rd)
             return
         if "origin" in s:
             self.metrics.observe_seconds("event_to_checkpoint", ack - s["origin"])

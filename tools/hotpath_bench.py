@@ -152,10 +152,27 @@ async def run(args) -> dict:
 
             prof = cProfile.Profile()
             prof.enable()
+        gc_t = {0: 0.0, 1: 0.0, 2: 0.0}
+        gc_n = {0: 0, 1: 0, 2: 0}
+        gc_start = [0.0]
+
+        def gc_cb(phase, info):
+            if phase == "start":
+                gc_start[0] = time.thread_time()
+            else:
+                g = info.get("generation", 0)
+                gc_t[g] += time.thread_time() - gc_start[0]
+                gc_n[g] += 1
+
+        gc.callbacks.append(gc_cb)
+        lws = [inf.lw for inf in factory.informers.values()]
+        d0 = sum(lw.decode_seconds for lw in lws)
+        l0 = {inf.kind: inf.lw.decoded_lines for inf in factory.informers.values()}
         c0, t0, n = time.thread_time(), time.perf_counter(), 0
         for data in batch:
             n += await step(data)
         cpu, wall = time.thread_time() - c0, time.perf_counter() - t0
+        gc.callbacks.remove(gc_cb)
         if prof is not None:
             prof.disable()
             prof.dump_stats(args.cprofile)
@@ -163,7 +180,12 @@ async def run(args) -> dict:
             with open(args.pprof, "wb") as f:
                 f.write(sampler.stop().encode_gz())
         results.append({"cpu_us_per_event": round(1e6 * cpu / n, 1), "events_per_s_cpu": round(n / cpu),
-                        "wall_s": round(wall, 2), "events": n})
+                        "wall_s": round(wall, 2), "events": n,
+                        "decode_us_per_event": round(1e6 * (sum(lw.decode_seconds for lw in lws) - d0) / n, 1),
+                        "lines_per_event": {inf.kind: round((inf.lw.decoded_lines - l0[inf.kind]) / n, 2)
+                                            for inf in factory.informers.values()},
+                        "gc_us_per_event": {g: round(1e6 * gc_t[g] / n, 2) for g in gc_t},
+                        "gc_collections": dict(gc_n)})
         del batch
         if args.sizes:
             results[-1]["containers"] = sorted(_containers(sup), reverse=True)[:12]
