@@ -268,16 +268,76 @@ class SharedInformer:
                     return self._watch_error(obj)
                 self._apply(etype, obj)
             return
-        n = 0
         apply = self._apply
         async for batch in batches(self._rv):
-            for etype, obj in batch:
-                if etype == ERROR:
-                    return self._watch_error(obj)
-                apply(etype, obj)
-                n += 1
-                if not n & 63:
+            if self.accept is not None or self.transform is not None:
+                n = 0
+                for etype, obj in batch:
+                    if etype == ERROR:
+                        return self._watch_error(obj)
+                    apply(etype, obj)
+                    n += 1
+                    if not n & 63:
+                        await asyncio.sleep(0)
+                continue
+            for i in range(0, len(batch), 64):
+                err = self._apply_lines(batch, i, i + 64)
+                if err is not None:
+                    return self._watch_error(err)
+                if i + 64 < len(batch):
                     await asyncio.sleep(0)
+
+    def _apply_lines(self, batch, start: int, end: int):
+        """:meth:`_apply` for ``batch[start:end]`` of a projecting transport (no transform,
+        no ingest filter), with the per-line lookups hoisted out of the loop; returns the
+        ERROR event's object if one is met (the lines before it are applied)."""
+        self.last_receive = self.stamp()
+        indexer = self.indexer
+        upsert, delete = indexer.upsert, indexer.delete
+        adds = [h.on_add for h in self.handlers if h.on_add]
+        updates = [h.on_update for h in self.handlers if h.on_update]
+        deletes = [h.on_delete for h in self.handlers if h.on_delete]
+        kind = self.kind
+        rv = None
+        seen = 0
+        try:
+            for etype, obj in batch[start:end]:
+                if etype == ERROR:
+                    return obj
+                seen += 1
+                m = obj.get("metadata")
+                if m:
+                    v = m.get("resourceVersion")
+                    if v:
+                        rv = v
+                if etype == BOOKMARK:
+                    continue
+                if etype == DELETED:
+                    old = delete(obj) or obj
+                    for f in deletes:
+                        try:
+                            f(old)
+                        except Exception:
+                            log.exception("%s delete handler failed", kind)
+                    continue
+                old = upsert(obj)
+                if old is None:
+                    for f in adds:
+                        try:
+                            f(obj)
+                        except Exception:  # handler bugs must not kill the informer
+                            log.exception("%s add handler failed", kind)
+                else:
+                    for f in updates:
+                        try:
+                            f(old, obj)
+                        except Exception:
+                            log.exception("%s update handler failed", kind)
+        finally:
+            self.watch_events += seen
+            if rv:
+                self._rv = rv
+        return None
 
     async def _resync_loop(self):
         while True:
