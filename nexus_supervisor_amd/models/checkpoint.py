@@ -160,3 +160,35 @@ class CheckpointedRequest:
 
     def to_dict(self) -> Dict[str, object]:
         return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+class StageRow:
+    """The projected stage read (``SELECT lifecycle_stage``) of the owned-columns path: the
+    key and the stage, every other column None.  One per decision, so it is a three-slot
+    object instead of the 19-field dataclass (whose generated ``__init__`` was ~1 % of a
+    shard worker's CPU)."""
+
+    __slots__ = ("algorithm", "id", "lifecycle_stage")
+
+    def __init__(self, algorithm: str, id: str, lifecycle_stage: Optional[str]):  # noqa: A002 - the column name
+        self.algorithm = algorithm
+        self.id = id
+        self.lifecycle_stage = lifecycle_stage
+
+    def __getattr__(self, name: str):
+        if name in _OTHER_COLUMNS:
+            return None
+        raise AttributeError(name)
+
+    def is_finished(self) -> bool:
+        return self.lifecycle_stage in FINISHED_STAGES
+
+    @property
+    def key(self) -> Tuple[str, str]:
+        return (self.algorithm, self.id)
+
+    def deep_copy(self) -> CheckpointedRequest:
+        return CheckpointedRequest(self.algorithm, self.id, self.lifecycle_stage)
+
+
+_OTHER_COLUMNS = frozenset(n for n in COLUMN_NAMES if n not in ("algorithm", "id", "lifecycle_stage"))

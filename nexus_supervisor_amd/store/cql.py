@@ -51,7 +51,7 @@ import zipfile
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
-from ..models.checkpoint import COLUMN_NAMES, COLUMNS, KEYSPACE, TABLE, CheckpointedRequest
+from ..models.checkpoint import COLUMN_NAMES, COLUMNS, KEYSPACE, TABLE, CheckpointedRequest, StageRow
 from .base import CheckpointStore, NotSent, StoreError
 
 log = logging.getLogger("nexus_supervisor_amd.cql")
@@ -1086,7 +1086,7 @@ class CqlCheckpointStore(CheckpointStore):
         rows = await self.session.execute(self.q_read_status, (algorithm, request_id), consistency=self.cl)
         if not rows.rows:
             return None
-        return CheckpointedRequest(algorithm, request_id, rows.rows[0][0])
+        return StageRow(algorithm, request_id, rows.rows[0][0])
 
     async def upsert_checkpoint(self, checkpoint: CheckpointedRequest) -> None:
         self.writes += 1

@@ -309,8 +309,12 @@ class Supervisor:
         """True when this replica must not write or delete for ``request_id``: leadership or
         the run's shard lost since the decision was dequeued (epoch), not held now, or the
         lease's hold lapsed (time-bounded: a stalled apiserver cannot extend it)."""
-        return (not self.active or token != self._token(request_id) or not self.shards.owns(request_id)
-                or time.monotonic() >= self.active_until)
+        if not self.active or token[0] != self.epoch or time.monotonic() >= self.active_until:
+            return True
+        sh = self.shards
+        if sh.owned is None:  # unsharded: the shard epoch is constant
+            return False
+        return token[1] != sh.token(request_id) or not sh.owns(request_id)
 
     def set_lease_deadline(self, until: float) -> None:
         self.active_until = until
