@@ -36,6 +36,16 @@ class HttpError(Exception):
     pass
 
 
+def _header(head: bytes, name: bytes) -> bytes:
+    """Value of header ``name`` (``b"\\r\\nname:"``, lower case) in a lower-cased response
+    head that ends with CRLF; empty when absent."""
+    i = head.find(name)
+    if i < 0:
+        return b""
+    i += len(name)
+    return head[i: head.index(b"\r\n", i)].strip()
+
+
 def _expire_and_reset(fut: asyncio.Future, conn: "_Conn", what: str) -> None:
     if not fut.done():
         fut.set_exception(HttpError(f"{what} timed out"))
@@ -56,7 +66,7 @@ class _Conn(asyncio.Protocol):
         self.closed = False
         # parser state for the response at the head of the queue
         self._status = 0
-        self._headers: Dict[str, str] = {}
+        self._close = False
         self._need = -1       # body bytes still needed (content-length mode)
         self._chunked = False
         self._body = bytearray()
@@ -91,19 +101,20 @@ class _Conn(asyncio.Protocol):
             end = buf.find(b"\r\n\r\n")
             if end < 0:
                 return False
-            head = bytes(buf[:end]).decode("latin-1").split("\r\n")
+            # only the status and the three framing headers matter: find them in the
+            # lower-cased head instead of building a header dict per response
+            head = bytes(buf[:end + 2]).lower()
             del buf[: end + 4]
-            parts = head[0].split(" ", 2)
-            if len(parts) < 2 or not parts[0].startswith("HTTP/1."):
-                raise HttpError(f"bad status line {head[0]!r}")
-            self._status = int(parts[1])
-            hdrs = {}
-            for line in head[1:]:
-                k, _, v = line.partition(":")
-                hdrs[k.strip().lower()] = v.strip()
-            self._headers = hdrs
-            self._chunked = "chunked" in hdrs.get("transfer-encoding", "").lower()
-            self._need = int(hdrs.get("content-length", "0")) if not self._chunked else -1
+            sp = head.find(b" ")
+            if not head.startswith(b"http/1.") or sp < 0:
+                raise HttpError(f"bad status line {head[:80]!r}")
+            try:
+                self._status = int(head[sp + 1: sp + 4])
+            except ValueError:
+                raise HttpError(f"bad status line {head[:80]!r}") from None
+            self._chunked = b"chunked" in _header(head, b"\r\ntransfer-encoding:")
+            self._need = -1 if self._chunked else int(_header(head, b"\r\ncontent-length:") or b"0")
+            self._close = _header(head, b"\r\nconnection:") == b"close"
             self._body = bytearray()
             self._in_body = True
         if self._chunked:
@@ -130,7 +141,7 @@ class _Conn(asyncio.Protocol):
         self.deadlines.popleft()
         if not fut.done():
             fut.set_result((self._status, bytes(self._body)))
-        if self._headers.get("connection", "").lower() == "close":
+        if self._close:
             self.transport.close()
         return True
 

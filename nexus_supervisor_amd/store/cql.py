@@ -69,6 +69,18 @@ def _ms_to_dt(ms: int) -> _dt.datetime:
     return EPOCH + _dt.timedelta(milliseconds=ms)
 
 
+def _build_execute_fast(stream, qid, vals, codes, types, cl, skip, serial):
+    """EXECUTE frame through the scalar fast encoder (one per decision read and write)."""
+    out = N.encode_execute_fast(stream, qid, vals, codes, cl, skip, serial)
+    if out is NotImplemented:  # a value of an unexpected Python type
+        out = N.encode_execute(stream, qid, vals, types, cl, skip, -1, None, serial, None)
+    return out
+
+
+def _build_execute(stream, qid, vals, codes, types, cl, skip, serial):
+    return N.encode_execute(stream, qid, vals, types, cl, skip, -1, None, serial, None)
+
+
 def _native():
     if N is None:
         raise StoreError("native CQL codec not built: run `python -m nexus_supervisor_amd._build`") from _IMPORT_ERROR
@@ -251,8 +263,8 @@ class CqlConnection:
         else:
             self._out = []
 
-    def request_nowait(self, build, hint=None, timeout: Optional[float] = None) -> asyncio.Future:
-        """Send one request frame built by ``build(stream)``; returns the response future."""
+    def request_nowait(self, build, hint=None, timeout: Optional[float] = None, args: Optional[tuple] = None) -> asyncio.Future:
+        """Send one request frame built by ``build(stream, *args)``; returns the response future."""
         if self.closed:
             raise ConnectionClosed(f"connection to {self.host}:{self.port} is closed")
         if not self._free:
@@ -263,7 +275,7 @@ class CqlConnection:
         self._deadline[stream] = self._loop.time() + (timeout or self.request_timeout)
         if hint is not None:
             self._reader.expect(stream, hint)
-        self._out.append(build(stream))
+        self._out.append(build(stream) if args is None else build(stream, *args))
         self.requests += 1
         if not self._flush_scheduled:
             self._flush_scheduled = True
@@ -841,18 +853,10 @@ class CqlSession:
                 self.stats["shard_routed"] += 1
             sent = True
             try:
-                qid = ps.query_id
                 codes = ps.codes
-                if codes is not None:
-                    def build(s, qid=qid):
-                        out = N.encode_execute_fast(s, qid, vals, codes, cl, skip, serial)
-                        if out is NotImplemented:  # a value of an unexpected Python type
-                            out = N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None)
-                        return out
-                else:
-                    def build(s, qid=qid):
-                        return N.encode_execute(s, qid, vals, ps.bind_types, cl, skip, -1, None, serial, None)
-                r = await conn.request_nowait(build, hint if skip else None, timeout)
+                r = await conn.request_nowait(_build_execute_fast if codes is not None else _build_execute,
+                                              hint if skip else None, timeout,
+                                              (ps.query_id, vals, codes, ps.bind_types, cl, skip, serial))
             except (ConnectionClosed, OSError) as exc:
                 last = exc
                 self._mark_down(h, exc)

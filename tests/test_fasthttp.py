@@ -92,3 +92,27 @@ def test_request_nowait_expires_by_sweep_and_resets_connection(arun):
         await srv.wait_closed()
 
     arun(main(), timeout=20)
+
+
+def test_connection_close_and_mixed_case_headers(arun):
+    async def handler(r, w):
+        try:
+            lines, _ = await _read_request(r)
+            w.write(b"HTTP/1.1 201 Created\r\nCONTENT-LENGTH: 2\r\nConnection: Close\r\nX-A: b\r\n\r\nok")
+            await w.drain()
+            await asyncio.sleep(0.5)
+        except (asyncio.IncompleteReadError, ConnectionError):
+            pass
+
+    async def main():
+        srv, url = await _server(handler)
+        c = PipelinedHttp(url, connections=1)
+        status, body = await c.request("GET", "/x")
+        assert (status, body) == (201, b"ok")
+        await asyncio.sleep(0.05)
+        assert all(conn.closed or conn.transport.is_closing() for conn in c._conns) or not c._conns
+        await c.close()
+        srv.close()
+        await srv.wait_closed()
+
+    arun(main(), timeout=20)
