@@ -23,8 +23,14 @@ def cpu_share(cpu_max_path: str = CPU_MAX) -> float:
     return max(n, 1.0)
 
 
-def auto_worker_processes(reserve: float = 1.0, cap: int = 64, share: float = 0.0) -> int:
+AUTO_WORKERS_CAP = 6
+
+
+def auto_worker_processes(reserve: float = 1.0, cap: int = AUTO_WORKERS_CAP, share: float = 0.0) -> int:
     """Shard workers for the CPU share, keeping ``reserve`` CPUs for the coordinating
-    parent (watch hub, lease, /metrics): at least 1 (= single-process supervisor)."""
+    parent (watch hub, lease, /metrics): at least 1 (= single-process supervisor), at most
+    six — the efficient point measured on MI355X hosts (``bench.py`` ``auto_procs``): six
+    saturated workers sustain 37–47k failures/s, more only add CPU per failure (and lower
+    burst latency; set ``runtime.worker-processes`` explicitly for that)."""
     n = share or cpu_share()
     return max(1, min(cap, int(n - reserve)))
