@@ -250,7 +250,7 @@ class RuntimeConfig:
     # process-per-core runtime: this many shard-worker processes, each owning the runs whose
     # job name hashes to it (informers filter at ingest), under one coordinating parent that
     # holds the lease and serves /metrics; 1 = single-process supervisor; 0 = one per CPU of
-    # the container's share (cgroup quota / affinity) minus one for the parent
+    # the container's share (cgroup quota / affinity) minus one for the parent, at most 6
     worker_processes: int = field(default=1, metadata=_k("worker-processes"))
     # set by the coordinator in each worker process (not a user knob)
     worker_index: int = field(default=0, metadata=_k("worker-index"))

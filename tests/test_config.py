@@ -128,6 +128,6 @@ def test_worker_processes_auto_from_cpu_share(tmp_path, monkeypatch):
     monkeypatch.setattr(cpus, "CPU_MAX", str(tmp_path / "missing"))
     monkeypatch.setattr(cpus.cpu_share, "__defaults__", (str(tmp_path / "missing"),))
     c = load_config(env={"NEXUS__RUNTIME__WORKER_PROCESSES": "0"})
-    assert c.runtime.worker_processes == 63
+    assert c.runtime.worker_processes == 6  # 64 CPUs: capped at the efficient point (utils/cpus.py)
     with pytest.raises(ConfigError):
         load_config(env={"NEXUS__RUNTIME__WORKER_PROCESSES": "-1"})
