@@ -12,6 +12,7 @@
 #include <Python.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -35,7 +36,19 @@ struct Enc {
     out.push_back('"');
     const char* run = p;
     const char* end = p + n;
-    for (const char* c = p; c < end; ++c) {
+    // most strings need no escaping: test 8 bytes at a time for a byte < 0x20, '"' or '\\'
+    // (SWAR zero-byte tests) and copy a clean run in one append
+    const char* c = p;
+    for (; c + 8 <= end; c += 8) {
+      uint64_t w;
+      memcpy(&w, c, 8);
+      const uint64_t ones = 0x0101010101010101ULL, high = 0x8080808080808080ULL;
+      uint64_t lt20 = (w - ones * 0x20) & ~w & high;
+      uint64_t xq = w ^ (ones * '"'), xb = w ^ (ones * '\\');
+      uint64_t q = (xq - ones) & ~xq & high, b = (xb - ones) & ~xb & high;
+      if (lt20 | q | b) break;
+    }
+    for (; c < end; ++c) {
       unsigned char ch = static_cast<unsigned char>(*c);
       if (ch >= 0x20 && ch != '"' && ch != '\\') continue;
       out.append(run, c - run);
@@ -74,6 +87,20 @@ struct Enc {
       out.append("-Infinity");
       return true;
     }
+    double a = std::fabs(d);
+    if (a == 0.0 || (a >= 1e-4 && a < 1e16)) {
+      // Python's repr: the shortest round-trip digits, fixed notation in this range (and a
+      // ".0" on integral values) — std::to_chars(fixed) gives exactly those digits without
+      // the malloc + format machinery of PyOS_double_to_string
+      char buf[64];
+      auto res = std::to_chars(buf, buf + sizeof buf, d, std::chars_format::fixed);
+      if (res.ec == std::errc()) {
+        size_t k = static_cast<size_t>(res.ptr - buf);
+        out.append(buf, k);
+        if (!memchr(buf, '.', k)) out.append(".0");
+        return true;
+      }
+    }
     char* s = PyOS_double_to_string(d, 'r', 0, Py_DTSF_ADD_DOT_0, nullptr);
     if (!s) return false;
     out.append(s);
@@ -87,8 +114,8 @@ struct Enc {
     if (overflow == 0) {
       if (v == -1 && PyErr_Occurred()) return false;
       char buf[24];
-      int k = snprintf(buf, sizeof buf, "%lld", v);
-      out.append(buf, k);
+      auto res = std::to_chars(buf, buf + sizeof buf, v);  // no locale / format parsing (snprintf)
+      out.append(buf, static_cast<size_t>(res.ptr - buf));
       return true;
     }
     PyObject* s = PyObject_Str(o);
@@ -239,7 +266,7 @@ extern "C" PyObject* nexus_json_dumps(PyObject*, PyObject* args, PyObject* kw) {
   Enc e;
   e.sort_keys = sort_keys != 0;
   e.dflt = dflt == Py_None ? nullptr : dflt;
-  e.out.reserve(1024);
+  e.out.reserve(2048);
   if (!e.value(obj, 0)) return nullptr;
   if (newline) e.out.push_back('\n');
   return PyBytes_FromStringAndSize(e.out.data(), static_cast<Py_ssize_t>(e.out.size()));

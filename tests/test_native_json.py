@@ -147,3 +147,27 @@ def test_feed_events_matches_python_envelope_unpacking():
     assert all(o["kind"] == "Pod" for _, o in got)
     with pytest.raises(ValueError):
         K.ProjectedDecoder(True).feed_events(b"[1, 2]\n", "Pod")
+
+
+def test_numbers_and_strings_match_json_module_exactly():
+    """The fast paths (std::to_chars for ints and for floats in Python repr's fixed range,
+    an 8-byte clean-run scan for strings) produce the json module's exact bytes."""
+    import json
+    import random
+    import struct
+
+    from nexus_supervisor_amd._kube_native import dumps
+
+    rng = random.Random(11)
+    floats = [0.0, -0.0, 1.0, -1.0, 0.5, 1e-4, 9.999e-5, 1e16, 9999999999999998.0, 1792219597.431, 0.1, 1 / 3,
+              5e-324, 1.7976931348623157e308]
+    while len(floats) < 20000:
+        v = struct.unpack("d", struct.pack("Q", rng.getrandbits(64)))[0] if rng.random() < 0.5 else \
+            rng.uniform(-1e17, 1e17) * 10 ** rng.randint(-25, 0)
+        if v == v and abs(v) != float("inf"):
+            floats.append(v)
+    ints = [0, -1, 2 ** 63 - 1, -2 ** 63, 2 ** 64, 10 ** 30] + [rng.randint(-10 ** 18, 10 ** 18) for _ in range(2000)]
+    alphabet = [chr(c) for c in range(128)] + ["é", "☃", "𝄞"]
+    strs = ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 40))) for _ in range(3000)]
+    for doc in ([floats], [ints], [strs], {s: i for s, i in zip(strs, ints)}):
+        assert dumps(doc).decode() == json.dumps(doc, separators=(",", ":"), ensure_ascii=False)
