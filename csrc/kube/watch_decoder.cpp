@@ -1552,6 +1552,7 @@ PyTypeObject DecoderType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 }  // namespace
 
 extern "C" PyObject* nexus_json_dumps(PyObject*, PyObject* args, PyObject* kw);  // json_encode.cpp
+extern "C" int nexus_register_histogram(PyObject* m);                            // histogram.cpp
 
 namespace {
 
@@ -1604,5 +1605,9 @@ PyMODINIT_FUNC PyInit__kube_native(void) {
   PyModule_AddObject(m, "ShardRouter", reinterpret_cast<PyObject*>(&RouterType));
   Py_INCREF(&SplitterType);
   PyModule_AddObject(m, "WatchSplitter", reinterpret_cast<PyObject*>(&SplitterType));
+  if (nexus_register_histogram(m) < 0) {
+    Py_DECREF(m);
+    return nullptr;
+  }
   return m;
 }

@@ -177,8 +177,7 @@ def metrics_state(m: Metrics) -> Dict[str, Any]:
     hists = []
     for name, series in m.hists.items():
         for k, h in series.items():
-            sparse = [[i, c] for i, c in enumerate(h.counts) if c]
-            hists.append([name, [list(p) for p in k], sparse, h.total, h.sum, h.min, h.max])
+            hists.append([name, [list(p) for p in k], h.sparse(), h.total, h.sum, h.min, h.max])
     return {"c": [[n, [list(p) for p in k], v] for n, s in m.counters.items() for k, v in s.items()],
             "g": [[n, [list(p) for p in k], v] for n, s in m.gauges.items() for k, v in s.items()],
             "h": hists, "help": m.help}
@@ -201,13 +200,7 @@ def merge_metrics_state(dst: Metrics, st: Dict[str, Any], gauge_labels: Optional
         h = series.get(key)
         if h is None:
             h = series[key] = LatencyHistogram()
-        for i, c in sparse:
-            h.counts[i] += c
-        h.total += total
-        h.sum += hsum
-        if hmin is not None and (h.min is None or hmin < h.min):
-            h.min = hmin
-        h.max = max(h.max, hmax)
+        h.merge_state(sparse, total, hsum, hmin, hmax)
     for name, text in (st.get("help") or {}).items():
         dst.help.setdefault(name, text)
 

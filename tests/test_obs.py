@@ -237,3 +237,37 @@ def test_buffered_log_handler_flushes_on_timer_warning_and_shutdown():
     shutdown_logging()
     assert b"last" in raw.getvalue()
     assert isinstance(BufferedStreamHandler(io.StringIO()), BufferedStreamHandler)
+
+
+def test_native_histogram_matches_python():
+    """``_kube_native.LatencyHist`` (the record path in C) keeps exactly the Python
+    histogram's buckets and statistics, and merges across both."""
+    import random
+
+    import pytest
+
+    from nexus_supervisor_amd.obs import histogram as H
+
+    if H._NativeHist is None:
+        pytest.skip("native extension not built")
+    rng = random.Random(3)
+    py, nat = H.PyLatencyHistogram(), H.NativeLatencyHistogram()
+    vals = [rng.choice([-5.0, 0.0, 0.4, 127.9, 128.0]) for _ in range(50)] + \
+        [rng.lognormvariate(6, 3) for _ in range(20000)] + [2.0 ** 45, 1e30]
+    for v in vals:
+        py.record(v)
+        nat.record(v)
+    nat.record(7, 3)
+    py.record(7, 3)
+    assert nat.counts == py.counts and nat.sparse() == py.sparse()
+    assert (nat.total, nat.sum, nat.min, nat.max) == (py.total, py.sum, py.min, py.max)
+    assert nat.summary() == py.summary() and nat.buckets() == py.buckets()
+    both = H.NativeLatencyHistogram()
+    both.merge(nat)
+    both.merge(py)
+    ref = H.PyLatencyHistogram()
+    ref.merge(py)
+    ref.merge(py)
+    assert both.counts == ref.counts and (both.total, both.sum, both.min, both.max) == (ref.total, ref.sum, ref.min, ref.max)
+    both.reset()
+    assert both.total == 0 and both.min is None and both.percentile(99) == 0.0
