@@ -76,7 +76,8 @@ for step in "$@"; do
       python tools/pprof_merge.py gpurun_out/prof/workers_merged.top.txt gpurun_out/prof/bench.pb.gz.w*.pb.gz > /dev/null
       rc=$?; summary+=("profile: $(tail -1 gpurun_out/prof/bench.log | cut -c1-200)"); [ $rc -eq 0 ] ;;
     scenarios)
-      timeout -k 10 900 python -u -m nexus_supervisor_amd.bench.scenarios --only "$val" \
+      gpuflag=""; [[ ",$val," == *",3,"* ]] && gpuflag="--gpu"
+      timeout -k 10 900 python -u -m nexus_supervisor_amd.bench.scenarios --only "$val" $gpuflag \
         --json-out "gpurun_out/scenarios_${val//,/_}.json" > "gpurun_out/scenarios_${val//,/_}.log" 2>&1 ;;
     rocprof)
       ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
