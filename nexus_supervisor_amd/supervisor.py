@@ -636,6 +636,11 @@ class Supervisor:
             self._label_check_at = now + 5.0
             return
         self._label_check_at = now + 60.0
+        owned = self.shards.owned
+        if (owned is not None and not owned) or self.pod_informer.rejected or self.job_informer.rejected:
+            # a shard replica holding no shard, or objects that matched the selector and were
+            # filtered as another replica's / worker's: empty caches are by design here
+            return
         if len(self.pod_informer.indexer) or len(self.job_informer.indexer):
             if self.label_mismatch:
                 self.label_mismatch = False

@@ -341,6 +341,24 @@ def test_label_mismatch_warning(arun):
     arun(go())
 
 
+def test_no_label_mismatch_alarm_for_a_shard_replica_holding_nothing(arun):
+    """Lease-mode shard replica that holds no shard (yet): its Pod/Job caches are empty by
+    design while the namespace's Events name Pods — not a selector mismatch (seen as a false
+    alarm in the 3-replica chaos scenario)."""
+    async def go():
+        cfg = _cfg(**{"leader-election": {"enabled": False}, "sharding": {"shards": 4, "mode": "lease"}})
+        events = [make_event("Pod", f"other-{i}", "Started", "x") for i in range(4)]
+        c = InProcCluster(cfg, MemoryStore(), events)
+        await c.start()
+        sup = c.supervisor
+        assert sup.shards.owned is not None and not sup.shards.owned
+        sup._check_labels(0.0)
+        assert not sup.label_mismatch
+        await c.stop()
+
+    arun(go())
+
+
 def test_unknown_yaml_keys_are_tolerated_with_a_warning(tmp_path, caplog):
     """viper tolerates unknown keys (a reference appconfig with extra keys must start);
     this build logs them (VERDICT r1 weak #14) and refuses only in strict mode."""
