@@ -465,7 +465,7 @@ class CqlSession:
         self._tokens: Dict[tuple, int] = {}  # partition key values → token (recent)
         # partition key values → (routing epoch, token, owner host, shard): a decision reads
         # then writes one partition; the second statement skips ring lookup and shard math
-        self._routes: Dict[tuple, Tuple[Any, int, Host, Optional[int]]] = {}
+        self._routes: Dict[tuple, Tuple[Any, int, Host, Optional[int], bool]] = {}
         self.per_shard = max(1, connections_per_shard)
         self.hosts: Dict[Tuple[str, int], Host] = {}
         self._ring: List[int] = []
@@ -803,19 +803,28 @@ class CqlSession:
         epoch = (_HOST_EPOCH[0], len(self.hosts))
         hit = self._routes.get(key)
         if hit is not None and hit[0] == epoch:
-            self.stats["token_routed"] += 1
+            if hit[4]:
+                self.stats["token_routed"] += 1
             return hit[1], hit[2], hit[3]
         tok = self.routing_token(ps, values)
-        if tok is None or not (self.token_aware and self._ring):
-            return tok, None, None
-        o = self.owner(tok)
+        if tok is None:
+            return None, None, None
+        by_ring = bool(self.token_aware and self._ring)
+        if by_ring:
+            o = self.owner(tok)
+        else:
+            # no ring (one node, or token-awareness off): with a single live host every
+            # plan starts there, so its shard can be cached the same way
+            up = [h for h in self.hosts.values() if h.up]
+            o = up[0] if len(up) == 1 else None
         if o is None or not o.up:
             return tok, None, None
         shard = o.shard_of(tok) if o.nr_shards else None
         if len(self._routes) > 8192:
             self._routes.clear()
-        self._routes[key] = (epoch, tok, o, shard)
-        self.stats["token_routed"] += 1
+        self._routes[key] = (epoch, tok, o, shard, by_ring)
+        if by_ring:
+            self.stats["token_routed"] += 1
         return tok, o, shard
 
     async def execute(self, ps_or_query, values: Sequence[Any] = (), *, consistency: Optional[int] = None,
