@@ -87,7 +87,16 @@ def read_tail(path: str, max_bytes: int = TAIL_BYTES, max_lines: int = TAIL_LINE
     return parse_log_lines(data)[-max_lines:]
 
 
-def container_log_dir(root: str, namespace: str, pod: str, uid: str, container: str) -> str:
+def _safe_part(s: str) -> bool:
+    """A path component from the API (namespace, pod, uid, container name): Kubernetes
+    validates them as DNS labels / UUIDs, but the agent runs privileged, so a name that could
+    leave ``/var/log/pods`` is refused rather than trusted."""
+    return bool(s) and "/" not in s and "\\" not in s and "\x00" not in s and s not in (".", "..")
+
+
+def container_log_dir(root: str, namespace: str, pod: str, uid: str, container: str) -> Optional[str]:
+    if not all(_safe_part(x) for x in (namespace, pod, uid, container)):
+        return None
     return os.path.join(root, f"{namespace}_{pod}_{uid}", container)
 
 
@@ -97,6 +106,8 @@ def container_log_file(root: str, namespace: str, pod: str, uid: str, container:
     match, the newest ``N.log`` of the container (rotated files are not read: the failure
     is at the end of the live file)."""
     d = container_log_dir(root, namespace, pod, uid, container)
+    if d is None:
+        return None
     if restart is not None:
         p = os.path.join(d, f"{int(restart)}.log")
         if os.path.isfile(p):

@@ -38,6 +38,8 @@ def write_cri_log(root: str, namespace: str, pod: str, uid: str, container: str,
                   streams: Iterable[Tuple[str, str]] = (), split_at: int = 0) -> str:
     """Write ``(stream, text)`` chunks as container instance ``restart``'s log; returns the path."""
     d = container_log_dir(root, namespace, pod, uid, container)
+    if d is None:
+        raise ValueError("namespace / pod / uid / container must be plain path components")
     os.makedirs(d, exist_ok=True)
     path = os.path.join(d, f"{int(restart)}.log")
     with open(path, "a", encoding="utf-8") as f:

@@ -396,3 +396,14 @@ class FailingPatch:
 
     async def patch_merge(self, *a, **kw):
         raise RuntimeError("apiserver unavailable")
+
+
+def test_log_reader_refuses_names_that_leave_the_log_root(tmp_path):
+    """The agent reads /var/log/pods as root: a namespace / pod / uid / container name that
+    is not a plain path component never reaches the filesystem."""
+    from nexus_supervisor_amd.gpu.logtail import container_log_file
+
+    (tmp_path / "secret.log").write_text("x")
+    for ns, pod, uid, ctr in (("..", "p", "u", "c"), ("ns", "p/../..", "u", "c"), ("ns", "p", "u", ".."),
+                              ("ns", "p", "", "c"), ("ns", "p", "u", "c\x00")):
+        assert container_log_file(str(tmp_path / "pods"), ns, pod, uid, ctr, 0) is None
