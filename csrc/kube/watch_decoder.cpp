@@ -753,6 +753,51 @@ class Scan {
     }
   }
 
+  // Everything routing needs from one watch line (or bare LIST item) in ONE pass:
+  // type, metadata.name / resourceVersion / labels[job_label], involvedObject.kind / name.
+  // Stops after the object's metadata (and involvedObject when wanted) — both come before
+  // the large spec / status — so a line costs one short prefix walk instead of the four
+  // from-the-start path lookups it used to (the hub's splitter: ~20 % less per line).
+  struct Info {
+    std::string_view type, name, rv, job, ikind, iname;
+    bool has_type = false, has_name = false, has_rv = false, has_job = false, has_ikind = false, has_iname = false;
+  };
+
+  bool envelope(bool wrapped, std::string_view job_label, bool want_involved, Info& in) {
+    i_ = 0;
+    try {
+      if (!wrapped) return object_fields(job_label, want_involved, in);
+      ws();
+      if (i_ >= n_ || s_[i_] != '{') return false;
+      ++i_;
+      while (true) {
+        ws();
+        if (i_ >= n_ || s_[i_] == '}') return true;
+        if (s_[i_] != '"') return false;
+        bool esc;
+        std::string_view k = str(esc);
+        ws();
+        if (i_ >= n_ || s_[i_] != ':') return false;
+        ++i_;
+        ws();
+        if (!esc && k == "type" && i_ < n_ && s_[i_] == '"') {
+          in.type = str(esc);
+          in.has_type = !esc;
+        } else if (!esc && k == "object" && i_ < n_ && s_[i_] == '{') {
+          // the scan stops inside the object: a type after it is left to the caller
+          // (the API server always writes "type" first)
+          return object_fields(job_label, want_involved, in);
+        } else {
+          skip_value();
+        }
+        ws();
+        if (i_ < n_ && s_[i_] == ',') ++i_;
+      }
+    } catch (const ParseError&) {
+      return false;
+    }
+  }
+
   // LIST body: metadata.resourceVersion and the byte range of every element of "items"
   bool list_items(std::string_view& rv, std::vector<std::pair<size_t, size_t>>& items) {
     static const char* const P_RV[] = {"metadata", "resourceVersion"};
@@ -851,6 +896,130 @@ class Scan {
     }
     while (i_ < n_ && s_[i_] != ',' && s_[i_] != '}' && s_[i_] != ']') ++i_;
   }
+  // string members of a flat object at i_ (on its '{'): each key in `keys` (with its slot in
+  // `vals` / `got`); other members are skipped
+  template <size_t N>
+  void members(const std::string_view (&keys)[N], std::string_view (&vals)[N], bool (&got)[N]) {
+    ++i_;
+    while (true) {
+      ws();
+      if (i_ >= n_) throw ParseError{"unexpected end", i_};
+      if (s_[i_] == '}') {
+        ++i_;
+        return;
+      }
+      if (s_[i_] != '"') throw ParseError{"expected key", i_};
+      bool esc;
+      std::string_view k = str(esc);
+      bool kesc = esc;
+      ws();
+      if (i_ >= n_ || s_[i_] != ':') throw ParseError{"expected ':'", i_};
+      ++i_;
+      ws();
+      size_t hit = N;
+      if (!kesc && i_ < n_ && s_[i_] == '"')
+        for (size_t j = 0; j < N; ++j)
+          if (!got[j] && k == keys[j]) {
+            hit = j;
+            break;
+          }
+      if (hit < N) {
+        std::string_view v = str(esc);
+        if (!esc) {
+          vals[hit] = v;
+          got[hit] = true;
+        }
+      } else {
+        skip_value();
+      }
+      ws();
+      if (i_ < n_ && s_[i_] == ',') ++i_;
+    }
+  }
+
+  // the object at i_: metadata (name, resourceVersion, labels[job_label]) and, when wanted,
+  // involvedObject (kind, name); returns once those are read, leaving i_ inside the object
+  bool object_fields(std::string_view job_label, bool want_involved, Info& in) {
+    ws();
+    if (i_ >= n_ || s_[i_] != '{') return false;
+    ++i_;
+    bool meta_done = false, inv_done = !want_involved;
+    while (true) {
+      ws();
+      if (i_ >= n_ || s_[i_] == '}') return true;
+      if (s_[i_] != '"') return false;
+      bool esc;
+      std::string_view k = str(esc);
+      ws();
+      if (i_ >= n_ || s_[i_] != ':') return false;
+      ++i_;
+      ws();
+      if (!esc && k == "metadata" && i_ < n_ && s_[i_] == '{') {
+        ++i_;
+        while (true) {
+          ws();
+          if (i_ >= n_) return false;
+          if (s_[i_] == '}') {
+            ++i_;
+            break;
+          }
+          if (s_[i_] != '"') return false;
+          std::string_view mk = str(esc);
+          bool kesc = esc;
+          ws();
+          if (i_ >= n_ || s_[i_] != ':') return false;
+          ++i_;
+          ws();
+          if (!kesc && i_ < n_ && s_[i_] == '"' && (mk == "name" || mk == "resourceVersion")) {
+            std::string_view v = str(esc);
+            if (!esc) {
+              if (mk == "name") {
+                in.name = v;
+                in.has_name = true;
+              } else {
+                in.rv = v;
+                in.has_rv = true;
+              }
+            }
+          } else if (!kesc && mk == "labels" && i_ < n_ && s_[i_] == '{' && !job_label.empty()) {
+            const std::string_view keys[1] = {job_label};
+            std::string_view vals[1];
+            bool got[1] = {false};
+            members(keys, vals, got);
+            if (got[0]) {
+              in.job = vals[0];
+              in.has_job = true;
+            }
+          } else {
+            skip_value();
+          }
+          ws();
+          if (i_ < n_ && s_[i_] == ',') ++i_;
+        }
+        meta_done = true;
+      } else if (!esc && k == "involvedObject" && want_involved && i_ < n_ && s_[i_] == '{') {
+        static const std::string_view keys[2] = {"kind", "name"};
+        std::string_view vals[2];
+        bool got[2] = {false, false};
+        members(keys, vals, got);
+        if (got[0]) {
+          in.ikind = vals[0];
+          in.has_ikind = true;
+        }
+        if (got[1]) {
+          in.iname = vals[1];
+          in.has_iname = true;
+        }
+        inv_done = true;
+      } else {
+        skip_value();
+      }
+      if (meta_done && inv_done) return true;
+      ws();
+      if (i_ < n_ && s_[i_] == ',') ++i_;
+    }
+  }
+
   bool walk(const char* const* path, size_t depth, std::string_view& out) {
     ws();
     if (i_ >= n_ || s_[i_] != '{') return false;
@@ -892,6 +1061,7 @@ struct PodOwner {
 struct Owners {
   std::unordered_map<std::string, PodOwner> pod;
   std::deque<std::pair<double, std::string>> gone;
+  std::string tmp;  // lookup key buffer
 };
 
 typedef struct {
@@ -959,52 +1129,48 @@ int pod_owner_now(const Router* r, const PodOwner& po) {
   return po.worker;
 }
 
-int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
-  static const char* const P_TYPE[] = {"type"};
-  static const char* const E_NAME[] = {"object", "metadata", "name"};
-  static const char* const E_IKIND[] = {"object", "involvedObject", "kind"};
-  static const char* const E_INAME[] = {"object", "involvedObject", "name"};
-  const char* const* P_NAME = envelope ? E_NAME : E_NAME + 1;
-  const char* const* P_IKIND = envelope ? E_IKIND : E_IKIND + 1;
-  const char* const* P_INAME = envelope ? E_INAME : E_INAME + 1;
-  const size_t d = envelope ? 3 : 2;
-  Scan sc(s, n);
-  std::string_view v;
+int route_info(Router* r, int role, const Scan::Info& in, bool envelope) {
   if (role == ROLE_JOB) {
-    if (!sc.find(P_NAME, d, v)) return OWNER_ALL;  // BOOKMARK / ERROR / unparsable
-    if (!replica_owns_hash(r, replica_hash(r, v))) return OWNER_NONE;
-    return owner_of(r, v);
+    if (!in.has_name) return OWNER_ALL;  // BOOKMARK / ERROR / unparsable
+    if (!replica_owns_hash(r, replica_hash(r, in.name))) return OWNER_NONE;
+    return owner_of(r, in.name);
   }
   if (role == ROLE_POD) {
-    std::string_view name;
-    if (!sc.find(P_NAME, d, name)) return OWNER_ALL;
-    const char* E_JOB[] = {"object", "metadata", "labels", r->job_label->c_str()};
+    if (!in.has_name) return OWNER_ALL;
     PodOwner po{0, 0, false};
-    if (sc.find(envelope ? E_JOB : E_JOB + 1, d + 1, v)) po = PodOwner{owner_of(r, v), replica_hash(r, v), true};
-    std::string key(name);
-    r->owners->pod[key] = po;
-    std::string_view type;
-    if (envelope && sc.find(P_TYPE, 1, type) && type == "DELETED")
-      r->owners->gone.emplace_back(mono_s() + r->forget_after, key);
+    if (in.has_job) po = PodOwner{owner_of(r, in.job), replica_hash(r, in.job), true};
+    Owners& ow = *r->owners;
+    ow.tmp.assign(in.name.data(), in.name.size());  // reused buffer: no allocation for a known pod
+    auto it = ow.pod.find(ow.tmp);
+    if (it == ow.pod.end()) ow.pod.emplace(ow.tmp, po);
+    else it->second = po;
+    if (envelope && in.has_type && in.type == "DELETED") ow.gone.emplace_back(mono_s() + r->forget_after, ow.tmp);
     expire_owners(r);
     return pod_owner_now(r, po);
   }
   if (role == ROLE_EVENT) {
-    std::string_view kind;
-    if (!sc.find(P_IKIND, d, kind)) return OWNER_ALL;
-    if (!sc.find(P_INAME, d, v)) return OWNER_ALL;
-    if (kind == "Job") {
-      if (!replica_owns_hash(r, replica_hash(r, v))) return OWNER_NONE;
-      return owner_of(r, v);
+    if (!in.has_ikind || !in.has_iname) return OWNER_ALL;
+    if (in.ikind == "Job") {
+      if (!replica_owns_hash(r, replica_hash(r, in.iname))) return OWNER_NONE;
+      return owner_of(r, in.iname);
     }
-    if (kind == "Pod") {
-      auto it = r->owners->pod.find(std::string(v));
+    if (in.ikind == "Pod") {
+      Owners& ow = *r->owners;
+      ow.tmp.assign(in.iname.data(), in.iname.size());
+      auto it = ow.pod.find(ow.tmp);
       // unknown pod: everyone parks it until the pod shows up
-      return it == r->owners->pod.end() ? OWNER_ALL : pod_owner_now(r, it->second);
+      return it == ow.pod.end() ? OWNER_ALL : pod_owner_now(r, it->second);
     }
     return 0;
   }
   return OWNER_ALL;
+}
+
+int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
+  Scan sc(s, n);
+  Scan::Info in;
+  sc.envelope(envelope, role == ROLE_POD ? std::string_view(*r->job_label) : std::string_view(), role == ROLE_EVENT, in);
+  return route_info(r, role, in, envelope);
 }
 
 // true = this worker owns (or must see) the watch line
@@ -1211,8 +1377,6 @@ PyObject* bytes_list(const std::vector<std::string>& outs) {
 
 // feed(chunk) -> (per-worker NDJSON bytes, last resourceVersion or None, [error lines])
 PyObject* Splitter_feed(Splitter* self, PyObject* arg) {
-  static const char* const P_TYPE[] = {"type"};
-  static const char* const P_RV[] = {"object", "metadata", "resourceVersion"};
   Py_buffer view;
   if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) != 0) return nullptr;
   std::string& buf = *self->buf;
@@ -1234,9 +1398,15 @@ PyObject* Splitter_feed(Splitter* self, PyObject* arg) {
     if (n == 0 || (n == 1 && line[0] == '\r')) continue;
     ++self->lines;
     Scan sc(line, n);
-    std::string_view type, rv;
-    sc.find(P_TYPE, 1, type);
-    if (sc.find(P_RV, 3, rv)) last_rv.assign(rv.data(), rv.size());
+    Scan::Info in;
+    sc.envelope(true, self->role == ROLE_POD ? std::string_view(*r->job_label) : std::string_view(),
+                self->role == ROLE_EVENT, in);
+    std::string_view type = in.has_type ? in.type : std::string_view();
+    if (!in.has_type) {  // an envelope whose object came before its type: look the type up
+      static const char* const P_TYPE1[] = {"type"};
+      sc.find(P_TYPE1, 1, type);
+    }
+    if (in.has_rv) last_rv.assign(in.rv.data(), in.rv.size());
     if (type == "BOOKMARK") continue;
     if (type == "ERROR") {
       PyObject* b = PyBytes_FromStringAndSize(line, static_cast<Py_ssize_t>(n));
@@ -1248,7 +1418,7 @@ PyObject* Splitter_feed(Splitter* self, PyObject* arg) {
       Py_DECREF(b);
       continue;
     }
-    int owner = route_owner(r, self->role, line, n, true);
+    int owner = route_info(r, self->role, in, true);
     if (owner == OWNER_NONE) {
       ++r->foreign;
       continue;

@@ -84,7 +84,7 @@ def test_request_nowait_expires_by_sweep_and_resets_connection(arun):
             await f1
         with pytest.raises(HttpError):
             await f2  # same connection: its response order is unknown after a timeout
-        assert asyncio.get_running_loop().time() - t0 < 1.0
+        assert asyncio.get_running_loop().time() - t0 < 3.0  # 0.2 s deadline + sweep period, with CI load slack
         await asyncio.sleep(0.4)
         assert c._sweeper is None  # nothing pending: the sweep is not re-armed
         await c.close()
