@@ -8,6 +8,7 @@
 # gpurun_out/<step>*.log; the last line of each bench is echoed at the end.
 #
 #   build                 in-tree native build (normally already done on the CPU side)
+#   topo                  CPU / NUMA / cgroup layout and the GPU's PCI locality (gpurun_out/topo.log)
 #   tests[=EXPR]          pytest -m gpu (optionally -k EXPR), per-test 120 s timeout
 #   smoke                 __graft_entry__.smoke()
 #   bench[=ARGS]          python bench.py --steps ${BENCH_STEPS:-30} --warmup 2 ARGS
@@ -44,6 +45,14 @@ for step in "$@"; do
   case "$key" in
     build)
       python -m nexus_supervisor_amd._build > gpurun_out/build.log 2>&1 ;;
+    topo)
+      { lscpu; echo "== cpu.max"; cat /sys/fs/cgroup/cpu.max; echo "== cpuset";
+        cat /sys/fs/cgroup/cpuset.cpus.effective 2>/dev/null;
+        echo "== affinity"; python -c 'import os; print(sorted(os.sched_getaffinity(0)))';
+        for d in /sys/class/drm/card*/device; do echo "== $d $(readlink -f $d)";
+          cat $d/numa_node $d/local_cpulist 2>/dev/null; done;
+        timeout -k 10 120 python -c 'import torch; p=torch.cuda.get_device_properties(0); print("pci", p.pci_domain_id, p.pci_bus_id, p.pci_device_id)';
+      } > gpurun_out/topo.log 2>&1 ;;
     tests)
       if [ -n "$val" ]; then
         timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$val" \
