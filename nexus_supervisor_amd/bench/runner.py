@@ -323,7 +323,13 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         readback = await _read_back(harness, tracker)
         probe = None
         if cfg.probe_events > 0:
+            before = _stage_counts(sup)
             probe = await _latency_probe(harness, tracker, cfg)
+            if sync is not None:
+                await sync()
+            if probe.get("events"):
+                # where the open-loop latency goes: the stage histograms' growth over the probe
+                probe["stages_ms"] = _stage_delta(before, _stage_counts(sup))
     finally:
         if sampler is not None:
             sampler.stop()
@@ -395,11 +401,48 @@ def _actuation(sc: SupervisorConfig) -> str:
     return "read+write" + (" (ToRunning conditional)" if cu == "auto" else " (conditional)" if cu == "always" else "")
 
 
+STAGES = ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_prepare", "stage_write",
+          "stage_delete")
+
+
+def _stage_counts(sup) -> Dict[str, Tuple[Dict[int, int], int, int]]:
+    """Bucket counts, total and sum of every stage histogram (cumulative, merged over workers)."""
+    out = {}
+    for name in STAGES:
+        h = sup.metrics.histogram(name)
+        if h is not None:
+            out[name] = ({int(i): int(c) for i, c in h.sparse()}, int(h.total), int(h.sum))
+    return out
+
+
+def _stage_delta(before, after) -> Dict[str, Any]:
+    """Stage summaries (ms) of what was recorded between two :func:`_stage_counts`
+    snapshots; min / max are the bounds of the outermost non-empty buckets."""
+    from ..obs.histogram import PyLatencyHistogram
+
+    out = {}
+    for name, (counts, total, hsum) in after.items():
+        b_counts, b_total, b_sum = before.get(name, ({}, 0, 0))
+        h = PyLatencyHistogram()
+        for i, c in counts.items():
+            d = c - b_counts.get(i, 0)
+            if d > 0 and i < len(h.counts):
+                h.counts[i] = d
+        nz = [i for i, c in enumerate(h.counts) if c]
+        h.total = sum(h.counts)
+        if not nz or total - b_total <= 0:
+            continue
+        h.sum = hsum - b_sum
+        h.min = h._bounds(nz[0])[0]
+        h.max = h._bounds(nz[-1])[1] - 1
+        out[name] = {k: (int(v) if k == "count" else round(v / 1000.0, 3)) for k, v in h.summary().items()}
+    return out
+
+
 def _stage_breakdown(sup) -> Dict[str, Any]:
     m = sup.metrics
     out = {}
-    for name in ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_prepare", "stage_write",
-                 "stage_delete"):
+    for name in STAGES:
         h = m.histogram(name)
         if h is not None:
             out[name] = {k: (int(v) if k == "count" else round(v / 1000.0, 3)) for k, v in h.summary().items()}

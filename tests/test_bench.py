@@ -194,3 +194,21 @@ def test_bench_two_ranks_per_rank_clusters_and_poisson_probe():
     assert out["config"]["cluster"] == "per-rank"
     probe = out["latency_at_rate"]
     assert probe["events"] == 40 and probe["arrivals"] == "poisson" and probe["p99_ms"] >= probe["p50_ms"] > 0
+
+
+def test_probe_stage_delta_counts_only_what_the_probe_recorded():
+    """The probe's stage breakdown is the growth of the cumulative stage histograms."""
+    from nexus_supervisor_amd.bench.runner import _stage_counts, _stage_delta
+    from nexus_supervisor_amd.obs.metrics import Metrics
+
+    m = Metrics("t")
+    sup = type("S", (), {"metrics": m})()
+    for _ in range(1000):
+        m.observe_seconds("stage_read", 0.050)  # saturated steps: 50 ms reads
+    before = _stage_counts(sup)
+    for v in (0.0002, 0.0003, 0.0004):
+        m.observe_seconds("stage_read", v)  # the probe: sub-millisecond reads
+    d = _stage_delta(before, _stage_counts(sup))
+    assert d["stage_read"]["count"] == 3
+    assert 0.19 < d["stage_read"]["p50"] < 0.32 and d["stage_read"]["max"] < 0.41
+    assert "stage_write" not in d
