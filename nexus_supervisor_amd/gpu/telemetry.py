@@ -413,6 +413,23 @@ def _links_of(g: Dict[str, Any]) -> Optional[List[Dict[str, Any]]]:
     return out
 
 
+class _LazyLinks(dict):
+    """GPU index → :func:`_links_of`, computed on first use per snapshot: a failure asks for
+    the links of the one or two GPUs its pod used, not all eight (at a low failure rate
+    every decision meets a fresh snapshot, and the eager table was most of its cost)."""
+
+    __slots__ = ("_by_index",)
+
+    def __init__(self, snap: Iterable[Dict[str, Any]]):
+        super().__init__()
+        self._by_index = {g["index"]: g for g in snap}
+
+    def __missing__(self, index: int):
+        g = self._by_index.get(index)
+        v = self[index] = _links_of(g) if g is not None else None
+        return v
+
+
 def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterable[int] = (), pids: Iterable[int] = (),
                  lookback: float = 300.0, now: Optional[float] = None, node: str = "",
                  snapshot: Optional[List[Dict[str, Any]]] = None,
@@ -457,7 +474,7 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
             rec["xgmi_error"] = g["xgmi_error"]
         if g.get("xgmi_hive_id"):
             rec["xgmi_hive_id"] = g["xgmi_hive_id"]
-        glinks = links[g["index"]] if links is not None and g["index"] in links else _links_of(g)
+        glinks = links[g["index"]] if links is not None else _links_of(g)
         if glinks is not None:
             rec["links"] = glinks
         if g.get("foreign_procs"):
@@ -503,7 +520,7 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
                 if u:
                     by_uid.setdefault(u, set()).add(g["index"])
         cache.update(t=now, wall=time.time(), snap=snap, by_uid=by_uid, by_index={g["index"]: g for g in snap},
-                     links={g["index"]: _links_of(g) for g in snap}, memo={})
+                     links=_LazyLinks(snap), memo={})
 
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         topo = topology_from_pod(pod, gpu_resource)

@@ -26,7 +26,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from nexus_supervisor_amd.bench.runner import BenchConfig, supervisor_config  # noqa: E402
+from nexus_supervisor_amd.bench.runner import BenchConfig, _stage_counts, _stage_delta, supervisor_config  # noqa: E402
 from nexus_supervisor_amd.bench.workload import Workload  # noqa: E402
 from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry, pod_evidence_provider  # noqa: E402
 from nexus_supervisor_amd.informer import InformerFactory  # noqa: E402
@@ -168,9 +168,12 @@ async def run(args) -> dict:
         lws = [inf.lw for inf in factory.informers.values()]
         d0 = sum(lw.decode_seconds for lw in lws)
         l0 = {inf.kind: inf.lw.decoded_lines for inf in factory.informers.values()}
+        stages0 = _stage_counts(sup)
         c0, t0, n = time.thread_time(), time.perf_counter(), 0
         for data in batch:
             n += await step(data)
+            if args.gap:
+                await asyncio.sleep(args.gap)
         cpu, wall = time.thread_time() - c0, time.perf_counter() - t0
         gc.callbacks.remove(gc_cb)
         if prof is not None:
@@ -185,7 +188,8 @@ async def run(args) -> dict:
                         "lines_per_event": {inf.kind: round((inf.lw.decoded_lines - l0[inf.kind]) / n, 2)
                                             for inf in factory.informers.values()},
                         "gc_us_per_event": {g: round(1e6 * gc_t[g] / n, 2) for g in gc_t},
-                        "gc_collections": dict(gc_n)})
+                        "gc_collections": dict(gc_n),
+                        "stages_ms": _stage_delta(stages0, _stage_counts(sup))})
         del batch
         if args.sizes:
             results[-1]["containers"] = sorted(_containers(sup), reverse=True)[:12]
@@ -205,6 +209,9 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--pprof", default="")
     ap.add_argument("--cprofile", default="")
+    ap.add_argument("--gap", type=float, default=0.0,
+                    help="idle seconds between steps (low-rate mode: with --events 1, what one failure costs when "
+                         "nothing is batched and every telemetry snapshot is stale)")
     ap.add_argument("--sizes", action="store_true", help="report the supervisor's large containers per repeat")
     args = ap.parse_args(argv)
     out = asyncio.run(run(args))
