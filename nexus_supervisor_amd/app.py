@@ -80,8 +80,13 @@ class Application:
         self.kube = kube
         self.store = store if store is not None else build_store(cfg)
         self.factory = factory if factory is not None else build_factory(cfg, kube)
-        self.supervisor = Supervisor(cfg, self.store, jobs if jobs is not None else kube, self.factory,
-                                     logger=self.log, metrics=self.metrics)
+        jobs = jobs if jobs is not None else kube
+        if cfg.dry_run:
+            from .dryrun import DryRunJobs, DryRunStore
+
+            self.store = DryRunStore(self.store, self.log, self.metrics)
+            jobs = DryRunJobs(jobs, self.log, self.metrics)
+        self.supervisor = Supervisor(cfg, self.store, jobs, self.factory, logger=self.log, metrics=self.metrics)
         self.telemetry = telemetry
         self.elector = None
         self.shard_leases = None
@@ -92,6 +97,8 @@ class Application:
         cfg = self.cfg
         self.log.info("Starting Nexus Supervisor", version=__version__, build=__build__, namespace=cfg.resource_namespace,
                       store=cfg.cql_store_type)
+        if cfg.dry_run:
+            self.log.warning("dry run: checkpoints are read but never written, Jobs are never deleted")
         await self.store.connect()
         if self.telemetry is None and cfg.gpu.attribution_enabled and cfg.gpu.local_telemetry:
             from .gpu.telemetry import make_telemetry

@@ -296,6 +296,9 @@ class SupervisorConfig:
     # issue the Job DELETE after the checkpoint write without holding a worker (retried
     # in the background with the failure backoff); false = delete inside the worker
     async_job_delete: bool = field(default=True, metadata=_k("async-job-delete"))
+    # shadow mode for a migration: classify and decide as usual, read checkpoints, but never
+    # write a row or delete a Job — each would-be action is logged and counted (dry_run_*)
+    dry_run: bool = field(default=False, metadata=_k("dry-run"))
     compat: CompatConfig = field(default_factory=CompatConfig, metadata=_k("compat"))
     labels: LabelConfig = field(default_factory=LabelConfig, metadata=_k("labels"))
     stages: StagesConfig = field(default_factory=StagesConfig, metadata=_k("stages"))

@@ -195,3 +195,12 @@ def test_role_name_override_and_log_tail_access():
     mounts = {m["mountPath"]: m for m in ds["containers"][0]["volumeMounts"]}
     assert mounts["/var/log/pods"]["readOnly"] is True
     assert {e["name"]: e.get("value") for e in ds["containers"][0]["env"]}["NEXUS_AGENT_LOG_ROOT"] == "/var/log/pods"
+
+
+def test_dry_run_value_renders_shadow_mode():
+    def cfg_of(values=None):
+        env = _env(_by_kind(render_docs(CHART, values=values))["Deployment"][0]["spec"]["template"]["spec"]["containers"][0])
+        return load_config(path=None, env={k: v for k, v in env.items() if k.startswith("NEXUS__") and v is not None})
+
+    assert cfg_of().dry_run is False
+    assert cfg_of({"supervisor": {"config": {"dryRun": True}}}).dry_run is True
