@@ -5,6 +5,7 @@
 ``worker``      one shard-worker process (spawned by the supervisor when
                 ``runtime.worker-processes`` > 1; not started by hand)
 ``config``      print the effective configuration (secrets masked)
+``explain``     what the supervisor would decide for ``kubectl get … -o json`` output, and why
 ``build``       build the native components in-tree
 ``cqlsrv``      run the native in-memory CQL server (tests / local runs)
 ``version``     print the version
@@ -51,6 +52,10 @@ def main(argv=None) -> int:
 
         print(json.dumps(redacted(load_config()), indent=2, default=str))
         return 0
+    if cmd == "explain":
+        from .explain import main as explain
+
+        return explain(argv)
     if cmd == "build":
         from ._build import main as build
 
