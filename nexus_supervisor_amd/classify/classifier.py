@@ -25,7 +25,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..config.schema import GpuConfig, LabelConfig, RulesConfig
-from ..gpu import logtail
+from ..gpu import collective, logtail
 from ..gpu import oom as oom_mod
 from ..gpu.telemetry import FAULT_EVENTS
 from ..gpu.topology import merge_process_ranks, resolve_devices, topology_from_pod, xgmi_from_evidence
@@ -438,6 +438,33 @@ class Classifier:
         while len(self.log_cache) > 4096:
             self.log_cache.popitem(last=False)
 
+    def _root_cause(self, pods: List[Dict[str, Any]]) -> Tuple[Optional[Dict[str, Any]], Dict[str, Any]]:
+        """Culprit pod and the ``ranks`` trace block of a multi-pod job (:mod:`..gpu.collective`):
+        the rank that ran out of memory or failed on its own, not one that died of its
+        collective's collateral."""
+        recs = []
+        by_name: Dict[str, Dict[str, Any]] = {}
+        for p in pods:
+            terms = list(kube.terminated_states(p))
+            if not terms:
+                continue
+            topo, gev = self._pod_ctx(p)
+            texts = [(f"termination message of container {t.get('container', '')}", t["message"])
+                     for t in terms if t.get("message")] + self._log_texts(p, gev)
+            if any(oom_mod.hbm_signature(x) for _s, x in texts):
+                kind = "hbm"
+            elif any(t.get("reason") == "OOMKilled" for t in terms) or any(oom_mod.host_signature(x) for _s, x in texts):
+                kind = "host"
+            else:
+                kind = None
+            name = kube.name_of(p)
+            rec = collective.pod_failure(name, terms, texts, kind, bool(self._gpu_faults(p)), topo.get("rank"))
+            if rec is not None:
+                recs.append(rec)
+                by_name[name] = p
+        culprit, block = collective.rank_summary(recs)
+        return (by_name[culprit["pod"]] if culprit else None), block
+
     def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
         if not self.gpu.attribution_enabled:
             return
@@ -445,6 +472,13 @@ class Classifier:
         key = res.key
         if pods:
             pod = pods[-1]
+            if len(pods) > 1:
+                culprit, block = self._root_cause(pods)
+                if culprit is not None:
+                    pod = culprit  # its topology maps the failing GPU, its evidence attributes it
+                    res.evidence["ranks"] = block
+                    if block["all_collective"] and res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE):
+                        res.failure_class = F.COLLECTIVE
             # a container that never started (image pull / config / scheduling) never touched a GPU
             want_gpu = res.failure_class not in NO_GPU_CLASSES
             topo, gev = self._pod_ctx(pod, want_gpu)
@@ -466,7 +500,7 @@ class Classifier:
             verdict = oom_mod.analyze(texts, (), None, None, self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
         if verdict is not None and verdict.kind:
             res.evidence["oom"] = verdict.as_dict()
-            if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.CRASH_LOOP):
+            if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.CRASH_LOOP, F.COLLECTIVE):
                 res.failure_class = F.HBM_OOM if verdict.kind == "hbm" else F.HOST_OOM
         if res.action != A.TO_RUNNING:
             self._apply_history(res)
@@ -487,16 +521,25 @@ class Classifier:
         been; this costs no extra latency."""
         if not self.gpu.attribution_enabled or res.action == A.TO_RUNNING or res.object_kind != "Job":
             return
-        if res.failure_class in (F.BACKOFF_LIMIT, F.FATAL, F.NONE):
+        if res.failure_class in (F.BACKOFF_LIMIT, F.FATAL, F.NONE, F.COLLECTIVE):
             pods = lookup.pods_of_job(res.request_id)
             for pod in pods:
                 st = pod.get("status") or {}
                 if st.get("reason") == "Evicted" or self._disruption(pod):
                     self.evidence.add(res.key, {"kind": "evicted", "message": st.get("message", ""), "pod": kube.name_of(pod)})
+            culprit = pods[-1] if pods else None
+            if len(pods) > 1:
+                # the pods' last updates may have landed after the Job's: rank them again
+                c, block = self._root_cause(pods)
+                if c is not None:
+                    culprit = c
+                    res.evidence["ranks"] = block
+                    if block["all_collective"] and res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE):
+                        res.failure_class = F.COLLECTIVE
             if pods and "oom" not in res.evidence:
                 terms = [t for p in pods for t in kube.terminated_states(p)]
                 if terms:
-                    topo, gev = self._pod_ctx(pods[-1])
+                    topo, gev = self._pod_ctx(culprit)
                     ltexts = [x for p in pods for x in self._log_texts(p, self._pod_ctx(p)[1])]
                     v = oom_mod.analyze(ltexts, terms, gev, topo.get("expected_gpu"),
                                         self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction, topo=topo)
@@ -596,12 +639,15 @@ def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
         ("gpu.procs:1", lambda: [g.__setitem__("procs", (g.get("procs") or [])[:1]) for g in gpus()]),
         ("gpu.events:2", lambda: [g.__setitem__("events", (g.get("events") or [])[-2:]) for g in gpus() if "events" in g]),
         ("history:4", lambda: d.__setitem__("history", (d.get("history") or [])[-4:]) if "history" in d else None),
+        ("ranks.pods:2", lambda: (d.get("ranks") or {}).__setitem__("pods", (d.get("ranks") or {}).get("pods", [])[:2])
+         if (d.get("ranks") or {}).get("pods") else None),
         ("topology.collective_env", lambda: topo.pop("collective_env", None)),
         ("logs.lines:1", lambda: [r.__setitem__("lines", [x[-300:] for x in (r.get("lines") or [])[-1:]])
                                   for r in (d.get("logs") or []) + ((d.get("gpu") or {}).get("logs") or [])]),
         ("oom.signals:4", lambda: (d.get("oom") or {}).__setitem__("signals", (d.get("oom") or {}).get("signals", [])[:4])
          if d.get("oom") else None),
         ("topology.rank_map", lambda: topo.pop("rank_map", None)),
+        ("ranks.pods", lambda: (d.get("ranks") or {}).pop("pods", None)),
         ("gpu.procs", lambda: [g.pop("procs", None) for g in gpus()]),
         ("gpu.events", lambda: [g.pop("events", None) for g in gpus()]),
         ("gpu.gpus:slim", lambda: [slim(g) for g in gpus()]),

@@ -36,6 +36,7 @@ class FailureClass:
     BACKOFF_LIMIT = "backoff-limit"      # BackoffLimitExceeded
     FATAL = "fatal"                      # PodFailurePolicy / other fatal exit
     CONFIG = "config"                    # CreateContainerConfigError
+    COLLECTIVE = "collective"            # every failed rank shows only RCCL / collective errors
 
 
 @dataclass
