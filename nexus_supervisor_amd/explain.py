@@ -106,9 +106,9 @@ def explain(objs: List[Dict[str, Any]], cfg: SupervisorConfig) -> List[Dict[str,
                 d["algorithm_failure_cause"] = R.failure_cause(r.action, r.run_status_message,
                                                                cfg.compat.doubled_fatal_cause)
                 d["algorithm_failure_details"] = render_trace(r, cfg.rules.trace_format, cfg.rules.trace_max_bytes)
-            oom = r.evidence.get("oom")
-            if oom:
-                d["oom"] = oom
+            for k in ("oom", "ranks"):  # the OOM verdict's signals; a multi-rank job's culprit
+                if r.evidence.get(k):
+                    d[k] = r.evidence[k]
             decisions.append(d)
         if decisions:
             rec["decisions"] = decisions
