@@ -465,6 +465,21 @@ class Classifier:
         culprit, block = collective.rank_summary(recs)
         return (by_name[culprit["pod"]] if culprit else None), block
 
+    def _apply_ranks(self, res: RunStatusAnalysisResult, pods: List[Dict[str, Any]]) -> Optional[Dict[str, Any]]:
+        """Record the ``ranks`` block of a multi-pod decision and refine a generic failure
+        class from it (every rank collective-only → ``collective``; a culprit with GPU fault
+        evidence, e.g. an xGMI link down → ``gpu-fault``); returns the culprit pod."""
+        culprit, block = self._root_cause(pods)
+        if culprit is None:
+            return None
+        res.evidence["ranks"] = block
+        if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.COLLECTIVE):
+            if block["all_collective"]:
+                res.failure_class = F.COLLECTIVE
+            elif block["culprit"]["kind"] == "gpu-fault":
+                res.failure_class = F.GPU_FAULT
+        return culprit
+
     def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
         if not self.gpu.attribution_enabled:
             return
@@ -473,12 +488,8 @@ class Classifier:
         if pods:
             pod = pods[-1]
             if len(pods) > 1:
-                culprit, block = self._root_cause(pods)
-                if culprit is not None:
-                    pod = culprit  # its topology maps the failing GPU, its evidence attributes it
-                    res.evidence["ranks"] = block
-                    if block["all_collective"] and res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE):
-                        res.failure_class = F.COLLECTIVE
+                # the culprit's topology maps the failing GPU, its evidence attributes it
+                pod = self._apply_ranks(res, pods) or pod
             # a container that never started (image pull / config / scheduling) never touched a GPU
             want_gpu = res.failure_class not in NO_GPU_CLASSES
             topo, gev = self._pod_ctx(pod, want_gpu)
@@ -530,12 +541,7 @@ class Classifier:
             culprit = pods[-1] if pods else None
             if len(pods) > 1:
                 # the pods' last updates may have landed after the Job's: rank them again
-                c, block = self._root_cause(pods)
-                if c is not None:
-                    culprit = c
-                    res.evidence["ranks"] = block
-                    if block["all_collective"] and res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE):
-                        res.failure_class = F.COLLECTIVE
+                culprit = self._apply_ranks(res, pods) or culprit
             if pods and "oom" not in res.evidence:
                 terms = [t for p in pods for t in kube.terminated_states(p)]
                 if terms:

@@ -94,3 +94,18 @@ def test_trace_with_many_ranks_stays_bounded():
     assert r.evidence["ranks"]["pods_total"] == 64 and len(r.evidence["ranks"]["pods"]) == 7
     out = render_trace(r, max_bytes=2048)
     assert len(out.encode()) <= 2048 and json.loads(out)["class"] == "collective"
+
+
+def test_xgmi_link_down_rank_makes_a_gpu_fault():
+    """A rank whose node agent saw its xGMI link go down is the culprit of the others'
+    collective timeouts: the Job-level decision is a GPU fault, not a generic one."""
+    ev = {"source": "agent", "gpus": [{"index": 1, "vram_total_mb": 294896, "vram_peak_mb": 1000, "procs": [],
+                                       "events": [{"type": "XGMI_LINK_DOWN", "t": 1.0, "message": "1/7 xGMI links down"}]}]}
+    bad = _rank_pod(1, "RuntimeError: NCCL communicator was aborted", finished="2026-10-17T10:00:05Z")
+    bad["metadata"]["annotations"] = {"nexus.amd.com/gpu-evidence": json.dumps(ev)}
+    pods = [_rank_pod(0, WATCHDOG.format(r=0), finished="2026-10-17T10:00:01Z"), bad]
+    _s, [r] = Classifier(LABELS).classify_event(make_event("Job", RUN, "BackoffLimitExceeded", "limit"),
+                                                _Lookup(make_job(RUN, LABELS), pods))
+    assert r.failure_class == F.GPU_FAULT
+    assert r.evidence["ranks"]["culprit"]["rank"] == 1 and r.evidence["ranks"]["culprit"]["kind"] == "gpu-fault"
+    assert r.evidence["ranks"]["culprit"]["collective"].startswith("NCCL communicator was aborted")
