@@ -145,16 +145,34 @@ class _V:
         return self.level <= self.parent.verbosity
 
 
+try:
+    from asyncio import _get_running_loop as _running_loop  # C accessor: no exception when there is none
+except ImportError:  # pragma: no cover
+    def _running_loop():
+        return None
+
+
 class BufferedStreamHandler(logging.StreamHandler):
     """``StreamHandler`` that does not flush per record: ``StreamHandler.emit`` flushes the
     stream after every line, one ``write`` syscall per decision logged at V(0).  Lines go
-    into the stream's buffer and are flushed at most ``interval`` seconds later (a timer
-    armed by the first unflushed line), at WARNING and above immediately, and on shutdown."""
+    into the stream's buffer and are flushed at most ``interval`` seconds later, at WARNING
+    and above immediately, and on shutdown.
+
+    On an asyncio loop the delayed flush is a ``call_later`` timer; elsewhere one long-lived
+    flusher thread does it and a line that dirties a clean buffer only sets an event.
+    (A ``threading.Timer`` per flush window started a thread
+    for the first line of every window: at the north-star churn — a decision every ~60 ms,
+    a window every few lines — that was ~130 µs of thread start-up on an MI355X host in
+    front of every logged decision's queueing, the largest item of an event-driven
+    decision's classification stage.)"""
 
     def __init__(self, stream=None, interval: float = 0.2):
         super().__init__(stream)
         self.interval = interval
-        self._timer: Optional[threading.Timer] = None
+        self._dirty = False
+        self._closed = False
+        self._wake = threading.Event()
+        self._flusher: Optional[threading.Thread] = None
 
     def emit(self, record: logging.LogRecord) -> None:
         try:
@@ -167,20 +185,42 @@ class BufferedStreamHandler(logging.StreamHandler):
             return
         if record.levelno >= logging.WARNING or self.interval <= 0:
             self.flush()
-        elif self._timer is None:
-            t = threading.Timer(self.interval, self._timed_flush)
-            t.daemon = True
-            self._timer = t
-            t.start()
+        elif not self._dirty:
+            self._dirty = True
+            loop = _running_loop()
+            if loop is not None:
+                # on an event loop (the supervisor's): a timer handle, no thread wake-up
+                loop.call_later(self.interval, self._loop_flush)
+                return
+            if self._flusher is None or not self._flusher.is_alive():
+                # (re)started lazily: also after a fork, whose child has no such thread
+                self._flusher = threading.Thread(target=self._run, name="log-flush", daemon=True)
+                self._flusher.start()
+            self._wake.set()
 
-    def _timed_flush(self) -> None:
-        self._timer = None
-        self.flush()
+    def _loop_flush(self) -> None:
+        self._dirty = False
+        try:
+            self.flush()
+        except Exception:  # noqa: BLE001 - e.g. the stream was closed under us
+            pass
+
+    def _run(self) -> None:
+        while not self._closed:
+            self._wake.wait()
+            self._wake.clear()
+            if self._closed:
+                break
+            time.sleep(self.interval)
+            self._dirty = False  # before the flush: a line written from here on re-arms
+            try:
+                self.flush()
+            except Exception:  # noqa: BLE001 - e.g. the stream was closed under us
+                pass
 
     def close(self) -> None:
-        t, self._timer = self._timer, None
-        if t is not None:
-            t.cancel()
+        self._closed = True
+        self._wake.set()
         self.flush()
         super().close()
 

@@ -2,10 +2,9 @@
 parity scenarios over HTTP watch + CQL decide exactly as they do live, but no row is
 written and no Job is deleted; each would-be action is logged and counted."""
 import datetime as dt
-import io
 
 from nexus_supervisor_amd.dryrun import DryRunJobs, DryRunStore
-from nexus_supervisor_amd.obs.logging import configure_logging
+from nexus_supervisor_amd.obs.logging import KLogger
 from nexus_supervisor_amd.obs.metrics import Metrics
 from nexus_supervisor_amd.store.memory import MemoryStore
 from nexus_supervisor_amd.testing.inproc import RecordingJobs
@@ -24,7 +23,7 @@ def test_dry_run_store_answers_like_the_store_without_writing(arun):
     async def go():
         inner = MemoryStore(seed_rows())
         m = Metrics("t")
-        log = configure_logging("INFO", stream=io.StringIO())
+        log = KLogger()  # (configure_logging would detach the package logger from caplog for later tests)
         s = DryRunStore(inner, log, m)
         running = next(r for r in seed_rows() if r.lifecycle_stage == "RUNNING")
         cancelled = next(r for r in seed_rows() if r.lifecycle_stage == "CANCELLED")

@@ -271,3 +271,50 @@ def test_native_histogram_matches_python():
     assert both.counts == ref.counts and (both.total, both.sum, both.min, both.max) == (ref.total, ref.sum, ref.min, ref.max)
     both.reset()
     assert both.total == 0 and both.min is None and both.percentile(99) == 0.0
+
+
+def test_buffered_log_handler_flushes_late_without_a_thread_per_window(arun):
+    """Lines are flushed within the interval — by a loop timer on an event loop, by one
+    long-lived flusher thread elsewhere — and no thread is started per flush window (a
+    threading.Timer per window cost ~130 µs of thread start-up per decision at 1000
+    failures/min)."""
+    import asyncio
+    import io
+    import logging
+    import threading
+    import time as _t
+
+    from nexus_supervisor_amd.obs.logging import BufferedStreamHandler, JsonFormatter
+
+    class Stream(io.StringIO):
+        flushed = 0
+
+        def flush(self):
+            Stream.flushed += 1
+
+    s = Stream()
+    h = BufferedStreamHandler(s, interval=0.05)
+    h.setFormatter(JsonFormatter())
+    lg = logging.getLogger("test_buffered_handler")
+    lg.propagate = False
+    lg.addHandler(h)
+    lg.setLevel(logging.INFO)
+    try:
+        before = threading.active_count()
+        for _ in range(3):  # off-loop: one flusher thread, reused
+            lg.info("x")
+            _t.sleep(0.12)
+        assert Stream.flushed >= 3 and threading.active_count() <= before + 1
+
+        async def on_loop():
+            n0, threads = Stream.flushed, threading.active_count()
+            for _ in range(3):
+                lg.info("y")
+                await asyncio.sleep(0.12)
+            assert Stream.flushed >= n0 + 3 and threading.active_count() == threads
+
+        arun(on_loop())
+        assert s.getvalue().count("\n") == 6
+    finally:
+        lg.removeHandler(h)
+        h.close()
