@@ -474,7 +474,8 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
             rec["xgmi_error"] = g["xgmi_error"]
         if g.get("xgmi_hive_id"):
             rec["xgmi_hive_id"] = g["xgmi_hive_id"]
-        glinks = links[g["index"]] if links is not None else _links_of(g)
+        glinks = (links[g["index"]] if links is not None and (type(links) is _LazyLinks or g["index"] in links)
+                  else _links_of(g))
         if glinks is not None:
             rec["links"] = glinks
         if g.get("foreign_procs"):
