@@ -514,6 +514,11 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
 
     def refresh(now: float) -> None:
         snap = telemetry.snapshot(True)
+        if snap is cache["snap"]:
+            # a mirror (RemoteTelemetry) hands back the same list until its owner's next
+            # update, which also carries the new VRAM samples: tables and memo stay exact
+            cache["t"] = now
+            return
         by_uid: Dict[str, set] = {}
         for g in snap:
             for p in g.get("procs", ()):

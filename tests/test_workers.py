@@ -414,6 +414,32 @@ def test_remote_telemetry_mirror_matches_owner():
     assert len(mirror._hist[1]) == 2 and mirror.updates == 2
 
 
+def test_evidence_provider_reuses_an_unchanged_mirror_snapshot():
+    """A mirror returns the same snapshot list until its owner's next update: the
+    provider keeps its per-snapshot memo across ttl expiries, and an update (which
+    brings new VRAM samples too) rebuilds it."""
+    import time
+
+    from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry, RemoteTelemetry, pod_evidence_provider, telemetry_message
+
+    owner = FakeTelemetry(n_gpus=2)
+    mirror = RemoteTelemetry(interval=0.01)
+    since = {}
+    owner.set_vram(1, 1000, t=time.time() - 1)
+    mirror.update(json.loads(json.dumps(telemetry_message(owner, since))))
+    prov = pod_evidence_provider(mirror)
+    pod = make_pod("r", LabelConfig(), env={"LOCAL_RANK": "1", "HIP_VISIBLE_DEVICES": "0,1"}, gpus=1)
+    a = prov(pod)
+    time.sleep(0.02)  # past the ttl, same snapshot object
+    b = prov(pod)
+    assert a["gpus"] is b["gpus"] and a["gpus"][0]["vram_peak_mb"] == 1000
+    owner.set_vram(1, 290000)
+    mirror.update(json.loads(json.dumps(telemetry_message(owner, since))))
+    time.sleep(0.02)
+    c = prov(pod)
+    assert c["gpus"] is not a["gpus"] and c["gpus"][0]["vram_peak_mb"] == 290000
+
+
 @pytest.mark.slow
 def test_worker_gpu_evidence_from_parent_monitor(arun, tmp_path):
     """Node-local attribution with worker processes: one monitor in the parent, mirrored into
