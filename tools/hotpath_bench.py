@@ -26,7 +26,16 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from nexus_supervisor_amd.bench.runner import BenchConfig, _stage_counts, _stage_delta, supervisor_config  # noqa: E402
+from nexus_supervisor_amd.bench.runner import BenchConfig, supervisor_config  # noqa: E402
+
+try:  # absent from older trees (the harness is also run against _ab/base snapshots)
+    from nexus_supervisor_amd.bench.runner import _stage_counts, _stage_delta  # noqa: E402
+except ImportError:  # pragma: no cover
+    def _stage_counts(sup):
+        return {}
+
+    def _stage_delta(before, after):
+        return {}
 from nexus_supervisor_amd.bench.workload import Workload  # noqa: E402
 from nexus_supervisor_amd.gpu.telemetry import FakeTelemetry, pod_evidence_provider  # noqa: E402
 from nexus_supervisor_amd.informer import InformerFactory  # noqa: E402
