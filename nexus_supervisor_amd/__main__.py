@@ -6,6 +6,7 @@
                 ``runtime.worker-processes`` > 1; not started by hand)
 ``config``      print the effective configuration (secrets masked)
 ``explain``     what the supervisor would decide for ``kubectl get … -o json`` output, and why
+``shadow-report`` how a dry-run (shadow) supervisor's decisions agree with the checkpoint store
 ``build``       build the native components in-tree
 ``cqlsrv``      run the native in-memory CQL server (tests / local runs)
 ``version``     print the version
@@ -56,6 +57,10 @@ def main(argv=None) -> int:
         from .explain import main as explain
 
         return explain(argv)
+    if cmd == "shadow-report":
+        from .shadow import main as shadow_report
+
+        return shadow_report(argv)
     if cmd == "build":
         from ._build import main as build
 

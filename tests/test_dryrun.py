@@ -2,6 +2,7 @@
 parity scenarios over HTTP watch + CQL decide exactly as they do live, but no row is
 written and no Job is deleted; each would-be action is logged and counted."""
 import datetime as dt
+import io
 
 from nexus_supervisor_amd.dryrun import DryRunJobs, DryRunStore
 from nexus_supervisor_amd.obs.logging import KLogger
@@ -72,3 +73,57 @@ def test_reference_scenarios_in_dry_run_touch_nothing(arun):
             await api.stop()
 
     arun(go(), timeout=60)
+
+
+def test_shadow_report_compares_the_shadow_log_with_the_store(arun):
+    """The shadow run's log lines against the rows the acting supervisor wrote: agreement,
+    differences (with the shadow's failure class), runs the other side has not finished."""
+    import logging
+
+    from nexus_supervisor_amd.obs.logging import JsonFormatter
+    from nexus_supervisor_amd.shadow import parse_shadow_log, report
+
+    scenarios = reference_scenarios()
+    buf = io.StringIO()
+    h = logging.StreamHandler(buf)
+    h.setFormatter(JsonFormatter())
+    pkg = logging.getLogger("nexus_supervisor_amd")
+    pkg.addHandler(h)
+    level = pkg.level
+    pkg.setLevel(logging.INFO)
+
+    async def go():
+        objs = [o for s in scenarios for o in s.objects]
+        api, srv, app, store, decisions = await _wire_cluster(objs, cfg=_cfg(**{"dry-run": True}))
+        try:
+            await _settle(app, decisions, 8)
+            shadow = parse_shadow_log(buf.getvalue().splitlines())
+            expected = {rid: st for s in scenarios for rid, st in s.expected.items()}
+            assert {rid for _a, rid in shadow} == {rid for rid, st in expected.items()
+                                                   if st != next(r.lifecycle_stage for r in seed_rows() if r.id == rid)}
+            # the "reference" acts: it agrees on all runs but one, which it marks differently,
+            # and has not got to another yet
+            keys = sorted(shadow)
+            other, pending = keys[0], keys[1]
+            for alg, rid in keys:
+                if rid == pending[1]:
+                    continue
+                stage = shadow[(alg, rid)]["stage"]
+                if rid == other[1]:
+                    stage = "FAILED" if stage == "DEADLINE_EXCEEDED" else "DEADLINE_EXCEEDED"
+                await store.update_status(alg, rid, stage, "c", "d", NOW)
+            rep = await report(shadow, store)
+            assert rep["runs"] == len(keys) and rep["differ"] == 1 and rep["missing"] == 0
+            assert rep["agree"] + rep["unfinished"] == len(keys) - 1
+            assert rep["differences"][0]["request_id"] == other[1]
+            assert rep["agreement"] == round(rep["agree"] / (rep["agree"] + 1), 4)
+        finally:
+            await app.stop()
+            srv.stop()
+            await api.stop()
+
+    try:
+        arun(go(), timeout=60)
+    finally:
+        pkg.removeHandler(h)
+        pkg.setLevel(level)
