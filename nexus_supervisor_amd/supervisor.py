@@ -36,7 +36,9 @@ from .kube.errors import NotFound
 from .models import kube
 from .models import checkpoint as _cp
 from .models.checkpoint import LifecycleStage
+from .gpu.telemetry import FAULT_EVENTS
 from .models.decisions import Decision, DecisionAction as A, RunStatusAnalysisResult
+from .models.decisions import FailureClass as F
 from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
@@ -50,6 +52,26 @@ STAGE_FOR_ACTION = {
     A.TO_FAIL_DEADLINE_EXCEEDED: lambda: LifecycleStage.DEADLINE_EXCEEDED,
     A.TO_RUNNING: lambda: LifecycleStage.RUNNING,
 }
+
+
+_GPU_CLASSES = frozenset((F.HBM_OOM, F.GPU_FAULT, F.COLLECTIVE))
+
+
+def failed_gpu(r: RunStatusAnalysisResult) -> Tuple[str, Optional[Any]]:
+    """(node, physical GPU index) a GPU-class decision is attributed to, best evidence
+    first: the OOM verdict's GPU, a GPU with fault events in the node agent's evidence,
+    then the rank's expected device (physical once the agent reported the allocation)."""
+    ev = r.evidence
+    topo = ev.get("topology") or {}
+    gev = ev.get("gpu") or {}
+    node = topo.get("node") or gev.get("node") or ""
+    oom = ev.get("oom") or {}
+    if oom.get("gpu_index") is not None:
+        return node, oom["gpu_index"]
+    for g in gev.get("gpus") or ():
+        if any(e.get("type") in FAULT_EVENTS for e in g.get("events") or ()):
+            return node, g.get("index")
+    return node, topo.get("expected_gpu")
 
 
 def fused_actuation(cfg: SupervisorConfig) -> bool:
@@ -785,6 +807,8 @@ class Supervisor:
         self._observe(r)
         self._remember(key, stage)
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
+        if r.failure_class in _GPU_CLASSES:
+            self._count_gpu_failure(r)
         if self._fenced(epoch, rid):  # durable, but the Job now belongs to the new leader's replay
             return Decision(r, "applied", stage, False)
         if self.cfg.async_job_delete:
@@ -898,6 +922,8 @@ class Supervisor:
         if running:
             return Decision(r, "applied", stage, False)
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
+        if r.failure_class in _GPU_CLASSES:
+            self._count_gpu_failure(r)
         if self._fenced(epoch, rid):
             return Decision(r, "applied", stage, False)
         if self.cfg.async_job_delete:
@@ -1052,6 +1078,17 @@ class Supervisor:
 
     _STAGE_HISTS = ("event_to_checkpoint", "receive_to_checkpoint", "stage_classify", "stage_queue",
                     "stage_prepare", "stage_write", "stage_read")
+
+    def _count_gpu_failure(self, r: RunStatusAnalysisResult) -> None:
+        """``gpu_failures{node,gpu,class}``: GPU-attributed failures per physical GPU.  The
+        supervisor is the one place that sees every run's attribution; a GPU whose count
+        keeps rising (VM faults, xGMI link loss, resets) is hardware to drain — an alert on
+        ``increase(nexus_supervisor_gpu_failures_total{class="gpu-fault"}[1h]) >= 3`` finds
+        it across replicas and shard workers (docs/OPERATIONS.md)."""
+        node, gpu = failed_gpu(r)
+        self.metrics.inc("gpu_failures", labels={"node": node or "unknown",
+                                                 "gpu": "unknown" if gpu is None else str(gpu),
+                                                 "class": r.failure_class})
 
     def _observe(self, r: RunStatusAnalysisResult):
         s = r.stamps
