@@ -204,3 +204,21 @@ def test_dry_run_value_renders_shadow_mode():
 
     assert cfg_of().dry_run is False
     assert cfg_of({"supervisor": {"config": {"dryRun": True}}}).dry_run is True
+
+
+def test_monitoring_objects_are_optional_and_name_real_metrics():
+    """PodMonitor + PrometheusRule (off by default); every metric an alert names is one the
+    supervisor exports (Prometheus exposition of the statsd namespace)."""
+    import re
+
+    assert not {"PodMonitor", "PrometheusRule"} & set(_by_kind(render_docs(CHART)))
+    k = _by_kind(render_docs(CHART, values={"supervisor": {"observability": {
+        "podMonitor": True, "prometheusRule": {"enabled": True, "gpuFaultThreshold": 2}}}}))
+    pm = k["PodMonitor"][0]["spec"]
+    assert pm["podMetricsEndpoints"][0] == {"port": "http-metrics", "path": "/metrics"}
+    rules = {r["alert"]: r for g in k["PrometheusRule"][0]["spec"]["groups"] for r in g["rules"]}
+    assert set(rules) == {"NexusGpuFailingRuns", "NexusDecisionsDeadLettered", "NexusNoActiveSupervisor"}
+    assert rules["NexusGpuFailingRuns"]["expr"].endswith(">= 2")
+    names = {n for r in rules.values() for n in re.findall(r"(nexus_supervisor_[a-z_]+)", r["expr"])}
+    assert names == {"nexus_supervisor_gpu_failures_total", "nexus_supervisor_decisions_dead_lettered_total",
+                     "nexus_supervisor_active"}
