@@ -107,6 +107,19 @@ class CompatConfig:
 
 
 @dataclass
+class CircuitBreakerConfig:
+    """Circuit breaker in front of the checkpoint store (parallel/breaker.py): during a
+    store outage decisions wait in the queue instead of burning their retries."""
+
+    enabled: bool = field(default=True, metadata=_k("enabled"))
+    # consecutive store failures that open the circuit
+    failure_threshold: int = field(default=5, metadata=_k("failure-threshold"))
+    # first open period; doubled on every re-open (failed probe) up to max-open-duration
+    open_duration: float = field(default=1.0, metadata=_k("open-duration", "duration"))
+    max_open_duration: float = field(default=30.0, metadata=_k("max-open-duration", "duration"))
+
+
+@dataclass
 class LabelConfig:
     """Label keys of nexus-core ``checkpoint/models`` (values unverified offline,
     SURVEY §8 q2) — configurable so a deployment can pin the real strings."""
@@ -300,6 +313,7 @@ class SupervisorConfig:
     # write a row or delete a Job — each would-be action is logged and counted (dry_run_*)
     dry_run: bool = field(default=False, metadata=_k("dry-run"))
     compat: CompatConfig = field(default_factory=CompatConfig, metadata=_k("compat"))
+    circuit_breaker: CircuitBreakerConfig = field(default_factory=CircuitBreakerConfig, metadata=_k("circuit-breaker"))
     labels: LabelConfig = field(default_factory=LabelConfig, metadata=_k("labels"))
     stages: StagesConfig = field(default_factory=StagesConfig, metadata=_k("stages"))
     rules: RulesConfig = field(default_factory=RulesConfig, metadata=_k("rules"))

@@ -70,6 +70,7 @@ class PipelineStage:
         on_done: Optional[Callable[[Any, Any], None]] = None,
         tags: Optional[Dict[str, str]] = None,
         clock: Callable[[], float] = time.monotonic,
+        gate=None,
     ):
         if workers < 1:
             raise ValueError("workers must be >= 1")
@@ -80,6 +81,10 @@ class PipelineStage:
         self.bucket = TokenBucket(elements_per_second, burst, clock)
         self.backoff = ExponentialBackoff(base_delay, max_delay)
         self.max_retries = max_retries
+        # optional admission gate before every attempt (``is_closed()`` / ``await wait()``:
+        # the store circuit breaker, parallel/breaker.py) — an item waiting there keeps its
+        # key's place and its retry budget
+        self.gate = gate
         self.key_fn = key_fn
         self.coalesce_key = coalesce_key
         self.on_dead_letter = on_dead_letter
@@ -170,7 +175,10 @@ class PipelineStage:
             delay = self.bucket.reserve()
             if delay > 0:
                 await asyncio.sleep(delay)
+            gate = self.gate
             try:
+                if gate is not None and not gate.is_closed():
+                    await gate.wait()
                 out = await self.processor(entry.item)
             except asyncio.CancelledError:
                 self._running.discard(key)

@@ -43,7 +43,7 @@ from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
 from .parallel.sharding import ShardSet
-from .store.base import CheckpointStore, NotSent
+from .store.base import CheckpointStore, NotSent, StoreError
 from .utils.gctune import GcTuner
 
 STAGE_FOR_ACTION = {
@@ -182,6 +182,7 @@ class Supervisor:
         self.job_informer = factory.informer("Job")
         self.lookup = _Lookup(self)
         self.pipeline: Optional[PipelineStage] = None
+        self.breaker = None  # store circuit breaker (init)
         self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
         self._applied_cap = 200_000
         self._hists: Optional["_StageHists"] = None  # _observe: the stage histograms, once looked up
@@ -235,9 +236,18 @@ class Supervisor:
     # ------------------------------------------------------------------ Init
     def init(self) -> None:
         c = self.cfg
+        cb = c.circuit_breaker
+        self.breaker = None
+        processor = self.supervise_action
+        if cb.enabled:
+            from .parallel.breaker import CircuitBreaker
+
+            self.breaker = CircuitBreaker(cb.failure_threshold, cb.open_duration, cb.max_open_duration, self.metrics)
+            processor = self._guarded_action
         self.pipeline = PipelineStage(
             "supervisor",
-            self.supervise_action,
+            processor,
+            gate=self.breaker,
             workers=c.workers,
             elements_per_second=c.rate_limit_elements_per_second,
             burst=c.rate_limit_elements_burst,
@@ -720,6 +730,25 @@ class Supervisor:
             if self.cfg.compat.delete_not_found_ok:
                 return False
             raise
+
+    async def _guarded_action(self, r: RunStatusAnalysisResult) -> Decision:
+        """:meth:`supervise_action` reporting to the store circuit breaker: a store error
+        counts against the store, a decision that read or wrote its row for it, one that
+        never reached the store (fenced) for neither."""
+        br = self.breaker
+        try:
+            d = await self.supervise_action(r)
+        except StoreError:
+            br.failure()
+            raise
+        except BaseException:
+            br.neutral()
+            raise
+        if d.outcome == "fenced":
+            br.neutral()
+        else:
+            br.success()
+        return d
 
     async def supervise_action(self, r: RunStatusAnalysisResult) -> Decision:
         """Reference ``superviseAction`` (``supervisor.go:261-374``) with the fixes of SURVEY §7.5."""
