@@ -281,6 +281,9 @@ class ObservabilityConfig:
     profiler_hz: int = field(default=97, metadata=_k("profiler-hz"))  # /debug/pprof sampling rate
     # per-decision stage timestamps -> stage_classify/queue/read/write/delete histograms
     stage_timestamps: bool = field(default=True, metadata=_k("stage-timestamps"))
+    # a Kubernetes Warning Event (reason NexusRunFailed) on the Job per failing decision:
+    # stage, failure class, GPU and cause in `kubectl describe job` (RBAC: events create)
+    record_events: bool = field(default=False, metadata=_k("record-events"))
 
 
 @dataclass

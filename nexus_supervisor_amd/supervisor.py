@@ -183,6 +183,7 @@ class Supervisor:
         self.lookup = _Lookup(self)
         self.pipeline: Optional[PipelineStage] = None
         self.breaker = None  # store circuit breaker (init)
+        self._event_tasks: set = set()  # observability.record-events posts in flight
         self._applied: "OrderedDict[Tuple[str, str], str]" = OrderedDict()
         self._applied_cap = 200_000
         self._hists: Optional["_StageHists"] = None  # _observe: the stage histograms, once looked up
@@ -838,6 +839,8 @@ class Supervisor:
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
         if r.failure_class in _GPU_CLASSES:
             self._count_gpu_failure(r)
+        if self.cfg.observability.record_events and not self.cfg.dry_run:
+            self._record_event(r, stage)
         if self._fenced(epoch, rid):  # durable, but the Job now belongs to the new leader's replay
             return Decision(r, "applied", stage, False)
         if self.cfg.async_job_delete:
@@ -953,6 +956,8 @@ class Supervisor:
         self.metrics.inc("decisions_applied", labels={"stage": stage, "class": r.failure_class or "none"})
         if r.failure_class in _GPU_CLASSES:
             self._count_gpu_failure(r)
+        if self.cfg.observability.record_events and not self.cfg.dry_run:
+            self._record_event(r, stage)
         if self._fenced(epoch, rid):
             return Decision(r, "applied", stage, False)
         if self.cfg.async_job_delete:
@@ -1107,6 +1112,38 @@ class Supervisor:
 
     _STAGE_HISTS = ("event_to_checkpoint", "receive_to_checkpoint", "stage_classify", "stage_queue",
                     "stage_prepare", "stage_write", "stage_read")
+
+    def _record_event(self, r: RunStatusAnalysisResult, stage: str) -> None:
+        """``observability.record-events``: a Warning Event on the run's Job, so ``kubectl
+        describe job`` says what the supervisor decided and why (the reference records none).
+        Fire-and-forget: an API error costs the Event, never the decision.  Its reason
+        (``NexusRunFailed``) matches no rule, so the supervisor's own Event informer ignores it."""
+        create = getattr(self.jobs, "create", None)
+        if create is None:
+            return
+        node, gpu = failed_gpu(r) if r.failure_class in _GPU_CLASSES else ("", None)
+        where = f", GPU {gpu}" + (f" on {node}" if node else "") if gpu is not None else ""
+        cause = R.failure_cause(r.action, r.run_status_message, self.cfg.compat.doubled_fatal_cause)
+        now = _dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+        ev = {"apiVersion": "v1", "kind": "Event",
+              "metadata": {"generateName": f"{r.request_id}.", "namespace": self.namespace},
+              "involvedObject": {"apiVersion": "batch/v1", "kind": "Job", "name": r.request_id,
+                                 "namespace": self.namespace},
+              "reason": "NexusRunFailed", "type": "Warning", "count": 1,
+              "message": f"{stage} ({r.failure_class or 'none'}{where}): {cause}"[:1024],
+              "source": {"component": "nexus-supervisor"}, "firstTimestamp": now, "lastTimestamp": now}
+
+        async def go():
+            try:
+                await create("Event", self.namespace, ev)
+                self.metrics.inc("kube_events_recorded")
+            except Exception as exc:  # noqa: BLE001 - best effort
+                self.metrics.inc("kube_event_errors")
+                self.log.v(1).info("recording a decision Event failed", requestId=r.request_id, err=str(exc))
+
+        t = asyncio.ensure_future(go())
+        self._event_tasks.add(t)
+        t.add_done_callback(self._event_tasks.discard)
 
     def _count_gpu_failure(self, r: RunStatusAnalysisResult) -> None:
         """``gpu_failures{node,gpu,class}``: GPU-attributed failures per physical GPU.  The

@@ -222,3 +222,19 @@ def test_monitoring_objects_are_optional_and_name_real_metrics():
     names = {n for r in rules.values() for n in re.findall(r"(nexus_supervisor_[a-z_]+)", r["expr"])}
     assert names == {"nexus_supervisor_gpu_failures_total", "nexus_supervisor_decisions_dead_lettered_total",
                      "nexus_supervisor_active"}
+
+
+def test_record_events_value_grants_event_create():
+    def role(values=None):
+        return [r for r in _by_kind(render_docs(CHART, values=values))["Role"]
+                if not r["metadata"]["name"].endswith("gpu-agent")][0]
+
+    def creates_events(r):
+        return any("events" in x["resources"] and "create" in x["verbs"] for x in r["rules"])
+
+    assert not creates_events(role())
+    vals = {"supervisor": {"observability": {"recordEvents": True}}}
+    assert creates_events(role(vals))
+    env = _env(_by_kind(render_docs(CHART, values=vals))["Deployment"][0]["spec"]["template"]["spec"]["containers"][0])
+    cfg = load_config(path=None, env={k: v for k, v in env.items() if k.startswith("NEXUS__") and v is not None})
+    assert cfg.observability.record_events is True

@@ -336,3 +336,35 @@ def test_background_job_delete_retries_on_api_errors(arun):
             srv.stop()
 
     arun(go())
+
+
+def test_record_events_puts_the_decision_on_the_job(arun):
+    """observability.record-events: each failing decision leaves a Warning Event
+    (NexusRunFailed) on its Job; the supervisor's own Event informer ignores it (no extra
+    decisions), and a RUNNING transition records nothing."""
+    scenarios = reference_scenarios()
+
+    async def go():
+        objs = [o for s in scenarios for o in s.objects]
+        api, srv, app, store, decisions = await _wire_cluster(objs, cfg=_cfg(**{"observability": {"record-events": True}}))
+        try:
+            await _settle(app, decisions, 8)
+            for _ in range(100):
+                if not app.supervisor._event_tasks:
+                    break
+                await asyncio.sleep(0.02)
+            evs = [e for e in api.objects["Event"].values() if e.get("reason") == "NexusRunFailed"]
+            failing = {rid for s in scenarios for rid, st in s.expected.items()
+                       if st in ("FAILED", "SCHEDULING_FAILED", "DEADLINE_EXCEEDED")}
+            assert {e["involvedObject"]["name"] for e in evs} == failing
+            assert all(e["type"] == "Warning" and e["involvedObject"]["kind"] == "Job" for e in evs)
+            pfp = next(e for e in evs if e["involvedObject"]["name"] == "1d7b6e8d-cc3c-fb5b-a3f6-5d7b9e2c7f2b")
+            assert pfp["message"].startswith("FAILED (fatal): Algorithm encountered a fatal error")
+            await asyncio.sleep(0.3)  # the informer has seen them: still one decision per run
+            assert len([d for d in decisions if d.outcome == "applied"]) == len(failing) + 1  # + the RUNNING run
+        finally:
+            await app.stop()
+            srv.stop()
+            await api.stop()
+
+    arun(go(), timeout=60)
