@@ -406,3 +406,55 @@ def test_previous_tenants_peak_does_not_make_a_crash_an_oom(stress_exe):
                     [{"container": "algorithm", "exitCode": 1, "reason": "Error", "message": ""}], ev)
     assert v.kind is None and not v.signature, v.as_dict()
     assert any("not an OOM verdict" in s for s in v.signals), v.signals
+
+
+def test_multi_rank_job_root_cause_from_a_real_hbm_oom(telemetry, stress_exe, tmp_path):
+    """A 2-rank job (one pod per rank): rank 1 hits a real HIP OOM on this MI355X, rank 0
+    dies later of its all-reduce's watchdog timeout.  The Job-level decision
+    (BackoffLimitExceeded) names rank 1 as the culprit, is an hbm-oom on GPU 0 from the real
+    evidence, and counts rank 0 as collateral (gpu/collective.py)."""
+    from nexus_supervisor_amd.classify import Classifier, render_trace
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.gpu.telemetry import evidence_for
+    from nexus_supervisor_amd.models.decisions import FailureClass
+    from nexus_supervisor_amd.testing.seed import make_event, make_job, make_pod
+
+    env = {"RANK": "1", "LOCAL_RANK": "0", "WORLD_SIZE": "2", "MASTER_ADDR": "10.0.0.9", "MASTER_PORT": "29500"}
+    pid, rc, msg, out, err, t0, t1 = _run_oom(stress_exe, tmp_path, env)
+    assert rc == 1 and ("hipErrorOutOfMemory" in msg or "out of memory" in msg.lower()), (rc, msg, err[-300:])
+    time.sleep(0.3)
+    ev = evidence_for(telemetry, pids=[pid], gpu_indices=[0], lookback=t1 - t0 + 5)
+    labels = LabelConfig()
+    run = "ddp-real-oom"
+
+    def rank_pod(r, message, finished, evidence=None):
+        p = make_pod(run, labels, suffix=f"r{r}", gpus=1, rv="4", node="mi355x-box",
+                     env={"RANK": str(r), "WORLD_SIZE": "2", "LOCAL_RANK": "0", "HIP_VISIBLE_DEVICES": "0"},
+                     status={"phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {
+                         "terminated": {"reason": "Error", "exitCode": 1, "message": message, "finishedAt": finished}}}]})
+        if evidence:
+            p["metadata"]["annotations"] = {"nexus.amd.com/gpu-evidence": json.dumps(evidence)}
+        return p
+
+    watchdog = ("[Rank 0] Watchdog caught collective operation timeout: WorkNCCL(SeqNum=77, OpType=ALLREDUCE) ran for "
+                "600010 milliseconds before timing out.")
+    pods = [rank_pod(0, watchdog, "2026-10-17T10:10:00Z"), rank_pod(1, msg, "2026-10-17T10:00:00Z", ev)]
+    job = make_job(run, labels)
+
+    class Lookup:
+        def get(self, kind, name):
+            return job if kind == "Job" and name == run else None
+
+        def pods_of_job(self, name):
+            return pods
+
+    _s, [r] = Classifier(labels).classify_event(make_event("Job", run, "BackoffLimitExceeded", "backoff limit"), Lookup())
+    assert r.failure_class == FailureClass.HBM_OOM, r.evidence
+    assert r.evidence["oom"]["gpu_index"] == 0
+    ranks = r.evidence["ranks"]
+    assert ranks["culprit"]["rank"] == 1 and ranks["culprit"]["kind"] == "hbm-oom" and ranks["collateral"] == 1
+    trace = json.loads(render_trace(r))
+    assert trace["ranks"]["culprit"]["pod"] == f"{run}-r1"
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/multi_rank_root_cause.json", "w") as f:
+        json.dump({"trace": trace, "message": msg}, f, indent=1)
