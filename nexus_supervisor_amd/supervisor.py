@@ -304,6 +304,12 @@ class Supervisor:
             for t in pending:
                 t.cancel()
             await asyncio.gather(*pending, return_exceptions=True)
+        if self._event_tasks:  # decision Events still being posted (best effort, short)
+            pending = list(self._event_tasks)
+            await asyncio.wait(pending, timeout=min(timeout, 2.0))
+            for t in pending:
+                t.cancel()
+            await asyncio.gather(*pending, return_exceptions=True)
 
     def set_active(self, active: bool) -> None:
         """Leader gating.  On gaining leadership replay the caches (idempotent) so nothing
