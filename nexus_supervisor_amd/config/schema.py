@@ -151,6 +151,13 @@ class RulesConfig:
     # cap on the trace column's size (bytes of JSON); larger documents are trimmed
     # deterministically (least telling detail first); 0 = no cap
     trace_max_bytes: int = field(default=8192, metadata=_k("trace-max-bytes"))
+    # a BackoffLimitExceeded Job decision whose pods died of an OOM found only at actuation
+    # time (late enrichment): true — write FAILED with the OOM cause, the same row the
+    # pod-status OOM rule writes, so the stage does not depend on which of the two
+    # decisions is applied first; false — keep the reference's DEADLINE_EXCEEDED for
+    # BackoffLimitExceeded (supervisor.go:183-193), the OOM class and evidence go into the
+    # trace only (docs/PARITY.md)
+    oom_fails_backoff_job: bool = field(default=True, metadata=_k("oom-fails-backoff-job"))
 
 
 @dataclass

@@ -6,8 +6,10 @@ recorded, so the trace row says *why*:
 host-OOM
   * container ``terminated.reason == "OOMKilled"`` (cgroup OOM, exit 137)  +1.0
   * bare exit 137 (SIGKILL) without reason                                  +0.35
-  * in-process host allocation failure (``MemoryError``, ``std::bad_alloc``,
-    ``Cannot allocate memory``)                                             +0.6
+  * in-process host allocation failure (Python ``MemoryError``, numpy
+    ``_ArrayMemoryError`` / ``Unable to allocate … for an array``, ``std::bad_alloc``,
+    ``java.lang.OutOfMemoryError``, Go ``runtime: out of memory``, V8 ``heap out of
+    memory``, ``Cannot allocate memory``)                                   +0.6
 HBM-OOM (288 GB HBM3E per MI355X)
   * HIP OOM signature in the termination / event message or in the container's log
     tail (``hipErrorOutOfMemory``, ``HIP out of memory``, torch ``OutOfMemoryError``,
@@ -20,10 +22,21 @@ HBM-OOM (288 GB HBM3E per MI355X)
   * VM-fault / queue-eviction event on that GPU                             +0.25
 
 A verdict needs ≥0.5 **and** at least one OOM *signature* (an allocation-failure message
-or log line, OOMKilled, exit 137, or the own-process peak): the device-wide peak and GPU
-events corroborate and attribute, they never make a plain crash an OOM on their own (a
-GPU left full by a previous tenant must not turn an exit-1 into an HBM-OOM that bypasses
-the Job's retry policy).  The larger score wins; a cgroup OOMKill (a hard kernel fact
+or log line, OOMKilled or exit 137).  VRAM numbers — even the pod's own processes filling
+the GPU — and GPU events corroborate and attribute, they never make a plain crash an OOM
+on their own: PyTorch's caching allocator routinely holds nearly all of a GPU, so an
+exit-1 from a NaN assert or an RCCL timeout on a full GPU is *not* an HBM-OOM, and a GPU
+left full by a previous tenant must not bypass the Job's retry policy either (the
+classifier reads the container log tail first, :class:`..classify.Classifier`).
+
+HBM needs a GPU.  ``gpu_involved=False`` (the pod requests no ``amd.com/gpu`` and no GPU
+process of its own was seen) turns every HBM signal into a recorded non-verdict: a
+CPU-only pod whose JVM runs out of heap is never written as "ran out of GPU memory" (the
+reference writes a plain fatal error and never claims a device,
+``/root/reference/services/supervisor.go:194-204,310-335``).  ``None`` = unknown (no pod
+in the cache): only the anchored HIP/torch texts count.
+
+The larger score wins; a cgroup OOMKill (a hard kernel fact
 about *host* memory) is beaten only by HIP's own words, never by VRAM numbers.  Every
 signal names its source (termination message, node-log / pods/log tail, own-process
 peak, device peak).
@@ -47,7 +60,8 @@ HBM_PATTERNS = [
     re.compile(r"hipErrorOutOfMemory", re.I),
     re.compile(r"\bHIP out of memory", re.I),
     re.compile(r"\bCUDA out of memory", re.I),  # torch wording on some ROCm builds
-    re.compile(r"OutOfMemoryError", re.I),
+    # torch's exception class only: a bare "OutOfMemoryError" is also Java's heap OOM
+    re.compile(r"\btorch(?:\.cuda)?\.OutOfMemoryError\b"),
     re.compile(r"hipMalloc(?:Managed|Async)?\b[^\n]{0,80}(?:fail|out of memory|error)", re.I),
     re.compile(r"(?:NCCL|RCCL)[^\n]{0,120}out of memory", re.I),
     re.compile(r"HSA_STATUS_ERROR_OUT_OF_RESOURCES", re.I),
@@ -56,7 +70,12 @@ HBM_PATTERNS = [
 ]
 HOST_PATTERNS = [
     re.compile(r"\bMemoryError\b"),
+    re.compile(r"\b_ArrayMemoryError\b"),                                  # numpy
+    re.compile(r"Unable to allocate [\d.]+ [KMGTP]?i?B for an array", re.I),  # numpy's message
     re.compile(r"std::bad_alloc"),
+    re.compile(r"\bjava\.lang\.OutOfMemoryError\b"),
+    re.compile(r"\bruntime: out of memory"),                                # Go
+    re.compile(r"JavaScript heap out of memory"),                           # Node / V8
     re.compile(r"Cannot allocate memory", re.I),
     re.compile(r"Memory cgroup out of memory", re.I),
     re.compile(r"\bOOMKilled\b"),
@@ -66,7 +85,8 @@ HOST_PATTERNS = [
 # lower-cased text rejects the common no-match message in well under a microsecond, where
 # the case-insensitive regex list costs ~10 µs per message.
 _HBM_KEYS = ("out of memory", "outofmemory", "hipmalloc", "out_of_resources")
-_HOST_KEYS = ("memoryerror", "bad_alloc", "cannot allocate memory", "out of memory", "oomkilled")
+_HOST_KEYS = ("memoryerror", "bad_alloc", "cannot allocate memory", "out of memory", "oomkilled",
+              "unable to allocate", "outofmemoryerror")
 _TORCH_KEYS = ("total capacity", "tried to allocate")
 
 
@@ -97,6 +117,13 @@ class OomVerdict:
     signature: bool = False
     oomkilled: bool = False
     hbm_text: bool = False
+    host_text: bool = False
+
+    @property
+    def text_signature(self) -> bool:
+        """Backed by an allocation-failure text or a cgroup OOMKill (not only exit codes
+        and VRAM numbers): nothing a container log could still overrule."""
+        return self.hbm_text or self.host_text or self.oomkilled
 
     def as_dict(self) -> Dict[str, Any]:
         d: Dict[str, Any] = {"kind": self.kind, "hbm_score": round(self.hbm_score, 3),
@@ -129,6 +156,17 @@ def host_signature(text: str) -> Optional[str]:
     return None
 
 
+def gpu_involved(gpus_requested: int, gpu_evidence: Optional[Dict[str, Any]]) -> bool:
+    """Did the pod use a GPU: it requests one, or the evidence matched its own processes
+    on one (a pod that reaches /dev/kfd without requesting amd.com/gpu)."""
+    if gpus_requested > 0:
+        return True
+    for g in (gpu_evidence or {}).get("gpus") or ():
+        if g.get("matched") or g.get("proc_peak_vram_bytes") or g.get("procs"):
+            return True
+    return False
+
+
 def analyze(
     texts: Iterable[Any] = (),
     terminated: Iterable[Dict[str, Any]] = (),
@@ -137,9 +175,11 @@ def analyze(
     hbm_capacity_gb: float = 288.0,
     hbm_oom_fraction: float = 0.97,
     topo: Optional[Dict[str, Any]] = None,
+    gpu_involved: Optional[bool] = None,
 ) -> OomVerdict:
     """``texts``: strings (a termination / event / condition message) or ``(source, text)``
-    pairs (container log tails, :mod:`.logtail`) — every signal names where it was found."""
+    pairs (container log tails, :mod:`.logtail`) — every signal names where it was found.
+    ``gpu_involved``: see the module docstring (False = no HBM verdict possible)."""
 
     v = OomVerdict()
     sourced: List[Tuple[str, str]] = []
@@ -169,19 +209,24 @@ def analyze(
     hbm_hit = host_hit = False
     logical = None
     for source, text in sourced:
-        s = hbm_signature(text)
-        if s and not hbm_hit:
-            hbm_hit = True
-            v.signature = True
-            v.hbm_text = True
-            v.hbm_score += 1.0
-            v.signals.append(f"HIP OOM signature in {source}: {s!r}")
         h = host_signature(text)
         if h and not host_hit and h != "OOMKilled":
             host_hit = True
             v.signature = True
+            v.host_text = True
             v.host_score += 0.6
             v.signals.append(f"host allocation failure in {source}: {h!r}")
+        s = hbm_signature(text)
+        if s and not hbm_hit:
+            hbm_hit = True
+            if gpu_involved is False:
+                v.signals.append(f"HIP OOM text in {source} ({s!r}) on a pod with no GPU (no GPU request, no GPU "
+                                 f"process of its own): not an HBM verdict")
+            else:
+                v.signature = True
+                v.hbm_text = True
+                v.hbm_score += 1.0
+                v.signals.append(f"HIP OOM signature in {source}: {s!r}")
         if not _mentions(text, _TORCH_KEYS):
             continue
         m = _TORCH_GPU.search(text)
@@ -191,14 +236,14 @@ def analyze(
         r = _TORCH_REQ.search(text)
         if r and v.requested_bytes is None:
             v.requested_bytes = int(float(r.group(1)) * _UNIT[r.group(2).lower()])
-    if logical is not None:
+    if logical is not None and gpu_involved is not False:
         v.gpu_logical_index = logical
         if topo is not None:
             ev = gpu_evidence or {}
             v.gpu_index = physical_gpu(topo, logical, ev.get("gpus") or (), ev.get("allocated"))
         else:
             v.gpu_index = logical  # no topology: the process saw the node's numbering
-    if gpu_evidence:
+    if gpu_evidence and gpu_involved is not False:
         cap = int(hbm_capacity_gb * (1 << 30))
         own_sig = False
         for g in _candidate_gpus(gpu_evidence, expected_gpu, v.gpu_index):
@@ -207,10 +252,9 @@ def analyze(
             own = int(g.get("proc_peak_vram_bytes") or 0)
             if own and own >= hbm_oom_fraction * total and failed_exit and not own_sig:
                 # the pod's OWN processes (matched by cgroup pod UID / PID) filled the GPU and
-                # the container then failed: an OOM signature in its own right — unlike the
-                # device-wide peak, which a previous tenant or a neighbour can produce
+                # the container then failed: strong corroboration (and the attribution), but
+                # not a signature — the caching allocator holds a full GPU in healthy runs too
                 own_sig = True
-                v.signature = True
                 v.hbm_score += 0.75
                 v.signals.append(f"own-process VRAM peak: the pod's processes on GPU {g.get('index')} peaked at "
                                  f"{own / (1 << 30):.1f} GiB of {total / (1 << 30):.1f} GiB, then the container "
@@ -245,8 +289,8 @@ def analyze(
         else:
             v.kind = "host"
     elif v.hbm_score >= 0.5:
-        v.signals.append("no OOM signature (allocation-failure message or log line, OOMKilled, exit 137, or the pod's "
-                         "own processes filling the GPU): not an OOM verdict")
+        v.signals.append("no OOM signature (allocation-failure message or log line, OOMKilled or exit 137): "
+                         "VRAM numbers alone are not an OOM verdict")
     return v
 
 

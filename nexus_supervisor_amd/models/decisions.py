@@ -57,6 +57,7 @@ class RunStatusAnalysisResult:
     event_uid: str = ""
     attempts: int = 0
     pending_delete: bool = False  # a concurrent Job DELETE failed; retry must still delete
+    answered: int = 0  # the attempt (``attempts``) in which the checkpoint store last answered
 
     @property
     def key(self):

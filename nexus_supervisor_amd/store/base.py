@@ -18,7 +18,16 @@ from ..models.checkpoint import CheckpointedRequest
 
 
 class StoreError(Exception):
-    """Transient or permanent store failure (the pipeline retries it)."""
+    """Transient or permanent store failure (the pipeline retries it).  ``availability``:
+    the error says the *store* is unreachable or overloaded (what the circuit breaker
+    counts), not that one request was refused (an invalid query, one partition's write
+    timeout, LWT contention)."""
+
+    availability = True
+
+
+def is_availability_error(exc: BaseException) -> bool:
+    return isinstance(exc, StoreError) and bool(getattr(exc, "availability", True))
 
 
 class NotSent(StoreError):

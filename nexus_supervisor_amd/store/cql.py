@@ -100,6 +100,7 @@ _TYPE_IDS = {"text": T_VARCHAR, "timestamp": T_TIMESTAMP}
 
 ERR_OVERLOADED, ERR_UNAVAILABLE, ERR_IS_BOOTSTRAPPING = 0x1001, 0x1000, 0x1002
 ERR_WRITE_TIMEOUT, ERR_READ_TIMEOUT, ERR_UNPREPARED, ERR_SERVER = 0x1100, 0x1200, 0x2500, 0x0000
+_AVAILABILITY = frozenset((ERR_OVERLOADED, ERR_UNAVAILABLE, ERR_IS_BOOTSTRAPPING))
 RETRYABLE = {ERR_OVERLOADED, ERR_UNAVAILABLE, ERR_IS_BOOTSTRAPPING, ERR_WRITE_TIMEOUT, ERR_READ_TIMEOUT, ERR_SERVER}
 
 
@@ -109,6 +110,10 @@ class CqlError(StoreError):
         self.code = code
         self.message = message
         self.extra = extra or {}
+        # the coordinator (or the whole cluster) cannot serve: Unavailable / Overloaded /
+        # IsBootstrapping.  A server-side Read/WriteTimeout is one partition's replicas
+        # being slow (or LWT contention), Invalid / Syntax a bad request: not the store
+        self.availability = code in _AVAILABILITY
 
 
 class ConnectionClosed(StoreError):

@@ -43,7 +43,7 @@ from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
 from .parallel.sharding import ShardSet
-from .store.base import CheckpointStore, NotSent, StoreError
+from .store.base import CheckpointStore, NotSent, is_availability_error
 from .utils.gctune import GcTuner
 
 STAGE_FOR_ACTION = {
@@ -739,17 +739,22 @@ class Supervisor:
             raise
 
     async def _guarded_action(self, r: RunStatusAnalysisResult) -> Decision:
-        """:meth:`supervise_action` reporting to the store circuit breaker: a store error
-        counts against the store, a decision that read or wrote its row for it, one that
-        never reached the store (fenced) for neither."""
+        """:meth:`supervise_action` reporting to the store circuit breaker: an
+        availability error (no host, connection lost, client timeout, Unavailable /
+        Overloaded / IsBootstrapping) counts against the store; a decision whose store call
+        returned counts for it — even when the Job DELETE after the write then fails; one
+        that never reached the store (fenced) or was refused as a request (Invalid, one
+        partition's WriteTimeout, LWT contention) for neither."""
         br = self.breaker
         try:
             d = await self.supervise_action(r)
-        except StoreError:
-            br.failure()
-            raise
-        except BaseException:
-            br.neutral()
+        except BaseException as exc:
+            if is_availability_error(exc):
+                br.failure()
+            elif r.answered == r.attempts:
+                br.success()  # the store answered (the Job DELETE after the write failed)
+            else:
+                br.neutral()  # never reached the store, or a request-level refusal (ADVICE r3)
             raise
         if d.outcome == "fenced":
             br.neutral()
@@ -789,6 +794,7 @@ class Supervisor:
             # UpsertCheckpoint of the deep copy) needs every column
             read = self.store.read_checkpoint if compat.full_row_upsert else self.store.read_status
             cp = await read(r.algorithm, r.request_id)
+            r.answered = r.attempts
         except Exception as exc:
             self.log.error(exc, "no checkpoint exists for the provided request, job will be deleted without metadata saved",
                            requestId=r.request_id, algorithm=r.algorithm)
@@ -929,6 +935,7 @@ class Supervisor:
         try:
             applied, current = await self.store.cas_update(r.algorithm, rid, stage, cause, details, now_dt,
                                                            only_if, set_failure=not running)
+            r.answered = r.attempts
         except Exception as exc:
             self.log.error(exc, "failed to update algorithm submission status", requestId=rid, algorithm=r.algorithm)
             # the reference deletes on a failed checkpoint *read* (supervisor.go:265-273); here

@@ -99,3 +99,76 @@ def test_outage_longer_than_the_retry_budget_loses_nothing(arun):
 def test_without_the_breaker_the_same_outage_dead_letters(arun):
     failed, dead, during, _ = arun(_scenario(breaker=False), timeout=30)
     assert dead > 0 and failed < 12
+
+
+class RefusingStore(MemoryStore):
+    """Every write is refused with the given CQL error (the read answers)."""
+
+    def __init__(self, rows, code):
+        super().__init__(rows)
+        self.code = code
+        self.refused = 0
+
+    async def update_status(self, *a, **kw):
+        from nexus_supervisor_amd.store.cql import CqlError
+        self.refused += 1
+        raise CqlError(self.code, "refused")
+
+
+def _classified(code, async_delete=True, jobs=None):
+    from nexus_supervisor_amd.testing.inproc import RecordingJobs
+
+    cfg = load_config(path=None, env={}, overrides={
+        "cql-store-type": "memory", "workers": 4, "rate-limit-elements-per-second": 0, "resync-period": "0s",
+        "failure-rate-base-delay": "5ms", "failure-rate-max-delay": "10ms", "max-retries": 2,
+        "async-job-delete": async_delete,
+        "circuit-breaker": {"enabled": True, "failure-threshold": 2, "open-duration": "5s"}})
+    rids = [f"refused-run-{i}" for i in range(6)]
+    rows = [CheckpointedRequest(algorithm=ALGORITHM, id=r, lifecycle_stage=S.RUNNING) for r in rids]
+    store = RefusingStore(rows, code) if code is not None else MemoryStore(rows)
+    objs = [o for r in rids for o in (make_job(r, cfg.labels), make_pod(r, cfg.labels))]
+
+    async def go():
+        c = InProcCluster(cfg, store, objs, jobs=jobs(objs) if jobs else None)
+        await c.start()
+        for r in rids:
+            p = make_pod(r, cfg.labels, rv="9")
+            p["status"] = {"phase": "Failed", "containerStatuses": [{"name": "algorithm", "state": {
+                "terminated": {"reason": "OOMKilled", "exitCode": 137}}}]}
+            c.push(p, "MODIFIED")
+        await c.settle(5)
+        await c.stop()
+        return c.supervisor, store
+
+    return go()
+
+
+def test_request_level_cql_errors_do_not_trip_the_breaker(arun):
+    """one partition's WriteTimeout (0x1100) or an Invalid query (0x2200)
+    is a refusal of that request, not a store outage: decisions dead-letter through their
+    own retry budget and the breaker stays closed.  Unavailable (0x1000) trips it."""
+    for code in (0x1100, 0x2200):
+        sup, store = arun(_classified(code), timeout=20)
+        assert sup.breaker.trips == 0 and sup.breaker.state is CLOSED, hex(code)
+        assert store.refused >= 6
+    sup, _ = arun(_classified(0x1000), timeout=20)
+    assert sup.breaker.trips >= 1
+
+
+def test_failed_job_delete_after_a_durable_write_counts_for_the_store(arun):
+    """the write landed, then the synchronous Job DELETE failed — the store
+    answered, so the breaker records a success (it never counts the API server's errors)."""
+    from nexus_supervisor_amd.testing.inproc import RecordingJobs
+
+    def failing_jobs(objs):
+        j = RecordingJobs(o["metadata"]["name"] for o in objs if o["kind"] == "Job")
+        j.fail_next = 100
+        return j
+
+    async def go():
+        sup, store = await _classified(None, async_delete=False, jobs=failing_jobs)
+        return sup, store
+
+    sup, store = arun(go(), timeout=20)
+    assert all(store.get(ALGORITHM, f"refused-run-{i}").lifecycle_stage == S.FAILED for i in range(6))
+    assert sup.breaker.trips == 0 and sup.breaker.failures == 0

@@ -112,10 +112,12 @@ def test_log_tail_makes_a_default_pod_an_hbm_oom():
     assert any(s.startswith("HIP OOM signature in pods/log tail of container algorithm") for s in oom["signals"]), oom
 
 
-def test_own_process_peak_is_a_signature_but_a_previous_tenants_peak_is_not():
-    """Exit 1, no OOM text anywhere.  (a) a previous tenant left the GPU's device-wide peak
-    at 99 %: corroboration only → a plain fatal error.  (b) the pod's OWN processes
-    (cgroup pod UID) peaked at 99 % of the GPU: an HBM-OOM, with the signal naming it."""
+def test_vram_numbers_alone_never_make_an_oom():
+    """exit 1 and no OOM text anywhere.  Neither a previous tenant's
+    device-wide peak nor the pod's OWN processes holding 99 % of the GPU (PyTorch's caching
+    allocator does that in healthy runs) makes an HBM-OOM: the Job decides.  With the
+    torch text the own-process peak corroborates and attributes; with exit 137 (SIGKILL,
+    an OOM signature) it tips the verdict to HBM; a cgroup OOMKill is never overruled."""
     labels = LabelConfig()
     pod = _failed(make_pod("r3", labels, gpus=1, env={"LOCAL_RANK": "0", "HIP_VISIBLE_DEVICES": "0"}))
     uid = pod["metadata"]["uid"]
@@ -124,13 +126,63 @@ def test_own_process_peak_is_a_signature_but_a_previous_tenants_peak_is_not():
     assert _classify(json.loads(json.dumps(pod)), gev=other_tenant) == []  # not an OOM: the Job decides
     own = {"source": "fake", "pod_uid": uid, "gpus": [dict(base, matched=True, proc_peak_vram_bytes=291000 << 20,
                                                           procs=[{"pid": 7, "peak_vram_bytes": 291000 << 20}])]}
-    r = _classify(json.loads(json.dumps(pod)), gev=own)[0]
+    assert _classify(json.loads(json.dumps(pod)), gev=own) == []
+    # the log tail names an ordinary error: still not an OOM
+    crash = [dict(logtail.scan(PLAIN_CRASH.splitlines()), container="algorithm", restart=0, source="pods/log")]
+    assert _classify(json.loads(json.dumps(pod)), gev=own, logs=crash) == []
+    # the log tail has the torch OOM: HBM, the own-process peak in the signals
+    recs = [dict(logtail.scan(TORCH_OOM.splitlines()), container="algorithm", restart=0, source="pods/log")]
+    r = _classify(json.loads(json.dumps(pod)), gev=own, logs=recs)[0]
     assert r.failure_class == FailureClass.HBM_OOM
     assert any(s.startswith("own-process VRAM peak") for s in r.evidence["oom"]["signals"])
     assert r.evidence["oom"]["peak_vram_bytes"] == 291000 << 20
+    sigkill = _failed(make_pod("r3", labels, gpus=1), reason="Error", code=137)
+    assert _classify(sigkill, gev=own)[0].failure_class == FailureClass.HBM_OOM
     # a cgroup OOMKill is never overruled by VRAM numbers
     killed = _failed(make_pod("r3", labels, gpus=1), reason="OOMKilled", code=137)
     assert _classify(killed, gev=own)[0].failure_class == FailureClass.HOST_OOM
+
+
+def test_log_fetch_is_asked_for_when_only_vram_numbers_speak():
+    """a verdict with no text signature defers for the pods/log read
+    (``allow_log_fetch``) instead of deciding from VRAM numbers."""
+    labels = LabelConfig()
+    pod = _failed(make_pod("r4", labels, gpus=1))
+    uid = pod["metadata"]["uid"]
+    own = {"source": "fake", "pod_uid": uid, "gpus": [{"vram_total_mb": 294896, "vram_peak_mb": 292000, "index": 0,
+                                                        "matched": True, "proc_peak_vram_bytes": 291000 << 20}]}
+    pod["metadata"]["annotations"] = {ANN: json.dumps(own)}
+    c = Classifier(labels, gpu=GpuConfig())
+    assert c.classify_pod(pod, allow_log_fetch=True) == [] and c.deferred
+    assert c.deferred_log == [{"container": "algorithm", "restart": 0, "previous": False, "exitCode": 1}]
+
+
+def test_crashloop_log_cache_is_per_container_instance():
+    """restart 0 of a CrashLoopBackOff pod failed with a
+    ValueError (its tail was read and cached); restart 1 then fails with a HIP OOM.  The
+    cache is keyed by (pod uid, container, restart), so restart 1's tail is fetched and the
+    decision is hbm-oom from it — restart 0's tail never speaks for restart 1."""
+    labels = LabelConfig()
+    c = Classifier(labels, gpu=GpuConfig())
+    base = make_pod("r5", labels, gpus=1, env={"LOCAL_RANK": "0", "HIP_VISIBLE_DEVICES": "0"})
+    first = _failed(base, restarts=1, last=True)  # lastState = restart 0
+    want = c._log_fetch_needed(first)
+    assert [(w["container"], w["restart"]) for w in want] == [("algorithm", 0)]
+    c.store_logs(first, [dict(logtail.scan(PLAIN_CRASH.splitlines()), container="algorithm", restart=0,
+                              source="pods/log")])
+    assert c._log_fetch_needed(first) == []  # read once per instance
+    r0 = c.classify_pod(first, allow_log_fetch=True)[0]  # an ordinary crash: crash-loop, no OOM
+    assert r0.failure_class == FailureClass.CRASH_LOOP and "oom" not in r0.evidence
+    second = _failed(base, restarts=2, last=True)  # lastState = restart 1
+    second["metadata"]["resourceVersion"] = "9"
+    assert c.classify_pod(second, allow_log_fetch=True) == [] and c.deferred
+    assert [(w["container"], w["restart"]) for w in c.deferred_log] == [("algorithm", 1)]
+    c.store_logs(second, [dict(logtail.scan(TORCH_OOM.splitlines()), container="algorithm", restart=1,
+                               source="pods/log")])
+    r = c.classify_pod(second, allow_log_fetch=True)[0]
+    assert r.failure_class == FailureClass.HBM_OOM
+    assert r.evidence["logs"][0]["restart"] == 1  # only the instance that just failed
+    assert len(c.log_cache[base["metadata"]["uid"]]) == 2
 
 
 # ----------------------------------------------------------------------------- end to end

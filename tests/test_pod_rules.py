@@ -70,8 +70,9 @@ def test_hip_oom_message_is_hbm_oom(arun):
     cfg = _cfg()
     msg = ("torch.OutOfMemoryError: HIP out of memory. Tried to allocate 12.00 GiB. GPU 3 has a total capacity of "
            "287.98 GiB of which 1.02 GiB is free.")
-    upd = _failed_pod(cfg.labels, RID, _status({"terminated": {"reason": "Error", "exitCode": 1, "message": msg}}))
-    store, _ = arun(_run(cfg, [make_pod(RID, cfg.labels)], [("MODIFIED", upd)]))
+    upd = _failed_pod(cfg.labels, RID, _status({"terminated": {"reason": "Error", "exitCode": 1, "message": msg}}),
+                      gpus=1)
+    store, _ = arun(_run(cfg, [make_pod(RID, cfg.labels, gpus=1)], [("MODIFIED", upd)]))
     t = _trace(store.get(ALGORITHM, RID))
     assert t["class"] == "hbm-oom" and t["oom"]["gpu_index"] == 3 and t["oom"]["requested_bytes"] == 12 << 30
 
@@ -82,12 +83,12 @@ def test_gpu_failures_are_counted_per_physical_gpu(arun):
     cfg = _cfg()
     msg = "torch.OutOfMemoryError: HIP out of memory. GPU 3 has a total capacity of 287.98 GiB"
     a = _failed_pod(cfg.labels, RID, _status({"terminated": {"reason": "Error", "exitCode": 1, "message": msg}}),
-                    node="n7")
+                    node="n7", gpus=1)
     ev = {"source": "agent", "node": "n7", "gpus": [{"index": 5, "vram_total_mb": 294896, "vram_peak_mb": 1000,
                                                      "events": [{"type": "VMFAULT", "t": 1.0}]}]}
     b = _failed_pod(cfg.labels, BID, _status({"terminated": {"reason": "Error", "exitCode": 134}}), node="n7",
-                    annotations={"nexus.amd.com/gpu-evidence": json.dumps(ev)})
-    store, c = arun(_run(cfg, [make_pod(RID, cfg.labels, node="n7"), make_pod(BID, cfg.labels, node="n7")],
+                    gpus=1, annotations={"nexus.amd.com/gpu-evidence": json.dumps(ev)})
+    store, c = arun(_run(cfg, [make_pod(RID, cfg.labels, node="n7", gpus=1), make_pod(BID, cfg.labels, node="n7", gpus=1)],
                          [("MODIFIED", a), ("MODIFIED", b)]))
     got = {dict(k)["gpu"] + "/" + dict(k)["class"]: v for k, v in c.supervisor.metrics.counters["gpu_failures"].items()}
     assert got == {"3/hbm-oom": 1, "5/gpu-fault": 1}
