@@ -325,6 +325,7 @@ def main(argv=None) -> int:
                 "inflight_steps": args.inflight,
                 "pregenerated_input": not args.no_pregen and args.transport == "wire",
                 "rate_limit_eps": res.get("eps"),
+                "kube_qps": res.get("kube_qps"),
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
                 "cql_latency_us": args.cql_latency_us,

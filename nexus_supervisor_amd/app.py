@@ -74,9 +74,11 @@ class Application:
         self.log = logger or KLogger()
         self.metrics = metrics or Metrics(cfg.observability.statsd_name, {"version": __version__})
         if kube is None and (factory is None or jobs is None):
-            from .kube.client import KubeClient, KubeConfig
+            from .kube.client import KubeClient
 
-            kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+            kube = KubeClient.for_config(cfg, self.metrics)
+        elif kube is not None and hasattr(kube, "apply_config") and not getattr(kube, "flow_configured", False):
+            kube.apply_config(cfg, self.metrics)
         self.kube = kube
         self.store = store if store is not None else build_store(cfg)
         self.factory = factory if factory is not None else build_factory(cfg, kube)
@@ -258,9 +260,9 @@ class ShardedApplication:
             from .parallel.watchhub import WatchHub
 
             if self.kube is None:
-                from .kube.client import KubeClient, KubeConfig
+                from .kube.client import KubeClient
 
-                self.kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+                self.kube = KubeClient.for_config(cfg, self.metrics)
             self.hub = WatchHub(cfg, self.kube, self.pool.count, self.pool.send_data, self.pool.data_buffered,
                                 self.pool.data_drain, metrics=self.metrics)
             self.pool.on_restart = lambda _index: self.hub.resync()
@@ -272,9 +274,9 @@ class ShardedApplication:
             await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
         if lease_mode or le.enabled:
             if self.kube is None:
-                from .kube.client import KubeClient, KubeConfig
+                from .kube.client import KubeClient
 
-                self.kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+                self.kube = KubeClient.for_config(cfg, self.metrics)
         if lease_mode:
             self.shard_leases = make_shard_leases(cfg, self.kube, self.set_shards, self.metrics,
                                                   on_renewed=self._shard_holds)

@@ -48,6 +48,9 @@ class BenchConfig:
     pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
     cluster: str = "per-rank"  # per-rank | shared (one apiserver + one CQL server for all ranks)
     pprof_hz: int = 199
+    # client-side API bucket (kube-qps; the uncapped profile sets it high so the limiter's
+    # path runs without pacing, the reference profile uses client-go's 5 / 10)
+    kube_qps: float = 1_000_000.0
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -56,8 +59,10 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
     sc.resource_namespace = "nexus"
     if cfg.profile == "reference":
         sc.workers, sc.rate_limit_elements_per_second, sc.rate_limit_elements_burst = 2, 10, 100
+        sc.kube_qps, sc.kube_burst = 5.0, 10
     else:
         sc.workers, sc.rate_limit_elements_per_second, sc.rate_limit_elements_burst = cfg.workers, 0, 1_000_000
+        sc.kube_qps, sc.kube_burst = cfg.kube_qps, max(1, int(min(cfg.kube_qps, 1_000_000)))
     sc.sharding.shards = cfg.world
     sc.sharding.shard_index = cfg.rank
     sc.resync_period = 0.0
@@ -339,7 +344,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             "wrong_stage": tracker.wrong_stage, "wrong_examples": tracker.wrong_examples, "readback": readback,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
             "actuation": _actuation(sc),
-            "eps": sc.rate_limit_elements_per_second, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
+            "eps": sc.rate_limit_elements_per_second, "kube_qps": sc.kube_qps, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
             "probe": probe, "step_done_ms": step_done_ms}
 
 

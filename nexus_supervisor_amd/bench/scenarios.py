@@ -46,8 +46,10 @@ from .wire import schema_statements
 from .workload import Workload
 
 PROFILES = {
-    "reference": {"workers": 2, "rate-limit-elements-per-second": 10, "rate-limit-elements-burst": 100},
-    "uncapped": {"workers": 256, "rate-limit-elements-per-second": 0, "rate-limit-elements-burst": 1_000_000},
+    "reference": {"workers": 2, "rate-limit-elements-per-second": 10, "rate-limit-elements-burst": 100,
+                  "kube-qps": 5, "kube-burst": 10},
+    "uncapped": {"workers": 256, "rate-limit-elements-per-second": 0, "rate-limit-elements-burst": 1_000_000,
+                 "kube-qps": 1_000_000, "kube-burst": 1_000_000},
 }
 
 

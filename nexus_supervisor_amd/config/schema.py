@@ -192,6 +192,9 @@ class GpuConfig:
     # longest a decision waits for an outstanding log-tail fetch
     log_tail_timeout: float = field(default=2.0, metadata=_k("log-tail-timeout", "duration"))
     log_tail_bytes: int = field(default=65536, metadata=_k("log-tail-bytes"))  # limitBytes of a tail
+    # pods/log reads in flight at once per process (proxied through the kubelet: the most
+    # expensive read there is); a GPU failure wave queues behind this bound
+    log_tail_concurrency: int = field(default=8, metadata=_k("log-tail-concurrency"))
 
 
 @dataclass
@@ -315,6 +318,17 @@ class SupervisorConfig:
     # server-side label selector on the Pod/Job informers (only Nexus runs are cached)
     informer_label_selector: bool = field(default=True, metadata=_k("informer-label-selector"))
     watch_timeout: float = field(default=300.0, metadata=_k("watch-timeout", "duration"))  # server-side watch timeout
+    # client-side API flow control (client-go rest.Config QPS / Burst): a token bucket in
+    # front of every API request of a replica (Job DELETEs, pods/log reads, Events, LIST /
+    # WATCH; Lease calls exempt), divided over its shard-worker processes.  The reference
+    # runs on client-go's defaults, 5 / 10 (app_dependencies.go:39-45) — that holds a
+    # 1,000-pod failure wave's DELETEs for 200 s; 50 / 100 is a controller-class client.
+    # 0 = no client-side limit (the server's API Priority and Fairness still answers 429)
+    kube_qps: float = field(default=50.0, metadata=_k("kube-qps", "number"))
+    kube_burst: int = field(default=100, metadata=_k("kube-burst"))
+    # 429 (and 5xx with Retry-After) answers re-sent after the server's Retry-After, at most
+    # this many times per request (client-go: 10); 0 = never
+    kube_max_retries: int = field(default=10, metadata=_k("kube-max-retries"))
     max_retries: int = field(default=16, metadata=_k("max-retries"))  # 0 = retry forever
     # issue the Job DELETE after the checkpoint write without holding a worker (retried
     # in the background with the failure backoff); false = delete inside the worker
@@ -395,6 +409,10 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("gpu.log-tail must be auto|api|node|off")
     if cfg.gpu.log_tail_bytes < 1024 or cfg.gpu.log_tail_timeout <= 0:
         raise ConfigError("gpu.log-tail-bytes must be >= 1024 and gpu.log-tail-timeout > 0")
+    if cfg.gpu.log_tail_concurrency < 1:
+        raise ConfigError("gpu.log-tail-concurrency must be >= 1")
+    if cfg.kube_qps < 0 or cfg.kube_burst < 1 or cfg.kube_max_retries < 0:
+        raise ConfigError("kube-qps must be >= 0 (0 = no limit), kube-burst >= 1, kube-max-retries >= 0")
     if cfg.leader_election.enabled or cfg.sharding.mode == "lease":
         le = cfg.leader_election
         if not le.lease_duration > le.renew_deadline > le.retry_period > 0:

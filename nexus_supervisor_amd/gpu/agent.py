@@ -268,7 +268,7 @@ async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process 
     from .telemetry import make_telemetry
     import os
 
-    kc = KubeClient(KubeConfig.load(cfg.kube_config_path))
+    kc = KubeClient.for_config(cfg)
     tel = make_telemetry("amdsmi" if cfg.gpu.backend == "auto" else cfg.gpu.backend, cfg.gpu.sample_interval)
     if tel is None:
         raise RuntimeError("no GPU telemetry backend on this node")

@@ -246,8 +246,10 @@ class SharedInformer:
             except asyncio.CancelledError:
                 raise
             except Exception as exc:  # connection errors: back off and re-list
-                log.warning("%s list/watch failed: %s; retrying in %.1fs", self.kind, exc, backoff)
-                await asyncio.sleep(backoff * (1 + random.random() * 0.2))
+                # a throttled list / watch (429) waits at least the server's Retry-After
+                wait = max(backoff * (1 + random.random() * 0.2), getattr(exc, "retry_after", None) or 0.0)
+                log.warning("%s list/watch failed: %s; retrying in %.1fs", self.kind, exc, wait)
+                await asyncio.sleep(wait)
                 backoff = min(backoff * 2, 30.0)
 
     def _watch_error(self, obj) -> None:

@@ -14,7 +14,11 @@ available offline, so the REST + watch protocol is spoken directl
   ``resourceVersion`` with ``allowWatchBookmarks`` and a server timeout, decoded
   line-by-line from the chunked stream; ``410 Gone`` surfaces as an ERROR event
   (the informer re-lists);
-* ``ListWatch`` adapter for :mod:`..informer`.
+* ``ListWatch`` adapter for :mod:`..informer`;
+* client-side flow control as client-go has it (:mod:`.flowcontrol`): a ``kube-qps`` /
+  ``kube-burst`` token bucket in front of every request (Lease calls exempt: leader
+  election must not starve behind a DELETE burst — APF gives it its own priority level
+  too), and ``429`` / ``5xx`` answers retried after the server's ``Retry-After``.
 """
 from __future__ import annotations
 
@@ -34,6 +38,7 @@ import aiohttp
 from ..informer.informer import ListWatch
 from ..models.kube import FINISHERS, PROJECTIONS, list_projection, watch_projection
 from .errors import ApiError, from_status
+from .flowcontrol import RetryPolicy, TokenBucket, retry_after
 
 
 def _native_decoder_available() -> bool:
@@ -227,10 +232,22 @@ class KubeConfig:
         return ctx
 
 
+def _exempt(path: str) -> bool:
+    """Lease calls bypass the client-side bucket (leader election / shard leases)."""
+    return "/coordination.k8s.io/" in path
+
+
 class KubeClient:
     def __init__(self, config: KubeConfig, *, request_timeout: float = 30.0, max_connections: int = 32,
-                 user_agent: str = "nexus-supervisor-amd/0.1", pipelined_writes: bool = True, write_connections: int = 4):
+                 user_agent: str = "nexus-supervisor-amd/0.1", pipelined_writes: bool = True, write_connections: int = 4,
+                 qps: float = 0.0, burst: int = 1, max_retries: int = 10, metrics=None):
         self.config = config
+        # client-go rest.Config QPS / Burst (kube-qps / kube-burst; 0 = no client-side limit)
+        self.limiter = TokenBucket(qps, burst)
+        self.retry = RetryPolicy(max_retries)
+        self.metrics = metrics  # obs.metrics.Metrics: kube_throttled / kube_retries / kube_ratelimit_waits
+        self.throttled = 0      # 429 / hinted 5xx answers seen
+        self.retried = 0        # requests re-sent after a Retry-After
         self.pipelined_writes = pipelined_writes
         self.write_connections = write_connections
         self._fast = None
@@ -278,40 +295,117 @@ class KubeClient:
                                        default_headers={"User-Agent": self.user_agent, "Accept": "application/json"})
         return self._fast
 
+    # ------------------------------------------------------------------ flow control
+    def set_flow_control(self, qps: float, burst: int, max_retries: int = 10, metrics=None) -> None:
+        """``kube-qps`` / ``kube-burst`` / ``kube-max-retries`` of this process's share."""
+        self.limiter = TokenBucket(qps, burst)
+        self.retry = RetryPolicy(max_retries)
+        if metrics is not None:
+            self.metrics = metrics
+
+    @classmethod
+    def for_config(cls, cfg, metrics=None, **kw) -> "KubeClient":
+        """A client for ``cfg.kube-config-path`` with this process's share of the flow
+        control (a replica split into K shard-worker processes gives each 1/K)."""
+        c = cls(KubeConfig.load(cfg.kube_config_path), **kw)
+        c.apply_config(cfg, metrics)
+        return c
+
+    def apply_config(self, cfg, metrics=None) -> None:
+        from .flowcontrol import split
+
+        parts = max(1, int(getattr(cfg.runtime, "worker_processes", 1) or 1))
+        qps, burst = split(cfg.kube_qps, cfg.kube_burst, parts)
+        self.set_flow_control(qps, burst, cfg.kube_max_retries, metrics)
+
+    async def _admit(self, path: str) -> None:
+        lim = self.limiter
+        if lim.qps > 0 and not _exempt(path):
+            d = await lim.wait()
+            if d > 0 and self.metrics is not None:
+                self.metrics.inc("kube_ratelimit_waits")
+                self.metrics.observe_seconds("kube_ratelimit_wait", d)
+
+    def _backoff(self, method: str, status: int, hint: Optional[float], attempt: int,
+                 deadline: Optional[float] = None) -> Optional[float]:
+        """Seconds to wait before re-sending an answer ``status`` (None: raise it)."""
+        if status < 429:
+            return None
+        self.throttled += 1
+        if self.metrics is not None:
+            self.metrics.inc("kube_throttled", labels={"verb": method, "code": str(status)})
+        d = self.retry.delay(status, hint)
+        if d is None or attempt >= self.retry.max_retries:
+            return None
+        if deadline is not None and time.monotonic() + d > deadline:
+            return None  # the caller's budget ends before the hint: give up now
+        self.retried += 1
+        if self.metrics is not None:
+            self.metrics.inc("kube_retries", labels={"verb": method})
+        return d
+
     async def request(self, method: str, path: str, *, params: Optional[Dict[str, Any]] = None, body: Any = None,
                       content_type: str = "application/json", timeout: Optional[float] = None,
                       decoder=None) -> Dict[str, Any]:
         s = await self._s()
-        self.requests += 1
         data = json.dumps(body) if body is not None else None
-        async with s.request(method, self.config.server + path, params=params, data=data,
-                             headers=self._headers({"Content-Type": content_type} if data is not None else None),
-                             timeout=aiohttp.ClientTimeout(total=timeout or self.request_timeout)) as r:
-            raw = await r.read()
+        attempt = 0
+        while True:
+            await self._admit(path)
+            self.requests += 1
+            async with s.request(method, self.config.server + path, params=params, data=data,
+                                 headers=self._headers({"Content-Type": content_type} if data is not None else None),
+                                 timeout=aiohttp.ClientTimeout(total=timeout or self.request_timeout)) as r:
+                raw = await r.read()
+                status = r.status
+                hint = retry_after(r.headers.get("Retry-After")) if status >= 429 else None
+            if status >= 400:
+                d = self._backoff(method, status, hint, attempt)
+                if d is not None:
+                    attempt += 1
+                    await asyncio.sleep(d)
+                    continue
             try:
-                if decoder is not None and r.status < 400 and raw:
+                if decoder is not None and status < 400 and raw:
                     doc = decoder.decode(raw)
                 else:
                     doc = json.loads(raw) if raw else {}
             except ValueError:
                 doc = {"message": raw[:500].decode("utf-8", "replace")}
-            if r.status >= 400:
-                raise from_status(r.status, doc)
+            if status >= 400:
+                raise from_status(status, doc, hint)
             return doc
 
     async def get_raw(self, path: str, params: Optional[Dict[str, str]] = None,
                       timeout: Optional[float] = None) -> Tuple[int, bytes]:
-        """GET returning ``(status, raw body)`` (the watch hub splits LIST bodies natively)."""
+        """GET returning ``(status, raw body)`` (the watch hub splits LIST bodies natively).
+        A 429 / hinted 5xx is re-sent after its ``Retry-After`` while that fits in
+        ``timeout`` (the whole call's budget)."""
         s = await self._s()
-        self.requests += 1
-        async with s.get(self.config.server + path, params=params, headers=self._headers(),
-                         timeout=aiohttp.ClientTimeout(total=timeout or max(60.0, self.request_timeout))) as r:
-            return r.status, await r.read()
+        total = timeout or max(60.0, self.request_timeout)
+        deadline = time.monotonic() + total
+        attempt = 0
+        while True:
+            await self._admit(path)
+            self.requests += 1
+            left = max(0.05, deadline - time.monotonic())
+            async with s.get(self.config.server + path, params=params, headers=self._headers(),
+                             timeout=aiohttp.ClientTimeout(total=left)) as r:
+                status, raw = r.status, await r.read()
+                hint = retry_after(r.headers.get("Retry-After")) if status >= 429 else None
+            if status >= 429:
+                d = self._backoff("GET", status, hint, attempt, deadline)
+                if d is not None:
+                    attempt += 1
+                    await asyncio.sleep(d)
+                    continue
+            return status, raw
 
     @contextlib.asynccontextmanager
     async def stream(self, path: str, params: Optional[Dict[str, str]] = None, timeout: float = 330.0):
         """Streaming GET (a watch); yields the response, its ``content`` read raw."""
         s = await self._s()
+        await self._admit(path)
         self.requests += 1
         async with s.get(self.config.server + path, params=params, headers=self._headers(),
                          timeout=aiohttp.ClientTimeout(total=timeout, sock_read=timeout)) as r:
@@ -357,6 +451,7 @@ class KubeClient:
             params["labelSelector"] = label_selector
         if field_selector:
             params["fieldSelector"] = field_selector
+        await self._admit(resource_path(kind, namespace))
         self.requests += 1
         async with s.get(self.config.server + resource_path(kind, namespace), params=params, headers=self._headers(),
                          timeout=aiohttp.ClientTimeout(total=timeout_seconds + 30, sock_read=timeout_seconds + 30)) as r:
@@ -369,7 +464,10 @@ class KubeClient:
                 if r.status == 410:
                     yield "ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": doc.get("message", "")}
                     return
-                raise from_status(r.status, doc)
+                hint = retry_after(r.headers.get("Retry-After")) if r.status >= 429 else None
+                if r.status >= 429:
+                    self._backoff("WATCH", r.status, hint, self.retry.max_retries)  # counted; the informer waits
+                raise from_status(r.status, doc, hint)
             decoder = _decoder(watch_projection(kind)) if projected else None
             if decoder is not None and router is not None:
                 decoder.set_router(*router)
@@ -424,18 +522,28 @@ class KubeClient:
         if not self.pipelined_writes:
             body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
             return await self.request("DELETE", path, body=body)
-        self.requests += 1
-        status, raw = await self._fast_client().request(
-            "DELETE", path, _delete_body(propagation_policy), self._headers({"Content-Type": "application/json"}))
-        if status < 400 and not want_body:
-            return {}  # the deleted object is not needed: skip decoding it
-        try:
-            doc = json.loads(raw) if raw else {}
-        except ValueError:
-            doc = {"message": raw[:500].decode("utf-8", "replace")}
-        if status >= 400:
-            raise from_status(status, doc)
-        return doc
+        attempt = 0
+        while True:
+            await self._admit(path)
+            self.requests += 1
+            status, raw = await self._fast_client().request(
+                "DELETE", path, _delete_body(propagation_policy), self._headers({"Content-Type": "application/json"}))
+            if status < 400 and not want_body:
+                return {}  # the deleted object is not needed: skip decoding it
+            hint = retry_after(getattr(raw, "retry_after", None)) if status >= 429 else None
+            if status >= 429:
+                d = self._backoff("DELETE", status, hint, attempt)
+                if d is not None:
+                    attempt += 1
+                    await asyncio.sleep(d)
+                    continue
+            try:
+                doc = json.loads(raw) if raw else {}
+            except ValueError:
+                doc = {"message": raw[:500].decode("utf-8", "replace")}
+            if status >= 400:
+                raise from_status(status, doc, hint)
+            return doc
 
     async def pod_log(self, namespace: str, name: str, container: str, *, previous: bool = False,
                       tail_lines: int = 200, limit_bytes: int = 65536, timeout: float = 2.0) -> Tuple[int, bytes]:
@@ -455,23 +563,33 @@ class KubeClient:
         ``(status, body)`` for :meth:`check_delete`, or ``None`` (use :meth:`delete_job`)."""
         if not self.pipelined_writes or self._fast is None:
             return None
+        if not self.limiter.try_accept():
+            return None  # no banked token: the retrying coroutine waits for one
         fut = self._fast.request_nowait("DELETE", resource_path("Job", namespace, name), _delete_body(propagation_policy),
                                         self._headers({"Content-Type": "application/json"}))
         if fut is not None:
             self.requests += 1
         return fut
 
-    @staticmethod
-    def check_delete(result) -> None:
-        """Raise the API error of a :meth:`delete_job_nowait` response (2xx: nothing)."""
+    def check_delete(self, result) -> None:
+        """Raise the API error of a :meth:`delete_job_nowait` response (2xx: nothing); a
+        429's ``Retry-After`` rides on the error (the caller's retry waits for it)."""
         status, raw = result
         if status < 400:
             return
+        hint = None
+        if status >= 429:
+            hint = retry_after(getattr(raw, "retry_after", None))
+            self.throttled += 1
+            if self.metrics is not None:
+                self.metrics.inc("kube_throttled", labels={"verb": "DELETE", "code": str(status)})
+            if hint is None and status == 429:
+                hint = self.retry.default_429
         try:
             doc = json.loads(raw) if raw else {}
         except ValueError:
             doc = {"message": raw[:500].decode("utf-8", "replace")}
-        raise from_status(status, doc)
+        raise from_status(status, doc, hint)
 
 
 class KubeListWatch(ListWatch):

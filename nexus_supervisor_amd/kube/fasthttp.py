@@ -46,6 +46,13 @@ def _header(head: bytes, name: bytes) -> bytes:
     return head[i: head.index(b"\r\n", i)].strip()
 
 
+class HintedBody(bytes):
+    """Body of an error answer that carried a ``Retry-After`` header (raw header value in
+    :attr:`retry_after`): the result stays ``(status, body)``."""
+
+    retry_after: bytes = b""
+
+
 def _expire_and_reset(fut: asyncio.Future, conn: "_Conn", what: str) -> None:
     if not fut.done():
         fut.set_exception(HttpError(f"{what} timed out"))
@@ -71,6 +78,7 @@ class _Conn(asyncio.Protocol):
         self._chunked = False
         self._body = bytearray()
         self._in_body = False
+        self._hint = b""
 
     # ----------------------------------------------------------- asyncio.Protocol
     def connection_made(self, transport):
@@ -115,6 +123,8 @@ class _Conn(asyncio.Protocol):
             self._chunked = b"chunked" in _header(head, b"\r\ntransfer-encoding:")
             self._need = -1 if self._chunked else int(_header(head, b"\r\ncontent-length:") or b"0")
             self._close = _header(head, b"\r\nconnection:") == b"close"
+            # 429 / 5xx: keep the server's Retry-After hint (API Priority and Fairness)
+            self._hint = _header(head, b"\r\nretry-after:") if self._status >= 429 else b""
             self._body = bytearray()
             self._in_body = True
         if self._chunked:
@@ -140,7 +150,12 @@ class _Conn(asyncio.Protocol):
         fut = self.waiting.popleft()
         self.deadlines.popleft()
         if not fut.done():
-            fut.set_result((self._status, bytes(self._body)))
+            if self._hint:
+                body = HintedBody(self._body)
+                body.retry_after = self._hint
+                fut.set_result((self._status, body))
+            else:
+                fut.set_result((self._status, bytes(self._body)))
         if self._close:
             self.transport.close()
         return True

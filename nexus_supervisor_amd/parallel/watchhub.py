@@ -159,7 +159,11 @@ class WatchHub:
                         if resp.status == 410:
                             raise _Gone()
                         if resp.status >= 400:
-                            raise RuntimeError(f"WATCH {kind}: HTTP {resp.status}")
+                            from ..kube.flowcontrol import retry_after
+
+                            err = RuntimeError(f"WATCH {kind}: HTTP {resp.status}")
+                            err.retry_after = retry_after(resp.headers.get("Retry-After"))  # 429: APF's hint
+                            raise err
                         async for chunk in resp.content.iter_any():
                             outs, last, errors = splitter.feed(chunk)
                             if last:
@@ -177,8 +181,9 @@ class WatchHub:
                 log.info("%s watch expired at rv=%s: re-listing", kind, rv)
                 continue
             except Exception as exc:  # noqa: BLE001 - connection errors: back off and re-list
-                log.warning("%s hub list/watch failed: %s; retrying in %.1fs", kind, exc, backoff)
-                await asyncio.sleep(backoff)
+                wait = max(backoff, getattr(exc, "retry_after", None) or 0.0)
+                log.warning("%s hub list/watch failed: %s; retrying in %.1fs", kind, exc, wait)
+                await asyncio.sleep(wait)
                 backoff = min(backoff * 2, 30.0)
 
 

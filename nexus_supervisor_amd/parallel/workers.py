@@ -624,12 +624,12 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
         # watch-hub mode: informers are fed by the parent's routed stream; the worker still
         # talks to the API server itself for Job DELETEs
         from ..informer import InformerFactory
-        from ..kube.client import KubeClient, KubeConfig
+        from ..kube.client import KubeClient
         from .watchhub import KINDS, HubFeed
 
         feed = HubFeed()
         await feed.start(data_sock)
-        kube = KubeClient(KubeConfig.load(cfg.kube_config_path))
+        kube = KubeClient.for_config(cfg, metrics)
         factory = InformerFactory(lambda kind: feed.list_watch(kind) if kind in KINDS else None,
                                   resync_period=cfg.resync_period)
         app = (app_factory or Application)(cfg, kube=kube, factory=factory, logger=logger, metrics=metrics, **extra)

@@ -194,6 +194,9 @@ class Supervisor:
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
         self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
+        self._log_sem: Optional[asyncio.Semaphore] = None  # gpu.log-tail-concurrency
+        self._log_inflight = 0
+        self.log_tail_inflight_max = 0
         g = cfg.gpu
         self._log_fetch = (g.attribution_enabled and g.log_tail in ("auto", "api")
                            and callable(getattr(jobs, "pod_log", None)))
@@ -555,10 +558,29 @@ class Supervisor:
         from .gpu.logtail import fetch_api_tail
 
         g = self.cfg.gpu
+        sem = self._log_sem
+        if sem is None:
+            sem = self._log_sem = asyncio.Semaphore(g.log_tail_concurrency)
+
+        async def one(w):
+            # pods/log is proxied through the kubelet: a GPU failure wave reads at most
+            # gpu.log-tail-concurrency tails at once per process, the rest queue here
+            if sem.locked():
+                self.metrics.inc("log_tail_queued")
+            async with sem:
+                self._log_inflight += 1
+                self.log_tail_inflight_max = max(self.log_tail_inflight_max, self._log_inflight)
+                self.metrics.set("log_tail_inflight", self._log_inflight)
+                try:
+                    return await fetch_api_tail(self.jobs, self.namespace, kube.name_of(pod), w["container"],
+                                                previous=w["previous"], limit_bytes=g.log_tail_bytes,
+                                                timeout=g.log_tail_timeout)
+                finally:
+                    self._log_inflight -= 1
+                    self.metrics.set("log_tail_inflight", self._log_inflight)
+
         try:
-            recs = await asyncio.gather(*(fetch_api_tail(self.jobs, self.namespace, kube.name_of(pod), w["container"],
-                                                         previous=w["previous"], limit_bytes=g.log_tail_bytes,
-                                                         timeout=g.log_tail_timeout) for w in want))
+            recs = await asyncio.gather(*(one(w) for w in want))
             for r, w in zip(recs, want):
                 r["restart"] = w["restart"]
                 if r.get("error"):
@@ -1039,7 +1061,9 @@ class Supervisor:
         if not self.active or not self.shards.owns(r.request_id):
             return  # fenced: the new leader's (shard owner's) replay owns this Job
         self.metrics.inc("job_delete_retries")
-        t = asyncio.ensure_future(self._delete_with_retry(r, first_delay=self.cfg.failure_rate_base_delay))
+        # a throttled DELETE (429) waits at least for the server's Retry-After hint
+        first = max(self.cfg.failure_rate_base_delay, getattr(exc, "retry_after", None) or 0.0)
+        t = asyncio.ensure_future(self._delete_with_retry(r, first_delay=first))
         self._deletes[t] = r.request_id
         t.add_done_callback(self._delete_done)
 
@@ -1082,7 +1106,7 @@ class Supervisor:
                 if c.max_retries and attempt >= c.max_retries:
                     cap = max(cap, 60.0)
                 self.metrics.inc("job_delete_retries")
-                await asyncio.sleep(delay)
+                await asyncio.sleep(max(delay, getattr(exc, "retry_after", None) or 0.0))
                 delay = min(delay * 2, cap)
 
     async def _write(self, cp, stage, cause, details, now_dt, set_failure, running=False) -> bool:

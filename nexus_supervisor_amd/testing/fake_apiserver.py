@@ -181,6 +181,16 @@ class FakeApiServer:
         self.deleted: List[Tuple[str, str, str, str]] = []  # (kind, ns, name, propagation)
         self._pods_by_job: Dict[Tuple[str, str], Set[str]] = {}  # (ns, job-name label) -> pod names (GC index)
         self.fail_next: Dict[Tuple[str, str], int] = {}  # (method, kind) -> count of 500s to inject
+        # (method, kind) -> count of 429s to inject, each with ``Retry-After: retry_after``
+        # (API Priority and Fairness rejecting the request); kind "PodLog" for pods/log
+        self.throttle_next: Dict[Tuple[str, str], int] = {}
+        self.retry_after = "1"
+        # (monotonic t, method, kind, name, status) of every throttled request and of every
+        # request to a name that was throttled before (to check retries honour the hint)
+        self.throttle_log: List[Tuple[float, str, str, str, int]] = []
+        self._throttled_names: Set[Tuple[str, str]] = set()
+        self.log_inflight = 0
+        self.log_inflight_max = 0
         self._snapshots: Dict[str, Tuple[int, List[Dict[str, Any]]]] = {}  # paginated LIST snapshots
         self.latency = 0.0
         # container logs served by GET …/pods/{name}/log: (ns, pod, container, previous) -> text
@@ -357,6 +367,20 @@ class FakeApiServer:
         if n:
             self.fail_next[(method, kind)] = n - 1
             return self._status(500, "InternalError", "injected failure")
+        return self._throttle(req, method, kind)
+
+    def _throttle(self, req: web.Request, method: str, kind: str) -> Optional[web.Response]:
+        name = req.match_info.get("name", "")
+        n = self.throttle_next.get((method, kind), 0)
+        if n:
+            self.throttle_next[(method, kind)] = n - 1
+            self._throttled_names.add((method, name))
+            self.throttle_log.append((time.monotonic(), method, kind, name, 429))
+            body = {"kind": "Status", "apiVersion": "v1", "status": "Failure", "code": 429, "reason": "TooManyRequests",
+                    "message": "too many requests, please try again later", "details": {"retryAfterSeconds": 1}}
+            return web.json_response(body, status=429, headers={"Retry-After": self.retry_after})
+        if (method, name) in self._throttled_names:
+            self.throttle_log.append((time.monotonic(), method, kind, name, 200))
         return None
 
     async def _h_collection(self, req: web.Request):
@@ -477,14 +501,22 @@ class FakeApiServer:
         bad = self._auth(req)
         if bad is not None:
             return bad
-        if self.latency or self.log_latency:
-            await asyncio.sleep(self.latency + self.log_latency)
+        self.log_inflight += 1
+        self.log_inflight_max = max(self.log_inflight_max, self.log_inflight)
+        try:
+            if self.latency or self.log_latency:
+                await asyncio.sleep(self.latency + self.log_latency)
+        finally:
+            self.log_inflight -= 1
         q = req.query
         self.log_requests.append(dict(q, pod=req.match_info["name"]))
         n = self.fail_next.get(("GET", "PodLog"), 0)
         if n:
             self.fail_next[("GET", "PodLog")] = n - 1
             return self._status(500, "InternalError", "injected failure")
+        hot = self._throttle(req, "GET", "PodLog")
+        if hot is not None:
+            return hot
         ns, name = req.match_info["ns"], req.match_info["name"]
         if (ns, name) not in self.objects["Pod"]:
             return self._status(404, "NotFound", f'pods "{name}" not found')

@@ -75,9 +75,10 @@ class Response:
         return ("\r\n".join(h) + "\r\n\r\n").encode("latin-1") + self.body
 
 
-def json_response(obj: Any, status: int = 200, dumps: Callable = None) -> Response:
+def json_response(obj: Any, status: int = 200, dumps: Callable = None,
+                  headers: Optional[Dict[str, str]] = None) -> Response:
     data = (dumps or (lambda o: json.dumps(o, separators=(",", ":"))))(obj)
-    return Response(body=data.encode() if isinstance(data, str) else data, status=status)
+    return Response(body=data.encode() if isinstance(data, str) else data, status=status, headers=headers)
 
 
 class StreamResponse:

@@ -103,8 +103,13 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
         assert not missing, f"{len(missing)} runs never reached their stage, e.g. {list(missing.items())[:3]}"
         survivor = apps[0]
         assert survivor.supervisor.active
-        # every failed run's Job was deleted through the API
-        deleted = {n for k, _ns, n, _p in api.deleted if k == "Job"}
+        # every failed run's Job was deleted through the API (paced by the client-side
+        # kube-qps bucket: 50/s by default, so the deletes trail the checkpoint writes)
+        for _ in range(200):
+            deleted = {n for k, _ns, n, _p in api.deleted if k == "Job"}
+            if set(expected) <= deleted:
+                break
+            await asyncio.sleep(0.05)
         assert set(expected) <= deleted
         # evicted runs were enriched with the eviction history (the Pod and Job watches are
         # separate streams, so a Job's failure can occasionally be decided before its pod's

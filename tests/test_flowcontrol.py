@@ -1,0 +1,222 @@
+"""Client-side API flow control (VERDICT r3 missing #1 / next #2).
+
+The reference's clientset runs on client-go's defaults (``/root/reference/app/
+app_dependencies.go:39-45``): a QPS 5 / burst 10 token bucket, and ``429`` answers
+retried after the server's ``Retry-After``.  Here: ``kube-qps`` / ``kube-burst`` shared by
+every request of a process, 429 / hinted 5xx retried never earlier than the hint, and a
+bound on concurrent ``pods/log`` reads.
+"""
+import asyncio
+import json
+import time
+
+import pytest
+
+from nexus_supervisor_amd.app import Application
+from nexus_supervisor_amd.config import load_config
+from nexus_supervisor_amd.config.schema import ConfigError
+from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig
+from nexus_supervisor_amd.kube.errors import TooManyRequests
+from nexus_supervisor_amd.kube.flowcontrol import RetryPolicy, TokenBucket, retry_after, split
+from nexus_supervisor_amd.models.checkpoint import CheckpointedRequest
+from nexus_supervisor_amd.store.memory import MemoryStore
+from nexus_supervisor_amd.testing.fake_apiserver import FakeApiServer
+from nexus_supervisor_amd.testing.seed import ALGORITHM, make_job, make_pod
+
+
+class Clock:
+    def __init__(self):
+        self.t = 100.0
+
+    def __call__(self):
+        return self.t
+
+
+def test_token_bucket_reservations_queue_at_qps():
+    c = Clock()
+    b = TokenBucket(10, 2, clock=c)
+    assert b.reserve() == 0 and b.reserve() == 0  # the burst
+    assert b.reserve() == pytest.approx(0.1)       # then one every 1/qps, in order
+    assert b.reserve() == pytest.approx(0.2)
+    c.t += 0.2
+    assert b.reserve() == pytest.approx(0.1)
+    assert not b.try_accept()
+    c.t += 10
+    assert b.try_accept() and b.try_accept() and not b.try_accept()  # refilled to burst only
+    assert TokenBucket(0, 1).reserve() == 0 and TokenBucket(0, 1).try_accept()
+
+
+def test_split_over_shard_workers():
+    assert split(50, 100, 1) == (50, 100)
+    assert split(50, 100, 4) == (12.5, 25)
+    assert split(0, 100, 4) == (0, 100)
+    assert split(5, 10, 16) == (5 / 16, 1)
+
+
+def test_retry_after_parsing_and_policy():
+    assert retry_after("3") == 3.0 and retry_after(b"1") == 1.0
+    assert retry_after("9999") == 60.0 and retry_after("-4") == 0.0
+    assert retry_after(None) is None and retry_after("soon") is None
+    assert retry_after("Wed, 21 Oct 2015 07:28:10 GMT", now=1445412480.0) == pytest.approx(10.0)
+    p = RetryPolicy()
+    assert p.delay(429, None) == 1.0 and p.delay(429, 4.0) == 4.0
+    assert p.delay(503, 2.0) == 2.0 and p.delay(503, None) is None and p.delay(404, 1.0) is None
+
+
+def test_config_keys_and_reference_defaults():
+    cfg = load_config(path=None, env={})
+    assert (cfg.kube_qps, cfg.kube_burst, cfg.kube_max_retries) == (50.0, 100, 10)
+    cfg = load_config(path=None, env={"NEXUS__KUBE_QPS": "5", "NEXUS__KUBE_BURST": "10"})
+    assert (cfg.kube_qps, cfg.kube_burst) == (5.0, 10)  # the reference's effective client-go limits
+    with pytest.raises(ConfigError):
+        load_config(path=None, env={}, overrides={"kube-burst": 0})
+    with pytest.raises(ConfigError):
+        load_config(path=None, env={}, overrides={"gpu": {"log-tail-concurrency": 0}})
+
+
+def test_client_retries_429_after_the_hint(arun):
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        api.create(make_job("j1", load_config(path=None, env={}).labels))
+        kc = KubeClient(KubeConfig(url))
+        api.throttle_next[("GET", "Job")] = 2
+        t0 = time.monotonic()
+        got = await kc.get("Job", "nexus", "j1")
+        assert got["metadata"]["name"] == "j1" and time.monotonic() - t0 >= 2.0
+        assert kc.throttled == 2 and kc.retried == 2
+        # out of retries: the 429 surfaces, typed, with the hint
+        kc.retry = RetryPolicy(max_retries=0)
+        api.throttle_next[("GET", "Job")] = 1
+        with pytest.raises(TooManyRequests) as ei:
+            await kc.get("Job", "nexus", "j1")
+        assert ei.value.retry_after == 1.0
+        await kc.close()
+        await api.stop()
+
+    arun(go(), timeout=20)
+
+
+def test_client_side_bucket_paces_requests(arun):
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        kc = KubeClient(KubeConfig(url), qps=20, burst=2)
+        t0 = time.monotonic()
+        await asyncio.gather(*(kc.list("Job", "nexus") for _ in range(12)))
+        took = time.monotonic() - t0
+        assert took >= (12 - 2) / 20 * 0.9, took  # burst 2, then 20/s
+        assert kc.limiter.waits >= 9
+        # Lease calls bypass the bucket (leader election never starves behind a DELETE burst)
+        kc.limiter = TokenBucket(0.5, 1)
+        kc.limiter.try_accept()
+        t0 = time.monotonic()
+        try:
+            await kc.get("Lease", "nexus", "none")
+        except Exception:
+            pass
+        assert time.monotonic() - t0 < 1.0
+        await kc.close()
+        await api.stop()
+
+    arun(go(), timeout=20)
+
+
+def _app_cfg(**over):
+    base = {"cql-store-type": "memory", "rate-limit-elements-per-second": 0, "resync-period": "0s",
+            "failure-rate-base-delay": "20ms", "failure-rate-max-delay": "200ms"}
+    base.update(over)
+    return load_config(path=None, env={}, overrides=base)
+
+
+def _oomkilled(pod):
+    p = json.loads(json.dumps(pod))
+    p["status"] = {"phase": "Failed", "containerStatuses": [
+        {"name": "algorithm", "restartCount": 0, "state": {"terminated": {"reason": "OOMKilled", "exitCode": 137}}}]}
+    p["metadata"]["resourceVersion"] = "2"
+    return p
+
+
+def test_throttled_job_deletes_all_land_and_honour_retry_after(arun):
+    """Done-criterion: the first 50 Job DELETEs get ``429 Retry-After: 1``.  Every Job is
+    deleted, no decision is dead-lettered, and no re-sent DELETE of a throttled Job comes
+    earlier than 1 s after its 429."""
+    n = 60
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        cfg = _app_cfg()
+        rids = [f"throttled-{i:03d}" for i in range(n)]
+        for r in rids:
+            api.create(make_pod(r, cfg.labels, status={"phase": "Running"}))
+            api.create(make_job(r, cfg.labels))
+        store = MemoryStore([CheckpointedRequest(algorithm=ALGORITHM, id=r, lifecycle_stage="RUNNING") for r in rids])
+        app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+        await app.start()
+        await app.factory.wait_for_cache_sync(5)
+        api.throttle_next[("DELETE", "Job")] = 50
+        for r in rids:
+            api.update(_oomkilled(api.get("Pod", "nexus", f"{r}-acdey")))
+        for _ in range(400):
+            if all(api.get("Job", "nexus", r) is None for r in rids):
+                break
+            await asyncio.sleep(0.02)
+        assert all(api.get("Job", "nexus", r) is None for r in rids)
+        assert all(store.get(ALGORITHM, r).lifecycle_stage == "FAILED" for r in rids)
+        assert app.supervisor.pipeline.stats.dead_lettered == 0
+        first_429 = {}
+        for t, method, _kind, name, status in api.throttle_log:
+            if status == 429:
+                first_429.setdefault(name, t)
+            else:
+                assert t - first_429[name] >= 0.99, (name, t - first_429[name])
+        assert len(first_429) == 50
+        assert app.kube.throttled >= 50
+        assert app.metrics.counters.get("kube_throttled")
+        await app.stop()
+        await api.stop()
+
+    arun(go(), timeout=40)
+
+
+def test_pods_log_wave_is_bounded(arun):
+    """Done-criterion: a 500-pod GPU failure wave (default pods: empty termination
+    messages, so every decision wants its container log) never has more than
+    ``gpu.log-tail-concurrency`` pods/log GETs in flight; every run is still decided."""
+    n, bound = 500, 8
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        cfg = _app_cfg(**{"kube-qps": 0, "gpu": {"log-tail-concurrency": bound}})
+        rids = [f"wave-{i:03d}" for i in range(n)]
+        for r in rids:
+            api.create(make_pod(r, cfg.labels, gpus=1, status={"phase": "Running"}))
+            api.create(make_job(r, cfg.labels))
+            api.set_pod_log("nexus", f"{r}-acdey", "algorithm", "torch.OutOfMemoryError: HIP out of memory.\n")
+        api.log_latency = 0.005
+        store = MemoryStore([CheckpointedRequest(algorithm=ALGORITHM, id=r, lifecycle_stage="RUNNING") for r in rids])
+        app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+        await app.start()
+        await app.factory.wait_for_cache_sync(5)
+        for r in rids:
+            p = json.loads(json.dumps(api.get("Pod", "nexus", f"{r}-acdey")))
+            p["status"] = {"phase": "Failed", "containerStatuses": [
+                {"name": "algorithm", "restartCount": 0,
+                 "state": {"terminated": {"reason": "Error", "exitCode": 1, "message": ""}}}]}
+            api.update(p)
+        for _ in range(1000):
+            if all(store.get(ALGORITHM, r).lifecycle_stage == "FAILED" for r in rids):
+                break
+            await asyncio.sleep(0.02)
+        assert all(store.get(ALGORITHM, r).lifecycle_stage == "FAILED" for r in rids)
+        assert json.loads(store.get(ALGORITHM, rids[-1]).algorithm_failure_details)["class"] == "hbm-oom"
+        assert len(api.log_requests) == n
+        assert api.log_inflight_max <= bound and app.supervisor.log_tail_inflight_max <= bound
+        assert app.supervisor.log_tail_inflight_max == bound  # the bound was reached, not idle
+        assert app.metrics.counter("log_tail_queued") > 0
+        await app.stop()
+        await api.stop()
+
+    arun(go(), timeout=60)
