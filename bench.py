@@ -74,6 +74,15 @@ def parse_args(argv=None):
     ap.add_argument("--cql-lwt-latency-us", type=int, default=-1,
                     help="extra CQL server latency of a conditional write (a Paxos round: ~4 round trips where a "
                          "plain write takes 1); -1 = 3 x --cql-latency-us")
+    ap.add_argument("--api-latency-us", type=int, default=0,
+                    help="simulated kube-apiserver answer latency of object requests (Job DELETE / GET / PATCH): "
+                         "the etcd write + admission a real apiserver spends; LIST / WATCH unaffected")
+    ap.add_argument("--api-write-qps", type=float, default=0.0,
+                    help="APF-like cap on the simulator's mutating requests: the excess is answered 429 + "
+                         "Retry-After (0 = no cap)")
+    ap.add_argument("--kube-qps", type=float, default=1_000_000.0,
+                    help="the supervisor's client-side kube-qps bucket (kube-burst = the same number); the "
+                         "production default is 50 / 100")
     ap.add_argument("--actuation", choices=("auto", "fused", "two-step"), default="auto",
                     help="compat.fused-write: auto (one conditional write per decision only under HA, else read + "
                          "write), fused (always one conditional write), two-step (the reference's read + write)")
@@ -225,6 +234,7 @@ def main(argv=None) -> int:
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
+                      api_latency_us=args.api_latency_us, api_write_qps=args.api_write_qps, kube_qps=args.kube_qps,
                       fused_write={"auto": "auto", "fused": "true", "two-step": "false"}[
                           "two-step" if args.two_step_write else args.actuation],
                       conditional_update=args.conditional_update, cql_lwt_latency_us=args.cql_lwt_latency_us,
@@ -329,6 +339,8 @@ def main(argv=None) -> int:
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
                 "cql_latency_us": args.cql_latency_us,
+                "api_latency_us": args.api_latency_us,
+                "api_write_qps": args.api_write_qps,
                 "actuation": res.get("actuation"),
                 "cql_lwt_latency_us": args.cql_lwt_latency_us,
                 "cpu_placement_rank0": placement,

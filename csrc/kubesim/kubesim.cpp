@@ -28,11 +28,19 @@
 //   POST   /sim/close-watches         cut every watch stream
 //   GET    /sim/stats                 counters
 //
+// Pricing the API server: --api-latency-us answers every object
+// request (GET / DELETE / POST / PUT / PATCH; not LIST / WATCH) that long after it was
+// applied, in order per connection (an etcd write + admission); --write-qps caps mutating
+// requests with a token bucket and answers the excess 429 + Retry-After, as API Priority and
+// Fairness does; --throttle-deletes N answers the first N Job DELETEs 429 + Retry-After
+// (--retry-after S) for the client's flow-control path.
+//
 // Paths: /api/v1/namespaces/{ns}/{plural}[/{name}], /apis/{group}/{version}/namespaces/…,
 // and the cluster-wide /api/v1/{plural}.  Optional bearer token (--token).
 //
 // nexus-kubesim [--host 127.0.0.1] [--port 0] [--ready-file F] [--history N]
-//               [--bookmark-ms 1000] [--token T]
+//               [--bookmark-ms 1000] [--token T] [--api-latency-us US] [--write-qps Q]
+//               [--write-burst B] [--throttle-deletes N] [--retry-after S]
 #include <arpa/inet.h>
 #include <dlfcn.h>
 #include <execinfo.h>
@@ -144,6 +152,11 @@ struct Options {
   // this many threads (the apiserver's watch cache serves many watchers in parallel; a
   // sharded supervisor deployment has every replica watching the whole namespace)
   int flush_threads = 1;
+  int64_t api_latency_us = 0;   // answer object requests this long after applying them
+  double write_qps = 0;         // mutating requests per second (token bucket); 0 = no cap
+  int write_burst = 0;          // bucket size (0 = max(1, write_qps))
+  int64_t throttle_deletes = 0; // answer this many first Job DELETEs 429
+  int retry_after_s = 1;        // Retry-After of every 429
 } g_opt;
 
 int64_t mono_ns() {
@@ -495,7 +508,7 @@ KindStore g_store[NKINDS];
 std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x01 job → pod names
 int64_t g_rv = 1000;
 struct Stats {
-  uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0;
+  uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0, throttled = 0, delayed = 0;
   uint64_t loops = 0;
   std::atomic<uint64_t> sends{0}, send_bytes{0}, eagain{0};  // also counted by fan-out threads
   // wall time spent per phase of the event loop (ns): where a saturated simulator goes
@@ -1028,6 +1041,9 @@ struct Conn {
   int fd;
   std::string in;
   std::string out;
+  // --api-latency-us: answers held until their due time (CLOCK_MONOTONIC ns), FIFO so a
+  // pipelined connection's answers keep their order
+  std::deque<std::pair<int64_t, std::string>> delayed;
   Watch* watch = nullptr;
   bool close_after = false;
   uint32_t mask = EPOLLIN | EPOLLRDHUP;  // registered epoll interest (skip redundant epoll_ctl)
@@ -1036,6 +1052,8 @@ struct Conn {
 int g_ep = -1;
 std::unordered_map<int, std::unique_ptr<Conn>> g_conns;
 std::set<Conn*> g_dirty;  // connections with queued output
+std::set<Conn*> g_delayed;  // connections holding answers for --api-latency-us
+bool g_delay_this = false;  // the request being handled is answered after the latency
 
 void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
@@ -1080,6 +1098,7 @@ void close_conn(int fd) {
   Conn* c = it->second.get();
   end_watch(*c, false);
   g_dirty.erase(c);
+  g_delayed.erase(c);
   epoll_ctl(g_ep, EPOLL_CTL_DEL, fd, nullptr);
   close(fd);
   g_conns.erase(it);
@@ -1272,18 +1291,79 @@ std::string status_text(int code) {
     case 409: return "Conflict";
     case 410: return "Gone";
     case 411: return "Length Required";
+    case 429: return "Too Many Requests";
     case 500: return "Internal Server Error";
   }
   return "Unknown";
 }
 
-void respond(Conn& c, int code, const std::string& body) {
-  char hdr[160];
-  snprintf(hdr, sizeof hdr, "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s\r\n", code,
-           status_text(code).c_str(), body.size(), c.close_after ? "Connection: close\r\n" : "");
+void respond(Conn& c, int code, const std::string& body, const char* extra = "") {
+  char hdr[200];
+  snprintf(hdr, sizeof hdr, "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s%s\r\n", code,
+           status_text(code).c_str(), body.size(), extra, c.close_after ? "Connection: close\r\n" : "");
+  if (g_delay_this || !c.delayed.empty()) {
+    // priced answer (or one queued behind a priced answer on this connection)
+    int64_t due = mono_ns() + (g_delay_this ? g_opt.api_latency_us * 1000 : 0);
+    if (!c.delayed.empty()) due = std::max(due, c.delayed.back().first);
+    std::string msg(hdr);
+    msg += body;
+    c.delayed.emplace_back(due, std::move(msg));
+    g_delayed.insert(&c);
+    ++g_stats.delayed;
+    return;
+  }
   c.out += hdr;
   c.out += body;
   g_dirty.insert(&c);
+}
+
+// move due answers to the output buffers; returns ms until the next one is due (-1: none)
+int release_delayed() {
+  if (g_delayed.empty()) return -1;
+  int64_t now = mono_ns(), next = INT64_MAX;
+  for (auto it = g_delayed.begin(); it != g_delayed.end();) {
+    Conn* c = *it;
+    while (!c->delayed.empty() && c->delayed.front().first <= now) {
+      c->out += c->delayed.front().second;
+      c->delayed.pop_front();
+      g_dirty.insert(c);
+    }
+    if (c->delayed.empty()) {
+      it = g_delayed.erase(it);
+    } else {
+      next = std::min(next, c->delayed.front().first);
+      ++it;
+    }
+  }
+  if (next == INT64_MAX) return -1;
+  return static_cast<int>(std::max<int64_t>(0, (next - now + 999999) / 1000000));
+}
+
+// --write-qps: token bucket over mutating requests
+double g_wtokens = -1;
+int64_t g_wlast = 0;
+bool write_admitted() {
+  if (g_opt.write_qps <= 0) return true;
+  double burst = g_opt.write_burst > 0 ? g_opt.write_burst : std::max(1.0, g_opt.write_qps);
+  int64_t now = mono_ns();
+  if (g_wtokens < 0) g_wtokens = burst;
+  else g_wtokens = std::min(burst, g_wtokens + (now - g_wlast) * 1e-9 * g_opt.write_qps);
+  g_wlast = now;
+  if (g_wtokens < 1.0) return false;
+  g_wtokens -= 1.0;
+  return true;
+}
+
+std::string status_body(int code, const std::string& reason, const std::string& message);
+
+void too_many(Conn& c) {
+  ++g_stats.throttled;
+  char extra[48];
+  snprintf(extra, sizeof extra, "Retry-After: %d\r\n", g_opt.retry_after_s);
+  bool d = g_delay_this;
+  g_delay_this = false;  // a rejection is cheap: answered at once (still in order)
+  respond(c, 429, status_body(429, "TooManyRequests", "too many requests, please try again later"), extra);
+  g_delay_this = d;
 }
 
 std::string status_body(int code, const std::string& reason, const std::string& message) {
@@ -1526,6 +1606,7 @@ void handle(Conn& c, Request& r) {
       std::string s = "{\"requests\":" + std::to_string(g_stats.requests) +
                       ",\"watch_requests\":" + std::to_string(g_stats.watch_requests) + ",\"rv\":" + std::to_string(g_rv) +
                       ",\"deleted\":" + std::to_string(g_stats.deleted) + ",\"applied\":" + std::to_string(g_stats.applied) +
+                      ",\"throttled\":" + std::to_string(g_stats.throttled) + ",\"delayed\":" + std::to_string(g_stats.delayed) +
                       ",\"loops\":" + std::to_string(g_stats.loops) + ",\"sends\":" + std::to_string(g_stats.sends) +
                       ",\"send_bytes\":" + std::to_string(g_stats.send_bytes) + ",\"eagain\":" + std::to_string(g_stats.eagain) +
                       ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
@@ -1563,6 +1644,17 @@ void handle(Conn& c, Request& r) {
     if (wq == "1" || wq == "true") return h_watch(c, r, kind, ns);
     return h_list(c, r, kind, ns);
   }
+  if (r.method != "GET") {
+    if (r.method == "DELETE" && kind == K_JOB && g_opt.throttle_deletes > 0) {
+      --g_opt.throttle_deletes;
+      return too_many(c);
+    }
+    if (!write_admitted()) return too_many(c);
+  }
+  struct DelayScope {
+    DelayScope() { g_delay_this = g_opt.api_latency_us > 0; }
+    ~DelayScope() { g_delay_this = false; }
+  } delay_scope;
   if (r.method == "GET") {
     auto it = g_store[kind].objs.find(okey(ns, name));
     if (it == g_store[kind].objs.end()) return respond(c, 404, status_body(404, "NotFound", lower + "s \"" + name + "\" not found"));
@@ -1713,7 +1805,8 @@ void on_signal(int) { g_stop = 1; }
 void usage() {
   fprintf(stderr,
           "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n"
-          "              [--flush-threads N]\n");
+          "              [--flush-threads N] [--api-latency-us US] [--write-qps Q] [--write-burst B]\n"
+          "              [--throttle-deletes N] [--retry-after S]\n");
 }
 
 }  // namespace
@@ -1735,6 +1828,11 @@ int main(int argc, char** argv) {
     else if (a == "--bookmark-ms") g_opt.bookmark_ms = atol(next().c_str());
     else if (a == "--token") g_opt.token = next();
     else if (a == "--flush-threads") g_opt.flush_threads = std::max(1, atoi(next().c_str()));
+    else if (a == "--api-latency-us") g_opt.api_latency_us = std::max(0L, atol(next().c_str()));
+    else if (a == "--write-qps") g_opt.write_qps = atof(next().c_str());
+    else if (a == "--write-burst") g_opt.write_burst = atoi(next().c_str());
+    else if (a == "--throttle-deletes") g_opt.throttle_deletes = atol(next().c_str());
+    else if (a == "--retry-after") g_opt.retry_after_s = std::max(0, atoi(next().c_str()));
     else {
       usage();
       return 2;
@@ -1801,7 +1899,13 @@ int main(int argc, char** argv) {
   int64_t last_tick = mono_ms();
   char buf[1 << 16];
   while (!g_stop) {
-    int n = epoll_wait(g_ep, evs.data(), static_cast<int>(evs.size()), 100);
+    int wait_ms = 100;
+    if (!g_delayed.empty()) {
+      int d = release_delayed();
+      if (d >= 0) wait_ms = std::min(wait_ms, d);
+    }
+    if (!g_dirty.empty()) wait_ms = 0;
+    int n = epoll_wait(g_ep, evs.data(), static_cast<int>(evs.size()), wait_ms);
     int64_t t_loop = mono_ns();
     ++g_stats.loops;
     if (n < 0 && errno != EINTR) {
@@ -1854,6 +1958,7 @@ int main(int argc, char** argv) {
       }
       if (evs[i].events & EPOLLOUT) g_dirty.insert(&c);
     }
+    if (!g_delayed.empty()) release_delayed();
     int64_t now = mono_ms();
     if (now - last_tick >= 50) {
       last_tick = now;

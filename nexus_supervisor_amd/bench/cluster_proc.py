@@ -47,7 +47,8 @@ async def amain(args) -> None:
         from ..testing.kubesim import KubeSim, SimControl, encode_events
 
         sim = KubeSim(host=args.host, port=args.port, history=args.history, bookmark_ms=2000,
-                      flush_threads=args.flush_threads).start()
+                      flush_threads=args.flush_threads, api_latency_us=args.api_latency_us,
+                      write_qps=args.write_qps, write_burst=args.write_burst).start()
         simctl = SimControl(sim.url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)
@@ -236,6 +237,9 @@ def main(argv=None) -> int:
     # fresh page-faulted allocation instead of a recycled one) and costs it throughput.
     ap.add_argument("--history", type=int, default=50_000)
     ap.add_argument("--flush-threads", type=int, default=1, help="simulator watch fan-out threads")
+    ap.add_argument("--api-latency-us", type=int, default=0, help="simulated API answer latency (kubesim)")
+    ap.add_argument("--write-qps", type=float, default=0.0, help="APF-like cap on mutating requests (kubesim)")
+    ap.add_argument("--write-burst", type=int, default=0)
     ap.add_argument("--api", choices=("kubesim", "python"), default="kubesim",
                     help="native apiserver simulator (default) or the Python fake")
     args = ap.parse_args(argv)

@@ -36,6 +36,8 @@ class BenchConfig:
     workdir: str = "/tmp"
     step_timeout: float = 300.0
     cql_latency_us: int = 0
+    api_latency_us: int = 0  # simulated apiserver answer latency of object requests (kubesim)
+    api_write_qps: float = 0.0  # APF-like cap on the simulator's mutating requests (429 + Retry-After)
     cql_lwt_latency_us: int = -1  # extra latency of a conditional write (Paxos); -1 = 3 x cql_latency_us
     fused_write: str = "auto"  # compat.fused-write: auto | true | false (the reference's read + write)
     conditional_update: str = "auto"  # compat.conditional-update

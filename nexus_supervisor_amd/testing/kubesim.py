@@ -33,7 +33,8 @@ def encode_events(events: Iterable[Tuple[str, Dict[str, Any]]]) -> bytes:
 
 class KubeSim:
     def __init__(self, *, host: str = "127.0.0.1", port: int = 0, history: int = 400_000, bookmark_ms: int = 1000,
-                 token: str = "", flush_threads: int = 1):
+                 token: str = "", flush_threads: int = 1, api_latency_us: int = 0, write_qps: float = 0.0,
+                 write_burst: int = 0, throttle_deletes: int = 0, retry_after: int = 1):
         from .._build import binary
 
         self.exe = os.environ.get("NEXUS_KUBESIM_BINARY") or binary("nexus-kubesim")
@@ -41,6 +42,10 @@ class KubeSim:
         self.host, self.port = host, port
         self.history, self.bookmark_ms, self.token = history, bookmark_ms, token
         self.flush_threads = flush_threads  # parallel watch fan-out (many watching replicas)
+        # pricing the API server: answer latency, APF-like write cap (429 + Retry-After) and
+        # injected 429s on the first Job DELETEs
+        self.api_latency_us, self.write_qps, self.write_burst = api_latency_us, write_qps, write_burst
+        self.throttle_deletes, self.retry_after = throttle_deletes, retry_after
         self.proc: Optional[subprocess.Popen] = None
         self.log_path = os.path.join(self.dir, "server.log")
         self.url = ""
@@ -55,6 +60,14 @@ class KubeSim:
             argv += ["--token", self.token]
         if self.flush_threads > 1:
             argv += ["--flush-threads", str(self.flush_threads)]
+        if self.api_latency_us:
+            argv += ["--api-latency-us", str(int(self.api_latency_us))]
+        if self.write_qps:
+            argv += ["--write-qps", str(self.write_qps), "--write-burst", str(int(self.write_burst))]
+        if self.throttle_deletes:
+            argv += ["--throttle-deletes", str(int(self.throttle_deletes))]
+        if self.throttle_deletes or self.write_qps:
+            argv += ["--retry-after", str(int(self.retry_after))]
         logf = open(self.log_path, "ab")
         self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True)
         logf.close()

@@ -283,3 +283,45 @@ def test_parallel_watch_fanout_under_tsan(arun, monkeypatch):
     arun(go(), timeout=120)
     log = holder["sim"].log()
     assert "ThreadSanitizer" not in log, log[-3000:]
+
+
+def test_priced_apiserver_latency_throttle_and_write_cap(arun):
+    """the simulator prices the API server.  --api-latency-us holds
+    object answers (in order on a pipelined connection; LIST unaffected), --throttle-deletes
+    answers the first Job DELETEs 429 + Retry-After (the client re-sends after the hint), and
+    --write-qps caps mutating requests the way APF rejects them."""
+    import time
+
+    async def go():
+        labels = _cfg().labels
+        with KubeSim(api_latency_us=30_000, throttle_deletes=2, retry_after=1) as sim:
+            ctl = SimControl(sim.url)
+            await ctl.apply([("ADDED", make_job(f"j{i}", labels)) for i in range(6)])
+            c = KubeClient(KubeConfig(sim.url))
+            t0 = time.monotonic()
+            await c.list("Job", "nexus")
+            assert time.monotonic() - t0 < 0.025  # LIST is not priced
+            t0 = time.monotonic()
+            await c.get("Job", "nexus", "j0")
+            assert time.monotonic() - t0 >= 0.029
+            # pipelined DELETEs: answers keep their order, each ≥ the latency
+            t0 = time.monotonic()
+            futs = [c.delete_job("nexus", f"j{i}") for i in range(3, 6)]
+            await asyncio.gather(*futs)
+            took = time.monotonic() - t0
+            assert took >= 1.0  # the first two DELETEs were throttled: re-sent after Retry-After 1
+            assert c.throttled == 2 and c.retried == 2
+            st = await ctl.stats()
+            assert st["throttled"] == 2 and st["deleted"] == 3 and st["delayed"] >= 4
+            await c.close()
+        with KubeSim(write_qps=5, write_burst=2, retry_after=1) as sim:
+            ctl = SimControl(sim.url)
+            await ctl.apply([("ADDED", make_job(f"k{i}", labels)) for i in range(4)])
+            c = KubeClient(KubeConfig(sim.url), max_retries=0)
+            res = await asyncio.gather(*(c.delete_job("nexus", f"k{i}") for i in range(4)), return_exceptions=True)
+            codes = sorted(getattr(r, "status", 200) for r in res)
+            assert codes == [200, 200, 429, 429], codes
+            assert all(r.retry_after == 1.0 for r in res if isinstance(r, ApiError))
+            await c.close()
+
+    arun(go(), timeout=30)
