@@ -94,18 +94,26 @@ class Tracker:
         self.wrong_examples: List[Tuple[str, Optional[str], str]] = []
         self.checked: Dict[str, str] = {}  # timed run → expected stage (read-back)
         self.record = False
+        # recorded decisions' push→ack decomposition (ms): api (push → hub read), hub (→ worker
+        # frame), feed (→ decoded), dispatch (→ handler), supervise (handler → checkpoint ack)
+        self.parts: List[Tuple[float, float, float, float, float, float]] = []
 
     def __call__(self, d: Decision):
-        self.report(d.result.request_id, d.outcome, d.result.stamps.get("ack_mono"), d.new_stage)
+        s = d.result.stamps
+        x = None
+        dl = s.get("delivery")
+        if dl is not None and "ack" in s and "receive" in s:
+            x = (dl[0], dl[1], dl[2], s["ack"] - s["receive"])
+        self.report(d.result.request_id, d.outcome, s.get("ack_mono"), d.new_stage, x)
 
-    def report(self, rid: str, outcome: str, ack: Optional[float], stage: Optional[str]) -> None:
+    def report(self, rid: str, outcome: str, ack: Optional[float], stage: Optional[str], x=None) -> None:
         # the metric is pod-fail → checkpoint *write ack* (the Job DELETE follows the write)
         t = ack or time.monotonic()
         st = self.owner.pop(rid, None)
         if st is None:
-            self.acks[rid] = (t, outcome, stage)  # ack raced ahead of the step response
+            self.acks[rid] = (t, outcome, stage, x)  # ack raced ahead of the step response
             return
-        st.settle(self, rid, t, outcome, stage)
+        st.settle(self, rid, t, outcome, stage, x)
 
     def arm(self, rids: List[str], t_push: float, expected: Optional[Dict[str, str]] = None) -> "StepState":
         st = StepState(set(rids), t_push, self.record, expected or {})
@@ -139,7 +147,7 @@ class StepState:
         self.expected = expected
         self.done = asyncio.Event()
 
-    def settle(self, tr: Tracker, rid: str, t: float, outcome: str, stage: Optional[str] = None) -> None:
+    def settle(self, tr: Tracker, rid: str, t: float, outcome: str, stage: Optional[str] = None, x=None) -> None:
         self.waiting.discard(rid)
         want = self.expected.get(rid)
         if outcome != "applied":
@@ -150,7 +158,12 @@ class StepState:
                 if len(tr.wrong_examples) < 5:
                     tr.wrong_examples.append((rid, stage, want))
             if self.record:
-                tr.latencies.append((t - self.t_push) * 1000.0)
+                total = (t - self.t_push) * 1000.0
+                tr.latencies.append(total)
+                if x is not None:
+                    hub, feed, dec, r2c = x
+                    tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
+                                     (t - r2c - dec) * 1e3, r2c * 1e3))
         if not self.waiting:
             self.done.set()
 
@@ -358,6 +371,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     import random
 
     saved, tracker.latencies = tracker.latencies, []
+    saved_parts, tracker.parts = tracker.parts, []
     rate = cfg.probe_rate_per_min / 60.0
     rng = random.Random(0x5EED + cfg.seed + cfg.rank)
     loop = asyncio.get_running_loop()
@@ -377,13 +391,48 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         except asyncio.TimeoutError:
             tracker.abandon(st)
     lat = sorted(tracker.latencies)
-    tracker.latencies = saved
+    parts = tracker.parts
+    tracker.latencies, tracker.parts = saved, saved_parts
     if not lat:
         return {"events": 0}
     q = lambda p: lat[min(len(lat) - 1, int(round(p * (len(lat) - 1))))]  # noqa: E731
-    return {"rate_per_min": cfg.probe_rate_per_min, "arrivals": "poisson", "events": len(lat),
-            "p50_ms": round(q(0.5), 3), "p90_ms": round(q(0.9), 3), "p99_ms": round(q(0.99), 3),
-            "max_ms": round(lat[-1], 3)}
+    out = {"rate_per_min": cfg.probe_rate_per_min, "arrivals": "poisson", "events": len(lat),
+           "p50_ms": round(q(0.5), 3), "p90_ms": round(q(0.9), 3), "p99_ms": round(q(0.99), 3),
+           "max_ms": round(lat[-1], 3)}
+    if parts:
+        out["delivery"] = decompose(parts)
+    return out
+
+
+PART_NAMES = ("api", "hub", "feed", "dispatch", "supervise")
+
+
+def decompose(parts) -> Dict[str, Any]:
+    """Per-decision push→ack decomposition: every stage's p50 / p99, and the mean of each
+    stage over the median band (p45–p55) and the tail (≥ p99) of the *total* — those means
+    sum to the band's mean total, so the tail is explained stage by stage."""
+    ps = sorted(parts)
+    n = len(ps)
+
+    def qs(vals, p):
+        v = sorted(vals)
+        return round(v[min(len(v) - 1, int(round(p * (len(v) - 1))))], 3)
+
+    out: Dict[str, Any] = {"events": n, "stages": {}}
+    for i, name in enumerate(PART_NAMES, start=1):
+        col = [p[i] for p in ps]
+        out["stages"][name] = {"p50": qs(col, 0.5), "p99": qs(col, 0.99)}
+
+    def band(lo, hi):
+        sel = ps[int(lo * (n - 1)):max(int(lo * (n - 1)) + 1, int(round(hi * (n - 1))) + 1)]
+        m = {name: round(sum(p[i] for p in sel) / len(sel), 3) for i, name in enumerate(PART_NAMES, start=1)}
+        m["total"] = round(sum(p[0] for p in sel) / len(sel), 3)
+        m["events"] = len(sel)
+        return m
+
+    out["median_band_mean_ms"] = band(0.45, 0.55)
+    out["tail_p99_mean_ms"] = band(0.99, 1.0)
+    return out
 
 
 async def _read_back(harness, tracker: "Tracker") -> Dict[str, Any]:
@@ -409,7 +458,7 @@ def _actuation(sc: SupervisorConfig) -> str:
 
 
 STAGES = ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_prepare", "stage_write",
-          "stage_delete")
+          "stage_delete", "stage_hub", "stage_feed", "stage_dispatch")
 
 
 def _stage_counts(sup) -> Dict[str, Tuple[Dict[int, int], int, int]]:

@@ -37,6 +37,7 @@ import aiohttp
 
 from ..informer.informer import ListWatch
 from ..models.kube import FINISHERS, PROJECTIONS, list_projection, watch_projection
+from ..obs import delivery as _delivery
 from .errors import ApiError, from_status
 from .flowcontrol import RetryPolicy, TokenBucket, retry_after
 
@@ -473,8 +474,14 @@ class KubeClient:
                 decoder.set_router(*router)
             if decoder is not None:
                 n = 0
+                current = _delivery.CURRENT
                 async for chunk in r.content.iter_any():
-                    for ev in decoder.feed(chunk):
+                    t_read = time.monotonic()
+                    evs = decoder.feed(chunk)
+                    if evs:
+                        # hub-less replica: the chunk's read is both the "hub" and "feed" stamp
+                        current[kind] = (t_read, t_read, time.monotonic())
+                    for ev in evs:
                         obj = ev.get("object") or {}
                         if obj.get("kind") is None:
                             obj["kind"] = kind

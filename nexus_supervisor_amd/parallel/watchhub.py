@@ -21,25 +21,30 @@ replica.  The parent process runs the hub:
   re-list path, so the informer's diff logic is unchanged.  A restarted worker gets a
   fresh snapshot the same way (:meth:`WatchHub.resync`).
 
-Frame: ``!BBI`` (type, kind index, payload length) + payload.
+Frame: ``!BBI`` (type, kind index, payload length) + payload.  ``LINES_T`` is ``LINES``
+with an ``!d`` prefix: the CLOCK_MONOTONIC time the hub read the chunk from the API server
+(:mod:`..obs.delivery` — the delivery-latency stages).
 """
 from __future__ import annotations
 
 import asyncio
 import logging
 import struct
+import time
 from time import thread_time as _thread_time
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..informer.informer import ListWatch
+from ..obs import delivery as _delivery
 from ..models.kube import PROJECTIONS, watch_projection
 
 log = logging.getLogger("nexus_supervisor_amd.watchhub")
 
 KINDS: Tuple[str, ...] = ("Event", "Pod", "Job")
 ROLES = {"Event": "event", "Pod": "pod", "Job": "job"}
-SNAPSHOT, LINES = 1, 2
+SNAPSHOT, LINES, LINES_T = 1, 2, 3
 HEADER = struct.Struct("!BBI")
+STAMP = struct.Struct("!d")
 HIGH_WATER = 32 << 20
 
 
@@ -165,11 +170,12 @@ class WatchHub:
                             err.retry_after = retry_after(resp.headers.get("Retry-After"))  # 429: APF's hint
                             raise err
                         async for chunk in resp.content.iter_any():
+                            t_read = time.monotonic()
                             outs, last, errors = splitter.feed(chunk)
                             if last:
                                 rv = last
                             if any(outs):
-                                await self._route(ki, outs, LINES)
+                                await self._route(ki, outs, LINES_T, STAMP.pack(t_read))
                             if errors:
                                 if any(_is_gone(e) for e in errors):
                                     raise _Gone()
@@ -212,15 +218,31 @@ class HubFeed:
         n = len(buf)
         pos = 0
         pending: Dict[int, List[bytes]] = {}
+        stamped: Dict[int, Tuple[float, float]] = {}  # kind -> (hub read time of its oldest lines, now)
         queues = self.queues
         view = memoryview(buf)
+        t_feed = 0.0
+
+        def lines_item(ki, parts):
+            payload = b"".join(parts) if len(parts) > 1 else parts[0]
+            st = stamped.pop(ki, None)
+            return (LINES, payload) if st is None else (LINES, payload, st)
+
         try:
             while n - pos >= hs:
                 ftype, ki, ln = HEADER.unpack_from(buf, pos)
                 end = pos + hs + ln
                 if end > n:
                     break
-                payload = bytes(view[pos + hs:end])
+                if ftype == LINES_T and ln >= 8:
+                    if not t_feed:
+                        t_feed = time.monotonic()
+                    if ki not in stamped:
+                        stamped[ki] = (STAMP.unpack_from(buf, pos + hs)[0], t_feed)
+                    payload = bytes(view[pos + hs + 8:end])
+                    ftype = LINES
+                else:
+                    payload = bytes(view[pos + hs:end])
                 pos = end
                 self.frames += 1
                 q = queues.get(ki)
@@ -231,12 +253,12 @@ class HubFeed:
                     continue
                 parts = pending.pop(ki, None)  # this kind's earlier lines go first
                 if parts:
-                    q.put_nowait((LINES, b"".join(parts) if len(parts) > 1 else parts[0]))
+                    q.put_nowait(lines_item(ki, parts))
                 q.put_nowait((ftype, payload))
         finally:
             view.release()
         for ki, parts in pending.items():
-            queues[ki].put_nowait((LINES, b"".join(parts) if len(parts) > 1 else parts[0]))
+            queues[ki].put_nowait(lines_item(ki, parts))
         return pos
 
     def _closed(self) -> None:
@@ -292,7 +314,8 @@ class HubListWatch(ListWatch):
 
     async def list(self) -> Tuple[List[Dict[str, Any]], str]:
         while self._pending is None:
-            ftype, payload = await self.queue.get()
+            item = await self.queue.get()
+            ftype, payload = item[0], item[1]
             if ftype == SNAPSHOT:
                 self._pending = payload
             elif ftype == 0:
@@ -313,14 +336,17 @@ class HubListWatch(ListWatch):
 
         decoder = _kube_native.ProjectedDecoder(self._watch_proj)
         kind = self.kind
+        current = _delivery.CURRENT
         while True:
-            ftype, payload = await self.queue.get()
+            item = await self.queue.get()
+            ftype, payload = item[0], item[1]
             if ftype == SNAPSHOT:
                 self._pending = payload
                 yield [("ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": "hub re-listed"})]
                 return
             if ftype == 0:
                 raise ConnectionError("watch hub closed")
+            stamp = item[2] if len(item) > 2 else None  # the oldest joined frame's (hub, feed)
             # lines queued behind this frame while the worker was busy join it: one decode call
             # and one informer batch for all of them (a snapshot or close stays queued first)
             q = self.queue
@@ -328,7 +354,10 @@ class HubListWatch(ListWatch):
             while q._queue and q._queue[0][0] == LINES:  # type: ignore[attr-defined]
                 if parts is None:
                     parts = [payload]
-                parts.append(q.get_nowait()[1])
+                nxt = q.get_nowait()
+                parts.append(nxt[1])
+                if stamp is None and len(nxt) > 2:
+                    stamp = nxt[2]
             if parts is not None:
                 payload = b"".join(parts)
             # (type, object) pairs with the object's kind defaulted, built by the decoder itself
@@ -337,7 +366,11 @@ class HubListWatch(ListWatch):
             self.decode_seconds += _thread_time() - t0
             self.decoded_lines += len(batch)
             if batch:
+                if stamp is not None:
+                    current[kind] = (stamp[0], stamp[1], time.monotonic())
                 yield batch
+                if stamp is not None:
+                    current.pop(kind, None)  # dispatched: later (timer) handler calls get no stamps
 
     async def watch(self, resource_version: str):
         from .. import _kube_native
@@ -346,7 +379,8 @@ class HubListWatch(ListWatch):
         kind = self.kind
         n = 0
         while True:
-            ftype, payload = await self.queue.get()
+            item = await self.queue.get()
+            ftype, payload = item[0], item[1]
             if ftype == SNAPSHOT:
                 self._pending = payload
                 yield "ERROR", {"kind": "Status", "code": 410, "reason": "Expired", "message": "hub re-listed"}

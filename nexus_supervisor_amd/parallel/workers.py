@@ -423,10 +423,10 @@ class WorkerPool:
             op = msg.get("op")
             if op == "dec":
                 for h in self.report_hooks:
-                    for rid, _alg, outcome, ack, stage in msg["d"]:
-                        h(rid, outcome, ack, stage)
+                    for d in msg["d"]:
+                        h(d[0], d[2], d[3], d[4], d[5] if len(d) > 5 else None)
                 if self.decision_hooks:
-                    for rid, alg, outcome, ack, stage in msg["d"]:
+                    for rid, alg, outcome, ack, stage, *_x in msg["d"]:
                         r = RunStatusAnalysisResult("", "", "", request_id=rid, algorithm=alg)
                         if ack is not None:
                             r.stamps["ack_mono"] = ack
@@ -649,7 +649,13 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
         r = d.result
         if not batch:
             loop.call_soon(flush)
-        batch.append([r.request_id, r.algorithm, d.outcome, r.stamps.get("ack_mono") if r.stamps else None, d.new_stage])
+        st = r.stamps
+        rec = [r.request_id, r.algorithm, d.outcome, st.get("ack_mono") if st else None, d.new_stage]
+        dl = st.get("delivery") if st else None
+        if dl is not None and "ack" in st and "receive" in st:
+            # delivery stamps + receive→ack: the bench decomposes push→ack per decision
+            rec.append([dl[0], dl[1], dl[2], st["ack"] - st["receive"]])
+        batch.append(rec)
 
     if report:
         sup.decision_hooks.append(reporter)

@@ -43,6 +43,7 @@ from .obs.logging import KLogger
 from .obs.metrics import Metrics
 from .parallel.pipeline import PipelineStage
 from .parallel.sharding import ShardSet
+from .obs.delivery import CURRENT as _DELIVERY
 from .store.base import CheckpointStore, NotSent, is_availability_error
 from .utils.gctune import GcTuner
 
@@ -231,6 +232,9 @@ class Supervisor:
         m.describe("event_to_checkpoint", "Latency from K8s event creation to checkpoint write ack")
         m.describe("receive_to_checkpoint", "Latency from watch receive to checkpoint write ack")
         m.describe("stage_classify", "Watch receive to pipeline enqueue (classification)")
+        m.describe("stage_hub", "Watch hub read of the API chunk to the shard worker's frame read")
+        m.describe("stage_feed", "Shard worker frame read to decoded batch (queue wait + native decode)")
+        m.describe("stage_dispatch", "Decoded batch to the supervisor's handler (informer dispatch)")
         m.describe("stage_queue", "Pipeline enqueue to worker dequeue (rate limit + queueing)")
         m.describe("stage_read", "Checkpoint read round trip (read + write actuation)")
         m.describe("stage_prepare", "Dequeue to conditional write sent: enrichment + trace (fused actuation)")
@@ -501,7 +505,7 @@ class Supervisor:
             if r.action != A.TO_RUNNING:
                 self.log.info("Algorithm run failed", requestId=r.request_id, algorithm=r.algorithm, reason=r.reason,
                               message=r.run_status_trace)
-            self._submit(r, origin, recv)
+            self._submit(r, origin, recv, "Event")
 
     def _on_event_update(self, old: Dict[str, Any], new: Dict[str, Any]) -> None:
         if not self.cfg.rules.handle_event_updates or old is new:
@@ -545,7 +549,7 @@ class Supervisor:
             return
         self._gpu_wait.pop(key, None)
         for r in results:
-            self._submit(r, recv, recv)
+            self._submit(r, recv, recv, "Pod")
 
     def _start_log_fetch(self, key: str, pod: Dict[str, Any], want: List[Dict[str, Any]], waited: bool) -> None:
         if key in self._log_fetches:
@@ -616,7 +620,7 @@ class Supervisor:
             return
         recv = self.wall()
         for r in self.classifier.classify_job(job, old, self.lookup):
-            self._submit(r, recv, recv)
+            self._submit(r, recv, recv, "Job")
 
     # ------------------------------------------------------------------ stale-event parking
     def _park(self, ev, recv):
@@ -721,7 +725,7 @@ class Supervisor:
                          namespace=self.namespace)
 
     # ------------------------------------------------------------------ submit
-    def _submit(self, r: RunStatusAnalysisResult, origin: float, recv: float) -> None:
+    def _submit(self, r: RunStatusAnalysisResult, origin: float, recv: float, kind: str = "") -> None:
         key = (r.algorithm, r.request_id)
         if not r.request_id:
             self.metrics.inc("decisions_unkeyed")
@@ -734,9 +738,13 @@ class Supervisor:
             self.metrics.inc("decisions_suppressed")
             return
         if self.cfg.observability.stage_timestamps:
-            r.stamps["origin"] = origin
-            r.stamps["receive"] = recv
-            r.stamps["enqueue"] = self.wall()
+            st = r.stamps
+            st["origin"] = origin
+            st["receive"] = recv
+            st["enqueue"] = self.wall()
+            d = _DELIVERY.get(kind)
+            if d is not None:  # the watch batch being dispatched: hub read / worker feed / decoded
+                st["delivery"] = d
         self.metrics.inc("decisions", labels={"action": r.action})
         self.pipeline.receive(r)
 
@@ -1148,7 +1156,7 @@ class Supervisor:
             self._applied.popitem(last=False)
 
     _STAGE_HISTS = ("event_to_checkpoint", "receive_to_checkpoint", "stage_classify", "stage_queue",
-                    "stage_prepare", "stage_write", "stage_read")
+                    "stage_prepare", "stage_write", "stage_read", "stage_hub", "stage_feed", "stage_dispatch")
 
     def _record_event(self, r: RunStatusAnalysisResult, stage: str) -> None:
         """``observability.record-events``: a Warning Event on the run's Job, so ``kubectl
@@ -1210,6 +1218,11 @@ class Supervisor:
             recv = s.get("receive")
             if recv is not None:
                 hs.rec(1, ack - recv)
+                dl = s.get("delivery")
+                if dl is not None:  # hub read → worker feed → decoded → handler (obs/delivery.py)
+                    hs.rec(7, dl[1] - dl[0])
+                    hs.rec(8, dl[2] - dl[1])
+                    hs.rec(9, s["ack_mono"] - (ack - recv) - dl[2])
                 enq, deq, rd, prep = s.get("enqueue"), s.get("dequeue"), s.get("read"), s.get("prepare")
                 if enq is not None and deq is not None and (rd is not None or prep is not None):
                     hs.rec(2, enq - recv)
@@ -1226,6 +1239,11 @@ class Supervisor:
         if "receive" in s:
             obs = self.metrics.observe_seconds
             obs("receive_to_checkpoint", ack - s["receive"])
+            dl = s.get("delivery")
+            if dl is not None:
+                obs("stage_hub", dl[1] - dl[0])
+                obs("stage_feed", dl[2] - dl[1])
+                obs("stage_dispatch", s["ack_mono"] - (ack - s["receive"]) - dl[2])
             # stage decomposition: classify → queue wait → CQL read → CQL write
             enq, deq, rd = s.get("enqueue"), s.get("dequeue"), s.get("read")
             prep = s.get("prepare")
