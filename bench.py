@@ -94,32 +94,7 @@ def parse_args(argv=None):
                          "simulator and CQL server; shared = one apiserver + one CQL server for all ranks, each "
                          "replica watching the whole namespace and owning its shard (a single-threaded simulator "
                          "then caps the whole curve: profiles/r3_kubesim_threads_ab)")
-    ap.add_argument("--cpu-placement", choices=("auto", "gpu-local", "none"), default="auto",
-                    help="gpu-local = pin the rank (its replica, shard workers and harness processes) to a block of "
-                         "physical cores on its GPU's NUMA node, disjoint from the other local ranks' blocks; "
-                         "auto = none: measured on MI355X the pinned rank is 20-25 %% slower (its dozen processes "
-                         "share two CCDs' L3 instead of one each; profiles/r3_placement_ab)")
     return ap.parse_args(argv)
-
-
-def place_rank(local_rank: int, local_world: int) -> dict:
-    """GPU-local CPU block for this rank (utils.placement), applied to the calling thread
-    before any harness or supervisor process is spawned, so every child inherits it."""
-    import torch
-
-    from nexus_supervisor_amd.utils import placement
-    from nexus_supervisor_amd.utils.cpus import cpu_share
-
-    bdfs = []
-    for i in range(min(local_world, torch.cuda.device_count() if torch.cuda.is_available() else 0)):
-        p = torch.cuda.get_device_properties(i)
-        bdfs.append(placement.pci_bdf(int(getattr(p, "pci_domain_id", 0)), int(p.pci_bus_id), int(p.pci_device_id)))
-    per_rank = max(1, int(cpu_share() / max(local_world, 1)))
-    got = placement.plan(local_rank, local_world, bdfs, sorted(os.sched_getaffinity(0)), per_rank)
-    got["applied"] = placement.apply(got["cpus"])
-    got["gpu_bdf"] = bdfs[local_rank] if local_rank < len(bdfs) else None
-    got["cpus"] = placement.format_cpulist(got["cpus"])
-    return got
 
 
 def auto_procs(local_world: int) -> int:
@@ -198,12 +173,6 @@ def main(argv=None) -> int:
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend=backend)
     device = torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")
-    placement = {"how": "none"}
-    if args.cpu_placement == "gpu-local":
-        try:
-            placement = place_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
-        except Exception as exc:  # noqa: BLE001 - placement is an optimisation, never a failure
-            placement = {"how": "none", "error": repr(exc)}
 
     from nexus_supervisor_amd.bench.runner import BenchConfig, run_rank
 
@@ -343,7 +312,6 @@ def main(argv=None) -> int:
                 "api_write_qps": args.api_write_qps,
                 "actuation": res.get("actuation"),
                 "cql_lwt_latency_us": args.cql_lwt_latency_us,
-                "cpu_placement_rank0": placement,
                 "stages_ms": res.get("stages"),
                 "cpu_util_rank0": res.get("cpu"),
                 "step_done_ms_rank0": res.get("step_done_ms"),

@@ -232,6 +232,9 @@ class SharedInformer:
                 items, rv = await self.lw.list()
                 self.relists += 1
                 self._relist_apply(items)
+                # this frame lives as long as the watch: holding the LIST's list would keep every
+                # listed object alive after the watch replaced it (a second copy of the cache)
+                del items
                 self._rv = rv
                 self._synced.set()
                 backoff = 0.2

@@ -7,6 +7,9 @@ ports and no probes, ``/root/reference/.helm/templates/deployment.yaml:37-120``)
 ``/debug/pprof/profile``   ``?seconds=N`` sampling profile in pprof ``profile.proto`` (gzip)
 ``/debug/pprof/top``       same sample, rendered as a flat/cumulative text table
 ``/debug/vars``            JSON snapshot: pipeline stats, store stats, queue depth, leadership
+``/debug/heap``            heap census of this process (Go's ``/debug/pprof/heap`` role): RSS, live
+                           objects by type and dict shape, the supervisor's bounded caches, and
+                           with ``PYTHONTRACEMALLOC`` set the top allocation sites (``?top=N``)
 """
 from __future__ import annotations
 
@@ -103,6 +106,21 @@ class ObsServer:
                              "observed_holder": self.app.elector.observed_holder}
         return web.json_response(doc, dumps=lambda o: __import__("json").dumps(o, default=str))
 
+    async def h_heap(self, req):
+        import json
+
+        from .heap import census
+
+        top = int(req.query.get("top", "25"))
+        sup = getattr(self.app, "supervisor", None)
+        doc = census(sup, top=top, trim=req.query.get("trim") == "1")
+        probe = req.query.get("retainers")
+        if probe:
+            from .heap import retainers
+
+            doc["retainers"] = retainers(sup, probe)
+        return web.Response(text=json.dumps(doc, indent=1, default=str), content_type="application/json")
+
     async def start(self, host: str, port: int) -> int:
         self._loop_thread = threading.get_ident()
         app = web.Application()
@@ -112,6 +130,7 @@ class ObsServer:
         app.router.add_get("/debug/pprof/profile", self.h_profile)
         app.router.add_get("/debug/pprof/top", self.h_top)
         app.router.add_get("/debug/vars", self.h_vars)
+        app.router.add_get("/debug/heap", self.h_heap)
         self._runner = web.AppRunner(app, access_log=None)
         await self._runner.setup()
         site = web.TCPSite(self._runner, host, port)

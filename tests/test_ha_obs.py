@@ -167,6 +167,11 @@ def test_http_endpoints(arun):
             async with s.get(base + "/debug/vars") as r:
                 doc = json.loads(await r.text())
                 assert doc["active"] is True and "pipeline" in doc
+            async with s.get(base + "/debug/heap?top=5&trim=1") as r:
+                heap = json.loads(await r.text())
+                assert heap["rss_mb"] > 0 and len(heap["types"]) == 5
+                assert heap["structures"]["informer.Pod"] >= 0 and "supervisor._applied" in heap["structures"]
+                assert heap["rss_after_trim_mb"] > 0
         await obs.stop()
         await app.stop()
         await api.stop()

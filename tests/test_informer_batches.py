@@ -80,3 +80,34 @@ def test_big_batch_yields_to_the_loop(arun):
 
     assert arun(main(), timeout=10) == 300
     assert any(0 < k < 300 for k in ticks)  # the loop ran between 64-line chunks
+
+
+def test_listed_objects_are_freed_once_the_watch_replaces_them(arun):
+    """The informer's run loop lives as long as its watch: it must not keep the LIST result
+    alive (that held a second copy of every listed object for the life of the watch —
+    ~20 MB per 10k jobs, found with /debug/heap)."""
+    import sys
+
+    from nexus_supervisor_amd.informer import InformerFactory, QueueListWatch
+
+    async def go():
+        listed = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "nexus",
+                                                                  "resourceVersion": "1", "uid": "u"}}
+        lw = QueueListWatch("Pod", [listed])
+        f = InformerFactory(lambda kind: lw, resync_period=0.0)
+        inf = f.informer("Pod")
+        f.start()
+        await f.wait_for_cache_sync(5)
+        lw.items.clear()
+        newer = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "namespace": "nexus",
+                                                                 "resourceVersion": "2", "uid": "u"}}
+        lw.push("MODIFIED", newer)
+        for _ in range(100):
+            if inf.indexer.get("nexus/p")["metadata"]["resourceVersion"] == "2":
+                break
+            await asyncio.sleep(0.01)
+        assert inf.indexer.get("nexus/p")["metadata"]["resourceVersion"] == "2"
+        assert sys.getrefcount(listed) == 2  # this frame + the call argument: nothing else holds it
+        await f.stop()
+
+    arun(go(), timeout=10)
