@@ -155,6 +155,9 @@ class WatchHub:
                 if self.metrics is not None:
                     self.metrics.inc("watchhub_relists", labels={"kind": kind})
                 await self._route(ki, parts, SNAPSHOT, rv.encode() + b"\n")
+                # this frame lives as long as the watch: do not pin the LIST body and its
+                # per-worker parts (tens of MB at 10k jobs) for the watch's lifetime
+                del body, parts
                 backoff = 0.2
                 while True:
                     params = dict(base, watch="1", resourceVersion=rv, allowWatchBookmarks="true",
