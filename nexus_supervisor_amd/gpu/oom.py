@@ -136,24 +136,43 @@ class OomVerdict:
         return d
 
 
-def hbm_signature(text: str) -> Optional[str]:
-    if not _mentions(text, _HBM_KEYS):
+# text -> (hbm signature, host signature): failures of one job template repeat the same
+# termination message (a torch OOM line, an OOMKilled reason) run after run, and the
+# keyword scan + up to ten regexes cost ~5-20 µs per text; a hit is one dict lookup
+_SIG_MEMO: Dict[str, Tuple[Optional[str], Optional[str]]] = {}
+_SIG_MEMO_MAX = 4096
+_SIG_MEMO_TEXT = 4096  # longer texts (log tails) are scanned, not memoised
+
+
+def _scan(text: str, keys, patterns) -> Optional[str]:
+    if not _mentions(text, keys):
         return None
-    for p in HBM_PATTERNS:
+    for p in patterns:
         m = p.search(text)
         if m:
             return m.group(0)
     return None
+
+
+def signatures(text: str) -> Tuple[Optional[str], Optional[str]]:
+    """``(hbm_signature(text), host_signature(text))``, memoised for short texts."""
+    hit = _SIG_MEMO.get(text)
+    if hit is not None:
+        return hit
+    got = (_scan(text, _HBM_KEYS, HBM_PATTERNS), _scan(text, _HOST_KEYS, HOST_PATTERNS))
+    if len(text) <= _SIG_MEMO_TEXT:
+        if len(_SIG_MEMO) >= _SIG_MEMO_MAX:
+            _SIG_MEMO.clear()
+        _SIG_MEMO[text] = got
+    return got
+
+
+def hbm_signature(text: str) -> Optional[str]:
+    return signatures(text)[0]
 
 
 def host_signature(text: str) -> Optional[str]:
-    if not _mentions(text, _HOST_KEYS):
-        return None
-    for p in HOST_PATTERNS:
-        m = p.search(text)
-        if m:
-            return m.group(0)
-    return None
+    return signatures(text)[1]
 
 
 def gpu_involved(gpus_requested: int, gpu_evidence: Optional[Dict[str, Any]]) -> bool:
@@ -209,14 +228,13 @@ def analyze(
     hbm_hit = host_hit = False
     logical = None
     for source, text in sourced:
-        h = host_signature(text)
+        s, h = signatures(text)
         if h and not host_hit and h != "OOMKilled":
             host_hit = True
             v.signature = True
             v.host_text = True
             v.host_score += 0.6
             v.signals.append(f"host allocation failure in {source}: {h!r}")
-        s = hbm_signature(text)
         if s and not hbm_hit:
             hbm_hit = True
             if gpu_involved is False:
