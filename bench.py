@@ -74,6 +74,9 @@ def parse_args(argv=None):
     ap.add_argument("--cql-lwt-latency-us", type=int, default=-1,
                     help="extra CQL server latency of a conditional write (a Paxos round: ~4 round trips where a "
                          "plain write takes 1); -1 = 3 x --cql-latency-us")
+    ap.add_argument("--no-shard-label", action="store_true",
+                    help="shared cluster: every replica watches the whole namespace (filtered before decode) "
+                         "instead of only its shard's Pods/Jobs by the sharding.shard-label selector")
     ap.add_argument("--api-latency-us", type=int, default=0,
                     help="simulated kube-apiserver answer latency of object requests (Job DELETE / GET / PATCH): "
                          "the etcd write + admission a real apiserver spends; LIST / WATCH unaffected")
@@ -204,6 +207,7 @@ def main(argv=None) -> int:
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
                       api_latency_us=args.api_latency_us, api_write_qps=args.api_write_qps, kube_qps=args.kube_qps,
+                      shard_label="" if args.no_shard_label else "nexus.amd.com/shard",
                       fused_write={"auto": "auto", "fused": "true", "two-step": "false"}[
                           "two-step" if args.two_step_write else args.actuation],
                       conditional_update=args.conditional_update, cql_lwt_latency_us=args.cql_lwt_latency_us,
@@ -294,6 +298,7 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "parallelism": f"shard{world}x{args.procs if args.transport == 'wire' else 1}proc",
                 "cluster": cluster if args.transport == "wire" else "in-process",
+                "shard_label": (not args.no_shard_label) if cluster == "shared" and world > 1 else None,
                 "concurrent_jobs_per_rank": args.jobs,
                 "events_per_step_per_rank": args.events,
                 "transport": args.transport,

@@ -296,8 +296,9 @@ std::shared_ptr<const Attrs> attrs_of(const Value& obj) {
 
 struct Req {
   std::string key;
-  char op;  // '=', '!', 'e' (exists), 'n' (not exists)
+  char op;  // '=', '!', 'e' (exists), 'n' (not exists), 'i' (in set), 'o' (notin set)
   std::string val;
+  std::vector<std::string> vals;  // 'i' / 'o'
 };
 using Selector = std::vector<Req>;
 
@@ -323,10 +324,38 @@ std::string trim(std::string_view s) {
   return std::string(s.substr(b, e - b));
 }
 
+// set-based requirement "key in (a,b)" / "key notin (a,b)": true and filled when `part` is one
+bool parse_set_req(const std::string& part, Req& r) {
+  size_t lp = part.find('(');
+  if (lp == std::string::npos || part.back() != ')') return false;
+  std::string head = trim(std::string_view(part).substr(0, lp));
+  size_t sp = head.find_last_of(" \t");
+  if (sp == std::string::npos) return false;
+  std::string op = trim(std::string_view(head).substr(sp + 1));
+  if (op != "in" && op != "notin") return false;
+  r.key = trim(std::string_view(head).substr(0, sp));
+  r.op = op == "in" ? 'i' : 'o';
+  std::string_view body(part.data() + lp + 1, part.size() - lp - 2);
+  size_t b = 0;
+  while (b <= body.size()) {
+    size_t c = body.find(',', b);
+    if (c == std::string_view::npos) c = body.size();
+    std::string v = trim(body.substr(b, c - b));
+    if (!v.empty()) r.vals.push_back(std::move(v));
+    b = c + 1;
+  }
+  return true;
+}
+
 void parse_selector(std::string_view sel, bool fields, Selector& out) {
   size_t pos = 0;
   while (pos <= sel.size()) {
     size_t comma = sel.find(',', pos);
+    size_t paren = sel.find('(', pos);
+    if (paren != std::string_view::npos && paren < comma) {  // a set: its commas are inside ( )
+      size_t close = sel.find(')', paren);
+      comma = close == std::string_view::npos ? sel.size() : sel.find(',', close);
+    }
     if (comma == std::string_view::npos) comma = sel.size();
     std::string part = trim(sel.substr(pos, comma - pos));
     pos = comma + 1;
@@ -336,16 +365,18 @@ void parse_selector(std::string_view sel, bool fields, Selector& out) {
     }
     Req r;
     size_t i;
-    if ((i = part.find("!=")) != std::string::npos) {
-      r = {trim(part.substr(0, i)), '!', trim(part.substr(i + 2))};
+    if (parse_set_req(part, r)) {
+      // "key in (...)" / "key notin (...)"
+    } else if ((i = part.find("!=")) != std::string::npos) {
+      r = {trim(part.substr(0, i)), '!', trim(part.substr(i + 2)), {}};
     } else if ((i = part.find("==")) != std::string::npos) {
-      r = {trim(part.substr(0, i)), '=', trim(part.substr(i + 2))};
+      r = {trim(part.substr(0, i)), '=', trim(part.substr(i + 2)), {}};
     } else if ((i = part.find('=')) != std::string::npos) {
-      r = {trim(part.substr(0, i)), '=', trim(part.substr(i + 1))};
+      r = {trim(part.substr(0, i)), '=', trim(part.substr(i + 1)), {}};
     } else if (part[0] == '!') {
-      r = {trim(part.substr(1)), 'n', ""};
+      r = {trim(part.substr(1)), 'n', "", {}};
     } else {
-      r = {part, 'e', ""};
+      r = {part, 'e', "", {}};
     }
     if (fields) r.key = "\x01" "f:" + r.key;
     out.push_back(std::move(r));
@@ -362,6 +393,8 @@ bool matches(const Attrs& a, const Selector& sel) {
       case '!': if (has && v == r.val) return false; break;
       case 'e': if (!has) return false; break;
       case 'n': if (has) return false; break;
+      case 'i': if (!has || std::find(r.vals.begin(), r.vals.end(), v) == r.vals.end()) return false; break;
+      case 'o': if (has && std::find(r.vals.begin(), r.vals.end(), v) != r.vals.end()) return false; break;
     }
   }
   return true;

@@ -55,15 +55,27 @@ def make_shard_leases(cfg: SupervisorConfig, kube, on_change, metrics, on_renewe
 
 def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
     from .kube.client import KubeListWatch
+    from .parallel.sharding import ShardSet, watch_selector
 
     ns = cfg.resource_namespace
-    sel = f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}" if cfg.informer_label_selector else ""
+    owned = ShardSet.from_config(cfg).owned  # static: {shard-index}; lease: none until a lease is won
 
     def lw(kind: str):
-        return KubeListWatch(client, kind, ns, label_selector=sel if kind in ("Pod", "Job") else "",
+        return KubeListWatch(client, kind, ns, label_selector=watch_selector(cfg, kind, owned),
                              watch_timeout=int(cfg.watch_timeout))
 
     return InformerFactory(lw, resync_period=cfg.resync_period)
+
+
+def _start_shard_audit(cfg, kube, metrics, log):
+    """The ``sharding.shard-label`` audit, in the process that owns the replica's API client
+    (a single-process replica, or a sharded replica's parent — not its shard workers)."""
+    if (not cfg.sharding.shard_label or cfg.sharding.shards <= 1 or kube is None or not hasattr(kube, "list")
+            or os.environ.get("NEXUS_WORKER_CONFIG")):
+        return None
+    from .parallel.sharding import audit_shard_labels
+
+    return asyncio.ensure_future(audit_shard_labels(cfg, kube, metrics, log))
 
 
 class Application:
@@ -141,6 +153,7 @@ class Application:
         await self.supervisor.start()
         if self.elector is not None:
             self.elector.start()
+        self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
 
     def ready(self) -> bool:
         return self.factory is not None and all(i.has_synced() for i in self.factory.informers.values())
@@ -149,6 +162,8 @@ class Application:
         return await self.factory.wait_for_cache_sync(timeout)
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
+        if getattr(self, "_audit", None) is not None:
+            self._audit.cancel()
         if self.elector is not None:
             await self.elector.stop(release=True)
         if self.shard_leases is not None:
@@ -291,6 +306,11 @@ class ShardedApplication:
                 on_stopped_leading=lambda: self.pool.set_active(False), metrics=self.metrics,
                 on_renewed=self.pool.set_lease_deadline)
             self.elector.start()
+        if self.kube is None and cfg.sharding.shard_label and cfg.sharding.shards > 1:
+            from .kube.client import KubeClient
+
+            self.kube = KubeClient.for_config(cfg, self.metrics)
+        self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
 
     def _shard_holds(self, until) -> None:
         """Shard hold deadlines renewed: the workers self-fence on them (no parent round trip)."""
@@ -320,6 +340,8 @@ class ShardedApplication:
         return self.merged_metrics
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
+        if getattr(self, "_audit", None) is not None:
+            self._audit.cancel()
         if self.elector is not None:
             await self.elector.stop(release=True)
         if self.shard_leases is not None:

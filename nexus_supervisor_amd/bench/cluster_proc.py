@@ -99,7 +99,8 @@ async def amain(args) -> None:
             # per-rank mode: the rank's workload (rank = its shard); shared mode: one per shard
             wl = Workload(p.get("jobs", 10_000), rank=k if len(indexes) > 1 else p.get("rank", 0),
                           world=p.get("world", 1), seed=p.get("seed", 0),
-                          hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=n_shards, shard_index=k)
+                          hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=n_shards, shard_index=k,
+                          shard_label=p.get("shard_label") or "")
             objs, rows = wl.initial()
             await write_rows(rows)
             await apply([("ADDED", o) for o in objs])

@@ -53,6 +53,9 @@ class BenchConfig:
     # client-side API bucket (kube-qps; the uncapped profile sets it high so the limiter's
     # path runs without pacing, the reference profile uses client-go's 5 / 10)
     kube_qps: float = 1_000_000.0
+    # shared cluster: the runs carry their shard as a label and every replica watches only
+    # its shard's Pods / Jobs (sharding.shard-label); "" = every replica gets the whole stream
+    shard_label: str = "nexus.amd.com/shard"
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -67,6 +70,8 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
         sc.kube_qps, sc.kube_burst = cfg.kube_qps, max(1, int(min(cfg.kube_qps, 1_000_000)))
     sc.sharding.shards = cfg.world
     sc.sharding.shard_index = cfg.rank
+    if cfg.cluster == "shared" and cfg.world > 1:
+        sc.sharding.shard_label = cfg.shard_label
     sc.resync_period = 0.0
     sc.rules.stale_event_grace = 5.0
     sc.observability.stage_timestamps = True

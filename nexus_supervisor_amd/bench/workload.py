@@ -57,7 +57,8 @@ def shard_of(algorithm: str, request_id: str, shards: int) -> int:
 class Workload:
     def __init__(self, concurrent_jobs: int = 10_000, rank: int = 0, world: int = 1, seed: int = 0,
                  labels: Optional[LabelConfig] = None, namespace: str = "nexus", algorithm: str = "bench-algorithm",
-                 hip_oom_message: str = DEFAULT_HIP_OOM, gpus_per_node: int = 8, shards: int = 1, shard_index: int = 0):
+                 hip_oom_message: str = DEFAULT_HIP_OOM, gpus_per_node: int = 8, shards: int = 1, shard_index: int = 0,
+                 shard_label: str = ""):
         self.rng = random.Random(seed * 7919 + rank)
         self.labels = labels or LabelConfig()
         self.ns = namespace
@@ -68,6 +69,8 @@ class Workload:
         self.gpus_per_node = gpus_per_node
         self.shards = shards
         self.shard_index = shard_index
+        # sharding.shard-label: the submitter stamps each run's shard on its Job and pod template
+        self.shard_label = shard_label if shards > 1 else ""
         self.live: List[str] = []
         self.pods: Dict[str, Dict[str, Any]] = {}
         self.jobs: Dict[str, Dict[str, Any]] = {}
@@ -119,6 +122,8 @@ class Workload:
         rid = self._new_id()
         env_t, mi, gpu, job_labels, node = self._templates()
         ns, lab = self.ns, self.labels
+        if self.shard_label:
+            job_labels = dict(job_labels, **{self.shard_label: str(self.shard_index)})
         job = {"apiVersion": "batch/v1", "kind": "Job",
                "metadata": {"name": rid, "namespace": ns, "uid": f"job-uid-{rid}", "resourceVersion": self._next_rv(),
                             "labels": dict(job_labels)},

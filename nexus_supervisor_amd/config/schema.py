@@ -257,6 +257,14 @@ class ShardingConfig:
     mode: str = field(default="static", metadata=_k("mode"))  # static | lease
     # expected replica count (Helm replicaCount) for the lease-mode fair share; 0 = greedy
     replicas: int = field(default=0, metadata=_k("replicas"))
+    # label carrying a run's shard (shard_of(job name, shards), ``python -m
+    # nexus_supervisor_amd shard-of``) on its Job and pod template, stamped by the component
+    # that submits the Job: a replica then watches only its shards' Pods and Jobs
+    # (``<label> in (owned…)``, filtered by the API server's watch cache) instead of every
+    # replica receiving the whole namespace.  Events carry no such label and stay a full
+    # stream (dropped before decode by the native router).  Empty = off.  Jobs without the
+    # label are invisible with it on: /metrics shard_label_missing counts them (audit)
+    shard_label: str = field(default="", metadata=_k("shard-label"))
 
 
 @dataclass

@@ -45,6 +45,68 @@ def shard_of(request_id: str, shards: int) -> int:
     return _fmix32(zlib.crc32(request_id.encode(), SHARD_SEED)) % shards
 
 
+def shard_selector(label: str, owned: Optional[Iterable[int]], shards: int) -> str:
+    """Server-side label selector requirement for the replica's shards of Pods and Jobs
+    (``sharding.shard-label``): ``"<label> in (k1,k2,…)"``; ``""`` when off or when the
+    replica owns every shard.  Owning none yields a set no run's label can match (a
+    lease-mode replica between leases watches nothing)."""
+    if not label or shards <= 1 or owned is None:
+        return ""
+    ks = sorted(int(k) for k in owned)
+    if len(ks) == shards:
+        return ""
+    return f"{label} in ({','.join(str(k) for k in ks) or 'none'})"
+
+
+def watch_selector(cfg, kind: str, owned: Optional[Iterable[int]] = None) -> str:
+    """The server-side label selector of a replica's ``kind`` watch: Nexus runs only
+    (``informer-label-selector``) and, with ``sharding.shard-label``, only the replica's
+    shards (Pods and Jobs; Events carry neither label)."""
+    if kind not in ("Pod", "Job"):
+        return ""
+    parts = []
+    if cfg.informer_label_selector:
+        parts.append(f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}")
+    s = cfg.sharding
+    if s.shard_label and s.shards > 1:
+        sel = shard_selector(s.shard_label, owned, s.shards)
+        if sel:
+            parts.append(sel)
+    return ",".join(parts)
+
+
+async def audit_shard_labels(cfg, kube, metrics, log, interval: float = 60.0) -> None:
+    """``sharding.shard-label`` safety net: with shard-narrowed watches a Nexus Job that
+    lacks the label is seen by no replica.  Every ``interval`` one LIST of Nexus Jobs
+    *without* the label (``!<label>``, at most 100) sets ``shard_label_missing`` and logs
+    their names, so an operator finds the submitter that does not stamp it."""
+    import asyncio
+
+    s = cfg.sharding
+    base = f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
+    warned = False
+    while True:
+        try:
+            items, _rv = await kube.list("Job", cfg.resource_namespace, label_selector=f"{base},!{s.shard_label}",
+                                         limit=100)
+            n = len(items)
+            metrics.set("shard_label_missing", float(n))
+            if n and not warned:
+                names = sorted(kube_name(i) for i in items)[:5]
+                log.warning("Nexus Jobs without the shard label are invisible to every replica",
+                            label=s.shard_label, jobs=n, examples=names)
+            warned = bool(n)
+        except asyncio.CancelledError:
+            raise
+        except Exception as exc:  # noqa: BLE001 - an audit, never a reason to stop
+            log.v(1).info("shard label audit failed", error=str(exc))
+        await asyncio.sleep(interval)
+
+
+def kube_name(obj) -> str:
+    return ((obj or {}).get("metadata") or {}).get("name", "")
+
+
 class ShardSet:
     """The shards this replica currently owns, with a fencing epoch per shard.
 

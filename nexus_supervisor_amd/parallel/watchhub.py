@@ -84,8 +84,7 @@ class WatchHub:
         self.tasks: Dict[str, asyncio.Task] = {}
         self.relists = 0
         self.bytes_routed = 0
-        self.selector = (f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
-                         if cfg.informer_label_selector else "")
+        self.owned = None  # the replica's shards (sharding.shard-label narrows the Pod/Job watches)
 
     def set_shards(self, shards) -> None:
         """Replica shard set: lines of runs this replica does not own are dropped in the
@@ -97,6 +96,7 @@ class WatchHub:
             self.router.set_replica(shards.shards, SHARD_SEED, sorted(shards.owned))
         else:
             self.router.set_replica(1, SHARD_SEED, [0])
+        self.owned = shards.owned
 
     def start(self) -> None:
         for i, kind in enumerate(KINDS):
@@ -123,9 +123,12 @@ class WatchHub:
     def _path_params(self, kind: str) -> Tuple[str, Dict[str, str]]:
         from ..kube.client import resource_path
 
+        from .sharding import watch_selector
+
         params: Dict[str, str] = {}
-        if kind in ("Pod", "Job") and self.selector:
-            params["labelSelector"] = self.selector
+        sel = watch_selector(self.cfg, kind, self.owned)
+        if sel:
+            params["labelSelector"] = sel
         return resource_path(kind, self.cfg.resource_namespace), params
 
     async def _route(self, ki: int, outs: List[bytes], ftype: int, prefix: bytes = b"") -> None:

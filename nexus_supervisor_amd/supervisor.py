@@ -365,6 +365,21 @@ class Supervisor:
     def set_lease_deadline(self, until: float) -> None:
         self.active_until = until
 
+    def _narrow_watches(self) -> bool:
+        """``sharding.shard-label``: point the Pod/Job watches at the shards owned now (the
+        caller re-lists); False when the watches are not this process's to narrow."""
+        if not self.cfg.sharding.shard_label or self.hub_fed:
+            return False
+        from .parallel.sharding import watch_selector
+
+        changed = False
+        for kind, inf in (("Pod", self.pod_informer), ("Job", self.job_informer)):
+            lw = getattr(inf, "lw", None)
+            if lw is not None and hasattr(lw, "label_selector"):
+                lw.label_selector = watch_selector(self.cfg, kind, self.shards.owned)
+                changed = True
+        return changed
+
     def set_shards(self, owned) -> Tuple[frozenset, frozenset]:
         """New owned replica-shard set (lease mode: a shard lease won or lost).  Lost shards
         are fenced like a lost leadership, but only for their runs: their queued and
@@ -377,13 +392,20 @@ class Supervisor:
             self.worker_shard.sync_replica()
         if lost:
             self.fence_shards(lost)
+            if not gained and self._narrow_watches():
+                for inf in (self.pod_informer, self.job_informer):
+                    inf.relist()  # stop receiving the lost shards' objects
         if gained:
             self.metrics.inc("shards_gained", len(gained))
             self.replay(lambda rid: self.shards.of(rid) in gained)
             infs = (self.event_informer, self.pod_informer, self.job_informer)
             before = [inf.relists for inf in infs]
+            narrowed = self._narrow_watches()
             if self.worker_shard is not None and not self.hub_fed:
                 for inf in infs:
+                    inf.relist()
+            elif narrowed:
+                for inf in (self.pod_informer, self.job_informer):
                     inf.relist()
             # the three kinds re-list independently: an Event of a gained run can be applied
             # before its Job and parked; replay the gained shards once more after every

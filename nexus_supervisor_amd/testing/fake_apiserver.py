@@ -22,6 +22,7 @@ import collections
 import copy
 import datetime as _dt
 import json
+import re
 import time
 import uuid
 from typing import Any, Deque, Dict, List, Optional, Set, Tuple
@@ -58,10 +59,33 @@ except ImportError:  # pragma: no cover
         return _ENCODE({"type": etype, "object": obj}).encode() + b"\n"
 
 
-def _parse_selector(sel: str) -> List[Tuple[str, str, Optional[str]]]:
-    out = []
-    for part in filter(None, (p.strip() for p in (sel or "").split(","))):
-        if "!=" in part:
+_SET_REQ = re.compile(r"^\s*(\S+)\s+(in|notin)\s*\(([^)]*)\)\s*$")
+
+
+def _split_selector(sel: str) -> List[str]:
+    """Comma-split a selector, keeping the commas inside a set's parentheses."""
+    parts, depth, cur = [], 0, []
+    for ch in sel or "":
+        if ch == "(":
+            depth += 1
+        elif ch == ")":
+            depth -= 1
+        if ch == "," and depth == 0:
+            parts.append("".join(cur))
+            cur = []
+        else:
+            cur.append(ch)
+    parts.append("".join(cur))
+    return [p.strip() for p in parts if p.strip()]
+
+
+def _parse_selector(sel: str) -> List[Tuple[str, str, Any]]:
+    out: List[Tuple[str, str, Any]] = []
+    for part in _split_selector(sel):
+        m = _SET_REQ.match(part)
+        if m:
+            out.append((m.group(1), m.group(2), frozenset(v.strip() for v in m.group(3).split(",") if v.strip())))
+        elif "!=" in part:
             k, v = part.split("!=", 1)
             out.append((k.strip(), "!=", v.strip()))
         elif "==" in part:
@@ -86,6 +110,10 @@ def _matches(labels: Dict[str, str], sel) -> bool:
         if op == "exists" and k not in labels:
             return False
         if op == "!" and k in labels:
+            return False
+        if op == "in" and labels.get(k) not in v:
+            return False
+        if op == "notin" and k in labels and labels[k] in v:
             return False
     return True
 
