@@ -319,10 +319,13 @@ class KubeClient:
         qps, burst = split(cfg.kube_qps, cfg.kube_burst, parts)
         self.set_flow_control(qps, burst, cfg.kube_max_retries, metrics)
 
-    async def _admit(self, path: str) -> None:
+    async def _admit(self, path: str, method: str = "GET") -> None:
         lim = self.limiter
         if lim.qps > 0 and not _exempt(path):
-            d = await lim.wait()
+            # reads (pods/log tails a decision waits for, LIST / WATCH) first, then mutations
+            # (background Job DELETEs, agent PATCHes), decision Events last
+            prio = 0 if method == "GET" else 2 if method == "POST" and path.endswith("/events") else 1
+            d = await lim.wait(prio)
             if d > 0 and self.metrics is not None:
                 self.metrics.inc("kube_ratelimit_waits")
                 self.metrics.observe_seconds("kube_ratelimit_wait", d)
@@ -352,7 +355,7 @@ class KubeClient:
         data = json.dumps(body) if body is not None else None
         attempt = 0
         while True:
-            await self._admit(path)
+            await self._admit(path, method)
             self.requests += 1
             async with s.request(method, self.config.server + path, params=params, data=data,
                                  headers=self._headers({"Content-Type": content_type} if data is not None else None),
@@ -531,7 +534,7 @@ class KubeClient:
             return await self.request("DELETE", path, body=body)
         attempt = 0
         while True:
-            await self._admit(path)
+            await self._admit(path, "DELETE")
             self.requests += 1
             status, raw = await self._fast_client().request(
                 "DELETE", path, _delete_body(propagation_policy), self._headers({"Content-Type": "application/json"}))

@@ -12,9 +12,10 @@ with exactly those 429s.
 Here:
 
 * :class:`TokenBucket` — ``kube-qps`` / ``kube-burst``, shared by every request of one
-  process (a replica split into shard workers divides them, ``split``).  Reservations
-  queue like ``x/time/rate``'s ``Reserve``: concurrent waiters are served in order at
-  ``qps``, never in a burst larger than ``burst``.  ``qps <= 0`` = no limit.
+  process (a replica split into shard workers divides them, ``split``).  Waiters are
+  released at ``qps`` (never in a burst larger than ``burst``) by priority, then in arrival
+  order: decision reads first, background Job DELETEs next, Events last.  ``qps <= 0`` = no
+  limit.
 * :func:`retry_after` — the server's hint (integer seconds, as client-go reads it; an
   HTTP-date is honoured too), bounded by ``cap``.
 * :class:`RetryPolicy` — which answers are retried and how long to wait: 429 always (1 s
@@ -25,6 +26,7 @@ from __future__ import annotations
 
 import asyncio
 import email.utils
+import heapq
 import time
 from typing import Callable, Optional
 
@@ -33,9 +35,15 @@ CLIENT_GO_QPS, CLIENT_GO_BURST, CLIENT_GO_MAX_RETRIES = 5.0, 10, 10
 
 
 class TokenBucket:
-    """Token bucket rate limiter (``qps`` tokens per second, at most ``burst`` banked)."""
+    """Token bucket rate limiter (``qps`` tokens per second, at most ``burst`` banked) whose
+    waiters are served by priority, then in arrival order.
 
-    __slots__ = ("qps", "burst", "tokens", "last", "clock", "waits", "waited_s")
+    client-go has one FIFO bucket; here a failure wave's background Job DELETEs (priority 1)
+    must not delay the ``pods/log`` reads (priority 0) that the waiting decisions need — a
+    FIFO reservation would put a read behind every DELETE queued before it (at 50 qps, a
+    1,000-pod wave is 20 s of DELETEs).  Decision Events are priority 2."""
+
+    __slots__ = ("qps", "burst", "tokens", "last", "clock", "waits", "waited_s", "_waiters", "_seq", "_timer")
 
     def __init__(self, qps: float, burst: int, clock: Callable[[], float] = time.monotonic):
         self.qps = float(qps)
@@ -45,10 +53,17 @@ class TokenBucket:
         self.last = clock()
         self.waits = 0        # requests that had to wait for a token
         self.waited_s = 0.0   # total time they waited
+        self._waiters: list = []  # heap of (priority, seq, future)
+        self._seq = 0
+        self._timer = None
 
     @property
     def unlimited(self) -> bool:
         return self.qps <= 0
+
+    @property
+    def queued(self) -> int:
+        return sum(1 for w in self._waiters if not w[2].done())
 
     def _refill(self) -> float:
         now = self.clock()
@@ -58,34 +73,57 @@ class TokenBucket:
         return now
 
     def try_accept(self) -> bool:
-        """Take a token if one is banked right now (client-go ``TryAccept``)."""
+        """Take a token if one is banked right now and nobody is queued (client-go
+        ``TryAccept``; a caller that gets False falls back to :meth:`wait`)."""
         if self.qps <= 0:
             return True
+        if self._waiters:
+            return False
         self._refill()
         if self.tokens >= 1.0:
             self.tokens -= 1.0
             return True
         return False
 
-    def reserve(self) -> float:
-        """Take a token now (possibly going into debt) and return how long the caller must
-        wait before using it: later reservations queue behind earlier ones."""
+    async def wait(self, priority: int = 1) -> float:
+        """client-go ``Wait``: block until this request may go; returns the time waited."""
         if self.qps <= 0:
             return 0.0
         self._refill()
-        self.tokens -= 1.0
-        if self.tokens >= 0.0:
+        if not self._waiters and self.tokens >= 1.0:
+            self.tokens -= 1.0
             return 0.0
-        return -self.tokens / self.qps
-
-    async def wait(self) -> float:
-        """client-go ``Wait``: block until this request may go; returns the time waited."""
-        d = self.reserve()
-        if d > 0.0:
-            self.waits += 1
-            self.waited_s += d
-            await asyncio.sleep(d)
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._seq += 1
+        heapq.heappush(self._waiters, (priority, self._seq, fut))
+        self._arm(loop)
+        t0 = self.clock()
+        await fut
+        d = self.clock() - t0
+        self.waits += 1
+        self.waited_s += d
         return d
+
+    def _arm(self, loop) -> None:
+        if self._timer is None and self._waiters:
+            self._refill()
+            self._timer = loop.call_later(max(0.0, (1.0 - self.tokens) / self.qps), self._release)
+
+    def _release(self) -> None:
+        self._timer = None
+        self._refill()
+        ws = self._waiters
+        while ws and self.tokens >= 1.0:
+            _p, _s, fut = heapq.heappop(ws)
+            if fut.done():  # the waiter was cancelled
+                continue
+            self.tokens -= 1.0
+            fut.set_result(None)
+        while ws and ws[0][2].done():
+            heapq.heappop(ws)
+        if ws:
+            self._arm(asyncio.get_event_loop())
 
 
 def split(qps: float, burst: int, parts: int):

@@ -24,26 +24,35 @@ from nexus_supervisor_amd.testing.fake_apiserver import FakeApiServer
 from nexus_supervisor_amd.testing.seed import ALGORITHM, make_job, make_pod
 
 
-class Clock:
-    def __init__(self):
-        self.t = 100.0
+def test_token_bucket_burst_then_qps_and_priorities(arun):
+    """Burst tokens go at once, then one per 1/qps; a decision read (priority 0) queued
+    after ten background DELETEs (priority 1) is served before all of them."""
+    async def go():
+        b = TokenBucket(100, 2)
+        assert b.try_accept() and b.try_accept() and not b.try_accept()  # the burst
+        order = []
 
-    def __call__(self):
-        return self.t
+        async def one(tag, prio):
+            await b.wait(prio)
+            order.append(tag)
 
+        t0 = time.monotonic()
+        tasks = [asyncio.ensure_future(one(f"delete{i}", 1)) for i in range(10)]
+        await asyncio.sleep(0)
+        tasks.append(asyncio.ensure_future(one("log-read", 0)))
+        await asyncio.gather(*tasks)
+        took = time.monotonic() - t0
+        assert order[0] == "log-read" and order[1:] == [f"delete{i}" for i in range(10)], order
+        assert 0.09 <= took < 0.5, took  # 11 tokens at 100/s with the bank empty
+        assert b.waits == 11 and b.queued == 0
+        # a cancelled waiter gives its turn away
+        w = asyncio.ensure_future(b.wait(1))
+        await asyncio.sleep(0)
+        w.cancel()
+        assert await asyncio.wait_for(b.wait(0), 1.0) >= 0.0
+        assert TokenBucket(0, 1).try_accept() and await TokenBucket(0, 1).wait() == 0.0
 
-def test_token_bucket_reservations_queue_at_qps():
-    c = Clock()
-    b = TokenBucket(10, 2, clock=c)
-    assert b.reserve() == 0 and b.reserve() == 0  # the burst
-    assert b.reserve() == pytest.approx(0.1)       # then one every 1/qps, in order
-    assert b.reserve() == pytest.approx(0.2)
-    c.t += 0.2
-    assert b.reserve() == pytest.approx(0.1)
-    assert not b.try_accept()
-    c.t += 10
-    assert b.try_accept() and b.try_accept() and not b.try_accept()  # refilled to burst only
-    assert TokenBucket(0, 1).reserve() == 0 and TokenBucket(0, 1).try_accept()
+    arun(go(), timeout=10)
 
 
 def test_split_over_shard_workers():
@@ -220,3 +229,49 @@ def test_pods_log_wave_is_bounded(arun):
         await api.stop()
 
     arun(go(), timeout=60)
+
+
+def test_log_reads_are_not_starved_by_a_delete_backlog(arun):
+    """kube-qps 20: a wave of 80 OOMKilled runs queues 80 background Job DELETEs (4 s of
+    tokens).  A GPU pod that fails right behind them with an empty termination message needs
+    its pods/log tail before it can be decided: the read jumps the DELETE queue (priority
+    0), so that run is decided within a second, not after the backlog drains."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        cfg = _app_cfg(**{"kube-qps": 20, "kube-burst": 5})
+        rids = [f"wave-{i:03d}" for i in range(80)]
+        for r in rids + ["gpu-run"]:
+            api.create(make_pod(r, cfg.labels, gpus=1 if r == "gpu-run" else 0, status={"phase": "Running"}))
+            api.create(make_job(r, cfg.labels))
+        api.set_pod_log("nexus", "gpu-run-acdey", "algorithm", "torch.OutOfMemoryError: HIP out of memory.\n")
+        store = MemoryStore([CheckpointedRequest(algorithm=ALGORITHM, id=r, lifecycle_stage="RUNNING")
+                             for r in rids + ["gpu-run"]])
+        app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+        await app.start()
+        await app.factory.wait_for_cache_sync(5)
+        for r in rids:
+            api.update(_oomkilled(api.get("Pod", "nexus", f"{r}-acdey")))
+        for _ in range(200):
+            if all(store.get(ALGORITHM, r).lifecycle_stage == "FAILED" for r in rids):
+                break
+            await asyncio.sleep(0.01)
+        assert app.kube.limiter.queued > 30  # the DELETE backlog is there
+        p = json.loads(json.dumps(api.get("Pod", "nexus", "gpu-run-acdey")))
+        p["status"] = {"phase": "Failed", "containerStatuses": [
+            {"name": "algorithm", "restartCount": 0, "state": {"terminated": {"reason": "Error", "exitCode": 1}}}]}
+        p["metadata"]["resourceVersion"] = "3"
+        t0 = time.monotonic()
+        api.update(p)
+        for _ in range(300):
+            if store.get(ALGORITHM, "gpu-run").lifecycle_stage == "FAILED":
+                break
+            await asyncio.sleep(0.01)
+        took = time.monotonic() - t0
+        assert store.get(ALGORITHM, "gpu-run").lifecycle_stage == "FAILED" and took < 1.0, took
+        assert json.loads(store.get(ALGORITHM, "gpu-run").algorithm_failure_details)["class"] == "hbm-oom"
+        assert app.kube.limiter.queued > 0  # ...while DELETEs were still waiting for tokens
+        await app.stop()
+        await api.stop()
+
+    arun(go(), timeout=40)
