@@ -56,7 +56,8 @@ def parse_args(argv=None):
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--procs", type=int, default=0,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport); "
-                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 8")
+                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 6 (the measured "
+                         "efficiency knee: auto_procs)")
     ap.add_argument("--inflight", type=int, default=4, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--no-pregen", action="store_true",
                     help="generate each step's synthetic traffic on demand instead of before the timed region")
@@ -111,7 +112,9 @@ def auto_procs(local_world: int) -> int:
     158 µs of replica CPU per failure, 7 workers 38.6k/s at 180 µs, 8 workers (profiled)
     36.8k/s at 187 µs — the apiserver simulator at 0.84–0.94 is the ceiling either way;
     round 2's sweep found the same (r2_sweep_procs_v16: 6 workers ≈ 12 in throughput at
-    ~40 % less CPU)."""
+    ~40 % less CPU), and so did round 4's (profiles/r4_sweep: 6 / 8 / 10 / 12 workers at
+    153 / 194 / 185 / 214 µs per failure for 36.6k / 36.4k / 48.8k / 38.7k failures/s — CPU
+    per failure up 20-40 % past six, throughput within the box's run-to-run spread)."""
     from nexus_supervisor_amd.utils.cpus import cpu_share
 
     return max(1, min(6, int(cpu_share() / max(local_world, 1)) - 4))

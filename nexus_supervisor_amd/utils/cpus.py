@@ -29,8 +29,10 @@ AUTO_WORKERS_CAP = 6
 def auto_worker_processes(reserve: float = 1.0, cap: int = AUTO_WORKERS_CAP, share: float = 0.0) -> int:
     """Shard workers for the CPU share, keeping ``reserve`` CPUs for the coordinating
     parent (watch hub, lease, /metrics): at least 1 (= single-process supervisor), at most
-    six — the efficient point measured on MI355X hosts (``bench.py`` ``auto_procs``): six
-    saturated workers sustain 37–47k failures/s, more only add CPU per failure (and lower
-    burst latency; set ``runtime.worker-processes`` explicitly for that)."""
+    six — the efficiency knee measured on MI355X hosts in rounds 2-4 (``bench.py``
+    ``auto_procs``, ``profiles/r4_sweep``): six saturated workers sustain 35-45k failures/s;
+    past six the CPU per failure rises 20-40 % while the throughput stays within the
+    run-to-run spread (more workers only lower burst latency; set
+    ``runtime.worker-processes`` explicitly for that)."""
     n = share or cpu_share()
     return max(1, min(cap, int(n - reserve)))
