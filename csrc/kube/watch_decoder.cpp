@@ -1723,12 +1723,16 @@ PyTypeObject DecoderType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
 extern "C" PyObject* nexus_json_dumps(PyObject*, PyObject* args, PyObject* kw);  // json_encode.cpp
 extern "C" int nexus_register_histogram(PyObject* m);                            // histogram.cpp
+extern "C" PyObject* nexus_apply_lines(PyObject*, PyObject* args);               // informer_apply.cpp
 
 namespace {
 
 PyMethodDef module_methods[] = {
     {"dumps", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(nexus_json_dumps)),
      METH_VARARGS | METH_KEYWORDS, "dumps(obj, sort_keys=False, default=None, newline=False) -> bytes (compact UTF-8 JSON)"},
+    {"apply_lines", nexus_apply_lines, METH_VARARGS,
+     "apply_lines(batch, start, end, items, labels, indices, adds, updates, deletes, on_error, kind) -> "
+     "(error_object, seen, resource_version): one watch batch into an informer cache + handlers"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_kube_native",

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import random
 import time
 from typing import Any, AsyncIterator, Callable, Dict, List, Optional, Tuple
@@ -298,11 +299,20 @@ class SharedInformer:
         ERROR event's object if one is met (the lines before it are applied)."""
         self.last_receive = self.stamp()
         indexer = self.indexer
-        upsert, delete = indexer.upsert, indexer.delete
         adds = [h.on_add for h in self.handlers if h.on_add]
         updates = [h.on_update for h in self.handlers if h.on_update]
         deletes = [h.on_delete for h in self.handlers if h.on_delete]
         kind = self.kind
+        native = _native_apply()
+        if native is not None and (indexer._labels is not None or not indexer._indexers):
+            # the same loop in C (csrc/kube/informer_apply.cpp): store, label index, handlers
+            err, seen, rv = native(batch, start, end, indexer._items, indexer._labels, indexer._indices,
+                                   adds, updates, deletes, _handler_failed, kind)
+            self.watch_events += seen
+            if rv:
+                self._rv = rv
+            return err
+        upsert, delete = indexer.upsert, indexer.delete
         rv = None
         seen = 0
         try:
@@ -351,6 +361,29 @@ class SharedInformer:
                 continue
             for obj in self.indexer.values():
                 self._dispatch_update(obj, obj)
+
+
+_NATIVE_APPLY: List[Any] = []
+
+
+def _native_apply():
+    """``_kube_native.apply_lines`` (None without the native build, or with
+    ``NEXUS_PY_INFORMER_APPLY=1``: the Python loop below, for A/B runs)."""
+    if not _NATIVE_APPLY:
+        fn = None
+        if os.environ.get("NEXUS_PY_INFORMER_APPLY") != "1":
+            try:
+                from .. import _kube_native
+
+                fn = getattr(_kube_native, "apply_lines", None)
+            except ImportError:
+                fn = None
+        _NATIVE_APPLY.append(fn)
+    return _NATIVE_APPLY[0]
+
+
+def _handler_failed(kind: str, exc: BaseException) -> None:
+    log.error("%s handler failed", kind, exc_info=(type(exc), exc, exc.__traceback__))
 
 
 def _has_loop() -> bool:
