@@ -70,7 +70,7 @@ def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
 def _start_shard_audit(cfg, kube, metrics, log):
     """The ``sharding.shard-label`` audit, in the process that owns the replica's API client
     (a single-process replica, or a sharded replica's parent — not its shard workers)."""
-    if (not cfg.sharding.shard_label or cfg.sharding.shards <= 1 or kube is None or not hasattr(kube, "list")
+    if (not cfg.sharding.shard_label or cfg.sharding.shards <= 1 or kube is None or not hasattr(kube, "request")
             or os.environ.get("NEXUS_WORKER_CONFIG")):
         return None
     from .parallel.sharding import audit_shard_labels

@@ -241,10 +241,13 @@ def _exempt(path: str) -> bool:
 class KubeClient:
     def __init__(self, config: KubeConfig, *, request_timeout: float = 30.0, max_connections: int = 32,
                  user_agent: str = "nexus-supervisor-amd/0.1", pipelined_writes: bool = True, write_connections: int = 4,
-                 qps: float = 0.0, burst: int = 1, max_retries: int = 10, metrics=None):
+                 qps: Optional[float] = None, burst: int = 1, max_retries: int = 10, metrics=None):
         self.config = config
-        # client-go rest.Config QPS / Burst (kube-qps / kube-burst; 0 = no client-side limit)
-        self.limiter = TokenBucket(qps, burst)
+        # client-go rest.Config QPS / Burst (kube-qps / kube-burst; 0 = no client-side limit).
+        # Given here, they stay: an Application only applies its config's to a client built
+        # without them
+        self.flow_configured = qps is not None
+        self.limiter = TokenBucket(qps or 0.0, burst)
         self.retry = RetryPolicy(max_retries)
         self.metrics = metrics  # obs.metrics.Metrics: kube_throttled / kube_retries / kube_ratelimit_waits
         self.throttled = 0      # 429 / hinted 5xx answers seen

@@ -85,11 +85,15 @@ async def audit_shard_labels(cfg, kube, metrics, log, interval: float = 60.0) ->
     s = cfg.sharding
     base = f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
     warned = False
+    from ..kube.client import resource_path
+
+    path = resource_path("Job", cfg.resource_namespace)
     while True:
         try:
-            items, _rv = await kube.list("Job", cfg.resource_namespace, label_selector=f"{base},!{s.shard_label}",
-                                         limit=100)
-            n = len(items)
+            # one page: the audit needs a count and a few names, not every unlabelled Job
+            doc = await kube.request("GET", path, params={"labelSelector": f"{base},!{s.shard_label}", "limit": "100"})
+            items = doc.get("items") or []
+            n = len(items) + int((doc.get("metadata") or {}).get("remainingItemCount") or 0)
             metrics.set("shard_label_missing", float(n))
             if n and not warned:
                 names = sorted(kube_name(i) for i in items)[:5]
