@@ -16,6 +16,7 @@ import os
 import signal
 import socket
 import sys
+import time
 from typing import Optional
 
 from . import __build__, __version__
@@ -246,9 +247,21 @@ class ShardedApplication:
 
         since: dict = {}
         interval = max(0.05, self.cfg.gpu.sample_interval)
+        last_snap = None
         while True:
             try:
-                self.pool.broadcast(dict(telemetry_message(self.telemetry, since), op="gpu"))
+                t0 = time.perf_counter()
+                msg = telemetry_message(self.telemetry, since)
+                if msg["snap"] == last_snap:
+                    # an unchanged snapshot (GPU processes, events) is not re-sent: the workers
+                    # keep theirs (RemoteTelemetry.update); only the new VRAM samples travel.
+                    # This runs on the watch hub's loop: every millisecond here is a watch line
+                    # waiting (the delivery tail, obs/delivery.py)
+                    del msg["snap"]
+                else:
+                    last_snap = msg["snap"]
+                self.pool.broadcast(dict(msg, op="gpu"))
+                self.metrics.observe_seconds("gpu_mirror_publish", time.perf_counter() - t0)
             except Exception as exc:  # noqa: BLE001 - telemetry must never stop the replica
                 self.log.error(exc, "GPU telemetry publish failed")
             await asyncio.sleep(interval)

@@ -345,6 +345,10 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         if sync is not None:
             await sync()
         stages = _stage_breakdown(sup)
+        # the replica parent's periodic GPU-telemetry mirror (it shares the watch hub's loop)
+        mirror = _stage_breakdown(sup, ("gpu_mirror_publish",)).get("gpu_mirror_publish")
+        if mirror:
+            cpu["gpu_mirror_publish_ms"] = mirror
         readback = await _read_back(harness, tracker)
         probe = None
         if cfg.probe_events > 0:
@@ -500,10 +504,10 @@ def _stage_delta(before, after) -> Dict[str, Any]:
     return out
 
 
-def _stage_breakdown(sup) -> Dict[str, Any]:
+def _stage_breakdown(sup, names=None) -> Dict[str, Any]:
     m = sup.metrics
     out = {}
-    for name in STAGES:
+    for name in names or STAGES:
         h = m.histogram(name)
         if h is not None:
             out[name] = {k: (int(v) if k == "count" else round(v / 1000.0, 3)) for k, v in h.summary().items()}
