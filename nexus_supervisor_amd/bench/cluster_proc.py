@@ -138,7 +138,14 @@ async def amain(args) -> None:
         events = int(p["events"])
         sh = shards[int(p["shard"])] if "shard" in p else next(iter(shards.values()))
         async with sh.lock:  # one step of a shard at a time (shards run concurrently)
-            return web.json_response(await _step(sh, events))
+            doc = await _step(sh, events)
+        hold = float(p.get("respond_after_ms") or 0.0)
+        if hold > 0:
+            # latency probe: answer after the failure has been delivered and decided, so the
+            # bench driver's handling of this answer never shares the replica parent's loop
+            # with the watch line it is timing (the driver is not part of the supervisor)
+            await asyncio.sleep(hold / 1000.0)
+        return web.json_response(doc)
 
     async def _step(sh, events):
         wl = sh.wl

@@ -386,14 +386,28 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     loop = asyncio.get_running_loop()
     start = loop.time()
     states = []
+    pending = []
     at = 0.0
+    hold = getattr(harness, "probe_hold_ms", 0.0)
+
+    async def one():
+        # the harness answers after the failure is delivered (hold): the driver's own work on
+        # the answer stays out of the replica parent's loop while the line is in flight; the
+        # decision's ack may arrive first (Tracker.report keeps it until the step is armed)
+        failed, t_push, expected = await (harness.step(1, hold) if hold else harness.step(1))
+        states.append(tracker.arm(failed, t_push, expected))
+
     for i in range(cfg.probe_events):
         at += rng.expovariate(rate)
         delay = start + at - loop.time()
         if delay > 0:
             await asyncio.sleep(delay)
-        failed, t_push, expected = await harness.step(1)
-        states.append(tracker.arm(failed, t_push, expected))
+        if hold:
+            pending.append(asyncio.ensure_future(one()))  # open loop: the next arrival does not wait
+        else:
+            await one()
+    if pending:
+        await asyncio.gather(*pending)
     for st in states:
         try:
             await asyncio.wait_for(st.done.wait(), cfg.step_timeout)

@@ -41,6 +41,8 @@ def schema_statements(ks: str = "nexus", table: str = "checkpoints") -> List[str
 
 class WireHarness:
     store_name = "cql (nexus-cqlsrv over TCP)"
+    # latency probe: the cluster answers a step this long after applying it (runner._latency_probe)
+    probe_hold_ms = 10.0
 
     def __init__(self, sc: SupervisorConfig, cfg, workdir: str, telemetry=None,
                  share: Optional[Callable[[Any], Any]] = None, barrier: Optional[Callable[[], None]] = None):
@@ -143,8 +145,11 @@ class WireHarness:
     def supervisor(self):
         return self.app.supervisor
 
-    async def step(self, events: int) -> Tuple[List[str], float, Dict[str, str]]:
-        async with self.http.post(self.ctl + "/bench/step", json={"events": events, "shard": self.cfg.rank}) as r:
+    async def step(self, events: int, respond_after_ms: float = 0.0) -> Tuple[List[str], float, Dict[str, str]]:
+        body = {"events": events, "shard": self.cfg.rank}
+        if respond_after_ms:
+            body["respond_after_ms"] = respond_after_ms
+        async with self.http.post(self.ctl + "/bench/step", json=body) as r:
             r.raise_for_status()
             doc = await r.json()
         return doc["rids"], doc["t_push"], doc.get("expected") or {}
