@@ -78,6 +78,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-shard-label", action="store_true",
                     help="shared cluster: every replica watches the whole namespace (filtered before decode) "
                          "instead of only its shard's Pods/Jobs by the sharding.shard-label selector")
+    ap.add_argument("--hbm-shape", choices=("default-pod", "termination-message"), default="default-pod",
+                    help="synthetic HBM-OOM failures: a default pod (empty termination message, the real HIP OOM "
+                         "text in the container log, read over pods/log) or the text in the termination message")
     ap.add_argument("--api-latency-us", type=int, default=0,
                     help="simulated kube-apiserver answer latency of object requests (Job DELETE / GET / PATCH): "
                          "the etcd write + admission a real apiserver spends; LIST / WATCH unaffected")
@@ -211,6 +214,7 @@ def main(argv=None) -> int:
                       workdir=workdir, cql_latency_us=args.cql_latency_us, inflight=args.inflight,
                       api_latency_us=args.api_latency_us, api_write_qps=args.api_write_qps, kube_qps=args.kube_qps,
                       shard_label="" if args.no_shard_label else "nexus.amd.com/shard",
+                      hbm_shape=args.hbm_shape if args.transport == "wire" else "termination-message",
                       fused_write={"auto": "auto", "fused": "true", "two-step": "false"}[
                           "two-step" if args.two_step_write else args.actuation],
                       conditional_update=args.conditional_update, cql_lwt_latency_us=args.cql_lwt_latency_us,
@@ -315,6 +319,7 @@ def main(argv=None) -> int:
                 "kube_qps": res.get("kube_qps"),
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
+                "hbm_oom_shape": args.hbm_shape if args.transport == "wire" else "termination-message",
                 "cql_latency_us": args.cql_latency_us,
                 "api_latency_us": args.api_latency_us,
                 "api_write_qps": args.api_write_qps,

@@ -27,6 +27,10 @@
 //   POST   /sim/expire[?kind=Pod]     compact history (resuming watches get 410) + cut streams
 //   POST   /sim/close-watches         cut every watch stream
 //   GET    /sim/stats                 counters
+//   GET    …/pods/{name}/log          the container log a bench LOG line stored for the pod
+//                                      (container / tailLines / limitBytes; 400 when none)
+//   (/sim/apply also takes {"type":"LOG","object":{"namespace","pod","container","text"}}:
+//    a failed container's log, never sent to watchers, dropped with its pod)
 //
 // Pricing the API server: --api-latency-us answers every object
 // request (GET / DELETE / POST / PUT / PATCH; not LIST / WATCH) that long after it was
@@ -539,6 +543,8 @@ struct KindStore {
 
 KindStore g_store[NKINDS];
 std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x01 job → pod names
+// ns \x01 pod → container → log text (bench LOG lines; pods/log answers from it)
+std::unordered_map<std::string, std::unordered_map<std::string, std::string>> g_pod_logs;
 int64_t g_rv = 1000;
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0, throttled = 0, delayed = 0;
@@ -1046,7 +1052,10 @@ bool remove(int kind, const std::string& ns, const std::string& name, const std:
   if (it == g_store[kind].objs.end()) return false;
   Obj o = std::move(it->second);
   g_store[kind].objs.erase(it);
-  if (kind == K_POD) index_pod(o, false);
+  if (kind == K_POD) {
+    index_pod(o, false);
+    if (!g_pod_logs.empty()) g_pod_logs.erase(okey(ns, name));
+  }
   if (o.rv_off != std::string::npos) {
     record(kind, "DELETED", o, ++g_rv);  // new resourceVersion spliced in on send
   } else {
@@ -1602,6 +1611,12 @@ void h_apply(Conn& c, const Request& r) {
     Value* obj = ev.get("object");
     std::string_view osrc = line;  // obj's source offsets are relative to the line
     if (!obj || obj->t != Value::OBJ) throw kjson::ParseError("event without object");
+    if (type == "LOG") {
+      g_pod_logs[okey(obj->path({"namespace"}), obj->path({"pod"}))][std::string(obj->path({"container"}))] =
+          std::string(obj->path({"text"}));
+      ++n;
+      continue;
+    }
     int kind = kind_by_name(obj->path({"kind"}));
     if (kind < 0) throw kjson::ParseError("unknown kind");
     if (type == "DELETED") {
@@ -1628,6 +1643,59 @@ void h_apply(Conn& c, const Request& r) {
   snprintf(buf, sizeof buf, "{\"applied\":%zu,\"rv\":%lld,\"t_push\":%.9f}", n, static_cast<long long>(g_rv),
            static_cast<double>(t0) / 1e9);
   respond(c, 200, buf);
+}
+
+// GET /api/v1/namespaces/{ns}/pods/{name}/log?container=&tailLines=&limitBytes= (kubelet-proxied
+// in a real cluster; priced like any object request with --api-latency-us)
+// false: not a pods/{name}/log path (the caller routes it as an object path)
+bool h_pod_log(Conn& c, const Request& r) {
+  std::string_view p(r.path);
+  const std::string_view pre = "/api/v1/namespaces/";
+  if (p.substr(0, pre.size()) != pre) return false;
+  p.remove_prefix(pre.size());
+  size_t a = p.find('/');
+  if (a == std::string_view::npos || p.substr(a, 6) != "/pods/") return false;
+  std::string ns(p.substr(0, a));
+  std::string_view rest = p.substr(a + 6);
+  if (rest.size() <= 4 || rest.find('/') != rest.size() - 4) return false;  // exactly "<name>/log"
+  std::string name(rest.substr(0, rest.size() - 4));
+  struct DelayScope {
+    DelayScope() { g_delay_this = g_opt.api_latency_us > 0; }
+    ~DelayScope() { g_delay_this = false; }
+  } delay_scope;
+  if (!g_store[K_POD].objs.count(okey(ns, name))) {
+    respond(c, 404, status_body(404, "NotFound", "pods \"" + name + "\" not found"));
+    return true;
+  }
+  std::string container = q(r, "container");
+  auto pit = g_pod_logs.find(okey(ns, name));
+  const std::string* text = nullptr;
+  if (pit != g_pod_logs.end()) {
+    auto cit = container.empty() ? pit->second.begin() : pit->second.find(container);
+    if (cit != pit->second.end()) text = &cit->second;
+  }
+  if (!text) {
+    respond(c, 400, status_body(400, "BadRequest", "container \"" + container + "\" has no log"));
+    return true;
+  }
+  std::string_view body(*text);
+  long tail = atol(q(r, "tailLines", "0").c_str());
+  if (tail > 0) {
+    size_t cut = body.size();
+    long lines = 0;
+    size_t end = body.size();
+    if (end && body[end - 1] == '\n') --end;
+    for (size_t i = end; i > 0; --i)
+      if (body[i - 1] == '\n' && ++lines == tail) {
+        cut = i;
+        break;
+      }
+    if (lines >= tail) body = body.substr(cut);
+  }
+  long limit = atol(q(r, "limitBytes", "0").c_str());
+  if (limit > 0 && static_cast<size_t>(limit) < body.size()) body = body.substr(0, static_cast<size_t>(limit));
+  respond(c, 200, std::string(body));
+  return true;
 }
 
 void handle(Conn& c, Request& r) {
@@ -1666,6 +1734,8 @@ void handle(Conn& c, Request& r) {
   }
   if (!g_opt.token.empty() && r.auth != "Bearer " + g_opt.token)
     return respond(c, 401, status_body(401, "Unauthorized", "Unauthorized"));
+  if (r.method == "GET" && r.path.size() > 4 && r.path.compare(r.path.size() - 4, 4, "/log") == 0 && h_pod_log(c, r))
+    return;
   int kind;
   std::string ns, name;
   if (!route(r.path, kind, ns, name)) return respond(c, 404, status_body(404, "NotFound", "the server could not find the requested resource"));

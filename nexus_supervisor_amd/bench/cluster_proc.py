@@ -63,6 +63,9 @@ async def amain(args) -> None:
             return t if t is not None else time.monotonic()
         t = time.monotonic()
         for i, (etype, obj) in enumerate(events):
+            if etype == "LOG":
+                api.set_pod_log(obj["namespace"], obj["pod"], obj["container"], obj["text"])
+                continue
             if etype == "ADDED":
                 api.create(obj, copy_obj=False)
             else:
@@ -100,7 +103,7 @@ async def amain(args) -> None:
             wl = Workload(p.get("jobs", 10_000), rank=k if len(indexes) > 1 else p.get("rank", 0),
                           world=p.get("world", 1), seed=p.get("seed", 0),
                           hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=n_shards, shard_index=k,
-                          shard_label=p.get("shard_label") or "")
+                          shard_label=p.get("shard_label") or "", hbm_shape=p.get("hbm_shape") or "termination-message")
             objs, rows = wl.initial()
             await write_rows(rows)
             await apply([("ADDED", o) for o in objs])

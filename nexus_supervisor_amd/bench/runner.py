@@ -56,6 +56,9 @@ class BenchConfig:
     # shared cluster: the runs carry their shard as a label and every replica watches only
     # its shard's Pods / Jobs (sharding.shard-label); "" = every replica gets the whole stream
     shard_label: str = "nexus.amd.com/shard"
+    # how the synthetic HBM-OOMs look: "default-pod" (empty termination message, the HIP text
+    # in the container log: the supervisor reads pods/log) or "termination-message"
+    hbm_shape: str = "default-pod"
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:

@@ -99,6 +99,7 @@ class WireHarness:
                     "shard_indexes": list(range(cfg.world)) if self.shared else [cfg.rank],
                     "hip_oom_message": cfg.hip_oom_message,
                     "shard_label": self.sc.sharding.shard_label if self.shared else "",
+                    "hbm_shape": cfg.hbm_shape,
                     "pregen": cfg.warmup + cfg.steps if cfg.pregen else 0, "events": cfg.events}) as r:
                 r.raise_for_status()
                 await r.json()

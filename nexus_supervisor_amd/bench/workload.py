@@ -58,7 +58,7 @@ class Workload:
     def __init__(self, concurrent_jobs: int = 10_000, rank: int = 0, world: int = 1, seed: int = 0,
                  labels: Optional[LabelConfig] = None, namespace: str = "nexus", algorithm: str = "bench-algorithm",
                  hip_oom_message: str = DEFAULT_HIP_OOM, gpus_per_node: int = 8, shards: int = 1, shard_index: int = 0,
-                 shard_label: str = ""):
+                 shard_label: str = "", hbm_shape: str = "termination-message"):
         self.rng = random.Random(seed * 7919 + rank)
         self.labels = labels or LabelConfig()
         self.ns = namespace
@@ -69,6 +69,10 @@ class Workload:
         self.gpus_per_node = gpus_per_node
         self.shards = shards
         self.shard_index = shard_index
+        # hbm-oom failures: "termination-message" (the HIP text in terminated.message) or
+        # "default-pod" (terminationMessagePolicy: File — an empty message, the text in the
+        # container log: a ("LOG", …) traffic line the apiserver serves from pods/log)
+        self.hbm_shape = hbm_shape
         # sharding.shard-label: the submitter stamps each run's shard on its Job and pod template
         self.shard_label = shard_label if shards > 1 else ""
         self.live: List[str] = []
@@ -169,8 +173,13 @@ class Workload:
                 st = {"terminated": {"reason": "OOMKilled", "exitCode": 137, "message": ""}}
                 status = {"phase": "Failed", "containerStatuses": [{"name": "algorithm", "state": st, "restartCount": 0}]}
             elif kind == "hbm-oom":
-                st = {"terminated": {"reason": "Error", "exitCode": 1, "message": self.hip_oom_message}}
+                default_pod = self.hbm_shape == "default-pod"
+                st = {"terminated": {"reason": "Error", "exitCode": 1,
+                                     "message": "" if default_pod else self.hip_oom_message}}
                 status = {"phase": "Failed", "containerStatuses": [{"name": "algorithm", "state": st, "restartCount": 0}]}
+                if default_pod:
+                    out.append(("LOG", {"namespace": self.ns, "pod": pod["metadata"]["name"], "container": "algorithm",
+                                        "text": f"epoch 3 step 1200 loss 0.412\n{self.hip_oom_message}\n"}))
             elif kind == "image-pull":
                 st = {"waiting": {"reason": "ImagePullBackOff",
                                   "message": f'Back-off pulling image "registry.local/algo:{rid[:8]}"'}}

@@ -325,3 +325,35 @@ def test_priced_apiserver_latency_throttle_and_write_cap(arun):
             await c.close()
 
     arun(go(), timeout=30)
+
+
+def test_pod_log_endpoint(arun):
+    """pods/{name}/log from the simulator: the bench's default-pod HBM-OOMs keep their HIP
+    text in the container log (a LOG line in /sim/apply, never sent to watchers)."""
+    async def go():
+        labels = _cfg().labels
+        with KubeSim() as sim:
+            ctl = SimControl(sim.url)
+            pod = make_pod("lg", labels)
+            text = "".join(f"line {i}\n" for i in range(50)) + "HIP out of memory\n"
+            await ctl.apply([("ADDED", pod), ("LOG", {"namespace": "nexus", "pod": pod["metadata"]["name"],
+                                                      "container": "algorithm", "text": text})])
+            kc = KubeClient(KubeConfig(sim.url))
+            st, body = await kc.pod_log("nexus", pod["metadata"]["name"], "algorithm", tail_lines=2, limit_bytes=1000)
+            assert st == 200 and body == b"line 49\nHIP out of memory\n"
+            st, body = await kc.pod_log("nexus", pod["metadata"]["name"], "algorithm", tail_lines=100, limit_bytes=12)
+            assert st == 200 and body == b"line 0\nline "
+            st, _ = await kc.pod_log("nexus", pod["metadata"]["name"], "sidecar")
+            assert st == 400
+            st, _ = await kc.pod_log("nexus", "nope", "algorithm")
+            assert st == 404
+            items, _ = await kc.list("Pod", "nexus")
+            assert len(items) == 1  # the LOG line made no object
+            await ctl.apply([("DELETED", pod)])
+            await ctl.apply([("ADDED", pod)])
+            st, _ = await kc.pod_log("nexus", pod["metadata"]["name"], "algorithm")
+            assert st == 400  # the log went with the deleted pod
+            await kc.close()
+            await ctl.close()
+
+    arun(go(), timeout=20)
