@@ -229,6 +229,14 @@ class Classifier:
             if allow_wait and not self.has_gpu_evidence(pod) and kube.gpu_request(pod, self.gpu.gpu_resource_name) > 0:
                 self.deferred = True
                 return []
+            if allow_log_fetch and not any(t.get("message") or t.get("reason") == "OOMKilled" for t in failed_terms):
+                # nothing here can be a text signature: ask for the tail of every instance not
+                # read yet before scoring (the second pass scores once, with the tail)
+                want = self._log_fetch_needed(pod)
+                if want:
+                    self.deferred_log = want
+                    self.deferred = True
+                    return []
             verdict = self._oom(pod, [], failed_terms)
             if allow_log_fetch and not verdict.text_signature:
                 # no verdict, or one resting only on exit codes / VRAM numbers: the log tail
