@@ -308,14 +308,14 @@ class PipelinedHttp:
                                                               len(body) if body else 0, body or b"")
 
     async def request(self, method: str, path: str, body: Optional[bytes] = None,
-                      headers: Optional[Dict[str, str]] = None) -> Tuple[int, bytes]:
+                      headers: Optional[Dict[str, str]] = None, timeout: Optional[float] = None) -> Tuple[int, bytes]:
         conn = await self._pick()
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         conn.send(self._encode(method, path, body, headers), fut)
         self.requests += 1
         # deadline as a timer on the future (asyncio.wait_for would cost a Task per request)
-        timer = loop.call_later(self.timeout, _expire, fut)
+        timer = loop.call_later(self.timeout if timeout is None else timeout, _expire, fut)
         try:
             return await fut
         except _Expired:

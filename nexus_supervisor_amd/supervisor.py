@@ -606,7 +606,8 @@ class Supervisor:
                     self.metrics.set("log_tail_inflight", self._log_inflight)
 
         try:
-            recs = await asyncio.gather(*(one(w) for w in want))
+            # one failed container (the common case): no gather, no Task per read
+            recs = [await one(want[0])] if len(want) == 1 else await asyncio.gather(*(one(w) for w in want))
             for r, w in zip(recs, want):
                 r["restart"] = w["restart"]
                 if r.get("error"):

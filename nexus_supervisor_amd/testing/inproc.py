@@ -23,6 +23,14 @@ class RecordingJobs(JobClient):
         self.deleted: List[str] = []
         self.latency = latency
         self.fail_next = 0
+        self.logs: Dict[Any, bytes] = {}  # (namespace, pod, container) → pods/log text
+
+    async def pod_log(self, namespace, name, container, *, previous=False, tail_lines=200, limit_bytes=65536,
+                      timeout=2.0):
+        text = self.logs.get((namespace, name, container))
+        if text is None:
+            return 400, b'{"kind":"Status","code":400}'
+        return 200, text[-limit_bytes:]
 
     async def delete_job(self, namespace, name, propagation_policy="Background"):
         if self.latency:
