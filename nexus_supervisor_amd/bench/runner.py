@@ -15,6 +15,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..config.schema import SupervisorConfig
 from ..models.decisions import Decision
+from ..obs.delivery import record as delivery_record
 from .workload import DEFAULT_HIP_OOM, Workload
 
 
@@ -103,15 +104,16 @@ class Tracker:
         self.checked: Dict[str, str] = {}  # timed run → expected stage (read-back)
         self.record = False
         # recorded decisions' push→ack decomposition (ms): api (push → hub read), hub (→ worker
-        # frame), feed (→ decoded), dispatch (→ handler), supervise (handler → checkpoint ack)
-        self.parts: List[Tuple[float, float, float, float, float, float]] = []
+        # frame), feed (→ decoded), dispatch (→ handler), classify (handler → enqueue, with any
+        # log-tail wait), queue (→ dequeue), actuate (→ checkpoint ack)
+        self.parts: List[Tuple[float, ...]] = []
 
     def __call__(self, d: Decision):
         s = d.result.stamps
         x = None
         dl = s.get("delivery")
         if dl is not None and "ack" in s and "receive" in s:
-            x = (dl[0], dl[1], dl[2], s["ack"] - s["receive"])
+            x = delivery_record(s, dl)
         self.report(d.result.request_id, d.outcome, s.get("ack_mono"), d.new_stage, x)
 
     def report(self, rid: str, outcome: str, ack: Optional[float], stage: Optional[str], x=None) -> None:
@@ -168,10 +170,10 @@ class StepState:
             if self.record:
                 total = (t - self.t_push) * 1000.0
                 tr.latencies.append(total)
-                if x is not None:
-                    hub, feed, dec, r2c = x
+                if x is not None and len(x) >= 6:
+                    hub, feed, dec, cls, que, r2c = x[:6]
                     tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
-                                     (t - r2c - dec) * 1e3, r2c * 1e3))
+                                     (t - r2c - dec) * 1e3, cls * 1e3, que * 1e3, (r2c - cls - que) * 1e3))
         if not self.waiting:
             self.done.set()
 
@@ -430,7 +432,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     return out
 
 
-PART_NAMES = ("api", "hub", "feed", "dispatch", "supervise")
+PART_NAMES = ("api", "hub", "feed", "dispatch", "classify", "queue", "actuate")
 
 
 def decompose(parts) -> Dict[str, Any]:

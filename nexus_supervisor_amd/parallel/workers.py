@@ -49,6 +49,7 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
 from ..models import kube
 from ..models.decisions import Decision, RunStatusAnalysisResult
+from ..obs.delivery import record as delivery_record
 
 try:
     from .._kube_native import dumps as _native_dumps
@@ -653,8 +654,9 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
         rec = [r.request_id, r.algorithm, d.outcome, st.get("ack_mono") if st else None, d.new_stage]
         dl = st.get("delivery") if st else None
         if dl is not None and "ack" in st and "receive" in st:
-            # delivery stamps + receive→ack: the bench decomposes push→ack per decision
-            rec.append([dl[0], dl[1], dl[2], st["ack"] - st["receive"]])
+            # delivery stamps + receive→ack split at enqueue and dequeue: the bench decomposes
+            # push→ack per decision
+            rec.append(delivery_record(st, dl))
         batch.append(rec)
 
     if report:

@@ -195,6 +195,9 @@ class Supervisor:
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
         self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
+        # pod key -> (first receive, watch-batch delivery stamps) of a deferred pod failure:
+        # its decision's stages start where the failure arrived, not at the re-classification
+        self._deferred_at: Dict[str, Tuple[float, Any]] = {}
         self._log_sem: Optional[asyncio.Semaphore] = None  # gpu.log-tail-concurrency
         self._log_inflight = 0
         self.log_tail_inflight_max = 0
@@ -557,19 +560,29 @@ class Supervisor:
         if not results and not self._gpu_wait and not self.classifier.deferred:
             return  # the common case (a new or unchanged pod): nothing to submit or un-defer
         key = kube.object_key(pod)
-        if self.classifier.deferred_log:
-            # failed GPU container, empty termination message: its OOM text (if any) is in
-            # the container log — fetch the tail, then decide (gpu.log-tail)
-            self._gpu_wait.pop(key, None)
-            self._start_log_fetch(key, pod, self.classifier.deferred_log, waited)
-            return
         if self.classifier.deferred:
+            if key not in self._deferred_at:
+                if len(self._deferred_at) >= 4096:  # a deferred pod deleted before its decision
+                    del self._deferred_at[next(iter(self._deferred_at))]
+                self._deferred_at[key] = (recv, _DELIVERY.get("Pod"))
+            if self.classifier.deferred_log:
+                # failed GPU container, empty termination message: its OOM text (if any) is in
+                # the container log — fetch the tail, then decide (gpu.log-tail)
+                self._gpu_wait.pop(key, None)
+                self._start_log_fetch(key, pod, self.classifier.deferred_log, waited)
+                return
             # failed GPU pod without node-agent evidence yet: give the annotation time to land
             if key not in self._gpu_wait:
                 self._gpu_wait[key] = time.monotonic() + wait
                 self.metrics.inc("decisions_deferred_for_gpu_evidence")
             return
         self._gpu_wait.pop(key, None)
+        first = self._deferred_at.pop(key, None) if self._deferred_at else None
+        if first is not None:
+            recv, delivery = first
+            for r in results:
+                self._submit(r, recv, recv, "Pod", delivery)
+            return
         for r in results:
             self._submit(r, recv, recv, "Pod")
 
@@ -748,7 +761,8 @@ class Supervisor:
                          namespace=self.namespace)
 
     # ------------------------------------------------------------------ submit
-    def _submit(self, r: RunStatusAnalysisResult, origin: float, recv: float, kind: str = "") -> None:
+    def _submit(self, r: RunStatusAnalysisResult, origin: float, recv: float, kind: str = "",
+                delivery: Optional[Tuple[float, float, float]] = None) -> None:
         key = (r.algorithm, r.request_id)
         if not r.request_id:
             self.metrics.inc("decisions_unkeyed")
@@ -765,8 +779,10 @@ class Supervisor:
             st["origin"] = origin
             st["receive"] = recv
             st["enqueue"] = self.wall()
-            d = _DELIVERY.get(kind)
-            if d is not None:  # the watch batch being dispatched: hub read / worker feed / decoded
+            # the watch batch being dispatched (hub read / worker feed / decoded), or the one
+            # that carried a deferred failure
+            d = delivery if delivery is not None else _DELIVERY.get(kind)
+            if d is not None:
                 st["delivery"] = d
         self.metrics.inc("decisions", labels={"action": r.action})
         self.pipeline.receive(r)

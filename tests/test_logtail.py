@@ -459,3 +459,64 @@ def test_log_reader_refuses_names_that_leave_the_log_root(tmp_path):
     for ns, pod, uid, ctr in (("..", "p", "u", "c"), ("ns", "p/../..", "u", "c"), ("ns", "p", "u", ".."),
                               ("ns", "p", "", "c"), ("ns", "p", "u", "c\x00")):
         assert container_log_file(str(tmp_path / "pods"), ns, pod, uid, ctr, 0) is None
+
+
+def test_deferred_decision_keeps_the_failure_arrival_stamps(arun):
+    """A default pod's decision waits for its pods/log read (here 0.15 s): its stages start
+    at the update that carried the failure — the receive time and the watch batch's delivery
+    stamps of the first pass, not of whatever batch is in flight when the log arrives — so
+    the wait shows up as the bench's ``classify`` stage instead of vanishing."""
+    from nexus_supervisor_amd.bench.runner import PART_NAMES, Tracker, decompose
+    from nexus_supervisor_amd.obs import delivery
+    from nexus_supervisor_amd.testing.inproc import InProcCluster, RecordingJobs
+
+    class SlowLogs(RecordingJobs):
+        async def pod_log(self, *a, **kw):
+            await asyncio.sleep(0.15)
+            return await super().pod_log(*a, **kw)
+
+    async def go():
+        cfg = _app_cfg()
+        cfg.observability.stage_timestamps = True
+        row = seed_rows()[1]
+        pod = make_pod(row.id, cfg.labels, gpus=1, status={"phase": "Running"})
+        jobs = SlowLogs([row.id])
+        jobs.logs[("nexus", pod["metadata"]["name"], "algorithm")] = (TORCH_OOM + "\n").encode()
+        cl = InProcCluster(cfg, MemoryStore([row]), [pod, make_job(row.id, cfg.labels)], jobs=jobs)
+        await cl.start()
+        delivery.CURRENT["Pod"] = (1.0, 2.0, 3.0)
+        cl.push(_failed(pod), "MODIFIED")
+        for _ in range(20):
+            await asyncio.sleep(0.01)
+            if cl.supervisor._log_fetches:
+                break
+        assert cl.supervisor._log_fetches  # deferred, reading the tail
+        delivery.CURRENT["Pod"] = (7.0, 8.0, 9.0)  # a later batch is being dispatched
+        for _ in range(200):
+            if any(x.outcome == "applied" for x in cl.decisions):
+                break
+            await asyncio.sleep(0.01)
+        d = [x for x in cl.decisions if x.outcome == "applied"][0]
+        st = d.result.stamps
+        assert d.result.failure_class == FailureClass.HBM_OOM
+        assert st["delivery"] == (1.0, 2.0, 3.0)
+        assert st["enqueue"] - st["receive"] >= 0.14  # the log wait is classification time
+        assert not cl.supervisor._deferred_at
+        rec = delivery.record(st, st["delivery"])
+        assert len(rec) == 6 and rec[3] >= 0.14 and rec[5] >= rec[3] + rec[4]
+        # the Tracker's decomposition: the stages of every band sum to its total
+        tr = Tracker()
+        parts = []
+        for i in range(100):
+            total = 1.0 + i / 100
+            parts.append((total, 0.1, 0.1, 0.05, 0.05, 0.2 + i / 200, 0.1, total - 0.6 - i / 200))
+        tr.parts = parts
+        out = decompose(parts)
+        assert list(out["stages"]) == list(PART_NAMES)
+        for band in ("median_band_mean_ms", "tail_p99_mean_ms"):
+            b = out[band]
+            assert abs(sum(b[n] for n in PART_NAMES) - b["total"]) < 0.01, b
+        delivery.CURRENT.pop("Pod", None)
+        await cl.supervisor.stop(drain=False)
+
+    arun(go(), timeout=20)
