@@ -239,7 +239,18 @@ class ShardedApplication:
         self.telemetry = telemetry
         self._owns_telemetry = telemetry is None
         self._gpu_task: Optional[asyncio.Task] = None
+        self._gc_task: Optional[asyncio.Task] = None
+        from .utils.gctune import GcTuner
+
+        # the parent's loop runs the watch hub: a generation-1/2 collection of its heap (the
+        # whole import graph, ~1 ms a pass) is a watch line waiting — the same freeze as the
+        # workers' informer caches, once every worker has synced
+        self.gc_tuner = GcTuner.from_config(cfg.runtime, self.metrics)
         self._stopped = asyncio.Event()
+
+    async def _tune_gc(self) -> None:
+        if await self.pool.wait_synced(None):
+            self.gc_tuner.after_sync()
 
     async def _publish_gpu(self) -> None:
         """Mirror the replica's one GPU monitor into every worker (``RemoteTelemetry``)."""
@@ -295,6 +306,7 @@ class ShardedApplication:
                                 self.pool.data_drain, metrics=self.metrics)
             self.pool.on_restart = lambda _index: self.hub.resync()
             self.hub.start()
+        self._gc_task = asyncio.create_task(self._tune_gc(), name="gc-tune")
         if cfg.observability.http_port:
             from .obs.http import ObsServer
 
@@ -361,6 +373,9 @@ class ShardedApplication:
             await self.shard_leases.stop(release=True)
         if self.hub is not None:
             await self.hub.stop()
+        if self._gc_task is not None:
+            self._gc_task.cancel()
+        self.gc_tuner.stop()
         if self._gpu_task is not None:
             self._gpu_task.cancel()
             try:
