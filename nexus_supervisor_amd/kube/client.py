@@ -602,11 +602,15 @@ class KubeClient:
             url += "&previous=true"
         deadline = time.monotonic() + timeout
         attempt = 0
+        reads = self._read_client()
         while True:
-            await self._admit(path)
+            if self.limiter.qps > 0:
+                await self._admit(path)
             self.requests += 1
-            status, raw = await self._read_client().request("GET", url, None, self._headers(),
-                                                            timeout=max(0.05, deadline - time.monotonic()))
+            left = max(0.05, deadline - time.monotonic())
+            # an idle keep-alive connection takes it without a coroutine or a timer per read
+            fut = reads.request_nowait("GET", url, None, self._headers(), timeout=left)
+            status, raw = await (fut if fut is not None else reads.request("GET", url, None, self._headers(), timeout=left))
             if status >= 429:
                 d = self._backoff("GET", status, retry_after(getattr(raw, "retry_after", None)), attempt, deadline)
                 if d is not None:

@@ -248,7 +248,8 @@ class PipelinedHttp:
         return best
 
     def request_nowait(self, method: str, path: str, body: Optional[bytes] = None,
-                       headers: Optional[Dict[str, str]] = None) -> Optional[asyncio.Future]:
+                       headers: Optional[Dict[str, str]] = None,
+                       timeout: Optional[float] = None) -> Optional[asyncio.Future]:
         """Send on an open connection with room in its pipeline and return the response
         future (``(status, body)``; fails with :class:`HttpError` on timeout / connection
         loss) — no coroutine, no Task.  ``None`` when no connection can take it right now
@@ -264,14 +265,16 @@ class PipelinedHttp:
         # no timer per request: the deadline rides with the request and one sweep per pool
         # fails an expired head of line (a TimerHandle + done-callback per DELETE was ~1 %
         # of a shard worker's CPU)
-        best.send(self._encode(method, path, body, headers), fut, (loop.time() + self.timeout, method, path))
+        limit = self.timeout if timeout is None else timeout
+        best.send(self._encode(method, path, body, headers), fut, (loop.time() + limit, method, path))
         self.requests += 1
         if self._sweeper is None:
-            self._arm_sweep(loop)
+            self._arm_sweep(loop, limit)
         return fut
 
-    def _arm_sweep(self, loop) -> None:
-        self._sweeper = loop.call_later(min(1.0, max(self.timeout / 4, 0.005)), self._sweep)
+    def _arm_sweep(self, loop, limit: Optional[float] = None) -> None:
+        t = min(self.timeout, limit) if limit is not None else self.timeout
+        self._sweeper = loop.call_later(min(1.0, max(t / 4, 0.005)), self._sweep)
 
     def _sweep(self) -> None:
         """Fail the connections whose oldest pipelined request is past its deadline (the
