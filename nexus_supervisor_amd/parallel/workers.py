@@ -459,8 +459,14 @@ class WorkerPool:
 
         d = self.workers[index].data
         if d is not None and not d.is_closing():
-            d.write(HEADER.pack(ftype, kind, len(payload)))
-            d.write(payload)
+            head = HEADER.pack(ftype, kind, len(payload))
+            if len(payload) <= 1 << 16:
+                # one send: written apart, an idle socket sends the 6-byte header at once and
+                # the worker wakes for it, then again for the payload (a watch frame is small)
+                d.write(head + payload)
+            else:  # a LIST snapshot: no copy of megabytes
+                d.write(head)
+                d.write(payload)
 
     def data_buffered(self, index: int) -> int:
         d = self.workers[index].data
