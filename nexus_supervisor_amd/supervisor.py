@@ -634,6 +634,14 @@ class Supervisor:
         latest = self.pod_informer.indexer.get(key)
         if latest is not None and self.active:
             self._on_pod_update(None, latest, waited=waited)
+        self._end_deferral(key)
+
+    def _end_deferral(self, key: str) -> None:
+        """A deferred failure was re-classified: unless it is waiting again, forget its
+        arrival stamps (no decision came of it, or the decision took them) — a later
+        failure of the same pod starts its own clock."""
+        if key not in self._gpu_wait and key not in self._log_fetches:
+            self._deferred_at.pop(key, None)
 
     def _expire_gpu_waits(self) -> None:
         now = time.monotonic()
@@ -645,6 +653,7 @@ class Supervisor:
             if pod is not None:
                 self.metrics.inc("gpu_evidence_wait_expired")
                 self._on_pod_update(None, pod, waited=True)
+            self._end_deferral(key)
 
     def _on_job_add(self, job):
         if self._parked:

@@ -520,3 +520,30 @@ def test_deferred_decision_keeps_the_failure_arrival_stamps(arun):
         await cl.supervisor.stop(drain=False)
 
     arun(go(), timeout=20)
+
+
+def test_a_log_read_without_a_decision_forgets_the_arrival_stamps(arun):
+    """A default pod whose tail shows an ordinary crash yields no pod-level decision (the
+    Job decides): its deferral's arrival stamps are dropped, so a later failure of the same
+    pod starts its own clock."""
+    from nexus_supervisor_amd.testing.inproc import InProcCluster, RecordingJobs
+
+    async def go():
+        cfg = _app_cfg()
+        row = seed_rows()[1]
+        pod = make_pod(row.id, cfg.labels, gpus=1, status={"phase": "Running"})
+        jobs = RecordingJobs([row.id])
+        jobs.logs[("nexus", pod["metadata"]["name"], "algorithm")] = (PLAIN_CRASH + "\n").encode()
+        cl = InProcCluster(cfg, MemoryStore([row]), [pod, make_job(row.id, cfg.labels)], jobs=jobs)
+        await cl.start()
+        cl.push(_failed(pod), "MODIFIED")
+        sup = cl.supervisor
+        for _ in range(100):
+            await asyncio.sleep(0.01)
+            if sup.metrics.counter("log_tail_fetches") >= 1 and not sup._log_fetches:
+                break
+        assert sup.metrics.counter("log_tail_fetches") == 1
+        assert not sup._deferred_at and not cl.decisions
+        await sup.stop(drain=False)
+
+    arun(go(), timeout=20)
