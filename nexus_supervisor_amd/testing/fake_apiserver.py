@@ -232,7 +232,9 @@ class FakeApiServer:
         self.url = ""
 
     # ------------------------------------------------------------------ lifecycle
-    async def start(self, host: str = "127.0.0.1", port: int = 0) -> str:
+    async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> str:
+        """Serve on ``host:port`` (0 = any free port); with ``ssl_context`` over TLS, the
+        way a real kube-apiserver always answers."""
         srv = web.Server()
         for kind, (prefix, plural) in RESOURCES.items():
             base = f"{prefix}/namespaces/{{ns}}/{plural}"
@@ -244,9 +246,9 @@ class FakeApiServer:
             srv.add_route("DELETE", base + "/{name}", self._h_delete)
             srv.add_route("GET", f"{prefix}/{plural}", self._h_collection)
         srv.add_route("GET", "/api/v1/namespaces/{ns}/pods/{name}/log", self._h_pod_log)
-        port = await srv.start(host, port)
+        port = await srv.start(host, port, ssl_context=ssl_context)
         self._server = srv
-        self.url = f"http://{host}:{port}"
+        self.url = f"{'https' if ssl_context is not None else 'http'}://{host}:{port}"
         return self.url
 
     async def stop(self) -> None:

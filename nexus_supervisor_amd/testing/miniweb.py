@@ -235,9 +235,9 @@ class Server:
                 return await handler(req)
         raise HTTPNotFound()
 
-    async def start(self, host: str, port: int, backlog: int = 4096) -> int:
+    async def start(self, host: str, port: int, backlog: int = 4096, ssl_context=None) -> int:
         loop = asyncio.get_running_loop()
-        self._srv = await loop.create_server(lambda: _Conn(self), host, port, backlog=backlog)
+        self._srv = await loop.create_server(lambda: _Conn(self), host, port, backlog=backlog, ssl=ssl_context)
         return self._srv.sockets[0].getsockname()[1]
 
     async def stop(self) -> None:

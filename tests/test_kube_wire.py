@@ -368,3 +368,81 @@ def test_record_events_puts_the_decision_on_the_job(arun):
             await api.stop()
 
     arun(go(), timeout=60)
+
+
+def _self_signed(tmp_path):
+    """A throw-away CA-less server certificate for 127.0.0.1 (the openssl CLI)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+    key, crt = tmp_path / "tls.key", tmp_path / "tls.crt"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                    "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, capture_output=True)
+    return str(crt), str(key)
+
+
+def test_tls_and_bearer_token_on_every_path(arun, tmp_path):
+    """A real kube-apiserver answers only over TLS and wants the ServiceAccount token: the
+    informers' LIST / WATCH (aiohttp), the pipelined Job DELETE and the keep-alive pods/log
+    read (the fast client) all verify the server against the kubeconfig's CA and send the
+    bearer token — a decision end to end over TLS, then the fast paths directly."""
+    import ssl
+
+    crt, key = _self_signed(tmp_path)
+    server_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    server_ctx.load_cert_chain(crt, key)
+    rows = [r for r in seed_rows() if r.lifecycle_stage == "RUNNING"][:2]
+    labels = _cfg().labels
+
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1, token="sa-token")
+        url = await api.start(ssl_context=server_ctx)
+        assert url.startswith("https://")
+        for r in rows:
+            api.create(make_job(r.id, labels))
+            api.create(make_pod(r.id, labels, status={"phase": "Running"}))
+        from nexus_supervisor_amd.store.memory import MemoryStore
+
+        store = MemoryStore(rows)
+        kc = KubeClient(KubeConfig(url, token="sa-token", ca_file=crt))
+        app = Application(_cfg(**{"cql-store-type": "memory", "rate-limit-elements-per-second": 0}), kube=kc,
+                          store=store)
+        await app.start()
+        assert await app.factory.wait_for_cache_sync(5)
+        p = api.get("Pod", "nexus", f"{rows[0].id}-acdey")
+        p = dict(p, status={"phase": "Failed", "containerStatuses": [
+            {"name": "algorithm", "state": {"terminated": {"reason": "OOMKilled", "exitCode": 137}}}]})
+        api.update(p)
+        for _ in range(200):
+            if store.get(ALGORITHM, rows[0].id).lifecycle_stage == "FAILED" and api.get("Job", "nexus", rows[0].id) is None:
+                break
+            await asyncio.sleep(0.02)
+        assert store.get(ALGORITHM, rows[0].id).lifecycle_stage == "FAILED"
+        assert api.get("Job", "nexus", rows[0].id) is None  # the pipelined DELETE, over TLS
+        # the fast paths directly: a pipelined DELETE future and a pods/log read
+        fut = kc.delete_job_nowait("nexus", rows[1].id)
+        assert fut is not None
+        kc.check_delete(await fut)
+        assert api.get("Job", "nexus", rows[1].id) is None
+        api.create(make_pod("tls-log", labels, status={"phase": "Running"}))  # the Jobs' pods were collected
+        logged = api.get("Pod", "nexus", "tls-log-acdey")["metadata"]["name"]
+        api.set_pod_log("nexus", logged, "algorithm", "hello over tls\n")
+        status, body = await kc.pod_log("nexus", logged, "algorithm")
+        assert status == 200 and body == b"hello over tls\n"
+        # a client without the token is refused on the fast path too
+        anon = KubeClient(KubeConfig(url, ca_file=crt))
+        status, _ = await anon.pod_log("nexus", logged, "algorithm")
+        assert status == 401
+        # and one that does not trust the server's certificate never gets an answer
+        untrusting = KubeClient(KubeConfig(url, token="sa-token"))
+        with pytest.raises(Exception):
+            await untrusting.pod_log("nexus", logged, "algorithm", timeout=2.0)
+        for c in (anon, untrusting):
+            await c.close()
+        await app.stop()
+        await api.stop()
+
+    arun(go(), timeout=30)
