@@ -351,9 +351,13 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             await sync()
         stages = _stage_breakdown(sup)
         # the replica parent's periodic GPU-telemetry mirror (it shares the watch hub's loop)
-        mirror = _stage_breakdown(sup, ("gpu_mirror_publish",)).get("gpu_mirror_publish")
-        if mirror:
-            cpu["gpu_mirror_publish_ms"] = mirror
+        mirror = _stage_breakdown(sup, ("gpu_mirror_publish", "worker_gpu_update"))
+        if mirror.get("gpu_mirror_publish"):
+            cpu["gpu_mirror_publish_ms"] = mirror["gpu_mirror_publish"]
+        if mirror.get("worker_gpu_update"):  # ... and each worker applying it
+            cpu["worker_gpu_update_ms"] = mirror["worker_gpu_update"]
+            sizes = (sup.metrics.gauges.get("worker_gpu_update_bytes") or {}).values()
+            cpu["worker_gpu_update_bytes_max"] = max(sizes, default=None)
         readback = await _read_back(harness, tracker)
         probe = None
         if cfg.probe_events > 0:

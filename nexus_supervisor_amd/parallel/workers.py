@@ -684,9 +684,11 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
     profiler = None
     try:
         while True:
-            msg = await chan.recv()
-            if msg is None:
+            line = await chan.recv_line()
+            if line is None:
                 break
+            t_msg = time.perf_counter()
+            msg = json.loads(line)
             op = msg.get("op")
             if op == "active":
                 if msg.get("until") is not None:
@@ -704,6 +706,9 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
                     sup.set_lease_deadline(float(msg["active_until"]))
             elif op == "gpu" and remote_tel is not None:
                 remote_tel.update(msg)
+                # the mirror runs on the worker's loop too: a watch frame arriving meanwhile waits
+                app.metrics.observe_seconds("worker_gpu_update", time.perf_counter() - t_msg)
+                app.metrics.set("worker_gpu_update_bytes", float(len(line)))
             elif op == "pprof":
                 profiler = _pprof_op(msg, profiler, cfg.runtime.worker_index)
             elif op == "stop":
