@@ -81,6 +81,9 @@ def parse_args(argv=None):
     ap.add_argument("--hbm-shape", choices=("default-pod", "termination-message"), default="default-pod",
                     help="synthetic HBM-OOM failures: a default pod (empty termination message, the real HIP OOM "
                          "text in the container log, read over pods/log) or the text in the termination message")
+    ap.add_argument("--diag-slow-callback-ms", type=float, default=0.0,
+                    help="diagnostic: count the event-loop callbacks (parent and workers) that run at least this "
+                         "long and list the probe's in latency_at_rate.slow_callbacks (obs/loopwatch.py)")
     ap.add_argument("--api-latency-us", type=int, default=0,
                     help="simulated kube-apiserver answer latency of object requests (Job DELETE / GET / PATCH): "
                          "the etcd write + admission a real apiserver spends; LIST / WATCH unaffected")
@@ -164,6 +167,8 @@ def real_hbm_oom(local_rank: int, workdir: str):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.diag_slow_callback_ms > 0:  # read by the replica parent and inherited by its workers
+        os.environ["NEXUS_SLOW_CALLBACK_MS"] = str(args.diag_slow_callback_ms)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -283,6 +283,9 @@ class ShardedApplication:
                       store=cfg.cql_store_type, worker_processes=self.pool.count)
         le = cfg.leader_election
         lease_mode = cfg.sharding.mode == "lease"
+        from .obs.loopwatch import install_from_env
+
+        install_from_env(self.metrics, "parent")  # diagnostic: NEXUS_SLOW_CALLBACK_MS (the watch hub's loop)
         if lease_mode:
             self.pool.owned_shards = []  # nothing until a shard lease is won
         await self.pool.start(active=lease_mode or not le.enabled)

@@ -15,6 +15,9 @@ upstream of the supervisor).  A small control API drives it:
 ``POST /bench/step {"events": E, "shard": k}``    fail E runs of shard k, replace them;
                                                     ``{"rids": [...], "t_push": monotonic,
                                                     "expected": {rid: stage}}``
+``POST /bench/probe {"n": N, "rate_per_min": R, "seed": s, "shard": k}``
+                                                    the open-loop probe: N one-failure steps
+                                                    at Poisson arrivals, ``{"steps": [...]}``
 
 Per-rank mode lists one shard (the rank's own cluster); shared mode (``bench.py
 --cluster shared``) lists every shard: one apiserver and one CQL server for the whole
@@ -150,6 +153,40 @@ async def amain(args) -> None:
             await asyncio.sleep(hold / 1000.0)
         return web.json_response(doc)
 
+    async def h_probe(req):
+        """The open-loop latency probe, played here: ``n`` single failures of shard ``shard``
+        at Poisson arrivals of mean rate ``rate_per_min`` (``seed``: the same schedule every
+        run), each one step; answers once every arrival is applied, with each step's
+        ``{"rids", "t_push", "expected"}`` in arrival order.  The bench driver makes ONE
+        request for the whole probe, so nothing of the driver runs on the replica parent's
+        loop while failures are in flight (an HTTP round trip per arrival there cost 1–4 ms
+        of that loop, overlapping the next arrivals' watch delivery)."""
+        import random
+
+        p = await req.json()
+        n = int(p["n"])
+        rate = float(p.get("rate_per_min", 1000.0)) / 60.0
+        rng = random.Random(int(p.get("seed", 0)))
+        sh = shards[int(p["shard"])] if "shard" in p else next(iter(shards.values()))
+        loop = asyncio.get_running_loop()
+        docs = [None] * n
+
+        async def one(i):
+            async with sh.lock:
+                docs[i] = await _step(sh, 1)
+
+        tasks = []
+        start = loop.time()
+        at = 0.0
+        for i in range(n):
+            at += rng.expovariate(rate)
+            delay = start + at - loop.time()
+            if delay > 0:
+                await asyncio.sleep(delay)
+            tasks.append(asyncio.ensure_future(one(i)))  # open loop: the next arrival never waits
+        await asyncio.gather(*tasks)
+        return web.json_response({"steps": docs})
+
     async def _step(sh, events):
         wl = sh.wl
         queue = sh.pregen
@@ -187,6 +224,7 @@ async def amain(args) -> None:
     ctl = web.Application(client_max_size=64 << 20)
     ctl.router.add_post("/bench/init", h_init)
     ctl.router.add_post("/bench/step", h_step)
+    ctl.router.add_post("/bench/probe", h_probe)
     ctl.router.add_get("/bench/stats", h_stats)
     runner = web.AppRunner(ctl, access_log=None)
     await runner.setup()

@@ -362,12 +362,16 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         probe = None
         if cfg.probe_events > 0:
             before = _stage_counts(sup)
+            slow0 = _slow_snapshot(sup)
             probe = await _latency_probe(harness, tracker, cfg)
             if sync is not None:
                 await sync()
             if probe.get("events"):
                 # where the open-loop latency goes: the stage histograms' growth over the probe
                 probe["stages_ms"] = _stage_delta(before, _stage_counts(sup))
+                slow = _slow_callbacks(slow0, _slow_snapshot(sup))
+                if slow:  # NEXUS_SLOW_CALLBACK_MS: what held a loop during the probe
+                    probe["slow_callbacks"] = slow
     finally:
         if sampler is not None:
             sampler.stop()
@@ -406,7 +410,13 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         failed, t_push, expected = await (harness.step(1, hold) if hold else harness.step(1))
         states.append(tracker.arm(failed, t_push, expected))
 
-    for i in range(cfg.probe_events):
+    played = getattr(harness, "probe", None)
+    if played is not None:
+        # the cluster process plays the schedule (same seed, same arrivals): one request for
+        # the whole probe, every decision's ack kept by the tracker until its step is armed
+        for doc in await played(cfg.probe_events, cfg.probe_rate_per_min, 0x5EED + cfg.seed + cfg.rank):
+            states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected") or {}))
+    for i in range(cfg.probe_events if played is None else 0):
         at += rng.expovariate(rate)
         delay = start + at - loop.time()
         if delay > 0:
@@ -437,6 +447,28 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
 
 
 PART_NAMES = ("api", "hub", "feed", "dispatch", "classify", "queue", "actuate")
+
+
+def _slow_callbacks(before: Dict[str, Dict[Any, float]], after: Dict[str, Dict[Any, float]],
+                    top: int = 15) -> List[Dict[str, Any]]:
+    """Growth of the ``slow_callbacks`` / ``slow_callback_seconds`` counters ``{name, where}``
+    (:mod:`..obs.loopwatch`) between two snapshots, longest total first."""
+    n0, s0 = before.get("slow_callbacks") or {}, before.get("slow_callback_seconds") or {}
+    n1, s1 = after.get("slow_callbacks") or {}, after.get("slow_callback_seconds") or {}
+    rows = []
+    for k, v in n1.items():
+        n = v - n0.get(k, 0.0)
+        if n > 0:
+            lab = dict(k)
+            rows.append({"where": lab.get("where", ""), "name": lab.get("name", ""), "count": int(n),
+                         "total_ms": round((s1.get(k, 0.0) - s0.get(k, 0.0)) * 1e3, 3)})
+    rows.sort(key=lambda r: -r["total_ms"])
+    return rows[:top]
+
+
+def _slow_snapshot(sup) -> Dict[str, Dict[Any, float]]:
+    c = sup.metrics.counters
+    return {n: dict(c.get(n) or {}) for n in ("slow_callbacks", "slow_callback_seconds")}
 
 
 def decompose(parts) -> Dict[str, Any]:

@@ -155,6 +155,16 @@ class WireHarness:
             doc = await r.json()
         return doc["rids"], doc["t_push"], doc.get("expected") or {}
 
+    async def probe(self, n: int, rate_per_min: float, seed: int) -> List[Dict[str, Any]]:
+        """The open-loop probe played by the cluster process (one request for all ``n``
+        arrivals): each arrival's ``{"rids", "t_push", "expected"}``."""
+        body = {"n": n, "rate_per_min": rate_per_min, "seed": seed, "shard": self.cfg.rank}
+        budget = aiohttp.ClientTimeout(total=n / max(rate_per_min / 60.0, 1e-3) * 3 + 120)
+        async with self.http.post(self.ctl + "/bench/probe", json=body, timeout=budget) as r:
+            r.raise_for_status()
+            doc = await r.json()
+        return doc["steps"]
+
     algorithm = "bench-algorithm"
 
     async def read_stages(self, algorithm: str, rids: List[str]) -> Dict[str, Optional[str]]:

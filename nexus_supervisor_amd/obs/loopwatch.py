@@ -1,0 +1,65 @@
+"""Opt-in event-loop watch: which callbacks hold a process's loop for longer than a
+threshold (``NEXUS_SLOW_CALLBACK_MS``).
+
+A watch line that reaches a worker while its loop runs something else waits for it; the
+bench probe's delivery split (:mod:`.delivery`) shows *that* a stage was late, this shows
+*what* held the loop.  :func:`install` wraps ``asyncio.Handle._run`` (every callback and
+task step of the process's loops): one ``perf_counter`` pair per callback — a diagnostic,
+not for production — and for each callback at or over the threshold increments
+``slow_callbacks{name, where}`` / ``slow_callback_seconds{name, where}`` and records its
+duration in the ``slow_callback`` histogram.
+asyncio's own debug mode does the same but slows every coroutine down.
+"""
+from __future__ import annotations
+
+import asyncio.events as _events
+import os
+import time
+from typing import Optional
+
+_INSTALLED = False
+
+
+def _name(handle) -> str:
+    cb = handle._callback
+    owner = getattr(cb, "__self__", None)
+    if owner is not None and hasattr(owner, "get_coro"):  # a Task step: the coroutine's name
+        coro = owner.get_coro()
+        return "task:" + getattr(coro, "__qualname__", type(coro).__name__)
+    name = getattr(cb, "__qualname__", None) or type(cb).__name__
+    return name if owner is None else f"{type(owner).__name__}.{name.rsplit('.', 1)[-1]}"
+
+
+def install(metrics, threshold_ms: float, where: str = "") -> bool:
+    """Watch every loop of this process (``where`` labels it: the replica parent's watch hub
+    or a shard worker); False when already installed or disabled."""
+    global _INSTALLED
+    if _INSTALLED or threshold_ms <= 0:
+        return False
+    threshold = threshold_ms / 1000.0
+    orig = _events.Handle._run
+    clock = time.perf_counter
+
+    def _run(self):
+        t0 = clock()
+        orig(self)
+        d = clock() - t0
+        if d >= threshold:
+            labels = {"name": _name(self), "where": where}
+            metrics.inc("slow_callbacks", labels=labels)
+            metrics.inc("slow_callback_seconds", d, labels=labels)
+            metrics.observe_seconds("slow_callback", d)
+
+    _events.Handle._run = _run
+    _INSTALLED = True
+    return True
+
+
+def install_from_env(metrics, where: str = "") -> Optional[float]:
+    """:func:`install` with ``NEXUS_SLOW_CALLBACK_MS`` (unset or 0: nothing)."""
+    raw = os.environ.get("NEXUS_SLOW_CALLBACK_MS", "")
+    try:
+        ms = float(raw) if raw else 0.0
+    except ValueError:
+        return None
+    return ms if install(metrics, ms, where) else None

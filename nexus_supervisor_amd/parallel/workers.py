@@ -673,6 +673,9 @@ async def run_worker(cfg, sock: socket.socket, *, start_active: bool = True, rep
         collect_gauges(sup, app.metrics)
         chan.send({"op": "metrics", "seq": seq, "s": metrics_state(app.metrics)})
 
+    from ..obs.loopwatch import install_from_env
+
+    install_from_env(app.metrics, "worker")  # diagnostic: NEXUS_SLOW_CALLBACK_MS
     await app.start()
 
     async def announce_sync():
