@@ -170,6 +170,18 @@ async def amain(args) -> None:
         sh = shards[int(p["shard"])] if "shard" in p else next(iter(shards.values()))
         loop = asyncio.get_running_loop()
         docs = [None] * n
+        async with sh.lock:
+            # the saturated steps left a prefetched 1000-failure step (and maybe pre-generated
+            # ones) whose replacement runs are live in the workload: create them in the cluster
+            # now and let the supervisor absorb that burst (thousands of ADDED lines) before the
+            # first timed arrival, instead of inside it
+            while sh.pregen:
+                await simctl.apply_raw(sh.pregen.popleft()[2])
+            nxt, sh.next = sh.next, None
+            if nxt is not None:
+                _f, stale = await nxt[1]
+                await apply([(e, o) for e, o in stale if e == "ADDED" and o.get("kind") in ("Pod", "Job")])
+        await asyncio.sleep(float(p.get("settle_s", 2.0)))
 
         async def one(i):
             async with sh.lock:
