@@ -970,7 +970,13 @@ class Supervisor:
                                 and self.job_informer.indexer.get_by_name(self.namespace, r.request_id) is not None):
             if self._fenced(epoch, r.request_id):
                 return Decision(r, "fenced", current, False)
-            deleted = await self._delete_job(r.request_id)
+            if self.cfg.async_job_delete and not r.pending_delete:
+                # the row is final: like a fresh decision's, the Job DELETE must not hold a
+                # worker — behind a kube-qps bucket full of DELETEs (a new leader finishing its
+                # predecessor's) it would stall the whole pipeline for seconds
+                self._spawn_delete(r)
+            else:
+                deleted = await self._delete_job(r.request_id)
             r.pending_delete = False
         self._remember((r.algorithm, r.request_id), current)
         self.metrics.inc("decisions_skipped_finished")

@@ -155,7 +155,9 @@ def test_missing_row_and_finished_row_skip_without_a_read(arun):
 
 def test_finished_failed_row_with_surviving_job_finishes_the_delete(arun):
     """A crash between the durable write and the Job DELETE: the replay's fused write is refused
-    with FAILED, and the Job still in the cache is deleted (the two-step path's rule)."""
+    with FAILED, and the Job still in the cache is deleted (the two-step path's rule) — in the
+    background, like a fresh decision's DELETE (``async-job-delete``): the worker does not
+    wait for it."""
     async def go():
         cfg = _cfg()
         failed = RUNNING_ROW.deep_copy()
@@ -166,7 +168,11 @@ def test_finished_failed_row_with_surviving_job_finishes_the_delete(arun):
         await c.start()
         c.push(make_event("Job", failed.id, "PodFailurePolicy", "exit 137"))
         assert await c.settle(5)
-        assert [(d.outcome, d.job_deleted) for d in c.decisions] == [("skipped-finished", True)]
+        assert [d.outcome for d in c.decisions] == ["skipped-finished"]
+        for _ in range(100):
+            if jobs.deleted:
+                break
+            await asyncio.sleep(0.01)
         assert jobs.deleted == [failed.id] and store.write_log == []
         await c.stop()
 
