@@ -56,8 +56,8 @@ def parse_args(argv=None):
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--procs", type=int, default=0,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport); "
-                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 6 (the measured "
-                         "efficiency knee: auto_procs)")
+                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 8 (the measured "
+                         "knee: auto_procs)")
     ap.add_argument("--inflight", type=int, default=4, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--no-pregen", action="store_true",
                     help="generate each step's synthetic traffic on demand instead of before the timed region")
@@ -107,23 +107,26 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+BENCH_WORKERS_KNEE = 8
+
+
 def auto_procs(local_world: int) -> int:
     """Shard-worker processes per replica: the rank's CPU share minus 4 (simulated
-    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 6].
+    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 8].
 
-    Six is the efficient point: a saturated worker shares every watch
-    frame, socket wakeup and CQL flush among more decisions, so CPU per failure falls as
-    the per-worker load rises.  MI355X box, one box back to back
-    (profiles/r3_cpu_ab/sweep_procs*.json, prof_procs8.json): 6 workers 36.5k/s at
-    158 µs of replica CPU per failure, 7 workers 38.6k/s at 180 µs, 8 workers (profiled)
-    36.8k/s at 187 µs — the apiserver simulator at 0.84–0.94 is the ceiling either way;
-    round 2's sweep found the same (r2_sweep_procs_v16: 6 workers ≈ 12 in throughput at
-    ~40 % less CPU), and so did round 4's (profiles/r4_sweep: 6 / 8 / 10 / 12 workers at
-    153 / 194 / 185 / 214 µs per failure for 36.6k / 36.4k / 48.8k / 38.7k failures/s — CPU
-    per failure up 20-40 % past six, throughput within the box's run-to-run spread)."""
+    The rule, measured: add workers while each pair of them still buys throughput and the
+    single-threaded apiserver simulator stays clear of saturation (the line must measure
+    the supervisor, not the harness).  On the default-pod workload (a `pods/log` read per
+    HBM-OOM decision), one MI355X box, interleaved (profiles/r4_sweep_final/): 6 workers
+    30.4k / 32.4k failures/s at 158 µs of replica CPU per failure, 8 workers 37.0k / 36.4k
+    at 177–183 µs (+16 % throughput for +13 % CPU), 10 workers 38.7k / 40.4k at 196–197 µs
+    (+7 % more, simulator at 0.87 of a core — at the harness bound on a slower box).  On
+    round 3's lighter workload six was already the knee (profiles/r3_cpu_ab/,
+    profiles/r4_sweep/): past six the CPU per failure rose 20–40 % with throughput inside
+    the run-to-run spread."""
     from nexus_supervisor_amd.utils.cpus import cpu_share
 
-    return max(1, min(6, int(cpu_share() / max(local_world, 1)) - 4))
+    return max(1, min(BENCH_WORKERS_KNEE, int(cpu_share() / max(local_world, 1)) - 4))
 
 
 def _harness_bound(cpu) -> dict:
