@@ -56,7 +56,7 @@ def parse_args(argv=None):
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--procs", type=int, default=0,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport); "
-                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 8 (the measured "
+                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 6 (the measured "
                          "knee: auto_procs)")
     ap.add_argument("--inflight", type=int, default=4, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--no-pregen", action="store_true",
@@ -107,23 +107,23 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-BENCH_WORKERS_KNEE = 8
+BENCH_WORKERS_KNEE = 6
 
 
 def auto_procs(local_world: int) -> int:
     """Shard-worker processes per replica: the rank's CPU share minus 4 (simulated
-    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 8].
+    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 6].
 
-    The rule, measured: add workers while each pair of them still buys throughput and the
-    single-threaded apiserver simulator stays clear of saturation (the line must measure
-    the supervisor, not the harness).  On the default-pod workload (a `pods/log` read per
-    HBM-OOM decision), one MI355X box, interleaved (profiles/r4_sweep_final/): 6 workers
-    30.4k / 32.4k failures/s at 158 µs of replica CPU per failure, 8 workers 37.0k / 36.4k
-    at 177–183 µs (+16 % throughput for +13 % CPU), 10 workers 38.7k / 40.4k at 196–197 µs
-    (+7 % more, simulator at 0.87 of a core — at the harness bound on a slower box).  On
-    round 3's lighter workload six was already the knee (profiles/r3_cpu_ab/,
-    profiles/r4_sweep/): past six the CPU per failure rose 20–40 % with throughput inside
-    the run-to-run spread."""
+    The rule, measured: add workers while they buy throughput the box resolves without
+    raising the CPU per failure, and keep the single-threaded apiserver simulator clear of
+    saturation (the line must measure the supervisor, not the harness).  Round 4, default-pod
+    workload (profiles/r4_procs_ab/, same box, interleaved, probe on): 6 workers 34.1k
+    failures/s (31.1-34.7k) at 152 µs of replica CPU per failure, probe 0.56 / 1.30 ms; 8
+    workers 33.3k (32.7-33.7k) at 188 µs, probe 0.66 / 1.43 ms.  Another box
+    (profiles/r4_sweep_final/, probe off) had 8 workers ahead (36.7k vs 31.4k) and 10 at
+    39.5k with the simulator at 0.87 of a core.  Rounds 2-3 found six the knee as well
+    (profiles/r3_cpu_ab/, profiles/r4_sweep/): past six the CPU per failure rises 15-40 %
+    while the throughput gain stays inside the box-to-box spread."""
     from nexus_supervisor_amd.utils.cpus import cpu_share
 
     return max(1, min(BENCH_WORKERS_KNEE, int(cpu_share() / max(local_world, 1)) - 4))
