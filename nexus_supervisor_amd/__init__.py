@@ -14,3 +14,8 @@ import os as _os
 # instrumented build directory first.
 if _os.environ.get("NEXUS_NATIVE_DIR"):
     __path__.insert(0, _os.environ["NEXUS_NATIVE_DIR"])  # type: ignore[name-defined]
+
+# hot-path modules as C extensions when built from the sources on disk (compiled.py)
+from . import compiled as _compiled  # noqa: E402
+
+_compiled.install()

@@ -178,6 +178,59 @@ def build_one(name: str, t: Dict, force: bool = False, verbose: bool = False) ->
     return f"{name}: built {os.path.relpath(t['out'], ROOT)}"
 
 
+def _compile_module(name: str, force: bool = False, verbose: bool = False) -> Optional[str]:
+    """One hot-path module through Cython (pure-Python mode) and the C compiler into
+    ``_compiled/`` with the hash of its source (:mod:`.compiled`); None when fresh."""
+    from . import compiled
+
+    if not force and compiled.fresh(name):
+        return None
+    src = compiled.source_path(name)
+    digest = compiled.source_hash(src)
+    os.makedirs(compiled.DIR, exist_ok=True)
+    tag = f"{name}.tmp{os.getpid()}"
+    c_file = os.path.join(compiled.DIR, tag + ".c")
+    so_tmp = os.path.join(compiled.DIR, tag + compiled.EXT)
+    steps = [
+        [sys.executable, "-m", "cython", "-3", "--module-name", name, "-X", "binding=True",
+         "-X", "embedsignature=False",
+         # annotations stay hints: as C types they would be enforced (a frozenset bound to a
+         # name annotated `set` raises) — Python semantics exactly, only the dispatch removed
+         "-X", "annotation_typing=False", "-o", c_file, src],
+        [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-fno-strict-aliasing", "-fwrapv", "-w",
+         f"-I{sysconfig.get_paths()['include']}", c_file, "-o", so_tmp],
+    ]
+    try:
+        for cmd in steps:
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            p = subprocess.run(cmd, capture_output=True, text=True)
+            if p.returncode != 0:
+                raise RuntimeError(f"compiled {name}: build failed\n$ {' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+        os.replace(so_tmp, compiled.extension_path(name))
+        with open(compiled.hash_path(name) + ".tmp", "w") as f:
+            f.write(digest + "\n")
+        os.replace(compiled.hash_path(name) + ".tmp", compiled.hash_path(name))
+    finally:
+        for leftover in (c_file, so_tmp):
+            if os.path.exists(leftover):
+                os.remove(leftover)
+    return f"compiled {name}"
+
+
+def build_compiled(force: bool = False, verbose: bool = False) -> str:
+    """Every :data:`.compiled.MODULES` entry whose extension is missing or stale."""
+    from . import compiled
+
+    try:
+        import Cython  # noqa: F401
+    except ImportError:
+        return "compiled: skipped (Cython not importable)"
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        done = [r for r in ex.map(lambda n: _compile_module(n, force, verbose), compiled.MODULES) if r]
+    return f"compiled: {len(done)} built, {len(compiled.MODULES) - len(done)} up to date"
+
+
 def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optional[str] = None, verbose: bool = False) -> List[str]:
     ts = targets(sanitize)
     names = [n for n in ts if not only or n in only]
@@ -185,7 +238,10 @@ def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optio
         names = [n for n in names if ts[n].get("exe") or ts[n].get("inproc")]
     with cf.ThreadPoolExecutor(max_workers=min(4, len(names) or 1)) as ex:
         futs = {ex.submit(build_one, n, ts[n], force, verbose): n for n in names}
-        return [f.result() for f in cf.as_completed(futs)]
+        out = [f.result() for f in cf.as_completed(futs)]
+    if not sanitize and (not only or "compiled" in only):
+        out.append(build_compiled(force, verbose))
+    return out
 
 
 def binary(name: str) -> str:
