@@ -325,6 +325,8 @@ def main(argv=None) -> int:
                 "pregenerated_input": not args.no_pregen and args.transport == "wire",
                 "rate_limit_eps": res.get("eps"),
                 "kube_qps": res.get("kube_qps"),
+                # hot-path modules running as C extensions (nexus_supervisor_amd/compiled.py)
+                "compiled_modules": len(__import__("nexus_supervisor_amd.compiled", fromlist=["loaded"]).loaded()),
                 "gpu_telemetry": res.get("telemetry"),
                 "real_hbm_oom": bool(hip_msg),
                 "hbm_oom_shape": args.hbm_shape if args.transport == "wire" else "termination-message",

@@ -376,7 +376,9 @@ class WorkerPool:
         dparent = dchild = None
         if self.hub:
             dparent, dchild = socket.socketpair()
-        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from .. import compiled
+
+        pkg_root = os.path.dirname(compiled.PKG_DIR)  # (this module may run compiled: no __file__ walk)
         env = dict(self.env if self.env is not None else os.environ)
         env["PYTHONPATH"] = os.pathsep.join(p for p in [pkg_root, env.get("PYTHONPATH", "")] if p)
         env["NEXUS_WORKER_CONFIG"] = json.dumps(self._child_mapping(w.index))
