@@ -125,7 +125,8 @@ class _Finder(importlib.abc.MetaPathFinder):
         so = extension_path(fullname)
         spec = importlib.util.spec_from_file_location(
             fullname, so, loader=importlib.machinery.ExtensionFileLoader(fullname, so))
-        _LOADED.append(fullname)
+        if fullname not in _LOADED:
+            _LOADED.append(fullname)
         return spec
 
 
