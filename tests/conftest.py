@@ -4,6 +4,10 @@ import sys
 
 import pytest
 
+# lease / wait timings of the HA tests are multiplied by this under a slow tracer (the
+# coverage gate sets NEXUS_TEST_TIME_SCALE: line tracing slows the code 3-10x)
+TIME_SCALE = float(os.environ.get("NEXUS_TEST_TIME_SCALE", "1") or 1)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

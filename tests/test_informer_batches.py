@@ -107,7 +107,8 @@ def test_listed_objects_are_freed_once_the_watch_replaces_them(arun):
                 break
             await asyncio.sleep(0.01)
         assert inf.indexer.get("nexus/p")["metadata"]["resourceVersion"] == "2"
-        assert sys.getrefcount(listed) == 2  # this frame + the call argument: nothing else holds it
+        if sys.gettrace() is None:  # a line tracer (the coverage gate) holds frames and their locals
+            assert sys.getrefcount(listed) == 2  # this frame + the call argument: nothing else holds it
         await f.stop()
 
     arun(go(), timeout=10)

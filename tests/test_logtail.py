@@ -11,6 +11,7 @@ signature of its own; a previous tenant's VRAM peak alone never is.
 import asyncio
 import json
 
+from conftest import TIME_SCALE
 from nexus_supervisor_amd.app import Application
 from nexus_supervisor_amd.classify import Classifier
 from nexus_supervisor_amd.config import load_config
@@ -383,7 +384,7 @@ def test_agent_retries_failed_patch_and_prunes_on_delete(arun, tmp_path):
         for n in names:
             api.update(_failed(api.get("Pod", "nexus", n)))
         anns = {}
-        for _ in range(200):
+        for _ in range(int(200 * TIME_SCALE)):
             anns = {n: (api.get("Pod", "nexus", n)["metadata"].get("annotations") or {}).get(ANN) for n in names}
             if all(anns.values()):
                 break

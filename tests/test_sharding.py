@@ -19,6 +19,7 @@ from nexus_supervisor_amd.parallel.sharding import SHARD_SEED, ShardSet, shard_o
 from nexus_supervisor_amd.parallel.workers import _SEED
 from nexus_supervisor_amd.store.memory import MemoryStore
 from nexus_supervisor_amd.testing.fake_apiserver import FakeApiServer
+from conftest import TIME_SCALE
 
 LABEL = "batch.kubernetes.io/job-name"
 
@@ -125,14 +126,18 @@ def test_pipeline_clear_with_predicate_keeps_other_keys(arun):
 def _cfg(ident, extra=None):
     over = {"cql-store-type": "memory", "workers": 8, "rate-limit-elements-per-second": 0, "resync-period": "0s",
             "rules": {"stale-event-grace": "2s"},
-            "leader-election": {"identity": ident, "lease-duration": "800ms", "renew-deadline": "500ms",
-                                "retry-period": "100ms"}}
+            "leader-election": {"identity": ident, "lease-duration": _ms(800), "renew-deadline": _ms(500),
+                                "retry-period": _ms(100)}}
     over.update(extra or {})
     return load_config(path=None, env={}, overrides=over)
 
 
+def _ms(v: float) -> str:
+    return f"{int(v * TIME_SCALE)}ms"
+
+
 async def _wait(pred, timeout):
-    deadline = time.monotonic() + timeout
+    deadline = time.monotonic() + timeout * TIME_SCALE
     while time.monotonic() < deadline:
         if pred():
             return True
@@ -231,7 +236,7 @@ def test_shard_leases_fail_over_individually_without_loss_or_double_writes(arun)
         assert await _wait(lambda: owners()[1] == [standby], 5), owners()
         took = time.monotonic() - t0
         # lease duration (0.8 s) + up to two retry periods of observation
-        assert took < 0.8 + 0.5, took
+        assert took < (0.8 + 0.5) * TIME_SCALE, took
         assert owners()[0] == own[0]  # the surviving owner kept its shard throughout
         assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 15)
         await asyncio.sleep(0.3)
@@ -551,14 +556,14 @@ def test_partitioned_shard_owner_stops_acting_before_anyone_takes_over(arun):
         purl = await proxy.start()
         wl = Workload(concurrent_jobs=400, seed=31)
         objs, rows = wl.initial()
-        store = MemoryStore(rows, latency=0.03)  # a slow store: A keeps a backlog past its hold
+        store = MemoryStore(rows, latency=0.03 * TIME_SCALE)  # a slow store: A keeps a backlog past its hold
         for o in objs:
             api.create(o)
         events = []
         apps = {}
         # twice the production ratios' minimum: a loaded CI box (the suite under xdist) must not
         # turn a scheduling delay into a lapsed hold
-        lease = {"lease-duration": "2400ms", "renew-deadline": "1600ms", "retry-period": "300ms"}
+        lease = {"lease-duration": _ms(2400), "renew-deadline": _ms(1600), "retry-period": _ms(300)}
         for ident, u in (("rep-a", purl), ("rep-b", url)):
             cfg = _cfg(ident, {"workers": 2, "sharding": {"shards": 2, "mode": "lease", "replicas": 2},
                                "leader-election": dict(lease, identity=ident)})
@@ -583,7 +588,7 @@ def test_partitioned_shard_owner_stops_acting_before_anyone_takes_over(arun):
         t_cut = time.monotonic()
         proxy.pause()
         hold_end = a.shard_leases.valid_until(ka)
-        assert hold_end <= t_cut + 1.6 + 0.01
+        assert hold_end <= t_cut + 1.6 * TIME_SCALE + 0.01
         assert await _wait(lambda: ka in b.shard_leases.owned, 10), "B never took A's shard"
         t_b = time.monotonic()
         assert await _wait(lambda: not _check_exactly_once(store, wl, expected)[0], 20)

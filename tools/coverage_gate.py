@@ -118,6 +118,8 @@ def main(argv: List[str] = None) -> int:
 
     child_dir = tempfile.mkdtemp(prefix="nexus-cov-")
     os.environ["NEXUS_COVERAGE_DIR"] = child_dir
+    # line tracing slows everything 3-10x: the lease-timing tests scale their clocks
+    os.environ.setdefault("NEXUS_TEST_TIME_SCALE", "3")
     os.chdir(ROOT)
     sys.path.insert(0, ROOT)
     import pytest
