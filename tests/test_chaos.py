@@ -17,6 +17,7 @@ from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig
 from nexus_supervisor_amd.store.cql import CqlCheckpointStore, CqlSession
 from nexus_supervisor_amd.testing.cqlsrv import CqlServer
 from nexus_supervisor_amd.testing.fake_apiserver import FakeApiServer
+from conftest import TIME_SCALE
 
 pytestmark = pytest.mark.slow
 
@@ -105,7 +106,7 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
         assert survivor.supervisor.active
         # every failed run's Job was deleted through the API (paced by the client-side
         # kube-qps bucket: 50/s by default, so the deletes trail the checkpoint writes)
-        for _ in range(200):
+        for _ in range(int(200 * TIME_SCALE)):
             deleted = {n for k, _ns, n, _p in api.deleted if k == "Job"}
             if set(expected) <= deleted:
                 break
