@@ -21,13 +21,19 @@ _INSTALLED = False
 
 
 def _name(handle) -> str:
-    cb = handle._callback
-    owner = getattr(cb, "__self__", None)
-    if owner is not None and hasattr(owner, "get_coro"):  # a Task step: the coroutine's name
-        coro = owner.get_coro()
-        return "task:" + getattr(coro, "__qualname__", type(coro).__name__)
-    name = getattr(cb, "__qualname__", None) or type(cb).__name__
-    return name if owner is None else f"{type(owner).__name__}.{name.rsplit('.', 1)[-1]}"
+    """A readable name of what a handle runs; never raises (a compiled module's finished
+    coroutine may report no ``__qualname__``)."""
+    try:
+        cb = handle._callback
+        owner = getattr(cb, "__self__", None)
+        if owner is not None and hasattr(owner, "get_coro"):  # a Task step: the coroutine's name
+            coro = owner.get_coro()
+            q = getattr(coro, "__qualname__", None) or getattr(coro, "__name__", None) or type(coro).__name__
+            return f"task:{q}"
+        name = getattr(cb, "__qualname__", None) or getattr(cb, "__name__", None) or type(cb).__name__
+        return name if owner is None else f"{type(owner).__name__}.{str(name).rsplit('.', 1)[-1]}"
+    except Exception:  # noqa: BLE001 - a diagnostic must never take the loop down
+        return "?"
 
 
 def install(metrics, threshold_ms: float, where: str = "") -> bool:
@@ -45,10 +51,13 @@ def install(metrics, threshold_ms: float, where: str = "") -> bool:
         orig(self)
         d = clock() - t0
         if d >= threshold:
-            labels = {"name": _name(self), "where": where}
-            metrics.inc("slow_callbacks", labels=labels)
-            metrics.inc("slow_callback_seconds", d, labels=labels)
-            metrics.observe_seconds("slow_callback", d)
+            try:
+                labels = {"name": _name(self), "where": where}
+                metrics.inc("slow_callbacks", labels=labels)
+                metrics.inc("slow_callback_seconds", d, labels=labels)
+                metrics.observe_seconds("slow_callback", d)
+            except Exception:  # noqa: BLE001 - never let the watch break the loop it watches
+                pass
 
     _events.Handle._run = _run
     _INSTALLED = True

@@ -52,3 +52,28 @@ def test_install_from_env(monkeypatch):
     assert loopwatch.install_from_env(m) is None
     monkeypatch.setenv("NEXUS_SLOW_CALLBACK_MS", "0.5")
     assert loopwatch.install_from_env(m, "parent") == 0.5
+
+
+def test_names_never_raise():
+    class Coro:  # a compiled module's finished coroutine: no name to report
+        def __getattribute__(self, name):
+            if name in ("__qualname__", "__name__"):
+                return None
+            return object.__getattribute__(self, name)
+
+    class NoName:
+        def get_coro(self):
+            return Coro()
+
+    class H:
+        def __init__(self, cb):
+            self._callback = cb
+
+    assert loopwatch._name(H(NoName().get_coro)).startswith("task:")
+
+    class Broken:
+        @property
+        def __self__(self):
+            raise RuntimeError("boom")
+
+    assert loopwatch._name(H(Broken())) == "?"
