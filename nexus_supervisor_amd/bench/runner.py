@@ -451,24 +451,27 @@ PART_NAMES = ("api", "hub", "feed", "dispatch", "classify", "queue", "actuate")
 
 def _slow_callbacks(before: Dict[str, Dict[Any, float]], after: Dict[str, Dict[Any, float]],
                     top: int = 15) -> List[Dict[str, Any]]:
-    """Growth of the ``slow_callbacks`` / ``slow_callback_seconds`` counters ``{name, where}``
-    (:mod:`..obs.loopwatch`) between two snapshots, longest total first."""
+    """Growth of the ``slow_callbacks`` / ``slow_callback_seconds`` /
+    ``slow_callback_gc_seconds`` counters ``{name, where}`` (:mod:`..obs.loopwatch`) between
+    two snapshots, longest total first."""
     n0, s0 = before.get("slow_callbacks") or {}, before.get("slow_callback_seconds") or {}
     n1, s1 = after.get("slow_callbacks") or {}, after.get("slow_callback_seconds") or {}
+    g0, g1 = before.get("slow_callback_gc_seconds") or {}, after.get("slow_callback_gc_seconds") or {}
     rows = []
     for k, v in n1.items():
         n = v - n0.get(k, 0.0)
         if n > 0:
             lab = dict(k)
             rows.append({"where": lab.get("where", ""), "name": lab.get("name", ""), "count": int(n),
-                         "total_ms": round((s1.get(k, 0.0) - s0.get(k, 0.0)) * 1e3, 3)})
+                         "total_ms": round((s1.get(k, 0.0) - s0.get(k, 0.0)) * 1e3, 3),
+                         "gc_ms": round((g1.get(k, 0.0) - g0.get(k, 0.0)) * 1e3, 3)})
     rows.sort(key=lambda r: -r["total_ms"])
     return rows[:top]
 
 
 def _slow_snapshot(sup) -> Dict[str, Dict[Any, float]]:
     c = sup.metrics.counters
-    return {n: dict(c.get(n) or {}) for n in ("slow_callbacks", "slow_callback_seconds")}
+    return {n: dict(c.get(n) or {}) for n in ("slow_callbacks", "slow_callback_seconds", "slow_callback_gc_seconds")}
 
 
 def decompose(parts) -> Dict[str, Any]:

@@ -7,17 +7,22 @@ bench probe's delivery split (:mod:`.delivery`) shows *that* a stage was late, t
 task step of the process's loops): one ``perf_counter`` pair per callback — a diagnostic,
 not for production — and for each callback at or over the threshold increments
 ``slow_callbacks{name, where}`` / ``slow_callback_seconds{name, where}`` and records its
-duration in the ``slow_callback`` histogram.
+duration in the ``slow_callback`` histogram.  ``slow_callback_gc_seconds{name, where}`` is
+the part of those callbacks the cyclic garbage collector ran in (a ``gc.callbacks`` clock):
+a collection triggered by whatever allocation crossed the threshold holds the loop as
+long as the callback's own work.
 asyncio's own debug mode does the same but slows every coroutine down.
 """
 from __future__ import annotations
 
 import asyncio.events as _events
+import gc
 import os
 import time
 from typing import Optional
 
 _INSTALLED = False
+_GC_HOOK = None  # the gc.callbacks entry of install()
 
 
 def _name(handle) -> str:
@@ -39,14 +44,22 @@ def _name(handle) -> str:
 def install(metrics, threshold_ms: float, where: str = "") -> bool:
     """Watch every loop of this process (``where`` labels it: the replica parent's watch hub
     or a shard worker); False when already installed or disabled."""
-    global _INSTALLED
+    global _INSTALLED, _GC_HOOK
     if _INSTALLED or threshold_ms <= 0:
         return False
     threshold = threshold_ms / 1000.0
     orig = _events.Handle._run
     clock = time.perf_counter
+    gc_s = [0.0, 0.0]  # [GC seconds so far, start of the running collection]
+
+    def _gc_clock(phase, _info):
+        if phase == "start":
+            gc_s[1] = clock()
+        else:
+            gc_s[0] += clock() - gc_s[1]
 
     def _run(self):
+        g0 = gc_s[0]
         t0 = clock()
         orig(self)
         d = clock() - t0
@@ -55,10 +68,13 @@ def install(metrics, threshold_ms: float, where: str = "") -> bool:
                 labels = {"name": _name(self), "where": where}
                 metrics.inc("slow_callbacks", labels=labels)
                 metrics.inc("slow_callback_seconds", d, labels=labels)
+                metrics.inc("slow_callback_gc_seconds", gc_s[0] - g0, labels=labels)
                 metrics.observe_seconds("slow_callback", d)
             except Exception:  # noqa: BLE001 - never let the watch break the loop it watches
                 pass
 
+    gc.callbacks.append(_gc_clock)
+    _GC_HOOK = _gc_clock
     _events.Handle._run = _run
     _INSTALLED = True
     return True

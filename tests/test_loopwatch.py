@@ -2,10 +2,21 @@
 --diag-slow-callback-ms`` — which callbacks held a process's loop at least the threshold."""
 import asyncio
 import asyncio.events
+import gc
 import time
+
+import pytest
 
 from nexus_supervisor_amd.obs import loopwatch
 from nexus_supervisor_amd.obs.metrics import Metrics
+
+
+@pytest.fixture(autouse=True)
+def _drop_gc_hook(monkeypatch):
+    monkeypatch.setattr(loopwatch, "_GC_HOOK", None)
+    yield
+    if loopwatch._GC_HOOK in gc.callbacks:
+        gc.callbacks.remove(loopwatch._GC_HOOK)
 
 
 def test_slow_callbacks_are_counted_by_name(monkeypatch):
@@ -40,6 +51,37 @@ def test_slow_callbacks_are_counted_by_name(monkeypatch):
     secs = sum(m.counters["slow_callback_seconds"].values())
     assert 0.007 < secs < 0.5
     assert m.histogram("slow_callback").total == 2
+
+
+def test_gc_time_inside_slow_callbacks(monkeypatch):
+    monkeypatch.setattr(asyncio.events.Handle, "_run", asyncio.events.Handle._run)
+    monkeypatch.setattr(loopwatch, "_INSTALLED", False)
+    m = Metrics("t")
+    assert loopwatch.install(m, 1.0, "parent")
+
+    def collects():
+        junk = []
+        for _ in range(20000):  # reference cycles for the collector to walk
+            a = []
+            a.append(a)
+            junk.append(a)
+        del junk
+        gc.collect()
+        time.sleep(0.002)
+
+    def plain():
+        time.sleep(0.002)
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        loop.call_soon(collects)
+        loop.call_soon(plain)
+        await asyncio.sleep(0.01)
+
+    asyncio.run(go())
+    gc_ms = {dict(k)["name"].rsplit(".", 1)[-1]: v * 1e3 for k, v in m.counters["slow_callback_gc_seconds"].items()}
+    assert gc_ms["collects"] > 0.0
+    assert gc_ms["plain"] == 0.0
 
 
 def test_install_from_env(monkeypatch):
@@ -77,3 +119,13 @@ def test_names_never_raise():
             raise RuntimeError("boom")
 
     assert loopwatch._name(H(Broken())) == "?"
+
+
+def test_bench_slow_callback_rows_carry_gc_time():
+    from nexus_supervisor_amd.bench.runner import _slow_callbacks
+
+    k = frozenset({"name": "task:WatchHub._pump", "where": "parent"}.items())
+    before = {"slow_callbacks": {k: 2.0}, "slow_callback_seconds": {k: 0.002}, "slow_callback_gc_seconds": {k: 0.0}}
+    after = {"slow_callbacks": {k: 5.0}, "slow_callback_seconds": {k: 0.0062}, "slow_callback_gc_seconds": {k: 0.003}}
+    (row,) = _slow_callbacks(before, after)
+    assert row == {"where": "parent", "name": "task:WatchHub._pump", "count": 3, "total_ms": 4.2, "gc_ms": 3.0}
