@@ -81,6 +81,11 @@ def parse_args(argv=None):
     ap.add_argument("--hbm-shape", choices=("default-pod", "termination-message"), default="default-pod",
                     help="synthetic HBM-OOM failures: a default pod (empty termination message, the real HIP OOM "
                          "text in the container log, read over pods/log) or the text in the termination message")
+    ap.add_argument("--workload", choices=("lifecycle", "failures"), default="lifecycle",
+                    help="lifecycle (default): every failed run is replaced by a new run that goes Pending -> "
+                         "scheduled -> Running with the kubelet's Events (its Started is a ToRunning decision: "
+                         "checkpoint read + RUNNING upsert), failures carry their Job / Event traffic and Events "
+                         "expire; failures: the round-4 shape (failure traffic only, new runs never start)")
     ap.add_argument("--diag-slow-callback-ms", type=float, default=0.0,
                     help="diagnostic: count the event-loop callbacks (parent and workers) that run at least this "
                          "long and list the probe's in latency_at_rate.slow_callbacks (obs/loopwatch.py)")
@@ -230,36 +235,47 @@ def main(argv=None) -> int:
                       conditional_update=args.conditional_update, cql_lwt_latency_us=args.cql_lwt_latency_us,
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
-                      pregen=not args.no_pregen, cluster=cluster,
+                      pregen=not args.no_pregen, cluster=cluster, run_starts=args.workload == "lifecycle",
                       pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz)
     res = asyncio.run(run_rank(cfg, barrier_sync, share))
 
     elapsed = res["elapsed"]
     rb = res.get("readback") or {}
+    wobj = res.get("watch_objects_per_failure")
     stats = torch.tensor([elapsed, float(res["events"]), float(res["errors"]), float(res["wrong_stage"]),
-                          float(rb.get("checked", 0)), float(rb.get("wrong", 0))], dtype=torch.float64, device=device)
-    lat = torch.tensor(res["latencies_ms"], dtype=torch.float64, device=device)
+                          float(rb.get("checked", 0)), float(rb.get("wrong", 0)), float(res.get("starts", 0)),
+                          float(res.get("failures", 0)), float(wobj if wobj is not None else 0.0)],
+                         dtype=torch.float64, device=device)
+
+    def gather_all(values):
+        """Every rank's latency samples, concatenated (ranks hold different counts)."""
+        t = torch.tensor(values, dtype=torch.float64, device=device)
+        if dist is None:
+            return t.cpu()
+        sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([t.numel()], dtype=torch.int64, device=device))
+        mlen = max(1, int(max(x.item() for x in sizes)))
+        padded = torch.full((mlen,), float("nan"), dtype=torch.float64, device=device)
+        padded[: t.numel()] = t
+        gathered = [torch.empty(mlen, dtype=torch.float64, device=device) for _ in range(world)]
+        dist.all_gather(gathered, padded)
+        cat = torch.cat(gathered)
+        return cat[~torch.isnan(cat)].cpu()
+
+    allat = gather_all(res["latencies_ms"])
+    start_lat = gather_all(res.get("start_latencies_ms") or [])
     if dist is not None:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = stats.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([lat.numel()], dtype=torch.int64, device=device))
-        mlen = int(max(s.item() for s in sizes))
-        padded = torch.full((mlen,), float("nan"), dtype=torch.float64, device=device)
-        padded[: lat.numel()] = lat
-        gathered = [torch.empty(mlen, dtype=torch.float64, device=device) for _ in range(world)]
-        dist.all_gather(gathered, padded)
-        allat = torch.cat(gathered)
-        allat = allat[~torch.isnan(allat)]
         max_elapsed, total_events, total_errors = mx[0].item(), sm[1].item(), sm[2].item()
         wrong_stage, rb_checked, rb_wrong = sm[3].item(), sm[4].item(), sm[5].item()
+        total_starts, total_failures, watch_objects = sm[6].item(), sm[7].item(), sm[8].item() / world
     else:
-        allat = lat
         max_elapsed, total_events, total_errors = elapsed, float(res["events"]), float(res["errors"])
         wrong_stage, rb_checked, rb_wrong = float(res["wrong_stage"]), float(rb.get("checked", 0)), float(rb.get("wrong", 0))
-    allat = allat.cpu()
+        total_starts, total_failures, watch_objects = float(res.get("starts", 0)), float(res.get("failures", 0)), wobj
     mine = {"rank": rank, "supervisor_cpu_us_per_event": (res.get("cpu") or {}).get("supervisor_cpu_us_per_event"),
             "harness_bound": _harness_bound(res.get("cpu") or {})}
     per_rank = [mine]
@@ -270,6 +286,8 @@ def main(argv=None) -> int:
     if rank == 0:
         eps = total_events / max_elapsed if max_elapsed > 0 else 0.0
         q = torch.quantile(allat, torch.tensor([0.5, 0.99], dtype=torch.float64)).tolist() if allat.numel() else [None, None]
+        qs = (torch.quantile(start_lat, torch.tensor([0.5, 0.99], dtype=torch.float64)).tolist()
+              if start_lat.numel() else [None, None])
         hb = dict(_harness_bound(res.get("cpu") or {}))
         bound_ranks = [r["rank"] for r in per_rank if r["harness_bound"]["bound"]]
         if world > 1:
@@ -281,8 +299,10 @@ def main(argv=None) -> int:
             print(f"[bench] WARNING: harness-bound run ({hb['limit_util']}): {hb['note']}", file=sys.stderr, flush=True)
         out = {
             "metric": METRIC,
+            # pod failures decided and acknowledged per second (each brings its replacement
+            # run's start: decisions_per_s counts both)
             "value": round(eps, 2),
-            "unit": "events/s",
+            "unit": "pod-failures/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -295,6 +315,16 @@ def main(argv=None) -> int:
             # latency of the timed (saturating) steps: 1000-failure bursts queue behind each other
             "p50_ms": round(q[0], 3) if q[0] is not None else None,
             "p99_ms": round(q[1], 3) if q[1] is not None else None,
+            # every decision the timed steps carried: the failures plus the replacement runs'
+            # ToRunning (Started Event -> checkpoint read + RUNNING upsert, the reference's most
+            # frequent decision)
+            "decisions_per_s": round((total_failures + total_starts) / max_elapsed, 2) if max_elapsed > 0 else 0.0,
+            "starts_per_s": round(total_starts / max_elapsed, 2) if max_elapsed > 0 else 0.0,
+            "start_p50_ms": round(qs[0], 3) if qs[0] is not None else None,
+            "start_p99_ms": round(qs[1], 3) if qs[1] is not None else None,
+            # Events / Pods / Jobs the namespace's watches carried per pod failure (apiserver
+            # resourceVersion growth over the timed steps, the supervisor's DELETEs included)
+            "watch_objects_per_failure": round(watch_objects, 2) if watch_objects else None,
             # open-loop latency at the north-star churn rate (1000 pod-fail events/min), rank 0
             "latency_at_rate": res.get("probe"),
             "errors": int(total_errors),
@@ -318,6 +348,7 @@ def main(argv=None) -> int:
                 "shard_label": (not args.no_shard_label) if cluster == "shared" and world > 1 else None,
                 "concurrent_jobs_per_rank": args.jobs,
                 "events_per_step_per_rank": args.events,
+                "workload": args.workload,
                 "transport": args.transport,
                 "profile": args.profile,
                 "store": res.get("store"),

@@ -22,7 +22,7 @@
 // xGMI: at discovery each GPU's hive id and physical links (peer BDF, type, bit rate,
 // max bandwidth) are read with amdsmi_get_link_metrics; the health poll refreshes the
 // link status and the per-link read/write counters.  That is the real fabric the
-// supervised job's RCCL ring ran on.
+// supervised job's RCCL ring ran on, recorded in the trace row.
 //
 // This header holds no Python types: the pybind module (gpu_monitor.cpp) converts the
 // plain snapshots, and the TSan self-test (monitor_selftest.cpp) drives the same class

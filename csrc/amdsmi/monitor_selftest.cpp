@@ -1,5 +1,5 @@
-// TSan / ASan self-test of the native GPU monitor (VERDICT r1 "Sanitize the in-process
-// native code"): the real sampler and event-listener threads of monitor_core.hpp run
+// TSan / ASan self-test of the native GPU monitor (the in-process native code runs
+// threads next to the interpreter, so it is sanitized): the real sampler and event-listener threads of monitor_core.hpp run
 // against the stub amd-smi (amdsmi_stub.cpp) and a fake procfs tree while the main
 // thread hammers every reader (snapshot, devices, history, peak_between, drain_events,
 // inject_event) and the test hooks mutate the stub.  Built with -fsanitize=thread (and

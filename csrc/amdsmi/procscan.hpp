@@ -1,6 +1,6 @@
 // Per-process GPU attribution sources that do not depend on amd-smi's process list
-// (on the MI355X box amd-smi reported host-namespace PIDs with
-// zero VRAM, so PID→GPU never matched).  Three sources, all plain file reads:
+// (on an MI355X box amd-smi reported host-namespace PIDs with zero VRAM, so PID→GPU
+// never matched from its process list alone).  Three sources, all plain file reads:
 //
 //   * DRM fdinfo (`/proc/<pid>/fdinfo/<fd>` of an amdgpu render node): `drm-pdev`
 //     (PCI BDF of the GPU) and `drm-memory-vram` / `drm-total-vram` (KiB) per DRM

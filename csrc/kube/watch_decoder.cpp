@@ -1724,6 +1724,7 @@ PyTypeObject DecoderType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 extern "C" PyObject* nexus_json_dumps(PyObject*, PyObject* args, PyObject* kw);  // json_encode.cpp
 extern "C" int nexus_register_histogram(PyObject* m);                            // histogram.cpp
 extern "C" PyObject* nexus_apply_lines(PyObject*, PyObject* args);               // informer_apply.cpp
+extern "C" int nexus_register_shared_bucket(PyObject* m);                        // shared_bucket.cpp
 
 namespace {
 
@@ -1779,7 +1780,7 @@ PyMODINIT_FUNC PyInit__kube_native(void) {
   PyModule_AddObject(m, "ShardRouter", reinterpret_cast<PyObject*>(&RouterType));
   Py_INCREF(&SplitterType);
   PyModule_AddObject(m, "WatchSplitter", reinterpret_cast<PyObject*>(&SplitterType));
-  if (nexus_register_histogram(m) < 0) {
+  if (nexus_register_histogram(m) < 0 || nexus_register_shared_bucket(m) < 0) {
     Py_DECREF(m);
     return nullptr;
   }

@@ -32,7 +32,7 @@
 //   (/sim/apply also takes {"type":"LOG","object":{"namespace","pod","container","text"}}:
 //    a failed container's log, never sent to watchers, dropped with its pod)
 //
-// Pricing the API server: --api-latency-us answers every object
+// Pricing the API server (a real apiserver is not free): --api-latency-us answers every object
 // request (GET / DELETE / POST / PUT / PATCH; not LIST / WATCH) that long after it was
 // applied, in order per connection (an etcd write + admission); --write-qps caps mutating
 // requests with a token bucket and answers the excess 429 + Retry-After, as API Priority and

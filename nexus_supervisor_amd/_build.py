@@ -77,7 +77,8 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
         "kube_native": {
             "out": os.path.join(ext_dir, "_kube_native" + EXT),
             "srcs": [os.path.join(CSRC, "kube", "watch_decoder.cpp"), os.path.join(CSRC, "kube", "json_encode.cpp"),
-                     os.path.join(CSRC, "kube", "histogram.cpp"), os.path.join(CSRC, "kube", "informer_apply.cpp")],
+                     os.path.join(CSRC, "kube", "histogram.cpp"), os.path.join(CSRC, "kube", "informer_apply.cpp"),
+                     os.path.join(CSRC, "kube", "shared_bucket.cpp")],
             "deps": [],
             "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, "-shared", "-fPIC",
                                       f"-I{sysconfig.get_paths()['include']}", *srcs, "-o", out],

@@ -226,6 +226,8 @@ class ShardedApplication:
         self.metrics = metrics or Metrics(cfg.observability.statsd_name, {"version": __version__})
         self.kube = kube
         self.pool = WorkerPool(cfg, report_decisions=report_decisions, log_dir=log_dir)
+        if kube is not None and hasattr(kube, "apply_config") and not getattr(kube, "flow_configured", False):
+            kube.apply_config(cfg, self.metrics, self.pool.qps_schedule)
         self.supervisor = _SupervisorFacade(self)
         self.merged_metrics = self.metrics
         self.store = None
@@ -304,7 +306,7 @@ class ShardedApplication:
             if self.kube is None:
                 from .kube.client import KubeClient
 
-                self.kube = KubeClient.for_config(cfg, self.metrics)
+                self.kube = KubeClient.for_config(cfg, self.metrics, schedule=self.pool.qps_schedule)
             self.hub = WatchHub(cfg, self.kube, self.pool.count, self.pool.send_data, self.pool.data_buffered,
                                 self.pool.data_drain, metrics=self.metrics)
             self.pool.on_restart = lambda _index: self.hub.resync()
@@ -319,7 +321,7 @@ class ShardedApplication:
             if self.kube is None:
                 from .kube.client import KubeClient
 
-                self.kube = KubeClient.for_config(cfg, self.metrics)
+                self.kube = KubeClient.for_config(cfg, self.metrics, schedule=self.pool.qps_schedule)
         if lease_mode:
             self.shard_leases = make_shard_leases(cfg, self.kube, self.set_shards, self.metrics,
                                                   on_renewed=self._shard_holds)
@@ -337,7 +339,7 @@ class ShardedApplication:
         if self.kube is None and cfg.sharding.shard_label and cfg.sharding.shards > 1:
             from .kube.client import KubeClient
 
-            self.kube = KubeClient.for_config(cfg, self.metrics)
+            self.kube = KubeClient.for_config(cfg, self.metrics, schedule=self.pool.qps_schedule)
         self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
 
     def _shard_holds(self, until) -> None:

@@ -12,9 +12,11 @@ upstream of the supervisor).  A small control API drives it:
                                                     one workload per listed replica shard
                                                     (N live runs each, + rows) and P
                                                     pre-generated steps of E failures each
-``POST /bench/step {"events": E, "shard": k}``    fail E runs of shard k, replace them;
+``POST /bench/step {"events": E, "shard": k}``    fail E runs of shard k, start the previous
+                                                    step's new runs, create E new ones;
                                                     ``{"rids": [...], "t_push": monotonic,
-                                                    "expected": {rid: stage}}``
+                                                    "expected": {rid: stage}, "started": [...],
+                                                    "start_expected": {rid: "RUNNING"}}``
 ``POST /bench/probe {"n": N, "rate_per_min": R, "seed": s, "shard": k}``
                                                     the open-loop probe: N one-failure steps
                                                     at Poisson arrivals, ``{"steps": [...]}``
@@ -66,13 +68,7 @@ async def amain(args) -> None:
             return t if t is not None else time.monotonic()
         t = time.monotonic()
         for i, (etype, obj) in enumerate(events):
-            if etype == "LOG":
-                api.set_pod_log(obj["namespace"], obj["pod"], obj["container"], obj["text"])
-                continue
-            if etype == "ADDED":
-                api.create(obj, copy_obj=False)
-            else:
-                api.update(obj, copy_obj=False)
+            api.apply(etype, obj, copy_obj=False)
             if i % 256 == 255:
                 await asyncio.sleep(0)  # keep serving DELETEs / watch writes during a burst
         return t
@@ -106,7 +102,8 @@ async def amain(args) -> None:
             wl = Workload(p.get("jobs", 10_000), rank=k if len(indexes) > 1 else p.get("rank", 0),
                           world=p.get("world", 1), seed=p.get("seed", 0),
                           hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=n_shards, shard_index=k,
-                          shard_label=p.get("shard_label") or "", hbm_shape=p.get("hbm_shape") or "termination-message")
+                          shard_label=p.get("shard_label") or "", hbm_shape=p.get("hbm_shape") or "termination-message",
+                          run_starts=bool(p.get("run_starts", True)))
             objs, rows = wl.initial()
             await write_rows(rows)
             await apply([("ADDED", o) for o in objs])
@@ -119,9 +116,10 @@ async def amain(args) -> None:
             pregen, events = int(p.get("pregen", 0)), int(p.get("events", 0))
             if pregen and events and simctl is not None:
                 for _ in range(pregen):
-                    failed, traffic, rows = wl.step(events)
-                    await write_rows(rows)
-                    sh.pregen.append((events, failed, encode_events(traffic)))
+                    st = wl.step(events)
+                    await write_rows(st.rows)
+                    sh.pregen.append((events, st, encode_events(st.traffic)))
+                    st.traffic = None  # encoded: only the ids and expected stages are kept
         # the simulated cluster holds the same 10k-run heap as the supervisor: keep it out
         # of full collections so the generator never paces the measured process
         gc.collect()
@@ -132,9 +130,9 @@ async def amain(args) -> None:
     async def prepare(wl, events: int):
         # generate the next step's traffic and insert its replacement runs' rows ahead of
         # time (overlapped with the supervisor working on the current step)
-        failed, traffic, rows = wl.step(events)
-        await write_rows(rows)
-        return failed, traffic
+        st = wl.step(events)
+        await write_rows(st.rows)
+        return st
 
     async def h_step(req):
         cp = state.pop("cprof", None)
@@ -179,8 +177,10 @@ async def amain(args) -> None:
                 await simctl.apply_raw(sh.pregen.popleft()[2])
             nxt, sh.next = sh.next, None
             if nxt is not None:
-                _f, stale = await nxt[1]
-                await apply([(e, o) for e, o in stale if e == "ADDED" and o.get("kind") in ("Pod", "Job")])
+                # its runs' starts and failures are part of the workload's state now: the
+                # cluster must see them (their decisions are absorbed in the settle below)
+                stale = await nxt[1]
+                await apply(stale.traffic)
         await asyncio.sleep(float(p.get("settle_s", 2.0)))
 
         async def one(i):
@@ -203,9 +203,9 @@ async def amain(args) -> None:
         wl = sh.wl
         queue = sh.pregen
         if queue and queue[0][0] == events and sh.next is None:
-            _, failed, body = queue.popleft()
+            _, st, body = queue.popleft()
             doc = await simctl.apply_raw(body)
-            return {"rids": failed, "t_push": doc["t_push"], "expected": {r: wl.expected[r] for r in failed}}
+            return st.doc(doc["t_push"])
         if queue:
             # a step of another size (latency probe): the pre-generated steps' runs are live
             # in the workload already, so they must exist in the cluster before we diverge
@@ -213,17 +213,18 @@ async def amain(args) -> None:
                 await simctl.apply_raw(queue.popleft()[2])
         nxt, sh.next = sh.next, None
         if nxt is not None and nxt[0] == events:
-            failed, traffic = await nxt[1]
+            st = await nxt[1]
         else:
             if nxt is not None:
-                # a prefetched step of another size is dropped: its replacement runs are
-                # already live in the workload, so they must exist in the cluster too
-                _f, stale = await nxt[1]
-                await apply([(e, o) for e, o in stale if e == "ADDED" and o.get("kind") in ("Pod", "Job")])
-            failed, traffic = await prepare(wl, events)
-        t_push = await apply(traffic)
+                # a prefetched step of another size is dropped: its starts and failures are
+                # already part of the workload's state, so the cluster must see them too
+                # (untimed: nobody waits for their decisions)
+                stale = await nxt[1]
+                await apply(stale.traffic)
+            st = await prepare(wl, events)
+        t_push = await apply(st.traffic)
         sh.next = (events, asyncio.ensure_future(prepare(wl, events)))
-        return {"rids": failed, "t_push": t_push, "expected": {r: wl.expected[r] for r in failed}}
+        return st.doc(t_push)
 
     async def h_stats(req):
         if simctl is not None:

@@ -1,7 +1,7 @@
 """Per-rank benchmark driver (see ``bench.py``).
 
-Harness protocol: ``start()``, ``step(events) -> (failed run ids, push time)``,
-``supervisor``, ``stop()``.  Times are ``time.monotonic()`` (CLOCK_MONOTONIC —
+Harness protocol: ``start()``, ``step(events) -> {"rids", "t_push", "expected", "started",
+"start_expected"}``, ``supervisor``, ``stop()``.  Times are ``time.monotonic()`` (CLOCK_MONOTONIC —
 comparable across the rank and cluster processes on one host).
 """
 from __future__ import annotations
@@ -60,6 +60,9 @@ class BenchConfig:
     # how the synthetic HBM-OOMs look: "default-pod" (empty termination message, the HIP text
     # in the container log: the supervisor reads pods/log) or "termination-message"
     hbm_shape: str = "default-pod"
+    # new runs go Pending -> Running with the kubelet's Events (a ToRunning decision each);
+    # False: the failure-only shape of round 4
+    run_starts: bool = True
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -85,24 +88,34 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
     return sc
 
 
-class Tracker:
-    """Decision hook: checkpoint-ack time per run; latency = ack − pod-fail push.
+_RUNNING = "RUNNING"
 
-    Several steps may be in flight at once (the generator runs ahead of the
-    supervisor, as a live cluster would); each step completes when every run it
-    failed has been acknowledged by the store.  Every acknowledged decision is checked
-    against the stage the workload expects for that failure (``wrong_stage``), and the
-    timed runs are remembered for the read-back check against the store afterwards."""
+
+class Tracker:
+    """Decision hook: checkpoint-ack time per run; latency = ack − push.
+
+    Two decisions are tracked per step: each failed run's failure decision (the north-star
+    latency, pod-fail → checkpoint) and each started run's ``ToRunning`` (Started →
+    ``RUNNING``).  A report is matched to one or the other by the stage it wrote, so a run
+    started in one step and failed in a later one — both possibly in flight — is tracked
+    twice.  Several steps may be in flight at once (the generator runs ahead of the
+    supervisor, as a live cluster would); each step completes when every decision it
+    carries has been acknowledged by the store.  Every acknowledged decision is checked
+    against the stage the workload expects (``wrong_stage``), and the timed runs are
+    remembered for the read-back check against the store afterwards."""
 
     def __init__(self):
-        self.acks: Dict[str, Tuple[float, str, Optional[str]]] = {}
-        self.owner: Dict[str, "StepState"] = {}
-        self.latencies: List[float] = []
+        self.acks: Dict[Tuple[str, bool], Tuple[float, str, Optional[str], Any]] = {}
+        self.owner: Dict[Tuple[str, bool], "StepState"] = {}
+        self.latencies: List[float] = []        # failures: pod-fail push → checkpoint ack
+        self.start_latencies: List[float] = []  # starts: Started push → RUNNING ack
         self.errors = 0
         self.wrong_stage = 0
         self.wrong_examples: List[Tuple[str, Optional[str], str]] = []
-        self.checked: Dict[str, str] = {}  # timed run → expected stage (read-back)
+        self.checked: Dict[str, str] = {}  # timed run → expected final stage (read-back)
         self.record = False
+        self.failures = 0  # recorded decisions acknowledged
+        self.starts = 0
         # recorded decisions' push→ack decomposition (ms): api (push → hub read), hub (→ worker
         # frame), feed (→ decoded), dispatch (→ handler), classify (handler → enqueue, with any
         # log-tail wait), queue (→ dequeue), actuate (→ checkpoint ack)
@@ -119,30 +132,45 @@ class Tracker:
     def report(self, rid: str, outcome: str, ack: Optional[float], stage: Optional[str], x=None) -> None:
         # the metric is pod-fail → checkpoint *write ack* (the Job DELETE follows the write)
         t = ack or time.monotonic()
-        st = self.owner.pop(rid, None)
+        key = (rid, stage == _RUNNING)
+        st = self.owner.pop(key, None)
         if st is None:
-            self.acks[rid] = (t, outcome, stage, x)  # ack raced ahead of the step response
+            # raced ahead of the step response (or a duplicate: the pod-status rule's ToRunning
+            # behind the Started Event's) — keep the applied one
+            prev = self.acks.get(key)
+            if prev is None or prev[1] != "applied":
+                self.acks[key] = (t, outcome, stage, x)
             return
-        st.settle(self, rid, t, outcome, stage, x)
+        st.settle(self, key, t, outcome, stage, x)
 
-    def arm(self, rids: List[str], t_push: float, expected: Optional[Dict[str, str]] = None) -> "StepState":
-        st = StepState(set(rids), t_push, self.record, expected or {})
-        if self.record and expected:
-            self.checked.update(expected)
-        for rid in rids:
-            a = self.acks.pop(rid, None)
+    def arm(self, rids: List[str], t_push: float, expected: Optional[Dict[str, str]] = None,
+            started: Optional[List[str]] = None, start_expected: Optional[Dict[str, str]] = None) -> "StepState":
+        expected = dict(expected or {})
+        keys = [(r, False) for r in rids]
+        for r in started or ():
+            keys.append((r, True))
+            expected.setdefault(r, (start_expected or {}).get(r, _RUNNING))
+        st = StepState(set(keys), t_push, self.record, expected or {})
+        if self.record:
+            for r in started or ():
+                self.checked[r] = _RUNNING
+            for r in rids:
+                if r in expected:
+                    self.checked[r] = expected[r]
+        for key in keys:
+            a = self.acks.pop(key, None)
             if a is not None:
-                st.settle(self, rid, *a)
+                st.settle(self, key, *a)
             else:
-                self.owner[rid] = st
+                self.owner[key] = st
         if not st.waiting:
             st.done.set()
         return st
 
     def abandon(self, st: "StepState") -> None:
         self.errors += len(st.waiting)
-        for rid in st.waiting:
-            self.owner.pop(rid, None)
+        for key in st.waiting:
+            self.owner.pop(key, None)
         st.waiting.clear()
         st.done.set()
 
@@ -157,9 +185,10 @@ class StepState:
         self.expected = expected
         self.done = asyncio.Event()
 
-    def settle(self, tr: Tracker, rid: str, t: float, outcome: str, stage: Optional[str] = None, x=None) -> None:
-        self.waiting.discard(rid)
-        want = self.expected.get(rid)
+    def settle(self, tr: Tracker, key, t: float, outcome: str, stage: Optional[str] = None, x=None) -> None:
+        self.waiting.discard(key)
+        rid, start = key
+        want = _RUNNING if start else self.expected.get(rid)
         if outcome != "applied":
             tr.errors += 1
         else:
@@ -169,11 +198,16 @@ class StepState:
                     tr.wrong_examples.append((rid, stage, want))
             if self.record:
                 total = (t - self.t_push) * 1000.0
-                tr.latencies.append(total)
-                if x is not None and len(x) >= 6:
-                    hub, feed, dec, cls, que, r2c = x[:6]
-                    tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
-                                     (t - r2c - dec) * 1e3, cls * 1e3, que * 1e3, (r2c - cls - que) * 1e3))
+                if start:
+                    tr.starts += 1
+                    tr.start_latencies.append(total)
+                else:
+                    tr.failures += 1
+                    tr.latencies.append(total)
+                    if x is not None and len(x) >= 6:
+                        hub, feed, dec, cls, que, r2c = x[:6]
+                        tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
+                                         (t - r2c - dec) * 1e3, cls * 1e3, que * 1e3, (r2c - cls - que) * 1e3))
         if not self.waiting:
             self.done.set()
 
@@ -186,7 +220,8 @@ class InProcHarness:
         from ..testing.inproc import InProcCluster
 
         self.wl = Workload(cfg.jobs, rank=cfg.rank, world=cfg.world, seed=cfg.seed,
-                           hip_oom_message=cfg.hip_oom_message or DEFAULT_HIP_OOM, shards=cfg.world, shard_index=cfg.rank)
+                           hip_oom_message=cfg.hip_oom_message or DEFAULT_HIP_OOM, shards=cfg.world, shard_index=cfg.rank,
+                           run_starts=cfg.run_starts)
         objs, rows = self.wl.initial()
         self.store = MemoryStore(rows)
         self.cluster = InProcCluster(sc, self.store, objs)
@@ -196,13 +231,14 @@ class InProcHarness:
         await self.cluster.start()
 
     async def step(self, events: int):
-        failed, traffic, rows = self.wl.step(events)
-        for r in rows:
+        st = self.wl.step(events)
+        for r in st.rows:
             self.store.rows[r.key] = r
         t = time.monotonic()
-        for etype, obj in traffic:
-            self.cluster.push(obj, etype)
-        return failed, t, {r: self.wl.expected[r] for r in failed}
+        for etype, obj in st.traffic:
+            if etype != "LOG":
+                self.cluster.push(obj, etype)
+        return st.doc(t)
 
     async def read_stages(self, algorithm: str, rids: List[str]) -> Dict[str, Optional[str]]:
         out = {}
@@ -265,8 +301,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             for _ in range(n):
                 while len(pending) >= cfg.inflight:
                     await finish(pending.pop(0))
-                failed, t_push, expected = await harness.step(cfg.events)
-                pending.append(tracker.arm(failed, t_push, expected))
+                doc = await harness.step(cfg.events)
+                pending.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
+                                           doc.get("start_expected")))
             for st in pending:
                 await finish(st)
 
@@ -293,6 +330,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         await run_steps(cfg.steps)
         barrier_sync()
         elapsed = time.perf_counter() - t0
+        timed = (tracker.failures, tracker.starts, list(tracker.start_latencies))
         step_done_ms = [round(1000.0 * (t - t0), 1) for t in done_at]
         cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3),
                "supervisor_max_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1)}
@@ -300,11 +338,17 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         for k in x1:
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
         s1 = await sim_stats() if s0 else None
+        watch_objects = None
         if s0 and s1:
             # shared cluster: the simulator serves every rank's failures
             n_ev = max(cfg.events * cfg.steps * (cfg.world if getattr(harness, "shared", False) else 1), 1)
             for k in ("requests", "loops", "sends"):
                 cpu[f"kubesim_{k}_per_event"] = round((s1.get(k, 0) - s0.get(k, 0)) / n_ev, 3)
+            # every committed change (ADDED / MODIFIED / DELETED of an Event, Pod or Job — the
+            # supervisor's own Job DELETEs and their pod GC included) bumps the resourceVersion:
+            # the watch objects the namespace carried per pod failure
+            if "rv" in s1 and "rv" in s0:
+                watch_objects = (s1["rv"] - s0["rv"]) / n_ev
             # event-loop phases (µs per pod failure): busy = everything but epoll_wait;
             # request includes apply (the synthetic traffic injection)
             for k in ("busy", "apply", "request", "recv", "flush"):
@@ -378,6 +422,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         await harness.stop()
         telemetry.stop()
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
+            "failures": timed[0], "starts": timed[1], "start_latencies_ms": timed[2],
+            "watch_objects_per_failure": watch_objects,
             "wrong_stage": tracker.wrong_stage, "wrong_examples": tracker.wrong_examples, "readback": readback,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
             "actuation": _actuation(sc),
@@ -394,6 +440,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
 
     saved, tracker.latencies = tracker.latencies, []
     saved_parts, tracker.parts = tracker.parts, []
+    saved_starts, tracker.start_latencies = tracker.start_latencies, []
     rate = cfg.probe_rate_per_min / 60.0
     rng = random.Random(0x5EED + cfg.seed + cfg.rank)
     loop = asyncio.get_running_loop()
@@ -407,15 +454,17 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         # the harness answers after the failure is delivered (hold): the driver's own work on
         # the answer stays out of the replica parent's loop while the line is in flight; the
         # decision's ack may arrive first (Tracker.report keeps it until the step is armed)
-        failed, t_push, expected = await (harness.step(1, hold) if hold else harness.step(1))
-        states.append(tracker.arm(failed, t_push, expected))
+        doc = await (harness.step(1, hold) if hold else harness.step(1))
+        states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
+                                  doc.get("start_expected")))
 
     played = getattr(harness, "probe", None)
     if played is not None:
         # the cluster process plays the schedule (same seed, same arrivals): one request for
         # the whole probe, every decision's ack kept by the tracker until its step is armed
         for doc in await played(cfg.probe_events, cfg.probe_rate_per_min, 0x5EED + cfg.seed + cfg.rank):
-            states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected") or {}))
+            states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
+                                      doc.get("start_expected")))
     for i in range(cfg.probe_events if played is None else 0):
         at += rng.expovariate(rate)
         delay = start + at - loop.time()
@@ -433,14 +482,19 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         except asyncio.TimeoutError:
             tracker.abandon(st)
     lat = sorted(tracker.latencies)
+    starts = sorted(tracker.start_latencies)
     parts = tracker.parts
-    tracker.latencies, tracker.parts = saved, saved_parts
+    tracker.latencies, tracker.parts, tracker.start_latencies = saved, saved_parts, saved_starts
     if not lat:
         return {"events": 0}
-    q = lambda p: lat[min(len(lat) - 1, int(round(p * (len(lat) - 1))))]  # noqa: E731
+    q = lambda p, v=lat: v[min(len(v) - 1, int(round(p * (len(v) - 1))))]  # noqa: E731
     out = {"rate_per_min": cfg.probe_rate_per_min, "arrivals": "poisson", "events": len(lat),
            "p50_ms": round(q(0.5), 3), "p90_ms": round(q(0.9), 3), "p99_ms": round(q(0.99), 3),
            "max_ms": round(lat[-1], 3)}
+    if starts:  # the replacement runs' Started → RUNNING at the same rate
+        out["starts"] = len(starts)
+        out["start_p50_ms"] = round(q(0.5, starts), 3)
+        out["start_p99_ms"] = round(q(0.99, starts), 3)
     if parts:
         out["delivery"] = decompose(parts)
     return out

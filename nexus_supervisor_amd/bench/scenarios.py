@@ -159,7 +159,7 @@ class Cluster:
         for rid in failed:
             self.clock.pushed[rid] = t
         for etype, obj in traffic:
-            (self.api.create if etype == "ADDED" else self.api.update)(obj, copy_obj=False)
+            self.api.apply(etype, obj, copy_obj=False)
         return failed
 
     async def final_stages(self, rids) -> Dict[str, Any]:
@@ -417,7 +417,7 @@ async def cfg3_gpu(profile: str, holders: int = 7, hold_gib: float = 30.0) -> Di
         c.clock.pushed[victim] = t
         # (workload pods are local rank 0 of an 8-way job: expected GPU = visible device 0)
         for etype, obj in traffic:
-            (c.api.create if etype == "ADDED" else c.api.update)(obj, copy_obj=False)
+            c.api.apply(etype, obj, copy_obj=False)
         await c.clock.wait([victim], 30)
         row = await c.store.read_checkpoint(c.wl.algorithm, victim)
         trace = json.loads(row.algorithm_failure_details) if row and (row.algorithm_failure_details or "").startswith("{") else {}

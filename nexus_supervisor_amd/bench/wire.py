@@ -99,7 +99,7 @@ class WireHarness:
                     "shard_indexes": list(range(cfg.world)) if self.shared else [cfg.rank],
                     "hip_oom_message": cfg.hip_oom_message,
                     "shard_label": self.sc.sharding.shard_label if self.shared else "",
-                    "hbm_shape": cfg.hbm_shape,
+                    "hbm_shape": cfg.hbm_shape, "run_starts": cfg.run_starts,
                     "pregen": cfg.warmup + cfg.steps if cfg.pregen else 0, "events": cfg.events}) as r:
                 r.raise_for_status()
                 await r.json()
@@ -146,14 +146,14 @@ class WireHarness:
     def supervisor(self):
         return self.app.supervisor
 
-    async def step(self, events: int, respond_after_ms: float = 0.0) -> Tuple[List[str], float, Dict[str, str]]:
+    async def step(self, events: int, respond_after_ms: float = 0.0) -> Dict[str, Any]:
+        """One step: ``{"rids", "t_push", "expected", "started", "start_expected"}``."""
         body = {"events": events, "shard": self.cfg.rank}
         if respond_after_ms:
             body["respond_after_ms"] = respond_after_ms
         async with self.http.post(self.ctl + "/bench/step", json=body) as r:
             r.raise_for_status()
-            doc = await r.json()
-        return doc["rids"], doc["t_push"], doc.get("expected") or {}
+            return await r.json()
 
     async def probe(self, n: int, rate_per_min: float, seed: int) -> List[Dict[str, Any]]:
         """The open-loop probe played by the cluster process (one request for all ``n``

@@ -306,10 +306,12 @@ class Classifier:
                 self._enrich(res, pods=[pod])
                 return [res]
             return []
-        # 7. running (backup for a lost "Started" event)
-        if status.get("phase") == "Running" and any(
-            (cs.get("state") or {}).get("running") for cs in (status.get("containerStatuses") or [])
-        ):
+        # 7. running (backup for a lost "Started" event): only the pod's transition to Running
+        # is a start — a pod already running when it is first listed (a restart's initial LIST
+        # of 10k live runs) is not, and its Started Event is replayed from the Event list; a
+        # pod being deleted is not starting either
+        if (old is not None and status.get("phase") == "Running" and not _running(old)
+                and not kube.meta(pod).get("deletionTimestamp") and _running(pod)):
             res = self._result(A.TO_RUNNING, "Started", "", inv, request_id, algorithm, "Running", F.NONE, "pod-status")
             return [res]
         return []
@@ -404,7 +406,7 @@ class Classifier:
 
     def _uses_gpu(self, pod, gev) -> bool:
         """HBM verdicts and GPU faults need a GPU: the pod requests ``gpu-resource-name``
-        or the evidence matched its own processes on one (VERDICT r3 weak #1)."""
+        or the evidence matched its own processes on one."""
         return oom_mod.gpu_involved(kube.gpu_request(pod, self.gpu.gpu_resource_name), gev)
 
     def _oom(self, pod, texts, terms) -> oom_mod.OomVerdict:
@@ -567,11 +569,27 @@ class Classifier:
         return any(self._uses_gpu(p, gev if p is pod else self._pod_ctx(p)[1]) for p in pods)
 
     def _apply_history(self, res: RunStatusAnalysisResult) -> None:
+        """Attach the run's non-decisive history and settle the cause of a Job's
+        BackoffLimitExceeded.  Called at the end of classification and again at actuation
+        (:meth:`late_enrich`), so the outcome is the same whichever watch stream — Pod or
+        Job / Event — delivered first."""
         prior = self.evidence.get(res.key)
         if prior:
             res.evidence["history"] = prior
             if res.failure_class == F.BACKOFF_LIMIT and any(p.get("kind") == "evicted" for p in prior):
                 res.failure_class = F.EVICTED
+        if (res.action == A.TO_FAIL_DEADLINE_EXCEEDED and res.reason == "BackoffLimitExceeded"
+                and self.rules.oom_fails_backoff_job):
+            # BackoffLimitExceeded of a run whose pods died of an OOM or were evicted: the run
+            # neither timed out nor ran out of retries of its own doing — write the row the
+            # pod-status OOM rule / ``evicted-policy: fail`` writes (FAILED with that cause).
+            # On by default; false keeps the reference's DEADLINE_EXCEEDED for
+            # BackoffLimitExceeded (supervisor.go:183-193), the class and evidence then go into
+            # the trace only (docs/PARITY.md)
+            msg = _BACKOFF_CAUSE.get(res.failure_class)
+            if msg is not None:
+                res.action = A.TO_FAIL_FATAL_ERROR
+                res.run_status_message = msg
 
     def late_enrich(self, res: RunStatusAnalysisResult, lookup: ObjectLookup) -> None:
         """Re-enrich a Job-level decision just before it is written.
@@ -603,18 +621,18 @@ class Classifier:
                     if v.kind:
                         res.evidence["oom"] = v.as_dict()
                         res.failure_class = F.HBM_OOM if v.kind == "hbm" else F.HOST_OOM
-                        if res.action == A.TO_FAIL_DEADLINE_EXCEEDED and self.rules.oom_fails_backoff_job:
-                            # BackoffLimitExceeded of a run whose pods died of an OOM: the run
-                            # failed, it did not time out (what the pod-status rule writes).
-                            # Off by default: the reference writes DEADLINE_EXCEEDED for
-                            # BackoffLimitExceeded (supervisor.go:183-193); the OOM is then in
-                            # the class and the trace only (docs/PARITY.md)
-                            res.action = A.TO_FAIL_FATAL_ERROR
-                            res.run_status_message = MSG_HBM_OOM if v.kind == "hbm" else MSG_HOST_OOM
         self._apply_history(res)
 
 
 _NO_EV: Dict[str, Any] = {}
+# BackoffLimitExceeded whose cause was found: the run's failure message per class
+_BACKOFF_CAUSE = {F.HBM_OOM: MSG_HBM_OOM, F.HOST_OOM: MSG_HOST_OOM, F.EVICTED: MSG_EVICTED}
+
+
+def _running(pod) -> bool:
+    """A container of the pod is running."""
+    st = pod.get("status") or {}
+    return any((cs.get("state") or {}).get("running") for cs in (st.get("containerStatuses") or []))
 _PLAIN_CLASSES = frozenset((F.NONE, F.SCHEDULING, F.DEADLINE, F.FATAL, F.BACKOFF_LIMIT))
 
 
@@ -629,7 +647,7 @@ def render_trace(res: RunStatusAnalysisResult, fmt: str = "auto", max_bytes: int
     ``json`` — message + reason + failure class + evidence; ``auto`` — json only
     when there is evidence beyond the message.
 
-    Bounded (``rules.trace-max-bytes``): per GPU the top
+    Bounded (``rules.trace-max-bytes``, the row is a text column): per GPU the top
     ``TRACE_TOP_PROCS`` processes by VRAM peak and the newest ``TRACE_MAX_EVENTS`` events,
     the xGMI fabric as a per-GPU summary (:func:`..gpu.topology.xgmi_from_evidence`), and a
     deterministic trimming ladder (:func:`_trim_trace`) when the document still exceeds

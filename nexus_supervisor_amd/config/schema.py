@@ -151,13 +151,18 @@ class RulesConfig:
     # cap on the trace column's size (bytes of JSON); larger documents are trimmed
     # deterministically (least telling detail first); 0 = no cap
     trace_max_bytes: int = field(default=8192, metadata=_k("trace-max-bytes"))
-    # a BackoffLimitExceeded Job decision whose pods died of an OOM found only at actuation
-    # time (late enrichment): true — write FAILED with the OOM cause, the same row the
-    # pod-status OOM rule writes, so the stage does not depend on which of the two
-    # decisions is applied first; false — keep the reference's DEADLINE_EXCEEDED for
-    # BackoffLimitExceeded (supervisor.go:183-193), the OOM class and evidence go into the
+    # a BackoffLimitExceeded Job decision whose pods died of an OOM or were evicted:
+    # true — write FAILED with the OOM / eviction cause, the same row the pod-status OOM
+    # rule and ``evicted-policy: fail`` write, so the stage does not depend on which
+    # decision is applied first; false — keep the reference's DEADLINE_EXCEEDED for
+    # BackoffLimitExceeded (supervisor.go:183-193), the class and evidence go into the
     # trace only (docs/PARITY.md)
     oom_fails_backoff_job: bool = field(default=True, metadata=_k("oom-fails-backoff-job"))
+    # a Job's BackoffLimitExceeded / PodFailurePolicy says one of its pods failed, but Pods
+    # and Jobs (and Events) arrive on separate watch streams: when no cached pod of the Job
+    # shows that failure yet, wait this long for the pod's update before the decision is
+    # written, so its cause (OOM, eviction, GPU) does not depend on stream order; 0 = off
+    job_pod_settle: float = field(default=1.0, metadata=_k("job-pod-settle", "duration"))
 
 
 @dataclass

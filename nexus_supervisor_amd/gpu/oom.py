@@ -67,6 +67,14 @@ HBM_PATTERNS = [
     re.compile(r"HSA_STATUS_ERROR_OUT_OF_RESOURCES", re.I),
     re.compile(r"\bGPU\b[^\n]{0,40}out of memory", re.I),
     re.compile(r"RESOURCE_EXHAUSTED: Out of memory while trying to allocate", re.I),
+    # runtime-check wordings: torch's C10_HIP_CHECK / C10_CUDA_CHECK ("HIP error: out of
+    # memory") when the HIP context, a hipBLAS handle or RCCL cannot allocate on a full GPU
+    re.compile(r"\b(?:HIP|CUDA) error: out of memory", re.I),
+    re.compile(r"hipErrorMemoryAllocation"),
+    # math-library allocation failures: hipBLAS(Lt) / cuBLAS workspace, rocBLAS, MIOpen
+    re.compile(r"\b(?:HIPBLAS|CUBLAS)(?:LT)?_STATUS_ALLOC_FAILED\b"),
+    re.compile(r"\brocblas_status_memory_error\b"),
+    re.compile(r"\bmiopenStatusAllocFailed\b"),
 ]
 HOST_PATTERNS = [
     re.compile(r"\bMemoryError\b"),
@@ -79,14 +87,18 @@ HOST_PATTERNS = [
     re.compile(r"Cannot allocate memory", re.I),
     re.compile(r"Memory cgroup out of memory", re.I),
     re.compile(r"\bOOMKilled\b"),
+    # torch's CPU allocator ("[enforce fail at alloc_cpu.cpp] . DefaultCPUAllocator: not
+    # enough memory: you tried to allocate N bytes")
+    re.compile(r"DefaultCPUAllocator: (?:not enough memory|can't allocate memory)", re.I),
 ]
 
 # Literal keywords every pattern of a list contains (lower-cased): a substring scan of the
 # lower-cased text rejects the common no-match message in well under a microsecond, where
 # the case-insensitive regex list costs ~10 µs per message.
-_HBM_KEYS = ("out of memory", "outofmemory", "hipmalloc", "out_of_resources")
+_HBM_KEYS = ("out of memory", "outofmemory", "hipmalloc", "out_of_resources", "memoryallocation",
+             "alloc_failed", "memory_error", "allocfailed")
 _HOST_KEYS = ("memoryerror", "bad_alloc", "cannot allocate memory", "out of memory", "oomkilled",
-              "unable to allocate", "outofmemoryerror")
+              "unable to allocate", "outofmemoryerror", "defaultcpuallocator")
 _TORCH_KEYS = ("total capacity", "tried to allocate")
 
 

@@ -407,7 +407,7 @@ def _links_of(g: Dict[str, Any]) -> Optional[List[Dict[str, Any]]]:
         if not peer or peer.startswith("ffff") or l.get("type") not in ("xgmi", None):
             continue
         # no cumulative read/write counters: they grow without bound and say nothing about
-        # a failure
+        # a failure, and the trace row is bounded
         out.append({"peer_bdf": peer, "peer": l.get("peer_index") if (l.get("peer_index") or 0) >= 0 else None,
                     "gbps": l.get("bit_rate_gbps"), "max_gbps": l.get("max_bandwidth_gbps")})
     return out

@@ -240,7 +240,7 @@ def xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, An
 
 
 def _xgmi_from_evidence(topo: Dict[str, Any], gpu_evidence: Dict[str, Any], gpus: List[Dict[str, Any]]) -> Dict[str, Any]:
-    """The measured fabric as a compact, bounded block: per GPU the
+    """The measured fabric as a compact, bounded block (the trace row has a size cap): per GPU the
     peers its xGMI ports reach — resolved to the peer's index when the peer is one of the
     node's enumerated GPUs (matched by PCI BDF in the native monitor), else its BDF — the
     link rate, and the port counts.  ``links_listed`` / ``links_up`` count those peer links

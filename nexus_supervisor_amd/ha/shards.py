@@ -32,7 +32,7 @@ makes that safe but leaves every replica but one idle.  Here the runs are split 
 Changes of the held set are reported through ``on_change(frozenset)``: the replica
 fences lost shards and replays gained ones (``Supervisor.set_shards``).
 
-Ownership is time-bounded (ADVICE r2 ha/shards.py:224): a shard
+Ownership is time-bounded, so a replica never acts on a shard it may have lost: a shard
 renewal that *started* at ``t0`` and succeeded is good until ``t0 + renew-deadline``;
 every API call (membership, renewals, observations, acquisitions) runs under a
 ``wait_for`` bounded by the time it may take, held shards are renewed concurrently, and

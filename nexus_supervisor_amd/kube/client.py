@@ -41,7 +41,7 @@ from ..informer.informer import ListWatch
 from ..models.kube import FINISHERS, PROJECTIONS, list_projection, watch_projection
 from ..obs import delivery as _delivery
 from .errors import ApiError, from_status
-from .flowcontrol import RetryPolicy, TokenBucket, retry_after
+from .flowcontrol import EVENT, MUTATE, READ, RetryPolicy, TokenBucket, retry_after
 
 
 def _native_decoder_available() -> bool:
@@ -324,37 +324,48 @@ class KubeClient:
         return self._fast
 
     # ------------------------------------------------------------------ flow control
-    def set_flow_control(self, qps: float, burst: int, max_retries: int = 10, metrics=None) -> None:
-        """``kube-qps`` / ``kube-burst`` / ``kube-max-retries`` of this process's share."""
-        self.limiter = TokenBucket(qps, burst)
+    def set_flow_control(self, qps: float, burst: int, max_retries: int = 10, metrics=None, shared=None) -> None:
+        """``kube-qps`` / ``kube-burst`` / ``kube-max-retries`` of this process's share
+        (``shared``: the replica's :class:`..flowcontrol.SharedSchedule` instead)."""
+        self.limiter = TokenBucket(qps, burst, shared=shared)
         self.retry = RetryPolicy(max_retries)
         if metrics is not None:
             self.metrics = metrics
 
     @classmethod
-    def for_config(cls, cfg, metrics=None, **kw) -> "KubeClient":
+    def for_config(cls, cfg, metrics=None, schedule=None, **kw) -> "KubeClient":
         """A client for ``cfg.kube-config-path`` with this process's share of the flow
-        control (a replica split into K shard-worker processes gives each 1/K)."""
+        control: the replica's shared budget when it has one (``schedule``, or the one a
+        shard worker inherited), else 1/K of it for each of K processes."""
         c = cls(KubeConfig.load(cfg.kube_config_path), **kw)
-        c.apply_config(cfg, metrics)
+        c.apply_config(cfg, metrics, schedule)
         return c
 
-    def apply_config(self, cfg, metrics=None) -> None:
-        from .flowcontrol import split
+    def apply_config(self, cfg, metrics=None, schedule=None) -> None:
+        from .flowcontrol import replica_schedule, split
 
-        parts = max(1, int(getattr(cfg.runtime, "worker_processes", 1) or 1))
-        qps, burst = split(cfg.kube_qps, cfg.kube_burst, parts)
-        self.set_flow_control(qps, burst, cfg.kube_max_retries, metrics)
+        if schedule is None:
+            schedule = replica_schedule(cfg)
+        if schedule is not None:
+            self.set_flow_control(cfg.kube_qps, cfg.kube_burst, cfg.kube_max_retries, metrics, shared=schedule)
+        else:
+            # K processes and no shared mapping: 1/K each, the hub parent counted as one more
+            parts = max(1, int(getattr(cfg.runtime, "worker_processes", 1) or 1))
+            if parts > 1:
+                parts += 1
+            qps, burst = split(cfg.kube_qps, cfg.kube_burst, parts)
+            self.set_flow_control(qps, burst, cfg.kube_max_retries, metrics)
         if self._reads is None:  # one connection per concurrent pods/log read
             self.read_connections = max(1, int(getattr(cfg.gpu, "log_tail_concurrency", self.read_connections)))
 
-    async def _admit(self, path: str, method: str = "GET") -> None:
+    async def _admit(self, path: str, method: str = "GET", timeout: Optional[float] = None) -> None:
         lim = self.limiter
         if lim.qps > 0 and not _exempt(path):
-            # reads (pods/log tails a decision waits for, LIST / WATCH) first, then mutations
-            # (background Job DELETEs, agent PATCHes), decision Events last
-            prio = 0 if method == "GET" else 2 if method == "POST" and path.endswith("/events") else 1
-            d = await lim.wait(prio)
+            # request classes (flowcontrol.CLASS_WEIGHTS): reads (pods/log tails a decision
+            # waits for, LIST / WATCH), mutations (background Job DELETEs, agent PATCHes),
+            # decision Events — each with a guaranteed share of the tokens
+            prio = READ if method == "GET" else EVENT if method == "POST" and path.endswith("/events") else MUTATE
+            d = await lim.wait(prio, timeout)
             if d > 0 and self.metrics is not None:
                 self.metrics.inc("kube_ratelimit_waits")
                 self.metrics.observe_seconds("kube_ratelimit_wait", d)
@@ -510,17 +521,23 @@ class KubeClient:
                 async for chunk in r.content.iter_any():
                     t_read = time.monotonic()
                     evs = decoder.feed(chunk)
-                    if evs:
-                        # hub-less replica: the chunk's read is both the "hub" and "feed" stamp
-                        current[kind] = (t_read, t_read, time.monotonic())
-                    for ev in evs:
-                        obj = ev.get("object") or {}
-                        if obj.get("kind") is None:
-                            obj["kind"] = kind
-                        yield ev.get("type", ""), obj
-                        n += 1
-                        if n % 64 == 0:
-                            await asyncio.sleep(0)  # let workers interleave with a large chunk
+                    if not evs:
+                        continue
+                    # hub-less replica: the chunk's read is both the "hub" and "feed" stamp
+                    current[kind] = (t_read, t_read, time.monotonic())
+                    try:
+                        for ev in evs:
+                            obj = ev.get("object") or {}
+                            if obj.get("kind") is None:
+                                obj["kind"] = kind
+                            yield ev.get("type", ""), obj
+                            n += 1
+                            if n % 64 == 0:
+                                await asyncio.sleep(0)  # let workers interleave with a large chunk
+                    finally:
+                        # stamps belong to this chunk only: a later resync / timer / log-fetch
+                        # submit must not pick them up
+                        current.pop(kind, None)
                 return
             loads = json.loads
             buf = b""
@@ -605,7 +622,14 @@ class KubeClient:
         reads = self._read_client()
         while True:
             if self.limiter.qps > 0:
-                await self._admit(path)
+                try:
+                    # the token wait counts against the read's own budget: a tail that cannot
+                    # be read in time is no evidence, and the decision must not wait longer
+                    await self._admit(path, "GET", max(0.0, deadline - time.monotonic()))
+                except asyncio.TimeoutError:
+                    if self.metrics is not None:
+                        self.metrics.inc("kube_ratelimit_gaveup", labels={"verb": "GET"})
+                    raise
             self.requests += 1
             left = max(0.05, deadline - time.monotonic())
             # an idle keep-alive connection takes it without a coroutine or a timer per read
@@ -632,7 +656,10 @@ class KubeClient:
             return None  # no banked token: the retrying coroutine waits for one
         fut = self._fast.request_nowait("DELETE", resource_path("Job", namespace, name), _delete_body(propagation_policy),
                                         self._headers({"Content-Type": "application/json"}))
-        if fut is not None:
+        if fut is None:
+            # no pipelined connection had room: the fallback DELETE takes its own token
+            self.limiter.give_back()
+        else:
             self.requests += 1
         return fut
 

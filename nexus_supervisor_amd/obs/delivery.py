@@ -1,6 +1,6 @@
 """Watch-delivery stamps: where an object's change spends its time between the API
-server's push and the supervisor's handler (~1.8 ms of the open-loop
-p99 sat there, unexplained).
+server's push and the supervisor's handler, so the open-loop p99 can be split into
+transport, hub, feed and dispatch time.
 
 The transport stamps each batch it hands to an informer (CLOCK_MONOTONIC, shared by every
 process on the host):

@@ -138,7 +138,7 @@ class ShardSet:
         s = cfg.sharding
         if s.mode == "lease":
             # nothing until a shard lease is won (also with one shard: the lease then is the
-            # replica's only ownership, ADVICE r2 parallel/sharding.py:61)
+            # replica's only ownership, so a replica that never won it writes nothing)
             return cls(max(1, s.shards), (), leased=True)
         if s.shards <= 1:
             return cls(1)

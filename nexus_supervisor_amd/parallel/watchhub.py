@@ -80,11 +80,11 @@ class WatchHub:
         self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label, POD_FORGET_AFTER)
         from .sharding import ShardSet
 
-        self.set_shards(ShardSet.from_config(cfg))
         self.tasks: Dict[str, asyncio.Task] = {}
         self.relists = 0
         self.bytes_routed = 0
         self.owned = None  # the replica's shards (sharding.shard-label narrows the Pod/Job watches)
+        self.set_shards(ShardSet.from_config(cfg))  # static mode: the owned set is final here
 
     def set_shards(self, shards) -> None:
         """Replica shard set: lines of runs this replica does not own are dropped in the

@@ -319,6 +319,11 @@ class WorkerPool:
         self.active_until: Optional[float] = None  # leader lease
         self._stopping = False
         self._watchdog: Optional[asyncio.Task] = None
+        # the replica's kube-qps / kube-burst as one shared budget for the parent and every
+        # worker (kube/flowcontrol.py SharedSchedule; None = a fixed 1/(K+1) split)
+        from ..kube.flowcontrol import replica_schedule
+
+        self.qps_schedule = replica_schedule(cfg, create=self.count > 1)
 
     def _child_mapping(self, index: int) -> Dict[str, Any]:
         m = copy.deepcopy(self._mapping)
@@ -387,6 +392,11 @@ class WorkerPool:
         env["NEXUS_WORKER_REPORT"] = "1" if self.report_decisions else "0"
         env["NEXUS_WORKER_REMOTE_GPU"] = "1" if self.remote_gpu else "0"
         fds = [child.fileno()]
+        if self.qps_schedule is not None:
+            env["NEXUS_WORKER_QPS_FD"] = str(self.qps_schedule.fd)
+            fds.append(self.qps_schedule.fd)
+        else:
+            env.pop("NEXUS_WORKER_QPS_FD", None)
         if dchild is not None:
             env["NEXUS_WORKER_DATA_FD"] = str(dchild.fileno())
             fds.append(dchild.fileno())

@@ -332,6 +332,22 @@ class FakeApiServer:
         self._record(kind, "MODIFIED", obj)
         return obj
 
+    def apply(self, etype: str, obj: Dict[str, Any], copy_obj: bool = True) -> None:
+        """One line of synthetic cluster traffic (``bench/workload.py``): ADDED / MODIFIED
+        (either creates or updates, as the native simulator's ``/sim/apply``), DELETED, or
+        LOG (a container log served from ``pods/log``)."""
+        if etype == "LOG":
+            self.set_pod_log(obj["namespace"], obj["pod"], obj["container"], obj["text"])
+        elif etype == "DELETED":
+            m = obj["metadata"]
+            self.delete(obj["kind"], m.get("namespace", ""), m["name"])
+        else:
+            key = (obj["metadata"].get("namespace", ""), obj["metadata"]["name"])
+            if key in self.objects[obj["kind"]]:
+                self.update(obj, copy_obj=copy_obj)
+            else:
+                self.create(obj, copy_obj=copy_obj)
+
     def upsert(self, obj: Dict[str, Any]) -> Dict[str, Any]:
         key = (obj["metadata"].get("namespace", ""), obj["metadata"]["name"])
         return self.update(obj) if key in self.objects[obj["kind"]] else self.create(obj)

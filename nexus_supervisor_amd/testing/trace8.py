@@ -1,4 +1,4 @@
-"""8-GPU node trace fixture: the native monitor over the stub amd-smi
+"""8-GPU node trace fixture (pins the trace-row size bound): the native monitor over the stub amd-smi
 (``NEXUS_STUB_GPUS=8``, every GPU pair xGMI-linked) watches an 8-rank job — several
 processes per GPU, a burst of GPU events — and one rank dies of an HBM-OOM.  Prints the
 rendered trace row and its size as one JSON line.  Run as its own process: the stub's GPU

@@ -27,10 +27,17 @@ def _check(out, n, steps, warmup, events):
     assert abs(out["vs_baseline"] - out["value"] / 10.0) < 0.05
     assert out["p50_ms"] is not None and out["p99_ms"] >= out["p50_ms"]
     # the bench checks what it measured: every decision wrote the workload's expected stage,
-    # and every timed run's row reads back with that stage
+    # and every timed run's row (failed and started) reads back with that stage
     assert out["wrong_stage"] == 0, out["readback"]
-    assert out["readback"]["checked"] == steps * events * n and out["readback"]["wrong"] == 0, out["readback"]
+    assert out["readback"]["checked"] >= steps * events * n and out["readback"]["wrong"] == 0, out["readback"]
     assert out["supervisor_cpu_us_per_event_rank0"] > 0
+    if out["config"].get("workload") == "lifecycle":
+        # every failure brings its replacement run's start: a ToRunning decision (read + write)
+        # per started run, and the Pending -> Running watch traffic with the kubelet's Events
+        assert out["starts_per_s"] > 0 and out["decisions_per_s"] > out["value"], out
+        assert out["start_p50_ms"] is not None
+        if out["config"]["transport"] == "wire":
+            assert out["watch_objects_per_failure"] >= 8, out["watch_objects_per_failure"]
 
 
 @pytest.mark.slow
@@ -169,7 +176,7 @@ def _torchrun(nproc, *args, timeout=400):
 
 @pytest.mark.slow
 def test_bench_four_ranks_shared_cluster_not_harness_bound():
-    """VERDICT r2 next-round #3: 4 gloo ranks on the shared cluster (one apiserver simulator
+    """4 gloo ranks on the shared cluster (one apiserver simulator
     + one CQL server, four replicas each owning a shard of the namespace): no harness
     process saturated, every decision in its expected stage, every timed row read back,
     and the replica CPU per failure reported for every rank."""
@@ -178,7 +185,7 @@ def test_bench_four_ranks_shared_cluster_not_harness_bound():
     _check(out, 4, 2, 1, 30)
     assert out["config"]["cluster"] == "shared" and out["config"]["parallelism"] == "shard4x1proc"
     assert out["harness_bound"]["bound"] is False and out["harness_bound"]["bound_ranks"] == [], out["harness_bound"]
-    assert out["wrong_stage"] == 0 and out["readback"]["wrong"] == 0 and out["readback"]["checked"] == 4 * 2 * 30
+    assert out["wrong_stage"] == 0 and out["readback"]["wrong"] == 0 and out["readback"]["checked"] >= 4 * 2 * 30
     assert len(out["supervisor_cpu_us_per_event_by_rank"]) == 4
     assert all(v and v > 0 for v in out["supervisor_cpu_us_per_event_by_rank"])
 

@@ -81,7 +81,7 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
                     except Exception:  # noqa: BLE001
                         await asyncio.sleep(0.05)
             for etype, obj in traffic:
-                (api.create if etype == "ADDED" else api.update)(obj)
+                api.apply(etype, obj)
             for rid in failed:
                 expected[rid] = wl.expected[rid]
 

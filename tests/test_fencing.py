@@ -51,7 +51,9 @@ def _cfg(**over):
     is covered by tests/test_fused_write.py."""
     base = {"cql-store-type": "memory", "rate-limit-elements-per-second": 0, "resync-period": "0s",
             "failure-rate-base-delay": "10ms", "failure-rate-max-delay": "50ms",
-            "leader-election": {"enabled": True}, "compat": {"fused-write": False}}
+            "leader-election": {"enabled": True}, "compat": {"fused-write": False},
+            # pod-less Job failures here: no wait for a pod update (tests/test_pod_rules.py covers it)
+            "rules": {"job-pod-settle": "0s"}}
     over = dict(over)
     if "compat" in over:
         over["compat"] = dict(base["compat"], **over["compat"])

@@ -1,4 +1,4 @@
-"""Client-side API flow control (VERDICT r3 missing #1 / next #2).
+"""Client-side API flow control.
 
 The reference's clientset runs on client-go's defaults (``/root/reference/app/
 app_dependencies.go:39-45``): a QPS 5 / burst 10 token bucket, and ``429`` answers
@@ -25,8 +25,9 @@ from nexus_supervisor_amd.testing.seed import ALGORITHM, make_job, make_pod
 
 
 def test_token_bucket_burst_then_qps_and_priorities(arun):
-    """Burst tokens go at once, then one per 1/qps; a decision read (priority 0) queued
-    after ten background DELETEs (priority 1) is served before all of them."""
+    """Burst tokens go at once, then one per 1/qps; a decision read (class 0) queued after
+    ten background DELETEs (class 1) gets its weighted turn instead of waiting for all of
+    them (it is first here: the round robin starts at the read class)."""
     async def go():
         b = TokenBucket(100, 2)
         assert b.try_accept() and b.try_accept() and not b.try_accept()  # the burst
@@ -234,8 +235,8 @@ def test_pods_log_wave_is_bounded(arun):
 def test_log_reads_are_not_starved_by_a_delete_backlog(arun):
     """kube-qps 20: a wave of 80 OOMKilled runs queues 80 background Job DELETEs (4 s of
     tokens).  A GPU pod that fails right behind them with an empty termination message needs
-    its pods/log tail before it can be decided: the read jumps the DELETE queue (priority
-    0), so that run is decided within a second, not after the backlog drains."""
+    its pods/log tail before it can be decided: the read class has its own share of the
+    tokens, so that run is decided within a second, not after the backlog drains."""
     async def go():
         api = FakeApiServer(bookmark_interval=0.1)
         url = await api.start()
@@ -275,3 +276,132 @@ def test_log_reads_are_not_starved_by_a_delete_backlog(arun):
         await api.stop()
 
     arun(go(), timeout=40)
+
+
+def _wave(qps, burst, reads, shared=None):
+    """A failure wave on default GPU pods: ``reads`` pods/log reads queued at once, and
+    each decided read queues that run's Job DELETE.  Returns (read waits, delete waits)."""
+    async def go():
+        b = TokenBucket(qps, burst, shared=shared)
+        read_w, del_w = [], []
+
+        async def delete():
+            t = time.monotonic()
+            await b.wait(1)
+            del_w.append(time.monotonic() - t)
+
+        dels = []
+
+        async def read():
+            t = time.monotonic()
+            await b.wait(0)
+            read_w.append(time.monotonic() - t)
+            dels.append(asyncio.ensure_future(delete()))
+
+        await asyncio.gather(*[read() for _ in range(reads)])
+        await asyncio.gather(*dels)
+        return read_w, del_w, b
+
+    return go()
+
+
+def _p99(xs):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(0.99 * len(xs)))]
+
+
+def test_delete_share_in_a_gpu_wave(arun):
+    """1,000 default-pod GPU failures at once: 1,000 pods/log reads and, behind each decided
+    read, its Job DELETE (which frees the job's GPUs).  The reference's bucket is one FIFO
+    (client-go); strict read priority made every DELETE wait for the whole read wave (at
+    kube-qps 50 that is 20 s, here scaled to qps 1000 = 1 s).  With the weighted round robin
+    a DELETE waits about one token turn, and the reads finish within 2x the time their
+    fair share (reads and DELETEs alternating) gives them."""
+    qps, n = 1000.0, 1000
+    read_w, del_w, b = arun(_wave(qps, 1, n), timeout=30)
+    wave = n / qps  # the read wave alone, at full rate
+    assert _p99(del_w) < 0.1 * wave, _p99(del_w)
+    fair = n / (qps / 2)  # reads' completion time when they share the tokens with the DELETEs
+    assert max(read_w) <= 2 * fair, (max(read_w), fair)
+    assert b.served[0] >= n - 1 and b.served[1] > 0.9 * n  # (the first read took the banked token)
+
+
+def test_wrr_cycle_and_idle_classes():
+    from nexus_supervisor_amd.kube.flowcontrol import _wrr_cycle
+
+    assert _wrr_cycle((2, 2, 1)) == (0, 1, 2, 0, 1)
+    assert sorted(_wrr_cycle((3, 1))) == [0, 0, 0, 1]
+
+    async def go():
+        # an idle class's share goes to the others: only Events queued -> full rate
+        b = TokenBucket(400, 1)
+        t0 = time.monotonic()
+        await asyncio.gather(*[b.wait(2) for _ in range(40)])
+        return time.monotonic() - t0
+
+    took = asyncio.run(go())
+    assert took < 0.2, took
+
+
+def test_bucket_wait_timeout_takes_no_token(arun):
+    async def go():
+        b = TokenBucket(10, 1)
+        assert b.try_accept()
+        with pytest.raises(asyncio.TimeoutError):
+            await b.wait(0, timeout=0.02)
+        assert b.queued == 0
+        # the next waiter gets the token the timed-out one would have had
+        d = await asyncio.wait_for(b.wait(0), 1.0)
+        assert d < 0.15
+
+    arun(go(), timeout=10)
+
+
+def test_give_back_refunds_try_accept():
+    b = TokenBucket(1, 1)
+    assert b.try_accept() and not b.try_accept()
+    b.give_back()
+    assert b.try_accept()
+
+
+def test_shared_schedule_adapts_to_skew(arun):
+    """Two processes' buckets on one replica budget (SharedSchedule): alone, one of them
+    gets the whole kube-qps (a fixed split would cap it at half); together they share it
+    and never exceed it."""
+    from nexus_supervisor_amd.kube.flowcontrol import SharedSchedule
+
+    async def go():
+        sh = SharedSchedule(500, 1)
+        a, b = TokenBucket(500, 1, shared=sh), TokenBucket(500, 1, shared=sh)
+        t0 = time.monotonic()
+        await asyncio.gather(*[a.wait(0) for _ in range(100)])
+        alone = time.monotonic() - t0
+        t0 = time.monotonic()
+        await asyncio.gather(*[a.wait(0) for _ in range(100)], *[b.wait(1) for _ in range(100)])
+        both = time.monotonic() - t0
+        return alone, both
+
+    alone, both = arun(go(), timeout=20)
+    assert 0.15 <= alone < 0.4, alone   # 100 tokens at 500/s, not at 250/s
+    assert 0.35 <= both < 0.8, both     # 200 tokens: the budget is shared, never doubled
+
+
+def test_shared_schedule_across_processes(tmp_path):
+    """The parent's GCRA word is inherited by a child process (memfd + pass_fds, as a shard
+    worker gets it): the child's takes count against the parent's budget."""
+    import os
+    import subprocess
+    import sys
+
+    from nexus_supervisor_amd.kube.flowcontrol import SharedSchedule
+
+    sh = SharedSchedule(100, 10)
+    code = ("import os,sys; from nexus_supervisor_amd.kube.flowcontrol import SharedSchedule as S; "
+            "s=S(100,10,fd=int(os.environ['FD'])); print(sum(s.try_take() for _ in range(50)))")
+    env = dict(os.environ, FD=str(sh.fd))
+    out = subprocess.run([sys.executable, "-c", code], env=env, pass_fds=(sh.fd,), capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert 10 <= int(out.stdout.strip()) <= 12  # the burst (plus what refilled meanwhile)
+    assert not sh.try_take() or sh.backlog() >= 0  # the parent sees the spent burst
+    assert sh.backlog() > 0.05

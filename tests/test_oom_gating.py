@@ -155,3 +155,40 @@ def test_cpu_pod_oom_end_to_end_counts_no_gpu_failure(arun):
         await api.stop()
 
     arun(go(), timeout=30)
+
+
+# Runtime-check and math-library wordings a ROCm job prints when the GPU is full: torch's
+# C10_HIP_CHECK (HIP context / hipBLAS handle / RCCL cannot allocate), the HIP enum, and
+# the hipBLAS / cuBLAS / rocBLAS / MIOpen allocation-failure statuses.
+LIB_TEXTS = {
+    "hip-check": "RuntimeError: HIP error: out of memory\nHIP kernel errors might be asynchronously reported",
+    "cuda-check": "RuntimeError: CUDA error: out of memory\nCompile with `TORCH_USE_CUDA_DSA` to enable",
+    "hip-enum": "hipMemcpy returned hipErrorMemoryAllocation",
+    "hipblas": "RuntimeError: HIPBLAS_STATUS_ALLOC_FAILED when calling `hipblasCreate(handle)`",
+    "cublas": "RuntimeError: CUDA error: CUBLAS_STATUS_ALLOC_FAILED when calling `cublasCreate(handle)`",
+    "hipblaslt": "hipBLASLt error: HIPBLASLT_STATUS_ALLOC_FAILED",
+    "rocblas": "rocBLAS error: rocblas_status_memory_error from rocblas_gemm_ex",
+    "miopen": "MIOpen Error: miopenStatusAllocFailed in convolution workspace",
+}
+
+
+@pytest.mark.parametrize("name", sorted(LIB_TEXTS))
+def test_hip_runtime_and_library_oom_texts(name):
+    text = LIB_TEXTS[name]
+    assert oom.hbm_signature(text), name
+    assert not oom.host_signature(text) or name in ("hip-check", "cuda-check"), name
+    term = [{"container": "c", "exitCode": 1, "reason": "Error"}]
+    assert oom.analyze([text], term, gpu_involved=True).kind == "hbm", name
+    # a CPU-only pod with the same words stays non-HBM
+    v = oom.analyze([text], term, gpu_involved=False)
+    assert v.kind != "hbm", (name, v.signals)
+
+
+def test_torch_default_cpu_allocator_is_host_oom():
+    text = ("RuntimeError: [enforce fail at alloc_cpu.cpp:117] data. DefaultCPUAllocator: not enough memory: "
+            "you tried to allocate 68719476736 bytes.")
+    assert oom.host_signature(text)
+    assert not oom.hbm_signature(text)
+    for involved in (True, False, None):
+        v = oom.analyze([text], [{"container": "c", "exitCode": 1, "reason": "Error"}], gpu_involved=involved)
+        assert v.kind == "host", (involved, v.signals)

@@ -129,9 +129,38 @@ def test_evicted_observe_then_backoff_limit_is_attributed(arun):
     assert store.get(ALGORITHM, RID).lifecycle_stage == S.RUNNING  # eviction alone decides nothing
     store2, c = arun(_run(cfg, [make_pod(RID, cfg.labels), job], [("MODIFIED", evicted), ("MODIFIED", job_failed)]))
     row = store2.get(ALGORITHM, RID)
-    assert row.lifecycle_stage == S.DEADLINE_EXCEEDED
+    # the same row evicted-policy "fail" writes (rules.oom-fails-backoff-job, default on)
+    assert row.lifecycle_stage == S.FAILED
+    assert row.algorithm_failure_cause == ("Algorithm encountered a fatal error during execution: "
+                                           "Algorithm pod was evicted from its node.")
     t = _trace(row)
     assert t["class"] == "evicted" and t["history"][0]["kind"] == "evicted"
+    # the compat switch off keeps the reference's stage for BackoffLimitExceeded
+    cfg3 = _cfg(**{"rules": {"oom-fails-backoff-job": False}})
+    store3, _ = arun(_run(cfg3, [make_pod(RID, cfg3.labels), job], [("MODIFIED", evicted), ("MODIFIED", job_failed)]))
+    row3 = store3.get(ALGORITHM, RID)
+    assert row3.lifecycle_stage == S.DEADLINE_EXCEEDED and _trace(row3)["class"] == "evicted"
+
+
+def test_eviction_storm_rows_name_the_eviction(arun):
+    """An eviction storm under both policies: every run's row ends FAILED with the eviction
+    cause — at the eviction itself (fail) or at the Job's BackoffLimitExceeded (observe)."""
+    rows = [type(RUNNING_ROW)(algorithm=ALGORITHM, id=f"storm-{i:02d}", lifecycle_stage="RUNNING") for i in range(20)]
+    for policy in ("fail", "observe"):
+        cfg = _cfg(**{"rules": {"evicted-policy": policy}})
+        objs, upd = [], []
+        for r in rows:
+            objs += [make_pod(r.id, cfg.labels), make_job(r.id, cfg.labels, rv="6")]
+            upd.append(("MODIFIED", make_pod(r.id, cfg.labels, rv="7", status={
+                "phase": "Failed", "reason": "Evicted", "message": "The node was low on resource: memory."})))
+            if policy == "observe":
+                upd.append(("MODIFIED", make_job(r.id, cfg.labels, rv="8", conditions=[
+                    {"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded", "message": "limit"}])))
+        store, _ = arun(_run(cfg, objs, upd, rows=rows))
+        for r in rows:
+            row = store.get(ALGORITHM, r.id)
+            assert row.lifecycle_stage == S.FAILED, (policy, r.id, row.lifecycle_stage)
+            assert row.algorithm_failure_cause.endswith("Algorithm pod was evicted from its node."), (policy, row)
 
 
 def test_unschedulable_timeout(arun):

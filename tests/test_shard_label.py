@@ -1,4 +1,4 @@
-"""Shard-narrowed watches (VERDICT r3 missing #2 / next #6): with ``sharding.shard-label``
+"""Shard-narrowed watches: with ``sharding.shard-label``
 each replica watches only its shards' Pods and Jobs (``<label> in (owned…)``, filtered by
 the API server), so N replicas on one namespace do not each receive — and the API server
 does not serialise N times — the whole stream.  The reference's only scale knob is more
@@ -36,6 +36,21 @@ def test_selectors():
     assert watch_selector(cfg, "Event", {1}) == ""
     cfg.sharding.shard_label = ""
     assert LABEL not in watch_selector(cfg, "Job", {1})
+
+
+def test_watchhub_static_mode_narrows_pod_and_job_watches():
+    """A static-mode sharded replica's watch hub (worker-processes > 1) must send the shard
+    selector on its Pod/Job LIST/WATCH: nothing calls ``set_shards`` after construction."""
+    from nexus_supervisor_amd.parallel.watchhub import WatchHub
+
+    cfg = _cfg(1, shards=4)
+    hub = WatchHub(cfg, kube=None, count=2, send=lambda *a: None, buffered=lambda w: 0, drain=lambda w: None)
+    assert hub.owned == frozenset({1})
+    for kind in ("Pod", "Job"):
+        _, params = hub._path_params(kind)
+        assert f"{LABEL} in (1)" in params["labelSelector"], (kind, params)
+    _, params = hub._path_params("Event")
+    assert "labelSelector" not in params
 
 
 def _labelled(rid, labels, shards=2, stamp=True):
