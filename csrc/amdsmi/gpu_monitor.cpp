@@ -225,6 +225,20 @@ PYBIND11_MODULE(NEXUS_MONITOR_MODULE, m) {
       "Parse one amdgpu DRM fdinfo text");
   m.def("kfd_gpu_bdfs", &kfd_gpu_bdfs, py::arg("sys_root") = "/sys", "KFD topology gpu_id -> PCI BDF");
   m.def(
+      "denials",
+      []() {
+        py::dict d;
+        for (int k = 0; k < kDenySources; ++k) d[deny_source_name(k)] = deny_counters()[k].load();
+        return d;
+      },
+      "Process / sysfs reads refused by the kernel (EACCES / EPERM) so far, by source");
+  m.def(
+      "reset_denials",
+      []() {
+        for (int k = 0; k < kDenySources; ++k) deny_counters()[k].store(0);
+      },
+      "Zero the refusal counters");
+  m.def(
       "kfd_proc_usage",
       [](const std::string& sys_root) { return uses_list(kfd_proc_usage(sys_root, kfd_gpu_bdfs(sys_root))); },
       py::arg("sys_root") = "/sys", "Per-process VRAM from KFD sysfs (init-namespace PIDs)");

@@ -442,7 +442,7 @@ class GpuMonitor {
       p.name = read_small(base + "/comm", 64);
       while (!p.name.empty() && p.name.back() == '\n') p.name.pop_back();
     }
-    std::string env = read_small(base + "/environ", 1 << 17);
+    std::string env = read_small(base + "/environ", 1 << 17, kDenyEnviron);
     size_t s = 0;
     while (s < env.size()) {
       size_t e = env.find('\0', s);

@@ -18,9 +18,12 @@
 #pragma once
 
 #include <dirent.h>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
+#include <cerrno>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -38,13 +41,48 @@ namespace nexus_gpu {
 // Inode of the initial PID namespace (PROC_PID_INIT_INO in the kernel).
 constexpr unsigned long long kInitPidNsIno = 0xEFFFFFFCULL;
 
-inline std::string read_small(const std::string& path, size_t cap = 1 << 16) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return {};
+// Reads refused by the kernel (EACCES / EPERM), per source.  An agent without the
+// privileges it needs — a non-root UID gets no effective capabilities even in a privileged
+// container — cannot open another user's /proc/<pid>/fd, fdinfo or environ (ptrace-read
+// check) and attribution silently degrades; these counters make that loud (the node
+// agent exports them as agent_proc_scan_denied{source} and logs the first one).
+enum DenySource { kDenyFdDir = 0, kDenyFdInfo, kDenyEnviron, kDenyProcMeta, kDenySysfs, kDenySources };
+inline const char* deny_source_name(int k) {
+  static const char* const names[kDenySources] = {"fd", "fdinfo", "environ", "proc", "sysfs"};
+  return (k >= 0 && k < kDenySources) ? names[k] : "other";
+}
+inline std::atomic<uint64_t>* deny_counters() {
+  static std::atomic<uint64_t> counters[kDenySources];
+  return counters;
+}
+inline void note_errno(int err, int source) {
+  if ((err == EACCES || err == EPERM) && source >= 0 && source < kDenySources)
+    deny_counters()[source].fetch_add(1, std::memory_order_relaxed);
+}
+
+// Up to `cap` bytes of a (proc / sys) file; empty when it cannot be read.  A refusal is
+// counted under `source`.
+inline std::string read_small(const std::string& path, size_t cap = 1 << 16, int source = kDenyProcMeta) {
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    note_errno(errno, source);
+    return {};
+  }
   std::string s;
   s.resize(cap);
-  f.read(&s[0], static_cast<std::streamsize>(cap));
-  s.resize(static_cast<size_t>(f.gcount()));
+  size_t n = 0;
+  while (n < cap) {
+    ssize_t r = ::read(fd, &s[n], cap - n);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      note_errno(errno, source);
+      break;
+    }
+    if (r == 0) break;
+    n += static_cast<size_t>(r);
+  }
+  ::close(fd);
+  s.resize(n);
   return s;
 }
 
@@ -66,7 +104,10 @@ inline bool host_pid_namespace(const std::string& proc_root) {
 inline std::vector<uint32_t> list_pids(const std::string& proc_root) {
   std::vector<uint32_t> out;
   DIR* d = opendir(proc_root.c_str());
-  if (!d) return out;
+  if (!d) {
+    note_errno(errno, kDenyProcMeta);
+    return out;
+  }
   while (dirent* e = readdir(d))
     if (is_digits(e->d_name)) out.push_back(static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10)));
   closedir(d);
@@ -94,7 +135,10 @@ inline std::vector<int> drm_render_fds(const std::string& proc_root, uint32_t pi
   std::vector<int> out;
   std::string dir = proc_root + "/" + std::to_string(pid) + "/fd";
   DIR* d = opendir(dir.c_str());
-  if (!d) return out;
+  if (!d) {
+    note_errno(errno, kDenyFdDir);
+    return out;
+  }
   char buf[256];
   while (dirent* e = readdir(d)) {
     if (!is_digits(e->d_name)) continue;
@@ -217,7 +261,8 @@ class DrmScanner {
       std::set<std::pair<std::string, uint64_t>> seen_clients;
       std::vector<int> keep;
       for (int fd : st.fds) {
-        std::string txt = read_small(root_ + "/" + std::to_string(pid) + "/fdinfo/" + std::to_string(fd), 8192);
+        std::string txt =
+            read_small(root_ + "/" + std::to_string(pid) + "/fdinfo/" + std::to_string(fd), 8192, kDenyFdInfo);
         if (txt.empty()) continue;  // fd closed since the last listing
         keep.push_back(fd);
         DrmFdInfo fi = parse_drm_fdinfo(txt);
@@ -261,9 +306,10 @@ inline std::map<uint32_t, std::string> kfd_gpu_bdfs(const std::string& sys_root)
   while (dirent* e = readdir(d)) {
     if (!is_digits(e->d_name)) continue;
     std::string node = base + "/" + e->d_name;
-    uint32_t gpu_id = static_cast<uint32_t>(strtoul(read_small(node + "/gpu_id", 64).c_str(), nullptr, 10));
+    uint32_t gpu_id =
+        static_cast<uint32_t>(strtoul(read_small(node + "/gpu_id", 64, kDenySysfs).c_str(), nullptr, 10));
     if (!gpu_id) continue;
-    std::string props = read_small(node + "/properties", 1 << 14);
+    std::string props = read_small(node + "/properties", 1 << 14, kDenySysfs);
     uint64_t loc = 0, dom = 0;
     bool have_loc = false;
     size_t p = 0;
@@ -318,7 +364,7 @@ inline std::vector<ProcGpuUse> kfd_proc_usage(const std::string& sys_root, const
       ProcGpuUse u;
       u.pid = static_cast<uint32_t>(strtoul(ps.c_str(), nullptr, 10));
       u.bdf = it->second;
-      u.vram_bytes = strtoull(read_small(dir + "/" + e->d_name, 64).c_str(), nullptr, 10);
+      u.vram_bytes = strtoull(read_small(dir + "/" + e->d_name, 64, kDenySysfs).c_str(), nullptr, 10);
       u.clients = 1;
       out.push_back(u);
     }

@@ -110,6 +110,8 @@ class Classifier:
         # with the GPUs, or a node agent in-process): pod -> evidence record or None.
         self.evidence_provider: Optional[Callable[[Dict[str, Any]], Optional[Dict[str, Any]]]] = None
         self.deferred = False
+        # defer _enrich of failing decisions to finish() (the Supervisor turns it on)
+        self.lazy_enrich = False
         # failed GPU pod whose OOM signature may only be in its container log: the
         # (container, previous) instances to fetch (set by classify_pod, see log_cache)
         self.deferred_log: List[Dict[str, Any]] = []
@@ -146,6 +148,10 @@ class Classifier:
         kind = inv.get("kind", "")
         if kind not in ("Job", "Pod"):
             return IGNORED, []
+        if event.get("reason", "") not in _EVENT_REASONS:
+            # most of a namespace's Events (Scheduled, Pulling, Pulled, Created, Killing,
+            # SuccessfulCreate, ...) decide nothing: no cache lookup, no stale-event parking
+            return NOOP, []
         obj = lookup.get(kind, inv.get("name", ""))
         if obj is None:
             return STALE, []
@@ -532,6 +538,25 @@ class Classifier:
     def _enrich(self, res: RunStatusAnalysisResult, pods=(), texts=(), verdict: Optional[oom_mod.OomVerdict] = None) -> None:
         if not self.gpu.attribution_enabled:
             return
+        if self.lazy_enrich:
+            # a run's failure usually arrives as two or three decisions (the pod's status, the
+            # Job's event and condition) of which one is written: enrich that one, at
+            # actuation (:meth:`finish`)
+            res.pending_enrich = (pods, texts, verdict)
+            return
+        self._enrich_now(res, pods, texts, verdict)
+
+    def finish(self, res: RunStatusAnalysisResult, lookup: ObjectLookup) -> None:
+        """Complete a decision about to be written: the deferred enrichment (with the pod
+        versions seen at classification), then :meth:`late_enrich`."""
+        p = res.pending_enrich
+        if p is not None:
+            res.pending_enrich = None
+            self._enrich_now(res, *p)
+        self.late_enrich(res, lookup)
+
+    def _enrich_now(self, res: RunStatusAnalysisResult, pods=(), texts=(),
+                    verdict: Optional[oom_mod.OomVerdict] = None) -> None:
         pods = [p for p in pods if p]
         key = res.key
         if pods:
@@ -625,6 +650,9 @@ class Classifier:
 
 
 _NO_EV: Dict[str, Any] = {}
+# Event reasons any rule reads (decisions and evidence)
+_EVENT_REASONS = frozenset(R.JOB_EVENT_RULES) | frozenset(R.POD_EVENT_RULES) | frozenset(EVICTION_EVENT_REASONS) | {
+    "FailedScheduling"}
 # BackoffLimitExceeded whose cause was found: the run's failure message per class
 _BACKOFF_CAUSE = {F.HBM_OOM: MSG_HBM_OOM, F.HOST_OOM: MSG_HOST_OOM, F.EVICTED: MSG_EVICTED}
 

@@ -56,6 +56,35 @@ def pod_failed(pod: Dict[str, Any]) -> bool:
     return False
 
 
+# capabilities a non-root agent would need (CapEff bits, linux/capability.h): ptrace-read
+# access to other users' /proc/<pid>/{fd,fdinfo,environ}, and reading root-owned 0640 logs
+_CAPS = {"CAP_DAC_OVERRIDE": 1, "CAP_DAC_READ_SEARCH": 2, "CAP_SYS_PTRACE": 19}
+
+
+def process_privileges(status_path: str = "/proc/self/status") -> Dict[str, Any]:
+    """euid and effective capabilities of this process, and whether they suffice for the
+    agent: root (uid 0 in a privileged container has every capability), or
+    CAP_SYS_PTRACE + CAP_DAC_READ_SEARCH.  A non-root UID in a ``privileged: true``
+    container has an empty effective set — Kubernetes adds capabilities to the bounding
+    set, the kernel gives a non-root process none of them."""
+    import os
+
+    eff = 0
+    try:
+        with open(status_path) as f:
+            for line in f:
+                if line.startswith("CapEff:"):
+                    eff = int(line.split()[1], 16)
+                    break
+    except OSError:
+        pass
+    have = {k for k, bit in _CAPS.items() if eff >> bit & 1}
+    need = {"CAP_SYS_PTRACE"} | ({"CAP_DAC_READ_SEARCH"} if "CAP_DAC_OVERRIDE" not in have else set())
+    missing = sorted(need - have)
+    return {"euid": os.geteuid(), "cap_eff": f"{eff:016x}", "caps": sorted(have), "missing": missing,
+            "sufficient": not missing}
+
+
 class NodeAgent:
     def __init__(self, kube_client, telemetry: GpuTelemetry, node_name: str, namespace: str, *,
                  label_selector: str = "", annotation: str = "nexus.amd.com/gpu-evidence",
@@ -93,9 +122,28 @@ class NodeAgent:
         self._bdf_index: Dict[str, int] = {}
         self.patches = 0
         self.patch_failures = 0
+        from ..obs.metrics import Metrics
+
+        # agent_proc_scan_denied{source} / agent_log_read_denied / agent_podresources_denied:
+        # attribution that silently degrades for lack of privileges is counted and logged once
+        self.metrics = Metrics("nexus_gpu_agent", {"node": node_name})
+        self._denied_seen: Dict[str, int] = {}
+        self._warned: Set[str] = set()
+        self.privileges: Dict[str, Any] = {}
 
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> None:
+        self.privileges = process_privileges()
+        self.metrics.set("agent_privileged", 1.0 if self.privileges.get("sufficient") else 0.0)
+        if not self.privileges.get("sufficient"):
+            self._warn_once("privileges", "node agent runs without the privileges per-process GPU attribution needs "
+                            "(uid %s, missing %s): other users' /proc/<pid>/fdinfo and environ, root-owned container "
+                            "logs and the kubelet pod-resources socket will be refused — run it as root "
+                            "(the chart's gpu-agent securityContext)", self.privileges.get("euid"),
+                            ",".join(self.privileges.get("missing") or []) or "-")
+        check = getattr(self.podres, "check", None)
+        if check is not None and check() == "denied":
+            self._denied("podresources")
         self.tel.start()
         self._bdf_index = {normalize_bdf(d.get("bdf", "")): d["index"] for d in self.tel.devices() if d.get("bdf")}
         self.pods.add_event_handler(on_add=lambda p: self._on_pod(None, p), on_update=self._on_pod,
@@ -155,10 +203,50 @@ class NodeAgent:
         if not self.log_root:
             return []
         try:
-            return logtail.node_log_evidence(self.log_root, pod, self.log_tail_bytes)
+            recs = logtail.node_log_evidence(self.log_root, pod, self.log_tail_bytes)
         except Exception as exc:  # noqa: BLE001 - logs are evidence, never a reason to skip the GPU record
             log.debug("log tail of %s failed: %s", kube.name_of(pod), exc)
             return []
+        for r in recs:
+            if r.get("denied"):
+                self._denied("log")
+        return recs
+
+    # ------------------------------------------------------------ privileges
+    def _warn_once(self, key: str, msg: str, *args) -> None:
+        if key not in self._warned:
+            self._warned.add(key)
+            log.warning(msg, *args)
+
+    def _denied(self, what: str, n: int = 1) -> None:
+        """A read the kernel refused: ``log`` (container log tail), ``podresources`` (the
+        kubelet socket)."""
+        name = {"log": "agent_log_read_denied", "podresources": "agent_podresources_denied"}[what]
+        self.metrics.inc(name, n)
+        self._warn_once(name, "node agent: %s refused (permission denied) — %s", what,
+                        "container log tails come from the pods/log API instead (through the supervisor's "
+                        "kube-qps budget)" if what == "log" else
+                        "GPU allocations are unknown; devices fall back to the pod's *_VISIBLE_DEVICES env")
+
+    def check_denials(self) -> Dict[str, int]:
+        """Fold the native monitor's refused /proc and sysfs reads into
+        ``agent_proc_scan_denied{source}``; returns the new ones by source."""
+        try:
+            cur = self.tel.denials()
+        except Exception:  # noqa: BLE001 - diagnostics only
+            return {}
+        new = {}
+        for src, n in cur.items():
+            d = int(n) - self._denied_seen.get(src, 0)
+            if d > 0:
+                new[src] = d
+                self.metrics.inc("agent_proc_scan_denied", d, labels={"source": src})
+            self._denied_seen[src] = int(n)
+        if new:
+            self._warn_once("agent_proc_scan_denied", "node agent: /proc and sysfs reads refused (permission denied, "
+                            "by source: %s) — per-process VRAM and rank env of other users' processes are not "
+                            "attributed; run the agent as root", new)
+        return new
 
     # ------------------------------------------------------------ publishing
     async def publish(self, pod: Dict[str, Any], reason: str) -> Optional[bool]:
@@ -238,12 +326,16 @@ class NodeAgent:
 
     async def _event_loop(self) -> None:
         next_prune = time.monotonic() + 60.0
+        next_check = time.monotonic() + 1.0
         while True:
             await asyncio.sleep(self.event_poll)
             now = time.monotonic()
             if now >= next_prune:
                 self._prune(now)
                 next_prune = now + 60.0
+            if now >= next_check:
+                self.check_denials()
+                next_check = now + 5.0
             try:
                 events = self.tel.drain_events()
             except Exception:  # noqa: BLE001
@@ -280,6 +372,10 @@ async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process 
                       log_root=log_root if cfg.gpu.log_tail != "off" and os.path.isdir(log_root) else None,
                       log_tail_bytes=cfg.gpu.log_tail_bytes)
     await agent.start()
+    runner = None
+    port = int(os.environ.get("NEXUS_AGENT_METRICS_PORT", "0") or 0)
+    if port:
+        runner = await serve_metrics(agent, port)
     stop = asyncio.Event()
     import signal
 
@@ -287,5 +383,27 @@ async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process 
     for s in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(s, stop.set)
     await stop.wait()
+    if runner is not None:
+        await runner.cleanup()
     await agent.stop()
     await kc.close()
+
+
+async def serve_metrics(agent: NodeAgent, port: int, host: str = "0.0.0.0"):
+    """``/metrics`` (Prometheus text) and ``/healthz`` of the node agent."""
+    from aiohttp import web
+
+    async def h_metrics(_req):
+        agent.check_denials()
+        return web.Response(text=agent.metrics.prometheus_text(), content_type="text/plain", charset="utf-8")
+
+    async def h_healthz(_req):
+        return web.Response(text="ok")
+
+    app = web.Application()
+    app.router.add_get("/metrics", h_metrics)
+    app.router.add_get("/healthz", h_healthz)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    await web.TCPSite(runner, host, port).start()
+    return runner

@@ -100,6 +100,20 @@ def container_log_dir(root: str, namespace: str, pod: str, uid: str, container: 
     return os.path.join(root, f"{namespace}_{pod}_{uid}", container)
 
 
+def _unreadable_dir(d: str) -> bool:
+    """``d`` (or a parent under the log root) exists but this process may not list it."""
+    while d and d != os.path.dirname(d):
+        try:
+            os.stat(d)
+        except PermissionError:
+            return True
+        except OSError:
+            d = os.path.dirname(d)
+            continue
+        return os.path.isdir(d) and not os.access(d, os.R_OK | os.X_OK)
+    return False
+
+
 def container_log_file(root: str, namespace: str, pod: str, uid: str, container: str,
                        restart: Optional[int] = None) -> Optional[str]:
     """The kubelet's file for one container instance: ``<restart>.log``; without an exact
@@ -171,12 +185,19 @@ def node_log_evidence(root: str, pod: Dict[str, Any], max_bytes: int = TAIL_BYTE
         path = container_log_file(root, ns, name, uid, fc["container"], fc["restart"])
         rec: Dict[str, Any] = {"container": fc["container"], "restart": fc["restart"], "source": "node-log"}
         if path is None:
-            rec["error"] = "no log file"
+            d = container_log_dir(root, ns, name, uid, fc["container"])
+            if d is not None and _unreadable_dir(d):
+                rec["error"] = "PermissionError: log directory not readable"
+                rec["denied"] = True
+            else:
+                rec["error"] = "no log file"
         else:
             try:
                 rec.update(scan(read_tail(path, max_bytes)))
             except OSError as exc:
                 rec["error"] = f"{type(exc).__name__}: {exc.strerror or exc}"
+                if isinstance(exc, PermissionError):
+                    rec["denied"] = True  # root-owned 0640 kubelet logs and a non-root reader
         out.append(rec)
     return out
 

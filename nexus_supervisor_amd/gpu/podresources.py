@@ -134,6 +134,26 @@ class PodResourcesClient:
                                          response_deserializer=lambda b: b)
         return decode_list_response(call(None, timeout=self.timeout))
 
+    def check(self) -> str:
+        """``ok``, ``missing`` or ``denied``: can this process connect to the kubelet's
+        socket at all (root-only on a default kubelet; gRPC would only say UNAVAILABLE)."""
+        import socket as _socket
+
+        path = self.target[len("unix://"):]
+        s = _socket.socket(_socket.AF_UNIX, _socket.SOCK_STREAM)
+        try:
+            s.settimeout(self.timeout)
+            s.connect(path)
+            return "ok"
+        except PermissionError:
+            return "denied"
+        except FileNotFoundError:
+            return "missing"
+        except OSError as exc:
+            return f"error: {exc.strerror or exc}"
+        finally:
+            s.close()
+
     def close(self) -> None:
         if self._channel is not None:
             self._channel.close()

@@ -60,6 +60,12 @@ class GpuTelemetry:
     def peak_between(self, gpu_index: int, t0: float, t1: float) -> int:  # pragma: no cover - interface
         raise NotImplementedError
 
+    def denials(self) -> Dict[str, int]:
+        """Process / sysfs reads the kernel refused so far, by source (``fd``, ``fdinfo``,
+        ``environ``, ``proc``, ``sysfs``): non-zero means per-process attribution is
+        degraded for lack of privileges."""
+        return {}
+
 
 def native_monitor_module(stub: bool = False):
     """Import the native monitor (``stub``: the build over the stub amd-smi, for CPU
@@ -86,6 +92,7 @@ class AmdSmiTelemetry(GpuTelemetry):
         sysfs fill-in when this process shares the host PID namespace, else DRM fdinfo of
         our own /proc), or forced ``amdsmi`` / ``kfd`` / ``drm``."""
         mod = native_monitor_module(stub)
+        self._mod = mod
         self.interval = interval
         self._m = mod.GpuMonitor(int(interval * 1000), events, retain, read_proc, proc_source, proc_root, sys_root)
         self._started = False
@@ -117,6 +124,10 @@ class AmdSmiTelemetry(GpuTelemetry):
 
     def history(self, gpu_index: int, since: float = 0.0):
         return self._m.history(gpu_index, since)
+
+    def denials(self) -> Dict[str, int]:
+        fn = getattr(self._mod, "denials", None)
+        return dict(fn()) if fn is not None else {}
 
     @property
     def samples(self) -> int:

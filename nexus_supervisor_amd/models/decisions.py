@@ -58,6 +58,9 @@ class RunStatusAnalysisResult:
     attempts: int = 0
     pending_delete: bool = False  # a concurrent Job DELETE failed; retry must still delete
     answered: int = 0  # the attempt (``attempts``) in which the checkpoint store last answered
+    # deferred enrichment (Classifier.lazy_enrich): (pods, texts, verdict) until the decision
+    # is actually written — duplicates of a decided run are never enriched
+    pending_enrich: Any = None
 
     @property
     def key(self):

@@ -191,6 +191,7 @@ class Supervisor:
         self.wall = wall
         self.sync_state = sync_state
         self.classifier = Classifier(cfg.labels, cfg.rules, cfg.gpu)
+        self.classifier.lazy_enrich = True  # enriched in supervise_action (finish), once per written decision
         self.event_informer = factory.informer("Event")
         self.pod_informer = factory.informer("Pod", indexers={"job-name": label_index(cfg.labels.job_name_label)})
         self.job_informer = factory.informer("Job")
@@ -876,6 +877,17 @@ class Supervisor:
         if self._fenced(epoch, rid):
             self.metrics.inc("decisions_fenced")
             return Decision(r, "fenced", None, False)
+        applied = self._applied.get((r.algorithm, rid))
+        if applied is not None and not r.pending_delete:
+            # queued behind the decision that wrote this row (a run's Started Event and its
+            # pod's Running transition; a pod's OOM and its Job's PodFailurePolicy): its stage
+            # is known, so the read is skipped — the outcome is what reading it would give
+            if applied in _cp.FINISHED_STAGES:
+                self.metrics.inc("decisions_suppressed")
+                return await self._skip_finished(r, epoch, failing, applied)
+            if r.action == A.TO_RUNNING and applied == LifecycleStage.RUNNING:
+                self.metrics.inc("decisions_suppressed")
+                return Decision(r, "skipped-already-running", applied, False)
         if failing and r.object_kind == "Job" and r.reason in _POD_FAILED_REASONS and self._settle_wait > 0:
             await self._await_pod_failure(r)
         if failing:
@@ -884,7 +896,7 @@ class Supervisor:
             # an OOM-killed run is FAILED, not DEADLINE_EXCEEDED), so it must precede the stage
             if self._log_fetches and r.object_kind == "Job":
                 await self._await_pod_logs(r)
-            self.classifier.late_enrich(r, self.lookup)
+            self.classifier.finish(r, self.lookup)
         if self._fused:
             d = await self._fused_action(r, epoch, failing)
             if d is not None:

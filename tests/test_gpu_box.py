@@ -458,3 +458,101 @@ def test_multi_rank_job_root_cause_from_a_real_hbm_oom(telemetry, stress_exe, tm
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/multi_rank_root_cause.json", "w") as f:
         json.dump({"trace": trace, "message": msg}, f, indent=1)
+
+
+def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, telemetry):
+    """The GPU is filled by another tenant (``gpu_stress hold``, all but ~0.25 GiB of the
+    HBM3E), then a fresh torch process needs a HIP context, a hipBLAS handle and a small
+    buffer.  Whatever ROCm prints there — torch's ``C10_HIP_CHECK`` ``HIP error: out of
+    memory``, a hipBLAS / rocBLAS allocation status, or torch's ``OutOfMemoryError`` — is the
+    real text of a default pod's log tail, and it must be classified hbm-oom on GPU 0."""
+    import sys
+
+    dev = telemetry.devices()[0]
+    snap = [g for g in telemetry.snapshot() if g.get("index") == 0][0]
+    free_mb = int(dev.get("vram_total_mb") or snap.get("vram_total_mb")) - int(snap.get("vram_used_mb") or 0)
+    hold_gib = max(1.0, free_mb / 1024.0 - 0.25)
+    holder = subprocess.Popen([stress_exe, "hold", "--gib", f"{hold_gib:.2f}", "--seconds", "90"],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(8.0)  # the hold is allocated and filled
+        assert holder.poll() is None, holder.stderr.read()[-400:]
+        code = ("import torch\n"
+                "a = torch.randn(256, 256, device='cuda')\n"
+                "b = a @ a\n"
+                "c = torch.empty(int(2 * 2**30), dtype=torch.uint8, device='cuda')\n"
+                "torch.cuda.synchronize()\n")
+        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    finally:
+        holder.terminate()
+        try:
+            holder.wait(30)
+        except subprocess.TimeoutExpired:
+            holder.kill()
+            holder.wait(30)
+    assert p.returncode != 0, (p.returncode, p.stderr[-800:])
+    from nexus_supervisor_amd.gpu import oom
+
+    sig = oom.hbm_signature(p.stderr)
+    assert sig, p.stderr[-1500:]
+    trace, _reqs = _supervise_default_pod(arun, tmp_path, p.stderr, p.returncode, agent=False)
+    assert trace["class"] == "hbm-oom", trace
+    assert trace["oom"].get("gpu_index", 0) == 0
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/hip_runtime_oom.json", "w") as f:
+        json.dump({"hold_gib": hold_gib, "free_mb_before": free_mb, "rc": p.returncode, "signature": sig,
+                   "runtime_check_wording": "error: out of memory" in p.stderr.lower(),
+                   "stderr_tail": p.stderr[-1500:], "trace": trace}, f, indent=1)
+
+
+def test_node_agent_privileges_reported_on_the_box(stress_exe, tmp_path):
+    """gpurun boxes run this suite as an ordinary user — the situation of an agent image's
+    default UID.  Its own processes are still attributed (same UID), every refused read of
+    another user's /proc entry is counted (agent_proc_scan_denied{source}), an unreadable
+    container log is reported as a denial, and the privilege check says the agent lacks
+    what the chart gives it (root)."""
+    from nexus_supervisor_amd.gpu.agent import NodeAgent, process_privileges
+    from nexus_supervisor_amd.gpu.telemetry import AmdSmiTelemetry, evidence_for
+
+    priv = process_privileges()
+    tel = AmdSmiTelemetry(interval=0.1, proc_source="drm")
+    tel.start()
+    try:
+        t0 = time.time()
+        p = subprocess.Popen([stress_exe, "hold", "--gib", "8", "--seconds", "2.0"], stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True)
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err[-400:]
+        time.sleep(0.3)
+        ev = evidence_for(tel, pids=[p.pid], gpu_indices=[0], lookback=time.time() - t0 + 2)
+
+        class _NullFactory:
+            def informer(self, kind, **kw):
+                return None
+
+        logs = tmp_path / "pods"
+        d = logs / "nexus_run-w0_uid-1" / "algorithm"
+        d.mkdir(parents=True)
+        (d / "0.log").write_text("x stderr F RuntimeError: HIP error: out of memory\n")
+        os.chmod(d / "0.log", 0)
+        agent = NodeAgent(None, tel, "box", "nexus", factory=_NullFactory(), log_root=str(logs))
+        pod = {"metadata": {"name": "run-w0", "namespace": "nexus", "uid": "uid-1"},
+               "status": {"phase": "Failed", "containerStatuses": [{"name": "algorithm", "restartCount": 0, "state": {
+                   "terminated": {"reason": "Error", "exitCode": 1, "message": ""}}}]}}
+        recs = agent.log_evidence(pod)
+        new = agent.check_denials()
+        denials = tel.denials()
+    finally:
+        tel.stop()
+    g = ev["gpus"][0]
+    assert any(x["pid"] == p.pid for x in g["procs"]), g  # the same UID's process: attributed
+    counters = {k: {tuple(sorted(lab)): v for lab, v in vals.items()} for k, vals in agent.metrics.counters.items()}
+    if os.geteuid() != 0:
+        assert not priv["sufficient"], priv
+        assert denials.get("fd", 0) > 0 and new.get("fd", 0) > 0, denials  # root's processes: refused, counted
+        assert counters["agent_proc_scan_denied"][(("source", "fd"),)] > 0
+        assert recs[0].get("denied") is True and counters["agent_log_read_denied"][()] == 1
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/agent_privileges.json", "w") as f:
+        json.dump({"euid": os.geteuid(), "privileges": priv, "denials": denials, "log_record": recs,
+                   "own_process_attributed": True}, f, indent=1)
