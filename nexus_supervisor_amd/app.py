@@ -79,6 +79,36 @@ def _start_shard_audit(cfg, kube, metrics, log):
     return asyncio.ensure_future(audit_shard_labels(cfg, kube, metrics, log))
 
 
+def _start_shard_relabel(cfg, kube, metrics, log, owned):
+    """``sharding.relabel``: re-stamp the shard label of the runs in ``owned`` (the process
+    that owns the replica's API client only)."""
+    s = cfg.sharding
+    if (not s.shard_label or s.shards <= 1 or not s.relabel or kube is None or not hasattr(kube, "patch_merge")
+            or os.environ.get("NEXUS_WORKER_CONFIG") or not owned):
+        return None
+    from .admission import relabel_owned
+
+    async def go():
+        try:
+            await relabel_owned(cfg, kube, frozenset(owned), metrics, log)
+        except asyncio.CancelledError:
+            raise
+        except Exception as exc:  # noqa: BLE001 - the audit keeps reporting unlabelled runs
+            log.error(exc, "shard re-label pass failed")
+
+    return asyncio.ensure_future(go())
+
+
+async def _start_webhook(cfg, metrics):
+    if not cfg.sharding.webhook_port or os.environ.get("NEXUS_WORKER_CONFIG"):
+        return None
+    from .admission import WebhookServer
+
+    ws = WebhookServer(cfg, metrics)
+    await ws.start(cfg.observability.http_host, cfg.sharding.webhook_port, cfg.sharding.webhook_cert_dir)
+    return ws
+
+
 class Application:
     def __init__(self, cfg: SupervisorConfig, *, kube=None, store: Optional[CheckpointStore] = None,
                  jobs: Optional[JobClient] = None, factory: Optional[InformerFactory] = None, telemetry=None,
@@ -133,7 +163,7 @@ class Application:
             await self.http.start(cfg.observability.http_host, cfg.observability.http_port)
         if cfg.sharding.mode == "lease":
             # one Lease per shard replaces the single leader lease (ha/shards.py)
-            self.shard_leases = make_shard_leases(cfg, self.kube, self.supervisor.set_shards, self.metrics,
+            self.shard_leases = make_shard_leases(cfg, self.kube, self._set_shards, self.metrics,
                                                   on_renewed=self.supervisor.shards.set_deadlines)
         elif cfg.leader_election.enabled:
             from .ha.leader import LeaderElector, LeaseLock
@@ -155,6 +185,16 @@ class Application:
         if self.elector is not None:
             self.elector.start()
         self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
+        self.webhook = await _start_webhook(cfg, self.metrics)
+        if cfg.sharding.mode != "lease":
+            self._relabel = _start_shard_relabel(cfg, self.kube, self.metrics, self.log,
+                                                 self.supervisor.shards.owned)
+
+    def _set_shards(self, owned):
+        gained, lost = self.supervisor.set_shards(owned)
+        if gained:  # their runs may carry labels of another shard count
+            _start_shard_relabel(self.cfg, self.kube, self.metrics, self.log, gained)
+        return gained, lost
 
     def ready(self) -> bool:
         return self.factory is not None and all(i.has_synced() for i in self.factory.informers.values())
@@ -163,8 +203,11 @@ class Application:
         return await self.factory.wait_for_cache_sync(timeout)
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
-        if getattr(self, "_audit", None) is not None:
-            self._audit.cancel()
+        for t in (getattr(self, "_audit", None), getattr(self, "_relabel", None)):
+            if t is not None:
+                t.cancel()
+        if getattr(self, "webhook", None) is not None:
+            await self.webhook.stop()
         if self.elector is not None:
             await self.elector.stop(release=True)
         if self.shard_leases is not None:
@@ -341,6 +384,9 @@ class ShardedApplication:
 
             self.kube = KubeClient.for_config(cfg, self.metrics, schedule=self.pool.qps_schedule)
         self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
+        self.webhook = await _start_webhook(cfg, self.metrics)
+        if not lease_mode:
+            self._relabel = _start_shard_relabel(cfg, self.kube, self.metrics, self.log, self.shards.owned)
 
     def _shard_holds(self, until) -> None:
         """Shard hold deadlines renewed: the workers self-fence on them (no parent round trip)."""
@@ -351,6 +397,8 @@ class ShardedApplication:
         """Shard leases won / lost: the workers fence and replay, the hub re-routes and
         re-lists so the workers receive the runs of gained shards."""
         gained, lost = self.shards.update(owned)
+        if gained:
+            _start_shard_relabel(self.cfg, self.kube, self.metrics, self.log, gained)
         self.pool.set_shards(owned, self.shard_leases.deadlines() if self.shard_leases is not None else None)
         if self.hub is not None:
             self.hub.set_shards(self.shards)
@@ -370,8 +418,11 @@ class ShardedApplication:
         return self.merged_metrics
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
-        if getattr(self, "_audit", None) is not None:
-            self._audit.cancel()
+        for t in (getattr(self, "_audit", None), getattr(self, "_relabel", None)):
+            if t is not None:
+                t.cancel()
+        if getattr(self, "webhook", None) is not None:
+            await self.webhook.stop()
         if self.elector is not None:
             await self.elector.stop(release=True)
         if self.shard_leases is not None:

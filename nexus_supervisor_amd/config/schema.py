@@ -270,6 +270,15 @@ class ShardingConfig:
     # stream (dropped before decode by the native router).  Empty = off.  Jobs without the
     # label are invisible with it on: /metrics shard_label_missing counts them (audit)
     shard_label: str = field(default="", metadata=_k("shard-label"))
+    # serve the mutating admission webhook that stamps shard-label on Nexus Jobs (and their
+    # pod templates) and Pods at CREATE (admission.py; the chart registers it with
+    # failurePolicy: Ignore); 0 = off
+    webhook_port: int = field(default=0, metadata=_k("webhook-port"))
+    # tls.crt / tls.key of the webhook's serving certificate (a Secret mounted here)
+    webhook_cert_dir: str = field(default="/etc/nexus/webhook-tls", metadata=_k("webhook-cert-dir"))
+    # at startup (static mode) / on gaining a shard (lease mode): re-stamp the label of this
+    # replica's runs whose label was computed for another shard count
+    relabel: bool = field(default=True, metadata=_k("relabel"))
 
 
 @dataclass

@@ -194,6 +194,34 @@ class _Watcher:
             self.wake = None
 
 
+def json_patch(obj: Dict[str, Any], ops) -> Dict[str, Any]:
+    """RFC 6902 ``add`` / ``replace`` / ``remove`` over JSON-pointer paths (what mutating
+    webhooks send); returns a patched deep copy."""
+    out = copy.deepcopy(obj)
+    for op in ops:
+        parts = [p.replace("~1", "/").replace("~0", "~") for p in op["path"].split("/")[1:]]
+        cur = out
+        for p in parts[:-1]:
+            cur = cur[int(p)] if isinstance(cur, list) else cur[p]
+        last = parts[-1]
+        if op["op"] in ("add", "replace"):
+            if isinstance(cur, list):
+                idx = len(cur) if last == "-" else int(last)
+                if op["op"] == "add":
+                    cur.insert(idx, op["value"])
+                else:
+                    cur[idx] = op["value"]
+            else:
+                if op["op"] == "replace" and last not in cur:
+                    raise KeyError(op["path"])
+                cur[last] = op["value"]
+        elif op["op"] == "remove":
+            del cur[int(last) if isinstance(cur, list) else last]
+        else:
+            raise ValueError(f"unsupported patch op {op['op']}")
+    return out
+
+
 class FakeApiServer:
     def __init__(self, *, token: str = "", history: int = 200_000, bookmark_interval: float = 1.0,
                  gc_pods_on_job_delete: bool = True):
@@ -207,6 +235,9 @@ class FakeApiServer:
         self.watchers: Dict[str, Set[_Watcher]] = {k: set() for k in RESOURCES}
         self.rv = 1000
         self.deleted: List[Tuple[str, str, str, str]] = []  # (kind, ns, name, propagation)
+        self.mutating_webhooks: List[Tuple[str, frozenset, Any]] = []  # (url, kinds, ssl context)
+        self.webhook_calls = 0
+        self.webhook_failures = 0
         self._pods_by_job: Dict[Tuple[str, str], Set[str]] = {}  # (ns, job-name label) -> pod names (GC index)
         self.fail_next: Dict[Tuple[str, str], int] = {}  # (method, kind) -> count of 500s to inject
         # (method, kind) -> count of 429s to inject, each with ``Retry-After: retry_after``
@@ -589,6 +620,36 @@ class FakeApiServer:
             return self._status(404, "NotFound", f'{kind.lower()}s "{req.match_info["name"]}" not found')
         return web.json_response(obj)
 
+    def add_mutating_webhook(self, url: str, kinds=("Job", "Pod"), ssl_ctx=None) -> None:
+        """Call ``url`` (an AdmissionReview v1 endpoint) on every API CREATE of ``kinds``
+        and apply its JSON patch, as the API server's mutating admission does;
+        ``failurePolicy: Ignore`` — an unreachable or failing webhook admits unchanged."""
+        self.mutating_webhooks.append((url, frozenset(kinds), ssl_ctx))
+
+    async def _mutate(self, obj: Dict[str, Any]) -> Dict[str, Any]:
+        import aiohttp
+
+        for url, kinds, ctx in self.mutating_webhooks:
+            if obj.get("kind") not in kinds:
+                continue
+            review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": {
+                "uid": uuid.uuid4().hex, "kind": {"group": "batch" if obj["kind"] == "Job" else "",
+                                                  "version": "v1", "kind": obj["kind"]},
+                "operation": "CREATE", "namespace": obj["metadata"].get("namespace", ""), "object": obj}}
+            try:
+                async with aiohttp.ClientSession() as s:
+                    async with s.post(url, json=review, ssl=ctx, timeout=aiohttp.ClientTimeout(total=5)) as r:
+                        resp = (await r.json()).get("response") or {}
+            except Exception:  # noqa: BLE001 - failurePolicy: Ignore
+                self.webhook_failures += 1
+                continue
+            self.webhook_calls += 1
+            if resp.get("patchType") == "JSONPatch" and resp.get("patch"):
+                import base64
+
+                obj = json_patch(obj, json.loads(base64.b64decode(resp["patch"])))
+        return obj
+
     async def _h_create(self, req: web.Request):
         bad = await self._pre(req, "POST")
         if bad is not None:
@@ -597,6 +658,8 @@ class FakeApiServer:
         obj = await req.json()
         obj["kind"] = kind
         obj.setdefault("metadata", {})["namespace"] = req.match_info["ns"]
+        if self.mutating_webhooks:
+            obj = await self._mutate(obj)
         try:
             return web.json_response(self.create(obj), status=201)
         except KeyError:
