@@ -104,6 +104,11 @@ def parse_args(argv=None):
     ap.add_argument("--two-step-write", action="store_true", help="alias of --actuation two-step")
     ap.add_argument("--conditional-update", choices=("auto", "always", "never"), default="auto",
                     help="compat.conditional-update of the two-step path (never = the reference's plain writes)")
+    ap.add_argument("--slot-mode", choices=("auto", "node", "replica"), default="auto",
+                    help="node (auto for N>1): ONE supervisor replica and ONE GPU monitor on rank 0 supervise every "
+                         "GPU slot of the node — each rank is a slot whose runs are on its GPU and whose real "
+                         "HBM-OOM must be attributed to that physical GPU (the production shape: one HA "
+                         "supervisor, one node agent); replica: one replica + monitor + apiserver per slot")
     ap.add_argument("--cluster", choices=("auto", "shared", "per-rank"), default="auto",
                     help="per-rank (default) = each GPU-job slot's replica has its own namespace shard, apiserver "
                          "simulator and CQL server; shared = one apiserver + one CQL server for all ranks, each "
@@ -177,13 +182,25 @@ def real_hbm_oom(local_rank: int, workdir: str):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    import faulthandler
+    import signal
+
+    try:  # diagnostics: `kill -USR1 <pid>` dumps the stacks
+        faulthandler.register(signal.SIGUSR1, all_threads=True)
+    except (ValueError, OSError, AttributeError):  # stderr without a file descriptor (pytest capture)
+        pass
     if args.diag_slow_callback_ms > 0:  # read by the replica parent and inherited by its workers
         os.environ["NEXUS_SLOW_CALLBACK_MS"] = str(args.diag_slow_callback_ms)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    slot_mode = args.slot_mode if args.slot_mode != "auto" else (
+        "node" if world > 1 and args.transport == "wire" else "replica")
+    if slot_mode == "node" and args.transport != "wire":
+        raise SystemExit("--slot-mode node needs --transport wire")
     if args.procs <= 0:
-        args.procs = auto_procs(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+        # node mode: the one replica gets the node's CPU share (the other ranks only run GPU work)
+        args.procs = auto_procs(1 if slot_mode == "node" else int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
 
     import torch
 
@@ -222,7 +239,22 @@ def main(argv=None) -> int:
         dist.broadcast_object_list(box, src=0)
         return box[0]
 
+    def oom_phase():
+        """Node mode, every rank at once: a real HBM-OOM on this rank's GPU (the text a
+        default pod on it would log), gathered on every rank."""
+        barrier_sync()
+        t0 = time.time()
+        msg = real_hbm_oom(local_rank, workdir) if has_gpu else None
+        mine = {"slot": rank, "message": msg, "real": bool(msg), "t0": t0, "t1": time.time()}
+        if dist is None:
+            return [mine]
+        out = [None] * world
+        dist.all_gather_object(out, mine)
+        return out
+
     cluster = args.cluster if args.cluster != "auto" else "per-rank"
+    if slot_mode == "node" and world > 1:
+        cluster = "node"
     cfg = BenchConfig(rank=rank, world=world, local_rank=local_rank, jobs=args.jobs, events=args.events,
                       steps=args.steps, warmup=args.warmup, transport=args.transport, profile=args.profile,
                       workers=args.workers, seed=args.seed, hip_oom_message=hip_msg, telemetry="amdsmi" if has_gpu else "fake",
@@ -236,15 +268,16 @@ def main(argv=None) -> int:
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster, run_starts=args.workload == "lifecycle",
-                      pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz)
-    res = asyncio.run(run_rank(cfg, barrier_sync, share))
+                      pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz, slot_mode=slot_mode)
+    res = asyncio.run(run_rank(cfg, barrier_sync, share, oom_phase if slot_mode == "node" and world > 1 else None))
 
     elapsed = res["elapsed"]
     rb = res.get("readback") or {}
     wobj = res.get("watch_objects_per_failure")
     stats = torch.tensor([elapsed, float(res["events"]), float(res["errors"]), float(res["wrong_stage"]),
                           float(rb.get("checked", 0)), float(rb.get("wrong", 0)), float(res.get("starts", 0)),
-                          float(res.get("failures", 0)), float(wobj if wobj is not None else 0.0)],
+                          float(res.get("failures", 0)), float(wobj if wobj is not None else 0.0),
+                          1.0 if wobj is not None else 0.0],
                          dtype=torch.float64, device=device)
 
     def gather_all(values):
@@ -271,7 +304,9 @@ def main(argv=None) -> int:
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         max_elapsed, total_events, total_errors = mx[0].item(), sm[1].item(), sm[2].item()
         wrong_stage, rb_checked, rb_wrong = sm[3].item(), sm[4].item(), sm[5].item()
-        total_starts, total_failures, watch_objects = sm[6].item(), sm[7].item(), sm[8].item() / world
+        # the mean over the ranks that measured it (node mode: rank 0's simulator only)
+        total_starts, total_failures = sm[6].item(), sm[7].item()
+        watch_objects = sm[8].item() / sm[9].item() if sm[9].item() else None
     else:
         max_elapsed, total_events, total_errors = elapsed, float(res["events"]), float(res["errors"])
         wrong_stage, rb_checked, rb_wrong = float(res["wrong_stage"]), float(rb.get("checked", 0)), float(rb.get("wrong", 0))
@@ -343,7 +378,15 @@ def main(argv=None) -> int:
                 "model": "nexus-supervisor (informer→classify→CQL write), 1 replica-shard per GPU-job slot",
                 "global_batch": args.events * world,
                 "seq_len": None,
-                "parallelism": f"shard{world}x{args.procs if args.transport == 'wire' else 1}proc",
+                "parallelism": (f"node{world}slots:1replica:{args.procs}proc" if cluster == "node" else
+                                f"shard{world}x{args.procs if args.transport == 'wire' else 1}proc"),
+                "slot_mode": slot_mode,
+                # GPU monitors over the node's GPUs: one (rank 0's, the node agent's role) in
+                # node mode, one per rank otherwise
+                "gpu_monitors": 1 if cluster == "node" or world == 1 else world,
+                "monitor": res.get("monitor"),
+                # node mode: every slot's real HBM-OOM, at once, attributed to its physical GPU
+                "attribution": res.get("attribution"),
                 "cluster": cluster if args.transport == "wire" else "in-process",
                 "shard_label": (not args.no_shard_label) if cluster == "shared" and world > 1 else None,
                 "concurrent_jobs_per_rank": args.jobs,

@@ -41,6 +41,12 @@ import time
 from aiohttp import web
 
 
+# watch lines per /sim/apply request: the simulator applies a request in one pass of its
+# event loop, so a whole 20k-line step in one request would hold every watch flush, Job
+# DELETE and pods/log answer for its duration (tens of ms); chunks interleave with them
+APPLY_CHUNK = int(os.environ.get("NEXUS_BENCH_APPLY_CHUNK", "1024"))
+
+
 async def amain(args) -> None:
     from ..store.cql import CqlCheckpointStore, CqlSession
     from ..testing.fake_apiserver import FakeApiServer
@@ -58,12 +64,20 @@ async def amain(args) -> None:
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)
 
+    async def apply_chunks(bodies):
+        """Apply pre-encoded chunks in order; the step's push time is the first commit."""
+        t = None
+        for b in bodies:
+            doc = await simctl.apply_raw(b)
+            t = doc["t_push"] if t is None else t
+        return t if t is not None else time.monotonic()
+
     async def apply(events):
         """Commit watch traffic to the API server; returns the commit (push) time."""
         if simctl is not None:
             t = None
-            for i in range(0, len(events), 4096):
-                doc = await simctl.apply(events[i:i + 4096])
+            for i in range(0, len(events), APPLY_CHUNK):
+                doc = await simctl.apply(events[i:i + APPLY_CHUNK])
                 t = doc["t_push"] if t is None else t
             return t if t is not None else time.monotonic()
         t = time.monotonic()
@@ -96,14 +110,19 @@ async def amain(args) -> None:
         indexes = p.get("shard_indexes")
         if indexes is None:
             indexes = [int(p.get("shard_index", 0))]
+        node_slots = int(p.get("node_slots", 0))
+        if node_slots:
+            indexes = list(range(node_slots))  # node mode: one workload per GPU slot, one replica
         total = 0
         for k in indexes:
-            # per-rank mode: the rank's workload (rank = its shard); shared mode: one per shard
+            # per-rank mode: the rank's workload (rank = its shard); shared mode: one per shard;
+            # node mode: slot k's runs on GPU k (one replica owns every slot: no shard filter)
             wl = Workload(p.get("jobs", 10_000), rank=k if len(indexes) > 1 else p.get("rank", 0),
                           world=p.get("world", 1), seed=p.get("seed", 0),
-                          hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM, shards=n_shards, shard_index=k,
+                          hip_oom_message=p.get("hip_oom_message") or DEFAULT_HIP_OOM,
+                          shards=1 if node_slots else n_shards, shard_index=0 if node_slots else k,
                           shard_label=p.get("shard_label") or "", hbm_shape=p.get("hbm_shape") or "termination-message",
-                          run_starts=bool(p.get("run_starts", True)))
+                          run_starts=bool(p.get("run_starts", True)), visible_devices=str(k) if node_slots else None)
             objs, rows = wl.initial()
             await write_rows(rows)
             await apply([("ADDED", o) for o in objs])
@@ -118,7 +137,8 @@ async def amain(args) -> None:
                 for _ in range(pregen):
                     st = wl.step(events)
                     await write_rows(st.rows)
-                    sh.pregen.append((events, st, encode_events(st.traffic)))
+                    sh.pregen.append((events, st, [encode_events(st.traffic[i:i + APPLY_CHUNK])
+                                                   for i in range(0, len(st.traffic), APPLY_CHUNK)]))
                     st.traffic = None  # encoded: only the ids and expected stages are kept
         # the simulated cluster holds the same 10k-run heap as the supervisor: keep it out
         # of full collections so the generator never paces the measured process
@@ -174,7 +194,7 @@ async def amain(args) -> None:
             # now and let the supervisor absorb that burst (thousands of ADDED lines) before the
             # first timed arrival, instead of inside it
             while sh.pregen:
-                await simctl.apply_raw(sh.pregen.popleft()[2])
+                await apply_chunks(sh.pregen.popleft()[2])
             nxt, sh.next = sh.next, None
             if nxt is not None:
                 # its runs' starts and failures are part of the workload's state now: the
@@ -204,13 +224,13 @@ async def amain(args) -> None:
         queue = sh.pregen
         if queue and queue[0][0] == events and sh.next is None:
             _, st, body = queue.popleft()
-            doc = await simctl.apply_raw(body)
-            return st.doc(doc["t_push"])
+            t_push = await apply_chunks(body)
+            return st.doc(t_push)
         if queue:
             # a step of another size (latency probe): the pre-generated steps' runs are live
             # in the workload already, so they must exist in the cluster before we diverge
             while queue:
-                await simctl.apply_raw(queue.popleft()[2])
+                await apply_chunks(queue.popleft()[2])
         nxt, sh.next = sh.next, None
         if nxt is not None and nxt[0] == events:
             st = await nxt[1]
@@ -226,6 +246,24 @@ async def amain(args) -> None:
         sh.next = (events, asyncio.ensure_future(prepare(wl, events)))
         return st.doc(t_push)
 
+    async def h_oom(req):
+        """One running run of slot ``slot`` dies of an HBM-OOM whose text is ``message`` (a
+        real OOM's, from that slot's GPU): ``{"rids", "t_push", "expected"}``."""
+        p = await req.json()
+        sh = shards[int(p["slot"])]
+        async with sh.lock:
+            # the slot's pending steps must exist in the cluster before the workload diverges
+            while sh.pregen:
+                await apply_chunks(sh.pregen.popleft()[2])
+            nxt, sh.next = sh.next, None
+            if nxt is not None:
+                stale = await nxt[1]
+                await apply(stale.traffic)
+            st = sh.wl.fail_with("hbm-oom", p.get("message"))
+            await write_rows(st.rows)
+            t_push = await apply(st.traffic)
+        return web.json_response(st.doc(t_push))
+
     async def h_stats(req):
         if simctl is not None:
             return web.json_response(await simctl.stats())
@@ -238,6 +276,7 @@ async def amain(args) -> None:
     ctl.router.add_post("/bench/init", h_init)
     ctl.router.add_post("/bench/step", h_step)
     ctl.router.add_post("/bench/probe", h_probe)
+    ctl.router.add_post("/bench/oom", h_oom)
     ctl.router.add_get("/bench/stats", h_stats)
     runner = web.AppRunner(ctl, access_log=None)
     await runner.setup()

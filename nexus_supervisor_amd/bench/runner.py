@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import asyncio
 import gc
+import json
+import os
 import resource
 import time
 from dataclasses import dataclass
@@ -35,7 +37,7 @@ class BenchConfig:
     hip_oom_message: Optional[str] = None
     telemetry: str = "fake"
     workdir: str = "/tmp"
-    step_timeout: float = 300.0
+    step_timeout: float = float(os.environ.get("NEXUS_BENCH_STEP_TIMEOUT", "300"))
     cql_latency_us: int = 0
     api_latency_us: int = 0  # simulated apiserver answer latency of object requests (kubesim)
     api_write_qps: float = 0.0  # APF-like cap on the simulator's mutating requests (429 + Retry-After)
@@ -63,6 +65,14 @@ class BenchConfig:
     # new runs go Pending -> Running with the kubelet's Events (a ToRunning decision each);
     # False: the failure-only shape of round 4
     run_starts: bool = True
+    # "replica": one replica (and GPU monitor) per GPU slot, each with its own shard; "node":
+    # ONE replica and ONE monitor on rank 0 supervise every slot of the node (the production
+    # shape: an HA supervisor and one node agent), the other ranks only run their GPU's work
+    slot_mode: str = "replica"
+
+    @property
+    def node(self) -> bool:
+        return self.slot_mode == "node" and self.world > 1
 
 
 def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
@@ -75,8 +85,8 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
     else:
         sc.workers, sc.rate_limit_elements_per_second, sc.rate_limit_elements_burst = cfg.workers, 0, 1_000_000
         sc.kube_qps, sc.kube_burst = cfg.kube_qps, max(1, int(min(cfg.kube_qps, 1_000_000)))
-    sc.sharding.shards = cfg.world
-    sc.sharding.shard_index = cfg.rank
+    sc.sharding.shards = 1 if cfg.node else cfg.world
+    sc.sharding.shard_index = 0 if cfg.node else cfg.rank
     if cfg.cluster == "shared" and cfg.world > 1:
         sc.sharding.shard_label = cfg.shard_label
     sc.resync_period = 0.0
@@ -116,6 +126,8 @@ class Tracker:
         self.record = False
         self.failures = 0  # recorded decisions acknowledged
         self.starts = 0
+        self.superseded = 0  # starts whose run's failure was decided first
+        self.failed_rids: set = set()
         # recorded decisions' push→ack decomposition (ms): api (push → hub read), hub (→ worker
         # frame), feed (→ decoded), dispatch (→ handler), classify (handler → enqueue, with any
         # log-tail wait), queue (→ dequeue), actuate (→ checkpoint ack)
@@ -133,6 +145,14 @@ class Tracker:
         # the metric is pod-fail → checkpoint *write ack* (the Job DELETE follows the write)
         t = ack or time.monotonic()
         key = (rid, stage == _RUNNING)
+        if not key[1]:
+            # the run's failure was decided: a start still waiting for its ToRunning is
+            # superseded (a finished row suppresses a later ToRunning — IsFinished, as in the
+            # reference — when the failure overtook the Started Event on another stream)
+            self.failed_rids.add(rid)
+            sst = self.owner.pop((rid, True), None)
+            if sst is not None:
+                sst.supersede(self, (rid, True))
         st = self.owner.pop(key, None)
         if st is None:
             # raced ahead of the step response (or a duplicate: the pod-status rule's ToRunning
@@ -161,6 +181,8 @@ class Tracker:
             a = self.acks.pop(key, None)
             if a is not None:
                 st.settle(self, key, *a)
+            elif key[1] and key[0] in self.failed_rids:
+                st.supersede(self, key)
             else:
                 self.owner[key] = st
         if not st.waiting:
@@ -168,6 +190,10 @@ class Tracker:
         return st
 
     def abandon(self, st: "StepState") -> None:
+        import sys
+
+        print(f"[bench] step abandoned: {len(st.waiting)} decisions never acknowledged, e.g. "
+              f"{sorted(st.waiting)[:5]}", file=sys.stderr, flush=True)
         self.errors += len(st.waiting)
         for key in st.waiting:
             self.owner.pop(key, None)
@@ -184,6 +210,12 @@ class StepState:
         self.record = record
         self.expected = expected
         self.done = asyncio.Event()
+
+    def supersede(self, tr: Tracker, key) -> None:
+        self.waiting.discard(key)
+        tr.superseded += 1
+        if not self.waiting:
+            self.done.set()
 
     def settle(self, tr: Tracker, key, t: float, outcome: str, stage: Optional[str] = None, x=None) -> None:
         self.waiting.discard(key)
@@ -258,15 +290,112 @@ class InProcHarness:
         return {}
 
 
+def _dump_tasks_on_sigusr2() -> None:
+    """Diagnostics: ``kill -USR2 <rank pid>`` prints every pending asyncio task's stack."""
+    import signal
+    import sys
+
+    def dump():
+        for t in asyncio.all_tasks():
+            print(f"--- task {t.get_name()}", file=sys.stderr)
+            t.print_stack(limit=8, file=sys.stderr)
+
+    try:
+        asyncio.get_running_loop().add_signal_handler(signal.SIGUSR2, dump)
+    except (NotImplementedError, RuntimeError):  # pragma: no cover - non-Unix / no loop
+        pass
+
+
+def monitor_cost(telemetry, seconds: float = 2.0) -> Optional[Dict[str, Any]]:
+    """CPU of the GPU monitor per sample (this process otherwise idle): what one node
+    agent's sampling of every local GPU costs."""
+    s0 = getattr(telemetry, "samples", None)
+    if not isinstance(s0, int):
+        return None
+    c0 = time.process_time()
+    time.sleep(seconds)
+    n = telemetry.samples - s0
+    if n <= 0:
+        return None
+    return {"gpus": len(telemetry.devices()), "samples": n, "interval_ms": round(1000 * telemetry.interval, 1),
+            "cpu_us_per_sample": round((time.process_time() - c0) * 1e6 / n, 1)}
+
+
+async def run_slot(cfg: BenchConfig, barrier_sync: Callable[[], None],
+                   oom_phase: Optional[Callable[[], Any]] = None) -> Dict[str, Any]:
+    """Node mode, ranks > 0: the GPU slot's own work only (its real HBM-OOM in the
+    attribution phase); the collectives mirror rank 0's :func:`run_rank`."""
+    barrier_sync()  # timed region starts
+    barrier_sync()  # ... and ends
+    if oom_phase is not None:
+        await asyncio.get_running_loop().run_in_executor(None, oom_phase)
+    return {"elapsed": 0.0, "events": 0, "errors": 0, "failures": 0, "starts": 0, "start_latencies_ms": [],
+            "watch_objects_per_failure": None, "wrong_stage": 0, "wrong_examples": [], "readback": {"checked": 0},
+            "latencies_ms": [], "store": None, "workers": 0, "actuation": None, "eps": None, "kube_qps": None,
+            "telemetry": None, "stages": {}, "cpu": {}, "probe": None, "step_done_ms": []}
+
+
+async def _node_attribution(harness, tracker: "Tracker", telemetry, ooms: List[Dict[str, Any]],
+                            cfg: "BenchConfig") -> Dict[str, Any]:
+    """Every slot's GPU ran out of HBM at about the same time (a real OOM on an MI355X, or the
+    synthetic text on CPU); one run per slot dies with its slot's message.  The single
+    replica must write each as hbm-oom on the *physical* GPU of that slot."""
+    from ..gpu.telemetry import FakeTelemetry
+
+    if isinstance(telemetry, FakeTelemetry):  # CPU: each slot's GPU filled for the monitor
+        for o in ooms:
+            telemetry.set_vram(o["slot"], int(telemetry.devices()[o["slot"]]["vram_total_mb"] * 0.99))
+    saved, tracker.latencies = tracker.latencies, []
+    states, slot_of = [], {}
+    for o in sorted(ooms, key=lambda x: x["slot"]):
+        d = await harness.oom(o["slot"], o.get("message"))
+        for rid in d["rids"]:
+            slot_of[rid] = o["slot"]
+        states.append(tracker.arm(d["rids"], d["t_push"], d.get("expected")))
+    for st in states:
+        try:
+            await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
+        except asyncio.TimeoutError:
+            tracker.abandon(st)
+    lat = tracker.latencies
+    tracker.latencies = saved
+    rows = await harness.read_rows(harness.algorithm, list(slot_of))
+    per = []
+    for rid, slot in sorted(slot_of.items(), key=lambda kv: kv[1]):
+        row = rows.get(rid)
+        trace = {}
+        try:
+            trace = json.loads(row.algorithm_failure_details) if row is not None else {}
+        except ValueError:
+            pass
+        g = (trace.get("oom") or {}).get("gpu_index")
+        per.append({"slot": slot, "stage": row.lifecycle_stage if row else None, "class": trace.get("class"),
+                    "gpu_index": g, "correct": g == slot and trace.get("class") == "hbm-oom",
+                    "real_oom": bool(next((o for o in ooms if o["slot"] == slot), {}).get("real"))})
+    out = {"slots": len(per), "correct": sum(1 for p in per if p["correct"]), "per_slot": per}
+    if lat:
+        ls = sorted(lat)
+        out["p50_ms"] = round(ls[len(ls) // 2], 3)
+        out["max_ms"] = round(ls[-1], 3)
+    return out
+
+
 async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
-                   share: Optional[Callable[[Any], Any]] = None) -> Dict[str, Any]:
+                   share: Optional[Callable[[Any], Any]] = None,
+                   oom_phase: Optional[Callable[[], Any]] = None) -> Dict[str, Any]:
     """One rank of the bench.  ``share(obj)`` returns rank 0's ``obj`` on every rank (the
-    shared-cluster rendezvous); ``barrier_sync`` brackets the timed region."""
+    shared-cluster rendezvous); ``barrier_sync`` brackets the timed region.  Node mode
+    (``cfg.node``): rank 0 runs the one replica and monitor for every slot; ``oom_phase``
+    (a collective: each rank's real OOM on its GPU) feeds the per-GPU attribution check."""
     from ..gpu.telemetry import FakeTelemetry, make_telemetry, pod_evidence_provider
 
+    _dump_tasks_on_sigusr2()
+    if cfg.node and cfg.rank != 0:
+        return await run_slot(cfg, barrier_sync, oom_phase)
     sc = supervisor_config(cfg)
     telemetry = make_telemetry(cfg.telemetry) if cfg.telemetry != "fake" else FakeTelemetry()
     telemetry.start()
+    monitor = await asyncio.get_running_loop().run_in_executor(None, monitor_cost, telemetry)
     if cfg.transport == "inproc":
         harness = InProcHarness(sc, cfg)
     else:
@@ -300,12 +429,14 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
 
             for _ in range(n):
                 while len(pending) >= cfg.inflight:
-                    await finish(pending.pop(0))
-                doc = await harness.step(cfg.events)
-                pending.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
-                                           doc.get("start_expected")))
-            for st in pending:
-                await finish(st)
+                    for st in pending.pop(0):
+                        await finish(st)
+                docs = await harness.step(cfg.events)
+                pending.append([tracker.arm(d["rids"], d["t_push"], d.get("expected"), d.get("started"),
+                                            d.get("start_expected")) for d in (docs if isinstance(docs, list) else [docs])])
+            for sts in pending:
+                for st in sts:
+                    await finish(st)
 
         await run_steps(cfg.warmup)
         gc.collect()
@@ -338,10 +469,13 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         for k in x1:
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
         s1 = await sim_stats() if s0 else None
+        if os.environ.get("NEXUS_BENCH_DEBUG"):
+            print("[bench] sim stats", s0, s1, file=__import__("sys").stderr)
         watch_objects = None
         if s0 and s1:
             # shared cluster: the simulator serves every rank's failures
-            n_ev = max(cfg.events * cfg.steps * (cfg.world if getattr(harness, "shared", False) else 1), 1)
+            # shared cluster / node mode: the simulator serves every slot's failures
+            n_ev = max(cfg.events * cfg.steps * (cfg.world if getattr(harness, "shared", False) or cfg.node else 1), 1)
             for k in ("requests", "loops", "sends"):
                 cpu[f"kubesim_{k}_per_event"] = round((s1.get(k, 0) - s0.get(k, 0)) / n_ev, 3)
             # every committed change (ADDED / MODIFIED / DELETED of an Event, Pod or Job — the
@@ -363,7 +497,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         # also the bench driver — plus its shard workers), whole-run CPU seconds ÷ failures.
         # The decision-report channel (workers → parent → tracker; it exists only so the bench
         # can time every decision) is measured in the parent and reported on its own line
-        n_ev = max(cfg.events * cfg.steps, 1)
+        n_ev = max(cfg.events * cfg.steps * (cfg.world if cfg.node else 1), 1)  # node mode: every slot's
         report_s = getattr(pool, "report_cpu_s", 0.0) - r0
         cpu["bench_report_cpu_us_per_event"] = round(report_s * 1e6 / n_ev, 1)
         sup_cpu = cpu["supervisor_util"] * elapsed - report_s + sum(workers) * elapsed
@@ -382,8 +516,6 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 f.write(prof.top(40))
             pool = getattr(getattr(harness, "app", None), "pool", None)
             if pool is not None:
-                import os
-
                 pool.broadcast({"op": "pprof", "on": False, "path": cfg.pprof_out})
                 want = [f"{cfg.pprof_out}.w{w.index}.top.txt" for w in pool.workers]
                 for _ in range(100):
@@ -403,6 +535,10 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             sizes = (sup.metrics.gauges.get("worker_gpu_update_bytes") or {}).values()
             cpu["worker_gpu_update_bytes_max"] = max(sizes, default=None)
         readback = await _read_back(harness, tracker)
+        attribution = None
+        if cfg.node and oom_phase is not None:
+            ooms = await asyncio.get_running_loop().run_in_executor(None, oom_phase)
+            attribution = await _node_attribution(harness, tracker, telemetry, ooms, cfg)
         probe = None
         if cfg.probe_events > 0:
             before = _stage_counts(sup)
@@ -421,14 +557,15 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             sampler.stop()
         await harness.stop()
         telemetry.stop()
-    return {"elapsed": elapsed, "events": cfg.events * cfg.steps, "errors": tracker.errors,
+    return {"elapsed": elapsed, "events": cfg.events * cfg.steps * (cfg.world if cfg.node else 1), "errors": tracker.errors,
             "failures": timed[0], "starts": timed[1], "start_latencies_ms": timed[2],
+            "starts_superseded": tracker.superseded,
             "watch_objects_per_failure": watch_objects,
             "wrong_stage": tracker.wrong_stage, "wrong_examples": tracker.wrong_examples, "readback": readback,
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
             "actuation": _actuation(sc),
             "eps": sc.rate_limit_elements_per_second, "kube_qps": sc.kube_qps, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
-            "probe": probe, "step_done_ms": step_done_ms}
+            "probe": probe, "step_done_ms": step_done_ms, "monitor": monitor, "attribution": attribution}
 
 
 async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dict[str, Any]:

@@ -32,6 +32,7 @@ from ..kube.client import KubeClient, KubeConfig
 from ..models.checkpoint import create_index_cql, create_table_cql
 from ..store.cql import CqlCheckpointStore, CqlSession
 from ..testing.cqlsrv import CqlServer
+from ..utils.proc import die_with_parent
 
 
 def schema_statements(ks: str = "nexus", table: str = "checkpoints") -> List[str]:
@@ -55,7 +56,10 @@ class WireHarness:
         self.app: Application = None
         self.ctl = ""
         self.http: aiohttp.ClientSession = None
-        self.shared = cfg.cluster == "shared" and cfg.world > 1
+        # node mode: ONE replica (this rank's) supervises every GPU slot of the node; the
+        # cluster holds one workload per slot (slot k's pods on GPU k)
+        self.node = getattr(cfg, "slot_mode", "replica") == "node" and cfg.world > 1
+        self.shared = cfg.cluster == "shared" and cfg.world > 1 and not self.node
         self.share = share or (lambda obj: obj)
         self.barrier = barrier or (lambda: None)
         self.owner = not self.shared or cfg.rank == 0  # this rank runs the harness servers
@@ -77,14 +81,15 @@ class WireHarness:
         env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
         self._log = open(os.path.join(self.workdir, "cluster.log"), "ab")
         # the apiserver's watch cache scales with the traffic it must hold (every shard's)
-        history = 50_000 * (cfg.world if self.shared else 1)
+        history = 50_000 * (cfg.world if self.shared or self.node else 1)
         self.proc = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd.bench.cluster_proc", "--cql",
                                       f"127.0.0.1:{self.cql.port}", "--ready-file", ready, "--history", str(history),
                                       # every rank's replica watches the shared namespace: fan out in parallel
                                       "--flush-threads", str(min(8, cfg.world) if self.shared else 1),
                                       "--api-latency-us", str(int(cfg.api_latency_us)),
                                       "--write-qps", str(float(cfg.api_write_qps))],
-                                     env=env, stdout=self._log, stderr=self._log, start_new_session=True)
+                                     env=env, stdout=self._log, stderr=self._log, start_new_session=True,
+                                     preexec_fn=die_with_parent())
         deadline = time.monotonic() + 120
         while not os.path.exists(ready):
             if self.proc.poll() is not None or time.monotonic() > deadline:
@@ -100,6 +105,7 @@ class WireHarness:
                     "hip_oom_message": cfg.hip_oom_message,
                     "shard_label": self.sc.sharding.shard_label if self.shared else "",
                     "hbm_shape": cfg.hbm_shape, "run_starts": cfg.run_starts,
+                    "node_slots": cfg.world if self.node else 0,
                     "pregen": cfg.warmup + cfg.steps if cfg.pregen else 0, "events": cfg.events}) as r:
                 r.raise_for_status()
                 await r.json()
@@ -146,14 +152,30 @@ class WireHarness:
     def supervisor(self):
         return self.app.supervisor
 
-    async def step(self, events: int, respond_after_ms: float = 0.0) -> Dict[str, Any]:
-        """One step: ``{"rids", "t_push", "expected", "started", "start_expected"}``."""
-        body = {"events": events, "shard": self.cfg.rank}
+    async def step(self, events: int, respond_after_ms: float = 0.0, shard: Optional[int] = None):
+        """One step: ``{"rids", "t_push", "expected", "started", "start_expected"}`` — in node
+        mode one per GPU slot (a list), the slots' steps pushed concurrently."""
+        if self.node and shard is None:
+            return list(await asyncio.gather(*(self.step(events, respond_after_ms, k) for k in range(self.cfg.world))))
+        body = {"events": events, "shard": self.cfg.rank if shard is None else shard}
         if respond_after_ms:
             body["respond_after_ms"] = respond_after_ms
         async with self.http.post(self.ctl + "/bench/step", json=body) as r:
             r.raise_for_status()
             return await r.json()
+
+    async def oom(self, slot: int, message: Optional[str]) -> Dict[str, Any]:
+        """A run of GPU slot ``slot`` dies of an HBM-OOM with the real ``message`` of that GPU."""
+        async with self.http.post(self.ctl + "/bench/oom", json={"slot": slot, "message": message}) as r:
+            r.raise_for_status()
+            return await r.json()
+
+    async def read_rows(self, algorithm: str, rids: List[str]) -> Dict[str, Any]:
+        """Full rows (stage, cause, trace) of ``rids`` as the CQL server holds them."""
+        if self.readback is None:
+            self.readback = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql_port)], connections_per_host=2))
+            await self.readback.connect()
+        return {rid: await self.readback.read_checkpoint(algorithm, rid) for rid in rids}
 
     async def probe(self, n: int, rate_per_min: float, seed: int) -> List[Dict[str, Any]]:
         """The open-loop probe played by the cluster process (one request for all ``n``

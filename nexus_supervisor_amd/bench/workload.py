@@ -114,7 +114,8 @@ class Workload:
     def __init__(self, concurrent_jobs: int = 10_000, rank: int = 0, world: int = 1, seed: int = 0,
                  labels: Optional[LabelConfig] = None, namespace: str = "nexus", algorithm: str = "bench-algorithm",
                  hip_oom_message: str = DEFAULT_HIP_OOM, gpus_per_node: int = 8, shards: int = 1, shard_index: int = 0,
-                 shard_label: str = "", hbm_shape: str = "termination-message", run_starts: bool = True):
+                 shard_label: str = "", hbm_shape: str = "termination-message", run_starts: bool = True,
+                 visible_devices: Optional[str] = None):
         self.rng = random.Random(seed * 7919 + rank)
         self.labels = labels or LabelConfig()
         self.ns = namespace
@@ -131,6 +132,10 @@ class Workload:
         self.hbm_shape = hbm_shape
         # False: the round-4 shape — new runs are ADDED and never start (rows seeded RUNNING)
         self.run_starts = run_starts
+        # the pods' HIP_VISIBLE_DEVICES: None = every GPU of the node (an 8-way torchrun job's
+        # rank on this slot), or one GPU ("3": a node-mode slot whose pods the device plugin
+        # gave GPU 3 — a process there calls it "GPU 0")
+        self.visible_devices = visible_devices
         # sharding.shard-label: the submitter stamps each run's shard on its Job and pod template
         self.shard_label = shard_label if shards > 1 else ""
         self.live: List[str] = []      # running runs (may fail)
@@ -172,7 +177,8 @@ class Workload:
         local = self.rank % self.gpus_per_node
         return {"RANK": str(local), "WORLD_SIZE": str(self.gpus_per_node), "LOCAL_RANK": str(local),
                 "LOCAL_WORLD_SIZE": str(self.gpus_per_node), "MASTER_ADDR": f"{rid[:8]}-0.nexus-headless",
-                "MASTER_PORT": "29500", "HIP_VISIBLE_DEVICES": ",".join(str(i) for i in range(self.gpus_per_node)),
+                "MASTER_PORT": "29500", "HIP_VISIBLE_DEVICES": self.visible_devices if self.visible_devices is not None
+                else ",".join(str(i) for i in range(self.gpus_per_node)),
                 "NCCL_IB_DISABLE": "1", "RCCL_MSCCLPP_ENABLE": "1"}
 
     def _templates(self):
@@ -399,6 +405,21 @@ class Workload:
         evs = self.events.pop(rid, None)
         if evs:
             self._expiring[-1].extend(evs)
+
+    def fail_with(self, kind: str, message: Optional[str] = None) -> StepTraffic:
+        """One running run fails as ``kind`` (``message``: the HIP text of an hbm-oom, e.g.
+        a real OOM's); its replacement is created."""
+        st = StepTraffic()
+        rid = self.live.pop(self.rng.randrange(len(self.live)))
+        saved = self.hip_oom_message
+        if message:
+            self.hip_oom_message = message
+        try:
+            self._fail(rid, kind, st)
+        finally:
+            self.hip_oom_message = saved
+        self._create(st)
+        return st
 
     def step(self, events: int, kinds: Optional[List[str]] = None) -> StepTraffic:
         """Fail ``events`` runs, start last step's new runs, create ``events`` new ones.

@@ -14,6 +14,8 @@ import tempfile
 import time
 from typing import List, Optional, Sequence
 
+from ..utils.proc import die_with_parent
+
 
 class CqlServer:
     def __init__(self, *, user: str = "", password: str = "", latency_us: int = 0, error_rate: float = 0.0,
@@ -75,7 +77,7 @@ class CqlServer:
         if os.path.exists(ready):
             os.unlink(ready)
         logf = open(self.log_path, "ab")
-        self.proc = subprocess.Popen(self._argv(), stdout=logf, stderr=logf, start_new_session=True)
+        self.proc = subprocess.Popen(self._argv(), stdout=logf, stderr=logf, start_new_session=True, preexec_fn=die_with_parent())
         logf.close()
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:

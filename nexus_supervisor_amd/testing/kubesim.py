@@ -16,6 +16,8 @@ import tempfile
 import time
 from typing import Any, Dict, Iterable, List, Optional, Tuple
 
+from ..utils.proc import die_with_parent
+
 try:
     from .._kube_native import dumps as _dumps
 
@@ -69,7 +71,7 @@ class KubeSim:
         if self.throttle_deletes or self.write_qps:
             argv += ["--retry-after", str(int(self.retry_after))]
         logf = open(self.log_path, "ab")
-        self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True)
+        self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True, preexec_fn=die_with_parent())
         logf.close()
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:

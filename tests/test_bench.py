@@ -116,7 +116,7 @@ def test_bench_two_ranks_torchrun_gloo():
 
 @pytest.mark.slow
 def test_bench_two_ranks_wire_worker_processes():
-    """The driver's N>1 path on the default (wire) transport: the shared cluster — ONE
+    """The replica slot mode on the wire transport: the shared cluster — ONE
     apiserver simulator and ONE CQL server for both ranks, each rank a 2-process replica
     watching the whole namespace with ``sharding.shards = 2`` — MAX-over-ranks timing,
     one JSON line, every timed run read back with its expected stage."""
@@ -128,7 +128,8 @@ def test_bench_two_ranks_wire_worker_processes():
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
                         "--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "50", "--procs", "2",
-                        "--probe-events", "0", "--cluster", "shared"], cwd=ROOT, env=env, capture_output=True,
+                        "--probe-events", "0", "--cluster", "shared", "--slot-mode", "replica"], cwd=ROOT, env=env,
+                       capture_output=True,
                        text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
@@ -181,7 +182,7 @@ def test_bench_four_ranks_shared_cluster_not_harness_bound():
     process saturated, every decision in its expected stage, every timed row read back,
     and the replica CPU per failure reported for every rank."""
     out = _torchrun(4, "--steps", "2", "--warmup", "1", "--jobs", "200", "--events", "30", "--procs", "1",
-                    "--probe-events", "0", "--cluster", "shared")
+                    "--probe-events", "0", "--cluster", "shared", "--slot-mode", "replica")
     _check(out, 4, 2, 1, 30)
     assert out["config"]["cluster"] == "shared" and out["config"]["parallelism"] == "shard4x1proc"
     assert out["harness_bound"]["bound"] is False and out["harness_bound"]["bound_ranks"] == [], out["harness_bound"]
@@ -196,7 +197,7 @@ def test_bench_two_ranks_per_rank_clusters_and_poisson_probe():
     and CQL server (weak scaling with nothing shared), plus the open-loop probe: Poisson
     arrivals, every probe event acknowledged."""
     out = _torchrun(2, "--steps", "2", "--warmup", "1", "--jobs", "200", "--events", "30", "--procs", "1",
-                    "--probe-events", "40", "--probe-rate", "6000")
+                    "--probe-events", "40", "--probe-rate", "6000", "--slot-mode", "replica")
     _check(out, 2, 2, 1, 30)
     assert out["config"]["cluster"] == "per-rank"
     probe = out["latency_at_rate"]
@@ -219,3 +220,22 @@ def test_probe_stage_delta_counts_only_what_the_probe_recorded():
     assert d["stage_read"]["count"] == 3
     assert 0.19 < d["stage_read"]["p50"] < 0.32 and d["stage_read"]["max"] < 0.41
     assert "stage_write" not in d
+
+
+@pytest.mark.slow
+def test_bench_node_mode_four_slots_one_replica_one_monitor():
+    """The default for N>1 (``--slot-mode node``): ONE supervisor replica and ONE GPU monitor
+    on rank 0 supervise every GPU slot of the node (the production shape: one HA
+    supervisor, one node agent); each rank is a slot whose runs sit on its GPU.  Every
+    slot's HBM-OOM at about the same moment is attributed to that slot's physical GPU."""
+    out = _torchrun(4, "--steps", "2", "--warmup", "1", "--jobs", "200", "--events", "30", "--procs", "1",
+                    "--probe-events", "10", "--probe-rate", "6000")
+    _check(out, 4, 2, 1, 30)
+    cfg = out["config"]
+    assert cfg["slot_mode"] == "node" and cfg["gpu_monitors"] == 1 and cfg["cluster"] == "node"
+    assert cfg["parallelism"] == "node4slots:1replica:1proc"
+    att = cfg["attribution"]
+    assert att["slots"] == 4 and att["correct"] == 4, att
+    assert [p["gpu_index"] for p in att["per_slot"]] == [0, 1, 2, 3]
+    # every slot's failures went through the one replica: the failures of all four slots
+    assert out["readback"]["checked"] >= 4 * 2 * 30 and out["wrong_stage"] == 0

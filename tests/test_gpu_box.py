@@ -461,22 +461,26 @@ def test_multi_rank_job_root_cause_from_a_real_hbm_oom(telemetry, stress_exe, tm
 
 
 def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, telemetry):
-    """The GPU is filled by another tenant (``gpu_stress hold``, all but ~0.25 GiB of the
-    HBM3E), then a fresh torch process needs a HIP context, a hipBLAS handle and a small
-    buffer.  Whatever ROCm prints there — torch's ``C10_HIP_CHECK`` ``HIP error: out of
+    """The GPU is filled by another tenant (``gpu_stress hbm-oom`` holding every 0.5 GiB
+    chunk it got), then a fresh torch process needs a HIP context, a hipBLAS handle and a
+    2 GiB buffer.  Whatever ROCm prints there — torch's ``C10_HIP_CHECK`` ``HIP error: out of
     memory``, a hipBLAS / rocBLAS allocation status, or torch's ``OutOfMemoryError`` — is the
     real text of a default pod's log tail, and it must be classified hbm-oom on GPU 0."""
     import sys
 
-    dev = telemetry.devices()[0]
-    snap = [g for g in telemetry.snapshot() if g.get("index") == 0][0]
-    free_mb = int(dev.get("vram_total_mb") or snap.get("vram_total_mb")) - int(snap.get("vram_used_mb") or 0)
-    hold_gib = max(1.0, free_mb / 1024.0 - 0.25)
-    holder = subprocess.Popen([stress_exe, "hold", "--gib", f"{hold_gib:.2f}", "--seconds", "90"],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    # the filler allocates 0.5 GiB chunks until HIP refuses one, writes its termination log
+    # and then holds every chunk (--linger): the GPU is left with less than a chunk free
+    done = tmp_path / "filler.termination"
+    holder = subprocess.Popen([stress_exe, "hbm-oom", "--chunk-gib", "0.5", "--linger", "120", "--termination-log",
+                               str(done), "--max-gib", "400"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True)
+    hold_gib = None
     try:
-        time.sleep(8.0)  # the hold is allocated and filled
-        assert holder.poll() is None, holder.stderr.read()[-400:]
+        deadline = time.time() + 150
+        while not done.exists() and holder.poll() is None and time.time() < deadline:
+            time.sleep(0.2)
+        assert done.exists() and holder.poll() is None, "filler did not reach its OOM"
+        hold_gib = done.read_text()[:300]
         code = ("import torch\n"
                 "a = torch.randn(256, 256, device='cuda')\n"
                 "b = a @ a\n"
@@ -500,7 +504,7 @@ def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, 
     assert trace["oom"].get("gpu_index", 0) == 0
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/hip_runtime_oom.json", "w") as f:
-        json.dump({"hold_gib": hold_gib, "free_mb_before": free_mb, "rc": p.returncode, "signature": sig,
+        json.dump({"filler": hold_gib, "rc": p.returncode, "signature": sig,
                    "runtime_check_wording": "error: out of memory" in p.stderr.lower(),
                    "stderr_tail": p.stderr[-1500:], "trace": trace}, f, indent=1)
 
