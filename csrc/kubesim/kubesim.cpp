@@ -161,6 +161,7 @@ struct Options {
   int write_burst = 0;          // bucket size (0 = max(1, write_qps))
   int64_t throttle_deletes = 0; // answer this many first Job DELETEs 429
   int retry_after_s = 1;        // Retry-After of every 429
+  size_t prefault_mb = 0;       // heap pages touched at startup (kept: trim threshold 1 GiB)
 } g_opt;
 
 int64_t mono_ns() {
@@ -568,6 +569,16 @@ std::string okey(std::string_view ns, std::string_view name) {
   return k;
 }
 
+// The same key in a reused buffer (lookups only: no allocation once it has grown).  The
+// apply loop runs on the event-loop thread; the flush threads never look objects up.
+const std::string& okey_scratch(std::string_view ns, std::string_view name) {
+  static std::string k;
+  k.assign(ns.data(), ns.size());
+  k += '\x01';
+  k.append(name.data(), name.size());
+  return k;
+}
+
 void watch_push(Watch* w, const Line& line);
 
 // `new_rv` > 0: a deletion at that resourceVersion of `o` (text still at o.rv), spliced on send
@@ -684,7 +695,7 @@ Obj finish(int kind, Value& doc, const Obj* prev, std::string_view src = {}) {
 }
 
 void index_pod(const Obj& o, bool add);
-bool remove(int kind, const std::string& ns, const std::string& name, const std::string& propagation);
+bool remove(int kind, std::string_view ns, std::string_view name, std::string_view propagation);
 
 // ------------------------------------------------------------ raw fast path (bulk apply)
 // The benchmark generator sends fully-formed objects by the thousand.  Building a DOM for
@@ -977,12 +988,11 @@ bool apply_raw(std::string_view line) {
   int kind = kind_by_name(r.kind);
   if (kind < 0) return false;
   if (type == "DELETED") {
-    remove(kind, std::string(r.ns), std::string(r.name), "Background");
+    remove(kind, r.ns, r.name, "Background");
     return true;
   }
   KindStore& ks = g_store[kind];
-  std::string key = okey(r.ns, r.name);
-  auto it = ks.objs.find(key);
+  auto it = ks.objs.find(okey_scratch(r.ns, r.name));
   const Obj* prev = it == ks.objs.end() ? nullptr : &it->second;
   Obj o = finish_raw(r, line, ob, oe, prev);
   if (kind == K_POD && !(prev && prev->job == o.job)) {  // job label unchanged: index stays
@@ -991,7 +1001,7 @@ bool apply_raw(std::string_view line) {
   }
   record(kind, prev ? "MODIFIED" : "ADDED", o);
   if (prev) it->second = std::move(o);
-  else ks.objs.emplace(std::move(key), std::move(o));
+  else ks.objs.emplace(okey(r.ns, r.name), std::move(o));
   return true;
 }
 
@@ -1047,14 +1057,14 @@ int update(int kind, Value& doc, bool check_rv, std::string* out_json, std::stri
   return 0;
 }
 
-bool remove(int kind, const std::string& ns, const std::string& name, const std::string& propagation) {
-  auto it = g_store[kind].objs.find(okey(ns, name));
+bool remove(int kind, std::string_view ns, std::string_view name, std::string_view propagation) {
+  auto it = g_store[kind].objs.find(okey_scratch(ns, name));
   if (it == g_store[kind].objs.end()) return false;
   Obj o = std::move(it->second);
   g_store[kind].objs.erase(it);
   if (kind == K_POD) {
     index_pod(o, false);
-    if (!g_pod_logs.empty()) g_pod_logs.erase(okey(ns, name));
+    if (!g_pod_logs.empty()) g_pod_logs.erase(okey_scratch(o.ns, o.name));
   }
   if (o.rv_off != std::string::npos) {
     record(kind, "DELETED", o, ++g_rv);  // new resourceVersion spliced in on send
@@ -1067,12 +1077,12 @@ bool remove(int kind, const std::string& ns, const std::string& name, const std:
   }
   ++g_stats.deleted;
   if (kind == K_JOB && (propagation == "Background" || propagation == "Foreground")) {
-    auto pit = g_pods_by_job.find(okey(ns, name));
+    auto pit = g_pods_by_job.find(okey_scratch(o.ns, o.name));
     if (pit != g_pods_by_job.end()) {
       // take the job's pod set out of the index (the pods' own unindexing then finds
       // nothing to do) instead of copying every name
       auto node = g_pods_by_job.extract(pit);
-      for (auto& p : node.mapped()) remove(K_POD, ns, p, propagation);
+      for (auto& p : node.mapped()) remove(K_POD, o.ns, p, propagation);
     }
   }
   return true;
@@ -1928,6 +1938,7 @@ int main(int argc, char** argv) {
     else if (a == "--port") g_opt.port = atoi(next().c_str());
     else if (a == "--ready-file") g_opt.ready_file = next();
     else if (a == "--history") g_opt.history = static_cast<size_t>(atol(next().c_str()));
+    else if (a == "--prefault-mb") g_opt.prefault_mb = static_cast<size_t>(atol(next().c_str()));
     else if (a == "--bookmark-ms") g_opt.bookmark_ms = atol(next().c_str());
     else if (a == "--token") g_opt.token = next();
     else if (a == "--flush-threads") g_opt.flush_threads = std::max(1, atoi(next().c_str()));
@@ -1953,6 +1964,17 @@ int main(int argc, char** argv) {
   // strings freed in between, that consolidation was most of malloc's time.  Small
   // chunks still go through the per-thread tcache.
   mallopt(M_MXFAST, 0);
+  if (g_opt.prefault_mb > 0) {
+    // Grow and touch the heap once: the watch history and the live objects fill hundreds of
+    // MB in the first steps of a benchmark, and every brk extension and first-touch page
+    // fault of that growth landed on the event loop (a quarter of its time in a 20-step run).
+    // Freed at once, the pages stay in the heap (M_TRIM_THRESHOLD above) for the run.
+    size_t n = g_opt.prefault_mb << 20;
+    if (char* p = static_cast<char*>(malloc(n))) {
+      for (size_t i = 0; i < n; i += 4096) p[i] = 1;
+      free(p);
+    }
+  }
   prof::start();
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);

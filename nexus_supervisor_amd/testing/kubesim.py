@@ -36,7 +36,7 @@ def encode_events(events: Iterable[Tuple[str, Dict[str, Any]]]) -> bytes:
 class KubeSim:
     def __init__(self, *, host: str = "127.0.0.1", port: int = 0, history: int = 400_000, bookmark_ms: int = 1000,
                  token: str = "", flush_threads: int = 1, api_latency_us: int = 0, write_qps: float = 0.0,
-                 write_burst: int = 0, throttle_deletes: int = 0, retry_after: int = 1):
+                 write_burst: int = 0, throttle_deletes: int = 0, retry_after: int = 1, prefault_mb: int = 0):
         from .._build import binary
 
         self.exe = os.environ.get("NEXUS_KUBESIM_BINARY") or binary("nexus-kubesim")
@@ -48,6 +48,7 @@ class KubeSim:
         # injected 429s on the first Job DELETEs
         self.api_latency_us, self.write_qps, self.write_burst = api_latency_us, write_qps, write_burst
         self.throttle_deletes, self.retry_after = throttle_deletes, retry_after
+        self.prefault_mb = prefault_mb  # heap grown and touched at startup (benchmarks)
         self.proc: Optional[subprocess.Popen] = None
         self.log_path = os.path.join(self.dir, "server.log")
         self.url = ""
@@ -62,6 +63,8 @@ class KubeSim:
             argv += ["--token", self.token]
         if self.flush_threads > 1:
             argv += ["--flush-threads", str(self.flush_threads)]
+        if self.prefault_mb:
+            argv += ["--prefault-mb", str(int(self.prefault_mb))]
         if self.api_latency_us:
             argv += ["--api-latency-us", str(int(self.api_latency_us))]
         if self.write_qps:
@@ -71,7 +74,12 @@ class KubeSim:
         if self.throttle_deletes or self.write_qps:
             argv += ["--retry-after", str(int(self.retry_after))]
         logf = open(self.log_path, "ab")
-        self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True, preexec_fn=die_with_parent())
+        # glibc's per-thread cache for every object-sized chunk (up to 4 KiB, no count limit):
+        # the simulator allocates and frees a dozen strings per watch line
+        env = dict(os.environ)
+        env.setdefault("GLIBC_TUNABLES", "glibc.malloc.tcache_count=65535:glibc.malloc.tcache_max=4096")
+        self.proc = subprocess.Popen(argv, stdout=logf, stderr=logf, start_new_session=True, env=env,
+                                     preexec_fn=die_with_parent())
         logf.close()
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:

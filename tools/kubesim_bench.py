@@ -77,7 +77,7 @@ async def main(argv=None):
     steps = [wl.step(args.events) for _ in range(args.steps + 2)]
     bodies = [(failed, encode_events(traffic)) for failed, traffic, _ in steps]
     ft = args.flush_threads or max(1, min(8, args.watchers))
-    with KubeSim(history=50_000, flush_threads=ft) as sim:
+    with KubeSim(history=50_000, flush_threads=ft, prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "0"))) as sim:
         host, port = sim.url.split("//")[1].split(":")
         port = int(port)
         ctl = SimControl(sim.url)
