@@ -12,6 +12,10 @@ cfg   BASELINE.json config                                                here
 3     1×MI355X: 8 ROCm stress pods, HBM-OOM injected, per-GPU             GPU only (``--gpu``): 7 VRAM-holding
       attribution in the checkpoint                                       pods + 1 driven to a real HBM-OOM on
                                                                           the box's GPU; attribution + latency
+3a    config 3 through the deployed path                                  no local telemetry; the node agent
+                                                                          process (amd-smi, /var/log/pods) PATCHes
+                                                                          the evidence annotation, the supervisor
+                                                                          waits ``gpu.evidence-wait`` for it
 4     1000 pod-fail events/min over 10k concurrent jobs, informer→CQL    open-loop at 1000/min for ``--seconds``
       p99                                                                 (1 slot here; 1/2/4/8 slots: bench.py)
 5     2 replicas + leader election + 10k concurrent jobs + chaos          1000/min churn with a CQL node restart,
@@ -23,7 +27,7 @@ cfg   BASELINE.json config                                                here
 Latency = failure pushed into the apiserver → checkpoint write acknowledged
 (``stamps["ack_mono"]``), both ``time.monotonic()`` in this process.
 
-    python -m nexus_supervisor_amd.bench.scenarios [--only 1,2,4,5] [--gpu] [--json-out F]
+    python -m nexus_supervisor_amd.bench.scenarios [--only 1,2,3a,4,5] [--gpu] [--json-out F]
 """
 from __future__ import annotations
 
@@ -93,8 +97,9 @@ class Cluster:
     """Fake apiserver (HTTP) + native CQL server + ``replicas`` supervisor applications."""
 
     def __init__(self, jobs: int, profile: str, replicas: int = 1, leader_election: bool = False, seed: int = 0,
-                 persist: bool = False, telemetry=None, shards: int = 0):
+                 persist: bool = False, telemetry=None, shards: int = 0, gpu: Optional[Dict[str, Any]] = None):
         self.jobs, self.profile, self.replicas, self.le = jobs, profile, replicas, leader_election
+        self.gpu = gpu or {}  # gpu.* overrides (the node-agent path: evidence-wait, no local telemetry)
         self.shards = shards  # > 0: runs split over this many shards held through per-shard Leases
         self.wl = Workload(concurrent_jobs=jobs, seed=seed)
         self.clock = AckClock()
@@ -107,6 +112,8 @@ class Cluster:
                 "failure-rate-max-delay": "500ms", "max-retries": 0,
                 "scylla-cql-store": {"hosts": [f"127.0.0.1:{self.srv.port}"], "request-timeout": "1s"}}
         over.update(PROFILES[self.profile])
+        if self.gpu:
+            over["gpu"] = dict(self.gpu)
         if self.le or self.shards:
             over["leader-election"] = {"enabled": bool(self.le and not self.shards), "identity": ident,
                                        "lease-duration": "2s", "renew-deadline": "1500ms", "retry-period": "200ms"}
@@ -434,15 +441,163 @@ async def cfg3_gpu(profile: str, holders: int = 7, hold_gib: float = 30.0) -> Di
         tel.stop()
 
 
-CONFIGS = {"1": cfg1_single, "2": cfg2_burst, "3": cfg3_gpu, "4": cfg4_rate, "5": cfg5_chaos, "5s": cfg5s_sharded_chaos}
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
 
 
-async def run_all(only: List[str], profiles: List[str], seconds: float, jobs: int) -> List[Dict[str, Any]]:
+async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wait: float = 2.0,
+                     sample_interval: float = 0.5) -> Dict[str, Any]:
+    """Config 3 through the production attribution path (the chart's deployment): the
+    supervisor has **no** local GPU telemetry and holds a failed GPU pod's decision up to
+    ``gpu.evidence-wait`` for the node agent's annotation; the agent is its own process
+    (``python -m nexus_supervisor_amd agent``, amd-smi monitor at the production 0.5 s
+    sample interval, ``/var/log/pods`` reader), watching the apiserver for its node's pods
+    and merge-PATCHing ``nexus.amd.com/gpu-evidence``.
+
+    ``runs`` default pods (``terminationMessagePolicy: File``: empty termination message,
+    the HIP OOM text on stderr only) fail one after another; with ``gpu`` each is preceded
+    by a real HIP OOM on the box's MI355X (``gpu_stress hbm-oom``) whose stderr becomes the
+    pod's container log.  Latency: the pod's failure pushed into the apiserver → checkpoint
+    write acknowledged, through watch → defer → agent watch → evidence → PATCH → watch →
+    decision → CQL.  Reported with the share of decisions whose wait expired
+    (``gpu_evidence_wait_expired``: written without the agent's evidence) and the pods/log
+    reads the supervisor made (0: the agent read the log)."""
+    import subprocess
+    import sys
+    import tempfile
+
+    import aiohttp
+
+    from ..testing.fakelogs import write_cri_log
+    from ..utils.proc import die_with_parent
+
+    work = tempfile.mkdtemp(prefix="cfg3a-")
+    logroot = os.path.join(work, "pods")
+    os.makedirs(logroot)
+    c = Cluster(jobs=runs + 8, profile=profile, gpu={
+        "evidence-wait": f"{evidence_wait}s", "local-telemetry": False, "backend": "none"})
+    c.wl.visible_devices = "0"  # the device plugin gave each pod GPU 0
+    c.wl.hbm_shape = "default-pod"
+    agent = None
+    exe = None
+    if gpu:
+        from .._build import binary
+
+        exe = binary("gpu_stress")
+    try:
+        await c.start()
+        kcfg = os.path.join(work, "kubeconfig.yaml")
+        with open(kcfg, "w") as f:
+            json.dump({"apiVersion": "v1", "kind": "Config", "current-context": "bench",
+                       "clusters": [{"name": "bench", "cluster": {"server": c.url}}],
+                       "contexts": [{"name": "bench", "context": {"cluster": "bench", "user": "bench"}}],
+                       "users": [{"name": "bench", "user": {}}]}, f)
+        port = _free_port()
+        env = dict(os.environ, NODE_NAME=c.wl._templates()[4], NEXUS__KUBE_CONFIG_PATH=kcfg,
+                   NEXUS__RESOURCE_NAMESPACE=c.wl.ns, NEXUS__GPU__BACKEND="amdsmi" if gpu else "fake",
+                   NEXUS__GPU__SAMPLE_INTERVAL=f"{int(sample_interval * 1000)}ms", NEXUS__KUBE_QPS="50",
+                   NEXUS__KUBE_BURST="100", NEXUS_AGENT_LOG_ROOT=logroot, NEXUS_AGENT_METRICS_PORT=str(port))
+        agent_log = open(os.path.join(work, "agent.log"), "wb")
+        agent = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd", "agent"], env=env, stdout=agent_log,
+                                 stderr=subprocess.STDOUT, preexec_fn=die_with_parent())
+        agent_log.close()
+        async with aiohttp.ClientSession() as http:
+            deadline = time.monotonic() + 120
+            while True:
+                if agent.poll() is not None:
+                    raise RuntimeError(f"node agent exited rc={agent.returncode}: {_tail(work)}")
+                try:
+                    async with http.get(f"http://127.0.0.1:{port}/healthz") as r:
+                        if r.status == 200:
+                            break
+                except aiohttp.ClientError:
+                    pass
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"node agent not ready: {_tail(work)}")
+                await asyncio.sleep(0.1)
+        sup = c.apps[0].supervisor
+        m0 = {k: sup.metrics.counter(k) for k in ("gpu_evidence_wait_expired", "decisions_deferred_for_gpu_evidence",
+                                                    "decisions_awaited_gpu_evidence")}
+        loop = asyncio.get_running_loop()
+        rids, rcs, wrong, ooms = [], [], [], []
+        t_start = time.monotonic()
+        for i in range(runs):
+            if gpu:
+                p = await loop.run_in_executor(None, lambda: subprocess.run(
+                    [exe, "hbm-oom", "--chunk-gib", "4", "--no-termination-log", "--linger", "0", "--max-gib", "400"],
+                    env=dict(os.environ, HIP_VISIBLE_DEVICES="0"), capture_output=True, text=True, timeout=180))
+                rcs.append(p.returncode)
+                text = p.stderr
+            else:
+                text = f"epoch 3 step 1200 loss 0.412\n{c.wl.hip_oom_message}\n"
+            rid = c.wl.live[-1]
+            pod = c.wl.pods[rid]
+            write_cri_log(logroot, c.wl.ns, pod["metadata"]["name"], pod["metadata"]["uid"], "algorithm", 0,
+                          [("stderr", text)])
+            st = c.wl.fail_with("hbm-oom", rid=rid)
+            await c._write_rows(st.rows)
+            c.clock.pushed[rid] = time.monotonic()
+            for etype, obj in st.traffic:
+                c.api.apply(etype, obj, copy_obj=False)
+            await c.clock.wait([rid], evidence_wait + 30)
+            rids.append(rid)
+            row = await c.store.read_checkpoint(c.wl.algorithm, rid)
+            trace = json.loads(row.algorithm_failure_details) if row and (row.algorithm_failure_details or "").startswith("{") else {}
+            oom = trace.get("oom") or {}
+            ooms.append(((trace.get("gpu") or {}).get("gpus") or [{}])[0])
+            if not (row and row.lifecycle_stage == "FAILED" and trace.get("class") == "hbm-oom"
+                    and oom.get("gpu_index") == 0 and any("node-log tail" in x for x in oom.get("signals") or ())):
+                wrong.append({"rid": rid, "stage": row.lifecycle_stage if row else None, "class": trace.get("class"),
+                              "oom": oom})
+        dt = time.monotonic() - t_start
+        m = {k: sup.metrics.counter(k) - v for k, v in m0.items()}
+        return _summary(f"3a: 1xMI355X via the node agent, {runs} default pods, real HBM-OOM" if gpu else
+                        f"3a: node agent (fake GPU backend), {runs} default pods", profile, c.clock.latencies_ms(rids),
+                        runs, dt, via="node-agent", evidence_wait_s=evidence_wait, sample_interval_s=sample_interval,
+                        oom_rcs=sorted(set(rcs)), wrong=len(wrong), wrong_examples=wrong[:3],
+                        evidence_wait_expired=int(m["gpu_evidence_wait_expired"]),
+                        evidence_wait_expired_share=round(m["gpu_evidence_wait_expired"] / max(1, runs), 4),
+                        deferred_for_gpu_evidence=int(m["decisions_deferred_for_gpu_evidence"]),
+                        job_decisions_awaited_evidence=int(m["decisions_awaited_gpu_evidence"]),
+                        supervisor_pod_log_reads=len(c.api.log_requests),
+                        vram_peak_mb=max((g.get("vram_peak_mb") or 0) for g in ooms) if ooms else None,
+                        vram_total_mb=max((g.get("vram_total_mb") or 0) for g in ooms) if ooms else None)
+    finally:
+        if agent is not None and agent.poll() is None:
+            agent.terminate()
+            try:
+                agent.wait(10)
+            except subprocess.TimeoutExpired:
+                agent.kill()
+                agent.wait(5)
+        await c.stop()
+
+
+def _tail(work: str) -> str:
+    try:
+        with open(os.path.join(work, "agent.log"), "rb") as f:
+            return f.read()[-2000:].decode(errors="replace")
+    except OSError:
+        return ""
+
+
+CONFIGS = {"1": cfg1_single, "2": cfg2_burst, "3": cfg3_gpu, "3a": cfg3_agent, "4": cfg4_rate, "5": cfg5_chaos,
+           "5s": cfg5s_sharded_chaos}
+
+
+async def run_all(only: List[str], profiles: List[str], seconds: float, jobs: int, gpu: bool = False
+                  ) -> List[Dict[str, Any]]:
     out = []
     for k in only:
         for prof in profiles:
             fn = CONFIGS[k]
             kw = {"seconds": seconds, "jobs": jobs} if k in ("4", "5", "5s") else {}
+            if k == "3a":
+                kw = {"gpu": gpu}  # without --gpu: the agent on the fake GPU backend
             t0 = time.monotonic()
             res = await fn(prof, **kw)
             res["wall_s"] = round(time.monotonic() - t0, 2)
@@ -463,7 +618,9 @@ def main(argv=None) -> int:
     only = [x for x in args.only.split(",") if x]
     if args.gpu and "3" not in only:
         only.insert(2, "3")
-    res = asyncio.run(run_all(only, args.profiles.split(","), args.seconds, args.jobs))
+    if args.gpu and "3a" not in only:
+        only.insert(only.index("3") + 1, "3a")
+    res = asyncio.run(run_all(only, args.profiles.split(","), args.seconds, args.jobs, args.gpu))
     if args.json_out:
         with open(args.json_out, "w") as f:
             json.dump(res, f, indent=1)

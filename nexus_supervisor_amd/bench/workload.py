@@ -406,11 +406,16 @@ class Workload:
         if evs:
             self._expiring[-1].extend(evs)
 
-    def fail_with(self, kind: str, message: Optional[str] = None) -> StepTraffic:
-        """One running run fails as ``kind`` (``message``: the HIP text of an hbm-oom, e.g.
-        a real OOM's); its replacement is created."""
+    def fail_with(self, kind: str, message: Optional[str] = None, rid: Optional[str] = None) -> StepTraffic:
+        """One running run (``rid``, else a random one) fails as ``kind`` (``message``: the
+        HIP text of an hbm-oom, e.g. a real OOM's); its replacement is created."""
         st = StepTraffic()
-        rid = self.live.pop(self.rng.randrange(len(self.live)))
+        if rid is None:
+            rid = self.live.pop(self.rng.randrange(len(self.live)))
+        else:
+            self.live.remove(rid)
+        if not self._expiring:
+            self._expiring.append([])
         saved = self.hip_oom_message
         if message:
             self.hip_oom_message = message

@@ -398,7 +398,10 @@ async def serve_metrics(agent: NodeAgent, port: int, host: str = "0.0.0.0"):
         return web.Response(text=agent.metrics.prometheus_text(), content_type="text/plain", charset="utf-8")
 
     async def h_healthz(_req):
-        return web.Response(text="ok")
+        # ready once the node's pods are listed: a failure before that is seen at the list
+        if all(i.has_synced() for i in agent.factory.informers.values()):
+            return web.Response(text="ok")
+        return web.Response(text="syncing", status=503)
 
     app = web.Application()
     app.router.add_get("/metrics", h_metrics)

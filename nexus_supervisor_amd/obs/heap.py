@@ -32,7 +32,7 @@ def _sizes(sup) -> Dict[str, Any]:
         return out
     for name, inf in getattr(getattr(sup, "factory", None), "informers", {}).items():
         out[f"informer.{name}"] = len(inf.indexer)
-    for attr in ("_applied", "_parked", "_gpu_wait", "_log_fetches", "_deletes", "_bg", "_event_tasks"):
+    for attr in ("_applied", "_parked", "_gpu_wait", "_gpu_waiters", "_log_fetches", "_deletes", "_bg", "_event_tasks"):
         v = getattr(sup, attr, None)
         if v is not None:
             out[f"supervisor.{attr}"] = len(v)

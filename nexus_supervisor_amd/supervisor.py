@@ -208,6 +208,8 @@ class Supervisor:
         self._guards: Dict[Any, Any] = {}
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
+        # pod key -> a Job decision waiting for that pod's GPU evidence wait to end
+        self._gpu_waiters: Dict[str, asyncio.Future] = {}
         self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
         self._settle: Dict[str, asyncio.Future] = {}  # job name -> a Job decision waiting for its pod's failure
         self._settle_wait = float(cfg.rules.job_pod_settle)
@@ -360,6 +362,8 @@ class Supervisor:
             t.cancel()
         self._deletes.clear()
         self._gpu_wait.clear()
+        for key in list(self._gpu_waiters):
+            self._gpu_wait_over(key)
         self._parked.clear()
         self._applied.clear()
         self.metrics.inc("fenced_decisions_dropped", dropped)
@@ -486,6 +490,7 @@ class Supervisor:
             del self._parked[key]
         for key in [k for k in self._gpu_wait if self._gpu_wait_run(k, ns, lost_run)]:
             del self._gpu_wait[key]
+            self._gpu_wait_over(key)
 
     def _gpu_wait_run(self, key, ns, lost_run) -> bool:
         pod = self.pod_informer.indexer.get(key)
@@ -589,7 +594,8 @@ class Supervisor:
             if self.classifier.deferred_log:
                 # failed GPU container, empty termination message: its OOM text (if any) is in
                 # the container log — fetch the tail, then decide (gpu.log-tail)
-                self._gpu_wait.pop(key, None)
+                if self._gpu_wait.pop(key, None) is not None:
+                    self._gpu_wait_over(key)
                 self._start_log_fetch(key, pod, self.classifier.deferred_log, waited)
                 return
             # failed GPU pod without node-agent evidence yet: give the annotation time to land
@@ -597,7 +603,8 @@ class Supervisor:
                 self._gpu_wait[key] = time.monotonic() + wait
                 self.metrics.inc("decisions_deferred_for_gpu_evidence")
             return
-        self._gpu_wait.pop(key, None)
+        if self._gpu_wait.pop(key, None) is not None and self._gpu_waiters:
+            self._gpu_wait_over(key)
         first = self._deferred_at.pop(key, None) if self._deferred_at else None
         if first is not None:
             recv, delivery = first
@@ -674,7 +681,15 @@ class Supervisor:
             if pod is not None:
                 self.metrics.inc("gpu_evidence_wait_expired")
                 self._on_pod_update(None, pod, waited=True)
+            self._gpu_wait_over(key)
             self._end_deferral(key)
+
+    def _gpu_wait_over(self, key: str) -> None:
+        """A pod's GPU evidence wait ended (the annotation landed, the wait expired, the
+        pod left this replica): release the Job decision waiting for it, if any."""
+        fut = self._gpu_waiters.pop(key, None)
+        if fut is not None and not fut.done():
+            fut.set_result(None)
 
     def _on_job_add(self, job):
         if self._parked:
@@ -894,6 +909,8 @@ class Supervisor:
             # a Job-level failure can overtake its pod's (deferred) log-tail read: wait for it,
             # then re-enrich — an OOM found now also fixes the action (BackoffLimitExceeded of
             # an OOM-killed run is FAILED, not DEADLINE_EXCEEDED), so it must precede the stage
+            if self._gpu_wait and r.object_kind == "Job":
+                await self._await_gpu_evidence(r)
             if self._log_fetches and r.object_kind == "Job":
                 await self._await_pod_logs(r)
             self.classifier.finish(r, self.lookup)
@@ -1007,6 +1024,24 @@ class Supervisor:
                 pass
         if waited:
             self.metrics.inc("job_pod_settle_waits")
+
+    async def _await_gpu_evidence(self, r: RunStatusAnalysisResult) -> None:
+        """A Job-level failure whose pod is held for the node agent's evidence annotation
+        (``gpu.evidence-wait``): wait for that wait to end, so the Job decision is enriched
+        with the same GPU evidence (an HBM-OOM found there also fixes the stage) instead of
+        writing the row without it ahead of the annotation."""
+        keys = [k for k in (kube.object_key(p) for p in self.lookup.pods_of_job(r.request_id)) if k in self._gpu_wait]
+        if not keys:
+            return
+        self.metrics.inc("decisions_awaited_gpu_evidence")
+        loop = asyncio.get_running_loop()
+        futs = []
+        for k in keys:
+            fut = self._gpu_waiters.get(k)
+            if fut is None or fut.done():
+                fut = self._gpu_waiters[k] = loop.create_future()
+            futs.append(fut)
+        await asyncio.wait(futs, timeout=self.cfg.gpu.evidence_wait + 0.5)
 
     async def _await_pod_logs(self, r: RunStatusAnalysisResult) -> None:
         keys = [kube.object_key(p) for p in self.lookup.pods_of_job(r.request_id)]

@@ -560,3 +560,21 @@ def test_node_agent_privileges_reported_on_the_box(stress_exe, tmp_path):
     with open("gpurun_out/agent_privileges.json", "w") as f:
         json.dump({"euid": os.geteuid(), "privileges": priv, "denials": denials, "log_record": recs,
                    "own_process_attributed": True}, f, indent=1)
+
+
+def test_cfg3a_agent_path_real_hbm_oom(arun):
+    """Config 3a on the MI355X: the node agent as its own process (amd-smi at the
+    production 0.5 s interval, /var/log/pods reader), the supervisor without local
+    telemetry waiting ``gpu.evidence-wait: 2s`` for its annotation.  Each of 10 default
+    pods is preceded by a real HIP OOM whose stderr is the pod's log; every row must be
+    FAILED / hbm-oom / GPU 0 from the agent's node-log reading, with no pods/log read and
+    no expired wait."""
+    from nexus_supervisor_amd.bench.scenarios import cfg3_agent
+
+    r = arun(cfg3_agent("uncapped", runs=10, gpu=True), timeout=600)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/cfg3a.json", "w") as f:
+        json.dump(r, f, indent=1)
+    assert r["oom_rcs"] == [1] and r["acked"] == 10 and r["wrong"] == 0, r
+    assert r["supervisor_pod_log_reads"] == 0 and r["evidence_wait_expired"] == 0, r
+    assert r["vram_peak_mb"] >= 0.9 * r["vram_total_mb"], r
