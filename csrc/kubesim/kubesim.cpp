@@ -62,6 +62,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <charconv>
+#include <functional>
 #include <cerrno>
 #include <condition_variable>
 #include <mutex>
@@ -156,6 +158,7 @@ struct Options {
   // this many threads (the apiserver's watch cache serves many watchers in parallel; a
   // sharded supervisor deployment has every replica watching the whole namespace)
   int flush_threads = 1;
+  int apply_threads = 1;  // threads scanning a /sim/apply chunk's lines before the in-order commit
   int64_t api_latency_us = 0;   // answer object requests this long after applying them
   double write_qps = 0;         // mutating requests per second (token bucket); 0 = no cap
   int write_burst = 0;          // bucket size (0 = max(1, write_qps))
@@ -553,6 +556,7 @@ struct Stats {
   std::atomic<uint64_t> sends{0}, send_bytes{0}, eagain{0};  // also counted by fan-out threads
   // wall time spent per phase of the event loop (ns): where a saturated simulator goes
   int64_t apply_ns = 0, request_ns = 0, flush_ns = 0, recv_ns = 0, busy_ns = 0;
+  int64_t prepare_ns = 0;  // the parallel part of apply_ns (wall time)
 } g_stats;
 
 struct Snapshot {
@@ -976,40 +980,171 @@ Obj finish_raw(const Raw& r, std::string_view src, size_t ob, size_t oe, const O
   return o;
 }
 
-// true when handled; false → caller takes the DOM path
-bool apply_raw(std::string_view line) {
-  RawScan sc(line.data(), line.size());
-  std::string_view type;
-  size_t ob = 0, oe = 0;
+// ------------------------------------------------------------ parallel prepare (bulk apply)
+// Most of a bulk apply reads nothing of the store: scanning a line and building its store
+// text and selectable attributes.  /sim/apply therefore prepares a chunk's lines on
+// `--apply-threads` threads (the event loop thread included) and then commits them in
+// order on the event loop — store lookup, resourceVersion, history, pod index — so the
+// store stays single-threaded.  The resourceVersion is not known while preparing: the text
+// gets a placeholder of the width the next one has, filled in at commit (a line whose
+// resourceVersion turned out wider — a power of ten crossed mid-chunk — is rebuilt there).
+struct Prep {
+  std::string_view line, type;
+  int kind = -1;
+  // 0: not raw (DOM path), 1: DELETED, 2: text prepared, 3: raw but needs the stored
+  // object (uid / creationTimestamp / resourceVersion to complete): built at commit
+  int mode = 0;
   Raw r;
-  r.labels.reserve(8);  // one allocation instead of growing 1 → 2 → 4 per object
-  if (!sc.envelope(type, ob, oe, r)) return false;
-  if (!r.has_kind || !r.has_api || !r.has_md || r.md_keys == 0 || r.name.empty() || r.has_gen) return false;
-  int kind = kind_by_name(r.kind);
-  if (kind < 0) return false;
-  if (type == "DELETED") {
-    remove(kind, r.ns, r.name, "Background");
+  size_t ob = 0, oe = 0;
+  Obj o;
+  std::shared_ptr<std::string> text;
+};
+
+size_t digits(int64_t v) {
+  size_t n = 1;
+  while (v >= 10) {
+    v /= 10;
+    ++n;
+  }
+  return n;
+}
+
+void prepare(Prep& p, size_t width) {
+  RawScan sc(p.line.data(), p.line.size());
+  Raw& r = p.r;
+  r.labels.reserve(8);
+  if (!sc.envelope(p.type, p.ob, p.oe, r)) return;
+  if (!r.has_kind || !r.has_api || !r.has_md || r.md_keys == 0 || r.name.empty() || r.has_gen) return;
+  p.kind = kind_by_name(r.kind);
+  if (p.kind < 0) return;
+  if (p.type == "DELETED") {
+    p.mode = 1;
+    return;
+  }
+  if (r.uid.empty() || !r.created.data() || !r.has_rv) {
+    p.mode = 3;
+    return;
+  }
+  Obj& o = p.o;
+  o.ns = std::string(r.ns);
+  o.name = std::string(r.name);
+  o.job = std::string(r.job);
+  o.uid = std::string(r.uid);
+  o.created = std::string(r.created);
+  auto j = std::make_shared<std::string>();
+  j->reserve(p.oe - p.ob + width);
+  j->append(p.line.data() + p.ob, r.rv_off - p.ob);
+  o.rv_off = j->size();
+  o.rv_len = width;
+  j->append(width, '0');
+  j->append(p.line.data() + r.rv_off + r.rv_len, p.oe - r.rv_off - r.rv_len);
+  p.text = std::move(j);
+  o.attrs = attrs_raw(r);
+  p.mode = 2;
+}
+
+// false → the caller takes the DOM path
+bool commit(Prep& p) {
+  if (p.mode == 0) return false;
+  if (p.mode == 1) {
+    remove(p.kind, p.r.ns, p.r.name, "Background");
     return true;
   }
-  KindStore& ks = g_store[kind];
-  auto it = ks.objs.find(okey_scratch(r.ns, r.name));
+  KindStore& ks = g_store[p.kind];
+  auto it = ks.objs.find(okey_scratch(p.r.ns, p.r.name));
   const Obj* prev = it == ks.objs.end() ? nullptr : &it->second;
-  Obj o = finish_raw(r, line, ob, oe, prev);
-  if (kind == K_POD && !(prev && prev->job == o.job)) {  // job label unchanged: index stays
+  Obj o;
+  if (p.mode == 2 && digits(g_rv + 1) == p.o.rv_len) {
+    o = std::move(p.o);
+    o.rv = ++g_rv;
+    std::to_chars(&(*p.text)[o.rv_off], &(*p.text)[o.rv_off] + o.rv_len, o.rv);
+    o.json = std::move(p.text);
+  } else {
+    o = finish_raw(p.r, p.line, p.ob, p.oe, prev);
+  }
+  if (p.kind == K_POD && !(prev && prev->job == o.job)) {
     if (prev) index_pod(*prev, false);
     index_pod(o, true);
   }
-  record(kind, prev ? "MODIFIED" : "ADDED", o);
+  record(p.kind, prev ? "MODIFIED" : "ADDED", o);
   if (prev) it->second = std::move(o);
-  else ks.objs.emplace(okey(r.ns, r.name), std::move(o));
+  else ks.objs.emplace(okey(p.r.ns, p.r.name), std::move(o));
   return true;
 }
 
+// fn(i) for i in [0, n) on `threads` threads (the caller's included), blocks of 16
+class ParallelFor {
+ public:
+  void start(int threads) {
+    for (int i = 1; i < threads; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+    workers_.clear();
+  }
+  void run(size_t n, const std::function<void(size_t)>& fn) {
+    if (workers_.empty() || n < 64) {
+      for (size_t i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      pending_ = workers_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    size_t b;
+    while ((b = next_.fetch_add(16)) < n_)
+      for (size_t i = b; i < std::min(n_, b + 16); ++i) (*fn_)(i);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    while (true) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t n_ = 0;
+  std::atomic<size_t> next_{0};
+  size_t pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+} g_apply_pool;
+
 void index_pod(const Obj& o, bool add) {
   if (o.job.empty()) return;
-  std::string k = okey(o.ns, o.job);
+  const std::string& k = okey_scratch(o.ns, o.job);
   if (add) {
-    g_pods_by_job[k].insert(o.name);
+    auto it = g_pods_by_job.find(k);
+    if (it == g_pods_by_job.end()) it = g_pods_by_job.emplace(okey(o.ns, o.job), std::set<std::string>()).first;
+    it->second.insert(o.name);
   } else {
     auto it = g_pods_by_job.find(k);
     if (it != g_pods_by_job.end()) {
@@ -1606,13 +1741,22 @@ void h_apply(Conn& c, const Request& r) {
   int64_t t0 = mono_ns();
   size_t pos = 0, n = 0;
   std::string_view b = r.body;
+  std::vector<Prep> preps;
+  preps.reserve(std::count(b.begin(), b.end(), '\n') + 1);
   while (pos < b.size()) {
     size_t nl = b.find('\n', pos);
     if (nl == std::string::npos) nl = b.size();
     std::string_view line(b.data() + pos, nl - pos);
     pos = nl + 1;
     if (line.find_first_not_of(" \t\r") == std::string_view::npos) continue;
-    if (apply_raw(line)) {
+    preps.emplace_back().line = line;
+  }
+  size_t width = digits(g_rv + 1);
+  g_apply_pool.run(preps.size(), [&](size_t i) { prepare(preps[i], width); });
+  g_stats.prepare_ns += mono_ns() - t0;
+  for (Prep& p : preps) {
+    std::string_view line = p.line;
+    if (commit(p)) {
       ++n;
       continue;
     }
@@ -1720,7 +1864,7 @@ void handle(Conn& c, Request& r) {
                       ",\"throttled\":" + std::to_string(g_stats.throttled) + ",\"delayed\":" + std::to_string(g_stats.delayed) +
                       ",\"loops\":" + std::to_string(g_stats.loops) + ",\"sends\":" + std::to_string(g_stats.sends) +
                       ",\"send_bytes\":" + std::to_string(g_stats.send_bytes) + ",\"eagain\":" + std::to_string(g_stats.eagain) +
-                      ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
+                      ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"prepare_ns\":" + std::to_string(g_stats.prepare_ns) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
                       ",\"flush_ns\":" + std::to_string(g_stats.flush_ns) + ",\"recv_ns\":" + std::to_string(g_stats.recv_ns) +
                       ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
                       ",\"objects\":{";
@@ -1918,7 +2062,7 @@ void on_signal(int) { g_stop = 1; }
 void usage() {
   fprintf(stderr,
           "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n"
-          "              [--flush-threads N] [--api-latency-us US] [--write-qps Q] [--write-burst B]\n"
+          "              [--flush-threads N] [--apply-threads N] [--api-latency-us US] [--write-qps Q] [--write-burst B]\n"
           "              [--throttle-deletes N] [--retry-after S]\n");
 }
 
@@ -1942,6 +2086,7 @@ int main(int argc, char** argv) {
     else if (a == "--bookmark-ms") g_opt.bookmark_ms = atol(next().c_str());
     else if (a == "--token") g_opt.token = next();
     else if (a == "--flush-threads") g_opt.flush_threads = std::max(1, atoi(next().c_str()));
+    else if (a == "--apply-threads") g_opt.apply_threads = std::max(1, std::min(16, atoi(next().c_str())));
     else if (a == "--api-latency-us") g_opt.api_latency_us = std::max(0L, atol(next().c_str()));
     else if (a == "--write-qps") g_opt.write_qps = atof(next().c_str());
     else if (a == "--write-burst") g_opt.write_burst = atoi(next().c_str());
@@ -1975,6 +2120,14 @@ int main(int argc, char** argv) {
       free(p);
     }
   }
+  // Sparse buckets sized for a benchmark's namespace (10k runs, their pods and tens of
+  // thousands of live Events): short chains, and no rehash of the whole table mid-run
+  for (auto& ks : g_store) {
+    ks.objs.max_load_factor(0.5f);
+    ks.objs.reserve(1 << 16);
+  }
+  g_pods_by_job.max_load_factor(0.5f);
+  g_pods_by_job.reserve(1 << 15);
   prof::start();
   signal(SIGTERM, on_signal);
   signal(SIGINT, on_signal);
@@ -2020,6 +2173,7 @@ int main(int argc, char** argv) {
   fflush(stdout);
 
   g_flush_pool.start(g_opt.flush_threads);
+  g_apply_pool.start(g_opt.apply_threads);
   std::vector<epoll_event> evs(512);
   int64_t last_tick = mono_ms();
   char buf[1 << 16];
@@ -2115,6 +2269,7 @@ int main(int argc, char** argv) {
     g_stats.busy_ns += mono_ns() - t_loop;
   }
   g_flush_pool.stop();
+  g_apply_pool.stop();
   for (auto& kv : g_conns) close(kv.first);
   close(lfd);
   prof::dump();

@@ -60,7 +60,8 @@ async def amain(args) -> None:
         sim = KubeSim(host=args.host, port=args.port, history=args.history, bookmark_ms=2000,
                       flush_threads=args.flush_threads, api_latency_us=args.api_latency_us,
                       write_qps=args.write_qps, write_burst=args.write_burst,
-                      prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "768"))).start()
+                      prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "768")),
+                      apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "3"))).start()
         simctl = SimControl(sim.url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)

@@ -485,9 +485,13 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 watch_objects = (s1["rv"] - s0["rv"]) / n_ev
             # event-loop phases (µs per pod failure): busy = everything but epoll_wait;
             # request includes apply (the synthetic traffic injection)
-            for k in ("busy", "apply", "request", "recv", "flush"):
+            for k in ("busy", "apply", "prepare", "request", "recv", "flush"):
                 if f"{k}_ns" in s1:
                     cpu[f"kubesim_{k}_us_per_event"] = round((s1[f"{k}_ns"] - s0.get(f"{k}_ns", 0)) / 1000.0 / n_ev, 2)
+            if "busy_ns" in s1:
+                # the event loop's busy share of the timed region: the simulator's serial part
+                # (its apply threads only prepare lines for it), what saturates first
+                cpu["kubesim_loop_util"] = round((s1["busy_ns"] - s0.get("busy_ns", 0)) / 1e9 / elapsed, 3)
         if getattr(harness, "cql_shards", None):
             cpu["cqlsrv_shards"] = harness.cql_shards
         workers = [v for k, v in cpu.items() if k.startswith("worker")]

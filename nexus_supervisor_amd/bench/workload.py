@@ -198,7 +198,7 @@ class Workload:
         self._ev += 1
         ev = {"apiVersion": "v1", "kind": "Event",
               "metadata": {"name": f"{name}.{self._ev:x}", "namespace": self.ns, "uid": f"ev-{self.rank}-{self._ev}",
-                           "resourceVersion": self._next_rv()},
+                           "resourceVersion": self._next_rv(), "creationTimestamp": _T0},
               "involvedObject": {"kind": kind, "name": name, "namespace": self.ns, "uid": uid,
                                  "apiVersion": "batch/v1" if kind == "Job" else "v1"},
               "reason": reason, "message": message, "type": etype, "count": 1,
@@ -235,7 +235,7 @@ class Workload:
             job_labels = dict(job_labels, **{self.shard_label: str(self.shard_index)})
         job = {"apiVersion": "batch/v1", "kind": "Job",
                "metadata": {"name": rid, "namespace": ns, "uid": f"job-uid-{rid}", "resourceVersion": self._next_rv(),
-                            "labels": dict(job_labels)},
+                            "creationTimestamp": _T0, "labels": dict(job_labels)},
                "spec": {"backoffLimit": 0, "podFailurePolicy": {"rules": [
                    {"action": "FailJob", "onExitCodes": {"operator": "In", "values": [137, 255]}}]}},
                "status": {"active": 1, "ready": 1, "startTime": _T0} if running else {"active": 1}}
@@ -254,7 +254,7 @@ class Workload:
             status = {"phase": "Pending"}
         pod = {"apiVersion": "v1", "kind": "Pod",
                "metadata": {"name": f"{rid}-w0", "namespace": ns, "uid": f"pod-uid-{rid}-w0",
-                            "resourceVersion": self._next_rv(), "labels": pod_labels},
+                            "resourceVersion": self._next_rv(), "creationTimestamp": _T0, "labels": pod_labels},
                "spec": spec, "status": status}
         now = _dt.datetime.now(_dt.timezone.utc)
         row = CheckpointedRequest(algorithm=self.algorithm, id=rid, lifecycle_stage=stage,

@@ -36,7 +36,8 @@ def encode_events(events: Iterable[Tuple[str, Dict[str, Any]]]) -> bytes:
 class KubeSim:
     def __init__(self, *, host: str = "127.0.0.1", port: int = 0, history: int = 400_000, bookmark_ms: int = 1000,
                  token: str = "", flush_threads: int = 1, api_latency_us: int = 0, write_qps: float = 0.0,
-                 write_burst: int = 0, throttle_deletes: int = 0, retry_after: int = 1, prefault_mb: int = 0):
+                 write_burst: int = 0, throttle_deletes: int = 0, retry_after: int = 1, prefault_mb: int = 0,
+                 apply_threads: int = 1):
         from .._build import binary
 
         self.exe = os.environ.get("NEXUS_KUBESIM_BINARY") or binary("nexus-kubesim")
@@ -49,6 +50,7 @@ class KubeSim:
         self.api_latency_us, self.write_qps, self.write_burst = api_latency_us, write_qps, write_burst
         self.throttle_deletes, self.retry_after = throttle_deletes, retry_after
         self.prefault_mb = prefault_mb  # heap grown and touched at startup (benchmarks)
+        self.apply_threads = apply_threads  # threads preparing a /sim/apply chunk's lines
         self.proc: Optional[subprocess.Popen] = None
         self.log_path = os.path.join(self.dir, "server.log")
         self.url = ""
@@ -65,6 +67,8 @@ class KubeSim:
             argv += ["--flush-threads", str(self.flush_threads)]
         if self.prefault_mb:
             argv += ["--prefault-mb", str(int(self.prefault_mb))]
+        if self.apply_threads > 1:
+            argv += ["--apply-threads", str(int(self.apply_threads))]
         if self.api_latency_us:
             argv += ["--api-latency-us", str(int(self.api_latency_us))]
         if self.write_qps:

@@ -77,7 +77,8 @@ async def main(argv=None):
     steps = [wl.step(args.events) for _ in range(args.steps + 2)]
     bodies = [(failed, encode_events(traffic)) for failed, traffic, _ in steps]
     ft = args.flush_threads or max(1, min(8, args.watchers))
-    with KubeSim(history=50_000, flush_threads=ft, prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "0"))) as sim:
+    with KubeSim(history=50_000, flush_threads=ft, prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "0")),
+                 apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "1"))) as sim:
         host, port = sim.url.split("//")[1].split(":")
         port = int(port)
         ctl = SimControl(sim.url)
@@ -109,7 +110,8 @@ async def main(argv=None):
                       "store_lock_us_per_failure": round((st.get("lock_ns", 0) - l0) / 1e3 / n, 2),
                       "threads": st.get("threads"),
                       "wall_s": round(t1 - t0, 2), "watch_bytes": counter[0], "watchers_per_kind": args.watchers,
-                      "sim": {k: st.get(k) for k in ("requests", "deleted", "applied", "sends")}}))
+                      "sim": {k: st.get(k) for k in ("requests", "deleted", "applied", "sends")},
+                      "us_per_failure": {k[:-3]: round((st.get(k, 0) - st0.get(k, 0)) / 1000 / n, 2) for k in st if k.endswith("_ns")}}))
 
 
 if __name__ == "__main__":
