@@ -109,6 +109,11 @@ def parse_args(argv=None):
                          "GPU slot of the node — each rank is a slot whose runs are on its GPU and whose real "
                          "HBM-OOM must be attributed to that physical GPU (the production shape: one HA "
                          "supervisor, one node agent); replica: one replica + monitor + apiserver per slot")
+    ap.add_argument("--gpu-evidence", choices=("local", "agent"), default="local",
+                    help="local: the supervisor reads the GPU monitor in-process (an in-node supervisor); agent: "
+                         "the chart's deployment — the node agent as its own process (amd-smi monitor) annotates "
+                         "each failed pod and the supervisor, with no local telemetry, holds the decision up to "
+                         "gpu.evidence-wait (2s) for it (wire transport; HBM-OOM text in the termination message)")
     ap.add_argument("--cluster", choices=("auto", "shared", "per-rank"), default="auto",
                     help="per-rank (default) = each GPU-job slot's replica has its own namespace shard, apiserver "
                          "simulator and CQL server; shared = one apiserver + one CQL server for all ranks, each "
@@ -202,6 +207,12 @@ def main(argv=None) -> int:
         "node" if world > 1 and args.transport == "wire" else "replica")
     if slot_mode == "node" and args.transport != "wire":
         raise SystemExit("--slot-mode node needs --transport wire")
+    if args.gpu_evidence == "agent":
+        if args.transport != "wire":
+            raise SystemExit("--gpu-evidence agent needs --transport wire")
+        if args.cluster == "shared" and world > 1:
+            raise SystemExit("--gpu-evidence agent: one agent per apiserver (per-rank cluster or node mode)")
+        args.hbm_shape = "termination-message"  # the agent's node-log reader has no /var/log/pods here
     if args.procs <= 0:
         # node mode: the one replica gets the node's CPU share (the other ranks only run GPU work)
         args.procs = auto_procs(1 if slot_mode == "node" else int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
@@ -272,7 +283,8 @@ def main(argv=None) -> int:
                       kube_connections=args.kube_connections, probe_events=args.probe_events,
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster, run_starts=args.workload == "lifecycle",
-                      pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz, slot_mode=slot_mode)
+                      pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz, slot_mode=slot_mode,
+                      gpu_evidence=args.gpu_evidence)
     res = asyncio.run(run_rank(cfg, barrier_sync, share, oom_phase if slot_mode == "node" and world > 1 else None))
 
     elapsed = res["elapsed"]
@@ -391,6 +403,9 @@ def main(argv=None) -> int:
                 "monitor": res.get("monitor"),
                 # node mode: every slot's real HBM-OOM, at once, attributed to its physical GPU
                 "attribution": res.get("attribution"),
+                # where the supervisor's GPU evidence comes from: its own monitor, or the node
+                # agent's pod annotation (with the agent's cost and the waits that expired)
+                "gpu_evidence": res.get("gpu_evidence"),
                 "cluster": cluster if args.transport == "wire" else "in-process",
                 "shard_label": (not args.no_shard_label) if cluster == "shared" and world > 1 else None,
                 "concurrent_jobs_per_rank": args.jobs,

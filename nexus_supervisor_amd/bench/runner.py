@@ -69,6 +69,10 @@ class BenchConfig:
     # ONE replica and ONE monitor on rank 0 supervise every slot of the node (the production
     # shape: an HA supervisor and one node agent), the other ranks only run their GPU's work
     slot_mode: str = "replica"
+    # "local": the supervisor reads the rank's GPU monitor in-process; "agent": the node agent
+    # process annotates failed pods and the supervisor waits gpu.evidence-wait for it
+    gpu_evidence: str = "local"
+    evidence_wait: float = 2.0
 
     @property
     def node(self) -> bool:
@@ -95,10 +99,16 @@ def supervisor_config(cfg: BenchConfig) -> SupervisorConfig:
     sc.scylla_cql_store.connections_per_host = 2
     sc.compat.fused_write = cfg.fused_write
     sc.compat.conditional_update = cfg.conditional_update
+    if cfg.gpu_evidence == "agent":
+        sc.gpu.evidence_wait = cfg.evidence_wait
+        sc.gpu.local_telemetry = False
+        sc.gpu.backend = "none"
     return sc
 
 
 _RUNNING = "RUNNING"
+# supervisor counters of the node-agent evidence path (the timed region's growth)
+_EVIDENCE_COUNTERS = ("decisions_deferred_for_gpu_evidence", "gpu_evidence_wait_expired", "decisions_awaited_gpu_evidence")
 
 
 class Tracker:
@@ -393,7 +403,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
     if cfg.node and cfg.rank != 0:
         return await run_slot(cfg, barrier_sync, oom_phase)
     sc = supervisor_config(cfg)
-    telemetry = make_telemetry(cfg.telemetry) if cfg.telemetry != "fake" else FakeTelemetry()
+    via_agent = cfg.gpu_evidence == "agent"
+    # agent mode: the real monitor is the agent's (its own process); the runner's is a stand-in
+    telemetry = make_telemetry(cfg.telemetry) if cfg.telemetry != "fake" and not via_agent else FakeTelemetry()
     telemetry.start()
     monitor = await asyncio.get_running_loop().run_in_executor(None, monitor_cost, telemetry)
     if cfg.transport == "inproc":
@@ -404,10 +416,19 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         harness = WireHarness(sc, cfg, cfg.workdir, telemetry=telemetry, share=share, barrier=barrier_sync)
     tracker = Tracker()
     sampler = None
+    agent = None
     try:
         await harness.start()
         sup = harness.supervisor
-        sup.classifier.evidence_provider = pod_evidence_provider(telemetry)
+        if via_agent:
+            from .agentproc import AgentProcess
+
+            agent = await AgentProcess(harness.api, cfg.workdir, f"mi355x-{cfg.rank // 8:03d}", namespace=sc.resource_namespace,
+                                       backend="amdsmi" if cfg.telemetry == "amdsmi" else "fake",
+                                       kube_qps=sc.kube_qps, kube_burst=sc.kube_burst).start()
+            ev0 = {k: sup.metrics.counter(k) for k in _EVIDENCE_COUNTERS}
+        else:
+            sup.classifier.evidence_provider = pod_evidence_provider(telemetry)
         if hasattr(sup, "report_hooks"):  # worker processes: their decision reports as plain tuples
             sup.report_hooks.append(tracker.report)
         else:
@@ -455,6 +476,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         r0 = getattr(pool, "report_cpu_s", 0.0)
         t0 = time.perf_counter()
         c0 = time.process_time()
+        a0 = agent.cpu_s() if agent is not None else 0.0
         x0 = harness.external_cpu()
         sim_stats = getattr(harness, "sim_stats", None)
         s0 = await sim_stats() if sim_stats is not None else None
@@ -466,6 +488,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3),
                "supervisor_max_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1)}
         x1 = harness.external_cpu()
+        if agent is not None:  # the node agent: product code, not harness
+            cpu["agent_util"] = round((agent.cpu_s() - a0) / elapsed, 3)
+            cpu["agent_cpu_us_per_event"] = round((agent.cpu_s() - a0) * 1e6 / max(1, cfg.events * cfg.steps), 1)
         for k in x1:
             cpu[f"{k}_util"] = round((x1[k] - x0.get(k, 0.0)) / elapsed, 3)
         s1 = await sim_stats() if s0 else None
@@ -538,6 +563,17 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             cpu["worker_gpu_update_ms"] = mirror["worker_gpu_update"]
             sizes = (sup.metrics.gauges.get("worker_gpu_update_bytes") or {}).values()
             cpu["worker_gpu_update_bytes_max"] = max(sizes, default=None)
+        gpu_evidence = {"via": "local-monitor"}
+        if agent is not None:
+            am = await agent.metrics()
+            ev = {k: int(sup.metrics.counter(k) - ev0[k]) for k in _EVIDENCE_COUNTERS}
+            deferred = ev["decisions_deferred_for_gpu_evidence"]
+            gpu_evidence = {"via": "node-agent", "evidence_wait_s": cfg.evidence_wait, "counted_over": "warmup+timed",
+                            "agent_annotations": int(sum(v for k, v in am.items() if k.endswith("agent_annotations_total"))),
+                            "agent_util": cpu.get("agent_util"), "agent_cpu_us_per_event": cpu.get("agent_cpu_us_per_event"),
+                            "deferred": deferred, "wait_expired": ev["gpu_evidence_wait_expired"],
+                            "wait_expired_share": round(ev["gpu_evidence_wait_expired"] / deferred, 4) if deferred else None,
+                            "job_decisions_awaited": ev["decisions_awaited_gpu_evidence"]}
         readback = await _read_back(harness, tracker)
         attribution = None
         if cfg.node and oom_phase is not None:
@@ -559,6 +595,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
     finally:
         if sampler is not None:
             sampler.stop()
+        if agent is not None:
+            agent.stop()
         await harness.stop()
         telemetry.stop()
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps * (cfg.world if cfg.node else 1), "errors": tracker.errors,
@@ -569,7 +607,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             "latencies_ms": tracker.latencies, "store": harness.store_name, "workers": sc.workers,
             "actuation": _actuation(sc),
             "eps": sc.rate_limit_elements_per_second, "kube_qps": sc.kube_qps, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
-            "probe": probe, "step_done_ms": step_done_ms, "monitor": monitor, "attribution": attribution}
+            "probe": probe, "step_done_ms": step_done_ms, "monitor": monitor, "attribution": attribution,
+            "gpu_evidence": gpu_evidence}
 
 
 async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dict[str, Any]:

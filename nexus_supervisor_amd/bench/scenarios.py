@@ -441,14 +441,6 @@ async def cfg3_gpu(profile: str, holders: int = 7, hold_gib: float = 30.0) -> Di
         tel.stop()
 
 
-def _free_port() -> int:
-    import socket
-
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
-
-
 async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wait: float = 2.0,
                      sample_interval: float = 0.5) -> Dict[str, Any]:
     """Config 3 through the production attribution path (the chart's deployment): the
@@ -467,13 +459,10 @@ async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wa
     (``gpu_evidence_wait_expired``: written without the agent's evidence) and the pods/log
     reads the supervisor made (0: the agent read the log)."""
     import subprocess
-    import sys
     import tempfile
 
-    import aiohttp
-
     from ..testing.fakelogs import write_cri_log
-    from ..utils.proc import die_with_parent
+    from .agentproc import AgentProcess
 
     work = tempfile.mkdtemp(prefix="cfg3a-")
     logroot = os.path.join(work, "pods")
@@ -490,35 +479,9 @@ async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wa
         exe = binary("gpu_stress")
     try:
         await c.start()
-        kcfg = os.path.join(work, "kubeconfig.yaml")
-        with open(kcfg, "w") as f:
-            json.dump({"apiVersion": "v1", "kind": "Config", "current-context": "bench",
-                       "clusters": [{"name": "bench", "cluster": {"server": c.url}}],
-                       "contexts": [{"name": "bench", "context": {"cluster": "bench", "user": "bench"}}],
-                       "users": [{"name": "bench", "user": {}}]}, f)
-        port = _free_port()
-        env = dict(os.environ, NODE_NAME=c.wl._templates()[4], NEXUS__KUBE_CONFIG_PATH=kcfg,
-                   NEXUS__RESOURCE_NAMESPACE=c.wl.ns, NEXUS__GPU__BACKEND="amdsmi" if gpu else "fake",
-                   NEXUS__GPU__SAMPLE_INTERVAL=f"{int(sample_interval * 1000)}ms", NEXUS__KUBE_QPS="50",
-                   NEXUS__KUBE_BURST="100", NEXUS_AGENT_LOG_ROOT=logroot, NEXUS_AGENT_METRICS_PORT=str(port))
-        agent_log = open(os.path.join(work, "agent.log"), "wb")
-        agent = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd", "agent"], env=env, stdout=agent_log,
-                                 stderr=subprocess.STDOUT, preexec_fn=die_with_parent())
-        agent_log.close()
-        async with aiohttp.ClientSession() as http:
-            deadline = time.monotonic() + 120
-            while True:
-                if agent.poll() is not None:
-                    raise RuntimeError(f"node agent exited rc={agent.returncode}: {_tail(work)}")
-                try:
-                    async with http.get(f"http://127.0.0.1:{port}/healthz") as r:
-                        if r.status == 200:
-                            break
-                except aiohttp.ClientError:
-                    pass
-                if time.monotonic() > deadline:
-                    raise RuntimeError(f"node agent not ready: {_tail(work)}")
-                await asyncio.sleep(0.1)
+        agent = await AgentProcess(c.url, work, c.wl._templates()[4], namespace=c.wl.ns,
+                                   backend="amdsmi" if gpu else "fake", sample_interval=sample_interval,
+                                   log_root=logroot).start()
         sup = c.apps[0].supervisor
         m0 = {k: sup.metrics.counter(k) for k in ("gpu_evidence_wait_expired", "decisions_deferred_for_gpu_evidence",
                                                     "decisions_awaited_gpu_evidence")}
@@ -555,6 +518,7 @@ async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wa
                               "oom": oom})
         dt = time.monotonic() - t_start
         m = {k: sup.metrics.counter(k) - v for k, v in m0.items()}
+        am = await agent.metrics()
         return _summary(f"3a: 1xMI355X via the node agent, {runs} default pods, real HBM-OOM" if gpu else
                         f"3a: node agent (fake GPU backend), {runs} default pods", profile, c.clock.latencies_ms(rids),
                         runs, dt, via="node-agent", evidence_wait_s=evidence_wait, sample_interval_s=sample_interval,
@@ -564,25 +528,14 @@ async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wa
                         deferred_for_gpu_evidence=int(m["decisions_deferred_for_gpu_evidence"]),
                         job_decisions_awaited_evidence=int(m["decisions_awaited_gpu_evidence"]),
                         supervisor_pod_log_reads=len(c.api.log_requests),
+                        agent_annotations=int(sum(v for k, v in am.items() if k.endswith("agent_annotations_total"))),
+                        agent_cpu_s=round(agent.cpu_s(), 2),
                         vram_peak_mb=max((g.get("vram_peak_mb") or 0) for g in ooms) if ooms else None,
                         vram_total_mb=max((g.get("vram_total_mb") or 0) for g in ooms) if ooms else None)
     finally:
-        if agent is not None and agent.poll() is None:
-            agent.terminate()
-            try:
-                agent.wait(10)
-            except subprocess.TimeoutExpired:
-                agent.kill()
-                agent.wait(5)
+        if agent is not None:
+            agent.stop()
         await c.stop()
-
-
-def _tail(work: str) -> str:
-    try:
-        with open(os.path.join(work, "agent.log"), "rb") as f:
-            return f.read()[-2000:].decode(errors="replace")
-    except OSError:
-        return ""
 
 
 CONFIGS = {"1": cfg1_single, "2": cfg2_burst, "3": cfg3_gpu, "3a": cfg3_agent, "4": cfg4_rate, "5": cfg5_chaos,

@@ -134,10 +134,13 @@ class WireHarness:
                            "users": [{"name": "bench", "user": {}}]}, f)
             sc.kube_config_path = kcfg
             sc.runtime.worker_processes = self.cfg.procs
-            # the rank's GPU monitor (owned by the runner) is mirrored into every worker
-            sc.gpu.local_telemetry = True
-            sc.gpu.backend = self.cfg.telemetry
-            self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir, telemetry=self.telemetry)
+            via_agent = self.cfg.gpu_evidence == "agent"
+            if not via_agent:
+                # the rank's GPU monitor (owned by the runner) is mirrored into every worker
+                sc.gpu.local_telemetry = True
+                sc.gpu.backend = self.cfg.telemetry
+            self.app = ShardedApplication(sc, report_decisions=True, log_dir=self.workdir,
+                                          telemetry=None if via_agent else self.telemetry)
         else:
             kube = KubeClient(KubeConfig(info["api"]), max_connections=self.cfg.kube_connections)
             store = CqlCheckpointStore(CqlSession([("127.0.0.1", self.cql_port)],

@@ -261,10 +261,12 @@ class NodeAgent:
             await self.kube.patch_merge("Pod", kube.namespace_of(pod), kube.name_of(pod), body)
         except Exception as exc:  # noqa: BLE001
             self.patch_failures += 1
+            self.metrics.inc("agent_annotation_failures")
             log.warning("annotating pod %s failed: %s", kube.name_of(pod), exc)
             return False
         self.published[kube.uid_of(pod)] = (reason, time.monotonic())
         self.patches += 1
+        self.metrics.inc("agent_annotations")
         return True
 
     async def _publish_with_retry(self, uid: str, key: str, pod: Dict[str, Any], reason: str) -> None:

@@ -21,3 +21,4 @@ def test_agent_process_attributes_default_pods_within_the_wait(arun):
     # the agent read the container log from the node: no pods/log read by the supervisor
     assert r["supervisor_pod_log_reads"] == 0, r
     assert r["p99_ms"] < 2000, r  # well inside the 2 s evidence wait
+    assert r["agent_annotations"] == 4, r  # one annotation PATCH per failed pod

@@ -64,6 +64,24 @@ def test_bench_wire_in_process(tmp_path, capsys):
 
 
 @pytest.mark.slow
+def test_bench_gpu_evidence_through_the_node_agent(capsys):
+    """``--gpu-evidence agent``: the node agent as its own process annotates every failed GPU
+    pod, the supervisor (no local telemetry) holds each decision for it; the line reports the
+    agent's cost and how many waits expired, and every row still reads back correct."""
+    import bench
+
+    rc = bench.main(["--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "40", "--probe-events", "5",
+                     "--probe-rate", "6000", "--gpu-evidence", "agent", "--procs", "2"])
+    assert rc == 0
+    out = json.loads([x for x in capsys.readouterr().out.splitlines() if x.startswith("{")][-1])
+    _check(out, 1, 2, 1, 40)
+    ev = out["config"]["gpu_evidence"]
+    assert ev["via"] == "node-agent" and ev["deferred"] > 0 and ev["agent_annotations"] >= ev["deferred"] * 0.9, ev
+    assert ev["wait_expired"] == 0 and ev["agent_util"] > 0, ev
+    assert out["config"]["hbm_oom_shape"] == "termination-message"
+
+
+@pytest.mark.slow
 def test_bench_fused_actuation_with_priced_lwt(capsys):
     """``--actuation fused`` at a CQL round trip of 2 ms, the LWT priced as a Paxos round
     (3 more round trips): the checkpoint-write stage of the fused path costs ~4 round trips
