@@ -258,7 +258,7 @@ class NodeAgent:
         ev["reason"] = reason
         body = {"metadata": {"annotations": {self.annotation: json.dumps(ev, separators=(",", ":"), sort_keys=True)}}}
         try:
-            await self.kube.patch_merge("Pod", kube.namespace_of(pod), kube.name_of(pod), body)
+            await self.kube.patch_merge("Pod", kube.namespace_of(pod), kube.name_of(pod), body, want_body=False)
         except Exception as exc:  # noqa: BLE001
             self.patch_failures += 1
             self.metrics.inc("agent_annotation_failures")
@@ -374,6 +374,12 @@ async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process 
                       log_root=log_root if cfg.gpu.log_tail != "off" and os.path.isdir(log_root) else None,
                       log_tail_bytes=cfg.gpu.log_tail_bytes)
     await agent.start()
+    sampler = None
+    prof_out = os.environ.get("NEXUS_AGENT_PPROF", "")
+    if prof_out:  # diagnostics: CPU profile of the agent's loop, written at exit
+        from ..obs.pprof import Sampler
+
+        sampler = Sampler(hz=199).start()
     runner = None
     port = int(os.environ.get("NEXUS_AGENT_METRICS_PORT", "0") or 0)
     if port:
@@ -385,6 +391,12 @@ async def run_agent(cfg, node_name: str) -> None:  # pragma: no cover - process 
     for s in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(s, stop.set)
     await stop.wait()
+    if sampler is not None:
+        prof = sampler.stop()
+        with open(prof_out, "wb") as f:
+            f.write(prof.encode_gz())
+        with open(prof_out + ".top.txt", "w") as f:
+            f.write(prof.top(40))
     if runner is not None:
         await runner.cleanup()
     await agent.stop()

@@ -568,9 +568,13 @@ class KubeClient:
     async def replace(self, kind: str, namespace: Optional[str], name: str, obj: Dict[str, Any]) -> Dict[str, Any]:
         return await self.request("PUT", resource_path(kind, namespace, name), body=obj)
 
-    async def patch_merge(self, kind: str, namespace: Optional[str], name: str, patch: Dict[str, Any]) -> Dict[str, Any]:
-        return await self.request("PATCH", resource_path(kind, namespace, name), body=patch,
-                                  content_type="application/merge-patch+json")
+    async def patch_merge(self, kind: str, namespace: Optional[str], name: str, patch: Dict[str, Any],
+                          want_body: bool = True) -> Dict[str, Any]:
+        path = resource_path(kind, namespace, name)
+        if not self.pipelined_writes:
+            return await self.request("PATCH", path, body=patch, content_type="application/merge-patch+json")
+        body = json.dumps(patch, separators=(",", ":")).encode()
+        return await self._write("PATCH", path, body, "application/merge-patch+json", want_body)
 
     async def delete(self, kind: str, namespace: Optional[str], name: str, propagation_policy: str = "Background",
                      want_body: bool = True) -> Dict[str, Any]:
@@ -578,17 +582,21 @@ class KubeClient:
         if not self.pipelined_writes:
             body = {"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": propagation_policy}
             return await self.request("DELETE", path, body=body)
+        return await self._write("DELETE", path, _delete_body(propagation_policy), "application/json", want_body)
+
+    async def _write(self, method: str, path: str, body: bytes, content_type: str, want_body: bool) -> Dict[str, Any]:
+        """A mutation over the pipelined keep-alive connections (an aiohttp request costs
+        several times the CPU): flow control, 429 / Retry-After backoff, API errors raised."""
         attempt = 0
         while True:
-            await self._admit(path, "DELETE")
+            await self._admit(path, method)
             self.requests += 1
-            status, raw = await self._fast_client().request(
-                "DELETE", path, _delete_body(propagation_policy), self._headers({"Content-Type": "application/json"}))
+            status, raw = await self._fast_client().request(method, path, body, self._headers({"Content-Type": content_type}))
             if status < 400 and not want_body:
-                return {}  # the deleted object is not needed: skip decoding it
+                return {}  # the object is not needed: skip decoding it
             hint = retry_after(getattr(raw, "retry_after", None)) if status >= 429 else None
             if status >= 429:
-                d = self._backoff("DELETE", status, hint, attempt)
+                d = self._backoff(method, status, hint, attempt)
                 if d is not None:
                     attempt += 1
                     await asyncio.sleep(d)
