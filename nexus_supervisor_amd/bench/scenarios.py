@@ -530,6 +530,7 @@ async def cfg3_agent(profile: str, runs: int = 20, gpu: bool = True, evidence_wa
                         supervisor_pod_log_reads=len(c.api.log_requests),
                         agent_annotations=int(sum(v for k, v in am.items() if k.endswith("agent_annotations_total"))),
                         agent_cpu_s=round(agent.cpu_s(), 2),
+                        rows_with_gpu_record=sum(1 for g in ooms if g.get("index") == 0),
                         vram_peak_mb=max((g.get("vram_peak_mb") or 0) for g in ooms) if ooms else None,
                         vram_total_mb=max((g.get("vram_total_mb") or 0) for g in ooms) if ooms else None)
     finally:

@@ -552,7 +552,13 @@ class Classifier:
         p = res.pending_enrich
         if p is not None:
             res.pending_enrich = None
-            self._enrich_now(res, *p)
+            pods, texts, verdict = p
+            if res.object_kind == "Job":
+                # a Job-level decision speaks for its pods as they are now: the node agent's
+                # evidence annotation (or the OOM termination) may have landed since the Job's
+                # update was classified
+                pods = lookup.pods_of_job(res.request_id) or pods
+            self._enrich_now(res, pods, texts, verdict)
         self.late_enrich(res, lookup)
 
     def _enrich_now(self, res: RunStatusAnalysisResult, pods=(), texts=(),
@@ -646,6 +652,8 @@ class Classifier:
                     if v.kind:
                         res.evidence["oom"] = v.as_dict()
                         res.failure_class = F.HBM_OOM if v.kind == "hbm" else F.HOST_OOM
+                        if gev and "gpu" not in res.evidence:
+                            res.evidence["gpu"] = gev
         self._apply_history(res)
 
 

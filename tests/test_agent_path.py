@@ -22,3 +22,5 @@ def test_agent_process_attributes_default_pods_within_the_wait(arun):
     assert r["supervisor_pod_log_reads"] == 0, r
     assert r["p99_ms"] < 2000, r  # well inside the 2 s evidence wait
     assert r["agent_annotations"] == 4, r  # one annotation PATCH per failed pod
+    # every row carries the agent's GPU record, whichever decision (pod's or Job's) wrote it
+    assert r["rows_with_gpu_record"] == 4, r

@@ -577,4 +577,5 @@ def test_cfg3a_agent_path_real_hbm_oom(arun):
         json.dump(r, f, indent=1)
     assert r["oom_rcs"] == [1] and r["acked"] == 10 and r["wrong"] == 0, r
     assert r["supervisor_pod_log_reads"] == 0 and r["evidence_wait_expired"] == 0, r
+    assert r["rows_with_gpu_record"] == 10 and r["vram_total_mb"] > 250_000, r
     assert r["vram_peak_mb"] >= 0.9 * r["vram_total_mb"], r
