@@ -95,7 +95,7 @@ def test_bench_fused_actuation_with_priced_lwt(capsys):
     _check(out, 1, 2, 1, 40)
     assert out["config"]["actuation"] == "fused conditional write"
     st = out["config"]["stages_ms"]
-    assert st["stage_write"]["p50"] >= 4 * 2.0 * 0.9  # the CAS itself, not local work (VERDICT r2 weak #8)
+    assert st["stage_write"]["p50"] >= 4 * 2.0 * 0.9  # the CAS itself, not local work
     assert "stage_read" not in st and st["stage_prepare"]["p50"] < 2.0
 
 

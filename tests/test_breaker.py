@@ -144,7 +144,7 @@ def _classified(code, async_delete=True, jobs=None):
 
 
 def test_request_level_cql_errors_do_not_trip_the_breaker(arun):
-    """one partition's WriteTimeout (0x1100) or an Invalid query (0x2200)
+    """One partition's WriteTimeout (0x1100) or an Invalid query (0x2200)
     is a refusal of that request, not a store outage: decisions dead-letter through their
     own retry budget and the breaker stays closed.  Unavailable (0x1000) trips it."""
     for code in (0x1100, 0x2200):
@@ -156,7 +156,7 @@ def test_request_level_cql_errors_do_not_trip_the_breaker(arun):
 
 
 def test_failed_job_delete_after_a_durable_write_counts_for_the_store(arun):
-    """the write landed, then the synchronous Job DELETE failed — the store
+    """The write landed, then the synchronous Job DELETE failed — the store
     answered, so the breaker records a success (it never counts the API server's errors)."""
     from nexus_supervisor_amd.testing.inproc import RecordingJobs
 

@@ -1,4 +1,4 @@
-"""Failover safety (ADVICE r1 app.py:106 / supervisor.py:545), configurable
+"""Failover safety, configurable
 lifecycle stages (weak #5) and the label-mismatch warning (weak #13).
 
 The reference runs every replica on every event with unconditional full-row upserts
@@ -190,7 +190,7 @@ def test_reference_mode_never_conditional():
 
 
 def test_background_delete_outlives_the_retry_budget(arun):
-    """an API outage longer than max-retries must not leak the Job — the key is
+    """An API outage longer than max-retries must not leak the Job — the key is
     marked finished, so the background DELETE is the only thing left that removes it."""
     async def go():
         cfg = _cfg(**{"leader-election": {"enabled": False}, "max-retries": 3})
@@ -222,7 +222,7 @@ def test_stage_strings_and_finished_set_from_yaml_and_env(tmp_path):
         assert cfg.stages.failed == "FAILED_V2" and cfg.stages.cancelled == "ABORTED"
         cfg.stages.apply()
         assert LifecycleStage.FAILED == "FAILED_V2"
-        # only the mapping given: the finished set follows the remapped strings (ADVICE r1)
+        # only the mapping given: the finished set follows the remapped strings
         assert cp_mod.finished_stages() == {"COMPLETED", "FAILED_V2", "SCHEDULING_FAILED", "DEADLINE_EXCEEDED", "ABORTED"}
         assert cp_mod.unfinished_stages() == ("NEW", "BUFFERED", "RUNNING")
         cfg2 = from_mapping(to_mapping(cfg))  # the hand-off to shard-worker processes keeps it
@@ -363,7 +363,7 @@ def test_no_label_mismatch_alarm_for_a_shard_replica_holding_nothing(arun):
 
 def test_unknown_yaml_keys_are_tolerated_with_a_warning(tmp_path, caplog):
     """viper tolerates unknown keys (a reference appconfig with extra keys must start);
-    this build logs them (VERDICT r1 weak #14) and refuses only in strict mode."""
+    this build logs them and refuses only in strict mode."""
     import logging
 
     import pytest

@@ -57,7 +57,7 @@ def _cfg(**over):
 
 
 def test_fused_default_follows_ha():
-    """an LWT is a Paxos round (~4 replica round trips, serialised per
+    """An LWT is a Paxos round (~4 replica round trips, serialised per
     partition), so the default fuses the decision into one conditional write only where
     its atomic stage check is needed — a deposed leader or shard owner may still hold a
     decision — and a lone replica keeps the reference's read + plain write."""
@@ -313,7 +313,7 @@ class FailingCas(MemoryStore):
 
 
 def test_fused_delete_on_store_error_only_when_the_write_never_left(arun):
-    """ADVICE r2 supervisor.py:757: with ``compat.delete-on-read-error`` the fused path used
+    """With ``compat.delete-on-read-error`` the fused path used
     to delete the Job whenever its conditional write failed — also on a timeout after which
     the write may have landed.  Now only a write that provably never reached the store
     (:class:`NotSent`) deletes; otherwise the retry (which sees the finished row) does."""

@@ -30,7 +30,7 @@ def test_oomkilled_wins_tie_with_hip_message():
 def test_vram_peak_alone_is_not_an_oom_verdict():
     """A full GPU without any OOM signature (exit 1, no allocation failure) is recorded as
     a signal, not a verdict: a GPU left full by a previous tenant must not turn a plain
-    crash into an HBM-OOM that bypasses the Job's retry policy (ADVICE r1)."""
+    crash into an HBM-OOM that bypasses the Job's retry policy."""
     ev = {"gpus": [{"index": 3, "vram_total_mb": 294896, "vram_peak_mb": 294000},
                    {"index": 4, "vram_total_mb": 294896, "vram_peak_mb": 1000}]}
     v = oom.analyze(["RuntimeError: something failed"], [{"exitCode": 1}], ev, expected_gpu="3")
@@ -42,7 +42,7 @@ def test_vram_peak_alone_is_not_an_oom_verdict():
 
 
 def test_torch_logical_gpu_maps_to_physical_through_visible_devices():
-    """torch's 'GPU 3' is the process's logical ordinal.  With
+    """Torch's 'GPU 3' is the process's logical ordinal.  With
     HIP_VISIBLE_DEVICES=4,5,6,7 and LOCAL_RANK=3 the failing GPU is physical 7; the trace
     records both and reads GPU 7's evidence, never GPU 3's."""
     from nexus_supervisor_amd.classify import Classifier

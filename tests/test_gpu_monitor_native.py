@@ -159,7 +159,7 @@ def test_classifier_attributes_through_native_monitor(tmp_path):
 
 
 def test_eight_gpu_trace_is_bounded_and_resolves_every_peer(tmp_path):
-    """an 8-GPU job (48 processes, 40 GPU events) on the stub node: the
+    """An 8-GPU job (48 processes, 40 GPU events) on the stub node: the
     trace stays under ``rules.trace-max-bytes``, every xGMI peer resolves to a GPU index,
     the fabric is fully connected by real pairs, the port counts agree with the listed
     links, no cumulative traffic counters are carried — and the OOM verdict survives."""

@@ -286,7 +286,7 @@ def test_parallel_watch_fanout_under_tsan(arun, monkeypatch):
 
 
 def test_priced_apiserver_latency_throttle_and_write_cap(arun):
-    """the simulator prices the API server.  --api-latency-us holds
+    """The simulator prices the API server.  --api-latency-us holds
     object answers (in order on a pipelined connection; LIST unaffected), --throttle-deletes
     answers the first Job DELETEs 429 + Retry-After (the client re-sends after the hint), and
     --write-qps caps mutating requests the way APF rejects them."""

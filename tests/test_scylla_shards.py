@@ -1,4 +1,4 @@
-"""Scylla shard-aware routing (VERDICT r1 missing #1).  The reference pins the
+"""Scylla shard-aware routing.  The reference pins the
 scylladb/gocql fork (``/root/reference/go.mod:93``), which keeps one connection per
 Scylla shard and sends each request to the shard owning its token.  ``nexus-cqlsrv
 --shards N`` emulates a sharded node (shard threads, ``SCYLLA_*`` SUPPORTED keys, the
@@ -103,7 +103,7 @@ def _closed_port():
 
 
 def test_unreachable_shard_aware_port_falls_back_without_leaks(arun):
-    """ADVICE r2 store/cql.py:478: a node advertises SCYLLA_SHARD_AWARE_PORT but the port is
+    """A node advertises SCYLLA_SHARD_AWARE_PORT but the port is
     refused (e.g. a Service exposing only 9042).  The host still comes up — every shard
     reached by reconnecting to the regular port — and nothing is left open but the
     per-shard connections."""
@@ -170,7 +170,7 @@ def test_failed_host_open_closes_what_it_opened(arun, monkeypatch):
 
 
 def test_conditional_writes_never_skip_metadata(arun):
-    """ADVICE r2 store/cql.py:1040: a conditional write prepares with result metadata
+    """A conditional write prepares with result metadata
     ``[applied]`` alone (as Cassandra), while its not-applied answer carries the row's
     stage.  The client must not execute it with skip_metadata, or the finished-row skip
     and the unknown-stage fallback would silently stop working."""

@@ -1,6 +1,6 @@
 """Replica sharding (``parallel/sharding.py``) and per-shard leases (``ha/shards.py``).
 
-VERDICT r1 next-round #7: horizontal scale that can actually be deployed with HA —
+Horizontal scale that can actually be deployed with HA —
 one Lease per shard, a dead owner's shard moves within the lease duration, and no
 run is lost or written twice.  The reference scales by running more replicas that
 all process everything (``/root/reference/.helm/values.yaml:124-125``)."""
@@ -545,7 +545,7 @@ class _Tagged:
 
 
 def test_partitioned_shard_owner_stops_acting_before_anyone_takes_over(arun):
-    """replica A is cut off from the apiserver (every request
+    """Replica A is cut off from the apiserver (every request
     stalls) while it still has a backlog of decisions for its shard.  Its hold lapses
     ``renew-deadline`` after its last renewal started: A issues no write and no Job DELETE
     after that, B acquires the shard only later (a lease duration after it last saw A
@@ -615,7 +615,7 @@ def test_partitioned_shard_owner_stops_acting_before_anyone_takes_over(arun):
 
 
 def test_single_shard_lease_mode_gates_the_whole_namespace(arun):
-    """ADVICE r2 parallel/sharding.py:61: ``mode: lease`` with one shard is one Lease for the
+    """``mode: lease`` with one shard is one Lease for the
     namespace — a replica that loses the race for it acts on nothing (it used to own
     "every shard" and run with leader election silently off)."""
     async def go():
