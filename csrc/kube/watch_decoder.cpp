@@ -759,8 +759,9 @@ class Scan {
   // the large spec / status — so a line costs one short prefix walk instead of the four
   // from-the-start path lookups it used to (the hub's splitter: ~20 % less per line).
   struct Info {
-    std::string_view type, name, rv, job, ikind, iname;
+    std::string_view type, name, rv, job, ikind, iname, reason;
     bool has_type = false, has_name = false, has_rv = false, has_job = false, has_ikind = false, has_iname = false;
+    bool has_reason = false;
   };
 
   bool envelope(bool wrapped, std::string_view job_label, bool want_involved, Info& in) {
@@ -938,12 +939,13 @@ class Scan {
   }
 
   // the object at i_: metadata (name, resourceVersion, labels[job_label]) and, when wanted,
-  // involvedObject (kind, name); returns once those are read, leaving i_ inside the object
+  // an Event's involvedObject (kind, name) and reason; returns once those are read, leaving
+  // i_ inside the object
   bool object_fields(std::string_view job_label, bool want_involved, Info& in) {
     ws();
     if (i_ >= n_ || s_[i_] != '{') return false;
     ++i_;
-    bool meta_done = false, inv_done = !want_involved;
+    bool meta_done = false, inv_done = !want_involved, reason_done = !want_involved;
     while (true) {
       ws();
       if (i_ >= n_ || s_[i_] == '}') return true;
@@ -1011,10 +1013,17 @@ class Scan {
           in.has_iname = true;
         }
         inv_done = true;
+      } else if (!esc && k == "reason" && want_involved && i_ < n_ && s_[i_] == '"') {
+        std::string_view v = str(esc);
+        if (!esc) {
+          in.reason = v;
+          in.has_reason = true;
+        }
+        reason_done = true;
       } else {
         skip_value();
       }
-      if (meta_done && inv_done) return true;
+      if (meta_done && inv_done && reason_done) return true;
       ws();
       if (i_ < n_ && s_[i_] == ',') ++i_;
     }
@@ -1080,6 +1089,11 @@ typedef struct {
   uint32_t rseed;
   std::vector<uint8_t>* owned;
   unsigned long long foreign;
+  // Event reasons the supervisor's rules read (empty = all): an Event with another reason
+  // (Scheduled, Pulling, Pulled, Created, Killing, SuccessfulCreate, ...) decides nothing,
+  // so it is dropped here — no worker decodes, caches or dispatches it
+  std::vector<std::string>* reasons;
+  unsigned long long unread;
 } Router;
 
 enum Role { ROLE_NONE = 0, ROLE_JOB, ROLE_POD, ROLE_EVENT };
@@ -1123,6 +1137,13 @@ void expire_owners(Router* r) {
 // Pod not seen yet).  Pod lines also record the pod's owner for Pod-Event routing.
 constexpr int OWNER_ALL = -1;
 constexpr int OWNER_NONE = -2;  // another replica's run: nobody here sees it
+constexpr int OWNER_SKIP = -3;  // an Event whose reason no rule reads: nobody decodes it
+
+bool reason_read(const Router* r, std::string_view reason) {
+  for (const auto& x : *r->reasons)
+    if (x == reason) return true;
+  return false;
+}
 
 int pod_owner_now(const Router* r, const PodOwner& po) {
   if (po.labeled && !replica_owns_hash(r, po.rhash)) return OWNER_NONE;
@@ -1149,6 +1170,7 @@ int route_info(Router* r, int role, const Scan::Info& in, bool envelope) {
     return pod_owner_now(r, po);
   }
   if (role == ROLE_EVENT) {
+    if (!r->reasons->empty() && in.has_reason && !reason_read(r, in.reason)) return OWNER_SKIP;
     if (!in.has_ikind || !in.has_iname) return OWNER_ALL;
     if (in.ikind == "Job") {
       if (!replica_owns_hash(r, replica_hash(r, in.iname))) return OWNER_NONE;
@@ -1177,6 +1199,7 @@ int route_owner(Router* r, int role, const char* s, size_t n, bool envelope) {
 bool route_line(Router* r, int role, const char* s, size_t n) {
   int owner = route_owner(r, role, s, n, true);
   if (owner == OWNER_NONE) ++r->foreign;
+  else if (owner == OWNER_SKIP) ++r->unread;
   return owner == OWNER_ALL || owner == r->index;
 }
 
@@ -1184,6 +1207,7 @@ void Router_dealloc(Router* self) {
   delete self->job_label;
   delete self->owners;
   delete self->owned;
+  delete self->reasons;
   Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
 }
 
@@ -1201,6 +1225,8 @@ PyObject* Router_new(PyTypeObject* type, PyObject*, PyObject*) {
     self->rseed = 0;
     self->owned = new std::vector<uint8_t>(1, 1);
     self->foreign = 0;
+    self->reasons = new std::vector<std::string>();
+    self->unread = 0;
   }
   return reinterpret_cast<PyObject*>(self);
 }
@@ -1287,9 +1313,30 @@ PyObject* Router_set_replica(Router* self, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+// set_event_reasons(reasons or None) — Event lines with another reason are dropped
+PyObject* Router_set_event_reasons(Router* self, PyObject* arg) {
+  std::vector<std::string> v;
+  if (arg != Py_None) {
+    PyObject* it = PyObject_GetIter(arg);
+    if (!it) return nullptr;
+    PyObject* item;
+    while ((item = PyIter_Next(it)) != nullptr) {
+      Py_ssize_t n;
+      const char* c = PyUnicode_AsUTF8AndSize(item, &n);
+      if (c) v.emplace_back(c, static_cast<size_t>(n));
+      Py_DECREF(item);
+      if (!c) break;
+    }
+    Py_DECREF(it);
+    if (PyErr_Occurred()) return nullptr;
+  }
+  *self->reasons = std::move(v);
+  Py_RETURN_NONE;
+}
+
 PyObject* Router_stats(Router* self, void*) {
-  return Py_BuildValue("{s:K,s:K,s:K,s:n}", "passed", self->passed, "dropped", self->dropped, "foreign",
-                       self->foreign, "pods", static_cast<Py_ssize_t>(self->owners->pod.size()));
+  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:n}", "passed", self->passed, "dropped", self->dropped, "foreign",
+                       self->foreign, "unread", self->unread, "pods", static_cast<Py_ssize_t>(self->owners->pod.size()));
 }
 
 PyMethodDef Router_methods[] = {
@@ -1300,6 +1347,8 @@ PyMethodDef Router_methods[] = {
      "Record a pod's owner (name, owner[, deleted[, job name]])"},
     {"set_replica", reinterpret_cast<PyCFunction>(Router_set_replica), METH_VARARGS,
      "Replica sharding: (shard count, seed, owned shard indexes)"},
+    {"set_event_reasons", reinterpret_cast<PyCFunction>(Router_set_event_reasons), METH_O,
+     "Event reasons any rule reads (None = all): Events with another reason are dropped"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef Router_getset[] = {{"stats", reinterpret_cast<getter>(Router_stats), nullptr, nullptr, nullptr},
@@ -1419,8 +1468,8 @@ PyObject* Splitter_feed(Splitter* self, PyObject* arg) {
       continue;
     }
     int owner = route_info(r, self->role, in, true);
-    if (owner == OWNER_NONE) {
-      ++r->foreign;
+    if (owner == OWNER_NONE || owner == OWNER_SKIP) {
+      ++(owner == OWNER_NONE ? r->foreign : r->unread);
       continue;
     }
     if (owner == OWNER_ALL) {
@@ -1463,8 +1512,8 @@ PyObject* Splitter_split_list(Splitter* self, PyObject* arg) {
   std::vector<std::string> outs(static_cast<size_t>(r->count), std::string("["));
   for (auto& it : items) {
     int owner = route_owner(r, self->role, s + it.first, it.second - it.first, false);
-    if (owner == OWNER_NONE) {
-      ++r->foreign;
+    if (owner == OWNER_NONE || owner == OWNER_SKIP) {
+      ++(owner == OWNER_NONE ? r->foreign : r->unread);
       continue;
     }
     for (int w = 0; w < r->count; ++w) {

@@ -661,6 +661,8 @@ _NO_EV: Dict[str, Any] = {}
 # Event reasons any rule reads (decisions and evidence)
 _EVENT_REASONS = frozenset(R.JOB_EVENT_RULES) | frozenset(R.POD_EVENT_RULES) | frozenset(EVICTION_EVENT_REASONS) | {
     "FailedScheduling"}
+# every Event reason a rule reads; the watch hub drops the others before decode
+EVENT_REASONS_READ = _EVENT_REASONS
 # BackoffLimitExceeded whose cause was found: the run's failure message per class
 _BACKOFF_CAUSE = {F.HBM_OOM: MSG_HBM_OOM, F.HOST_OOM: MSG_HOST_OOM, F.EVICTED: MSG_EVICTED}
 

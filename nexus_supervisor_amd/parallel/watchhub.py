@@ -16,6 +16,10 @@ replica.  The parent process runs the hub:
   frames: ``SNAPSHOT`` (resourceVersion + the worker's items as a JSON array) and
   ``LINES`` (NDJSON watch lines); the hub pauses reading the API server while any
   worker's socket buffer is above a high-water mark (back-pressure end to end);
+* Events whose reason no rule reads (``Scheduled``, ``Pulling``, ``Pulled``, ``Created``,
+  ``Killing``, ``SuccessfulCreate``, … — most of a namespace's Events) are dropped by the
+  splitter before any worker decodes them (:data:`..classify.classifier.EVENT_REASONS_READ`;
+  ``watch_events_unread`` counts them);
 * on ``410 Gone`` / stream errors the hub re-lists and sends every worker a fresh
   snapshot; a worker's :class:`HubListWatch` turns that into the informer's 410 →
   re-list path, so the informer's diff logic is unchanged.  A restarted worker gets a
@@ -78,6 +82,11 @@ class WatchHub:
         self.drain = drain
         self.metrics = metrics
         self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label, POD_FORGET_AFTER)
+        from ..classify.classifier import EVENT_REASONS_READ
+
+        # an Event no rule reads decides nothing: no worker decodes, caches or dispatches it
+        self.router.set_event_reasons(sorted(EVENT_REASONS_READ))
+        self._unread_seen = 0
         from .sharding import ShardSet
 
         self.tasks: Dict[str, asyncio.Task] = {}
@@ -182,6 +191,11 @@ class WatchHub:
                                 rv = last
                             if any(outs):
                                 await self._route(ki, outs, LINES_T, STAMP.pack(t_read))
+                            if ki == 0 and self.metrics is not None:
+                                unread = self.router.stats["unread"]
+                                if unread != self._unread_seen:
+                                    self.metrics.inc("watch_events_unread", unread - self._unread_seen)
+                                    self._unread_seen = unread
                             if errors:
                                 if any(_is_gone(e) for e in errors):
                                     raise _Gone()

@@ -172,6 +172,39 @@ def test_watch_splitter_routes_lines_and_list_items():
         sp_pod.split_list(b'{"kind":"Status"}')
 
 
+def test_splitter_drops_events_no_rule_reads():
+    """With the rules' reasons set, a Scheduled / Pulled / Created Event (most of a
+    namespace's Events) reaches no worker — watch line or LIST item — and is counted as
+    unread; a Started or BackOff Event is routed as before, and without the set everything
+    passes."""
+    from nexus_supervisor_amd.classify.classifier import EVENT_REASONS_READ
+
+    labels = LabelConfig()
+    router = _kube_native.ShardRouter(0, 2, _SEED, JOB_LABEL)
+    sp_ev = _kube_native.WatchSplitter(router, "event")
+    pods = [make_pod(f"job-{i}", labels) for i in range(4)]
+    sp_pod = _kube_native.WatchSplitter(router, "pod")
+    sp_pod.feed(b"".join(_line("ADDED", p) for p in pods))  # pod owners known
+    names = [p["metadata"]["name"] for p in pods]
+    evs = [make_event("Pod", n, r) for n, r in zip(names, ("Scheduled", "Started", "Pulled", "BackOff"))]
+    evs.append(make_event("Job", "job-9", "SuccessfulCreate"))
+    stream = b"".join(_line("ADDED", e) for e in evs)
+    outs, _, _ = sp_ev.feed(stream)
+    assert sum(len(o.splitlines()) for o in outs) == 5  # no reason set: everything routed
+    router.set_event_reasons(sorted(EVENT_REASONS_READ))
+    outs, _, _ = sp_ev.feed(stream)
+    got = sorted(json.loads(l)["object"]["reason"] for o in outs for l in o.splitlines())
+    assert got == ["BackOff", "Started"] and router.stats["unread"] == 3
+    body = _kube_native.dumps({"kind": "EventList", "apiVersion": "v1", "metadata": {"resourceVersion": "7"},
+                               "items": evs})
+    _, parts = sp_ev.split_list(body)
+    assert sorted(e["reason"] for p in parts for e in json.loads(p)) == ["BackOff", "Started"]
+    assert router.stats["unread"] == 6
+    router.set_event_reasons(None)
+    outs, _, _ = sp_ev.feed(stream)
+    assert sum(len(o.splitlines()) for o in outs) == 5
+
+
 def test_hub_feed_batched_watch_matches_per_line(arun):
     """HubListWatch.watch_batches (one list per frame, the informer's path) yields the same
     (type, object) stream as the per-line watch(), and a newer snapshot ends both with a 410

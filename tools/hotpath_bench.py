@@ -109,6 +109,13 @@ async def run(args) -> dict:
     sup.init()
     await sup.start(wait_sync_timeout=60)
 
+    from nexus_supervisor_amd import _kube_native
+    from nexus_supervisor_amd.classify.classifier import EVENT_REASONS_READ
+
+    ev_router = _kube_native.ShardRouter(0, 1, 0, sc.labels.job_name_label)
+    ev_router.set_event_reasons(sorted(EVENT_REASONS_READ))
+    ev_splitter = _kube_native.WatchSplitter(ev_router, "event")
+
     def push(lines_by_kind):
         for k, lines in lines_by_kind.items():
             for i in range(0, len(lines), FRAME_LINES):
@@ -127,7 +134,12 @@ async def run(args) -> dict:
                 o = latest.pop((kind, key), None)
                 if o is not None:
                     echo.append(("DELETED", dict(o, metadata=dict(o["metadata"], resourceVersion=wl._next_rv()))))
-        return failed, new_rows, _lines(traffic, getattr(jobs, "logs", None)), _lines(echo)
+        by_kind = _lines(traffic, getattr(jobs, "logs", None))
+        if by_kind.get("Event"):
+            # the watch hub's splitter (parent process) drops the Events no rule reads
+            outs, _, _ = ev_splitter.feed(b"\n".join(by_kind["Event"]) + b"\n")
+            by_kind["Event"] = outs[0].splitlines()
+        return failed, new_rows, by_kind, _lines(echo)
 
     async def step(data):
         failed, new_rows, traffic, echo = data
