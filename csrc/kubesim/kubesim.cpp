@@ -549,14 +549,18 @@ KindStore g_store[NKINDS];
 std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x01 job → pod names
 // ns \x01 pod → container → log text (bench LOG lines; pods/log answers from it)
 std::unordered_map<std::string, std::unordered_map<std::string, std::string>> g_pod_logs;
-int64_t g_rv = 1000;
+// the store's resourceVersion counter: per-kind commit threads take from it concurrently
+// (each kind's history stays increasing; rvs are unique, not contiguous per kind)
+std::atomic<int64_t> g_rv{1000};
 struct Stats {
-  uint64_t requests = 0, watch_requests = 0, deleted = 0, applied = 0, throttled = 0, delayed = 0;
+  uint64_t requests = 0, watch_requests = 0, applied = 0, throttled = 0, delayed = 0;
+  std::atomic<uint64_t> deleted{0};  // also counted by per-kind commit threads
   uint64_t loops = 0;
   std::atomic<uint64_t> sends{0}, send_bytes{0}, eagain{0};  // also counted by fan-out threads
   // wall time spent per phase of the event loop (ns): where a saturated simulator goes
   int64_t apply_ns = 0, request_ns = 0, flush_ns = 0, recv_ns = 0, busy_ns = 0;
   int64_t prepare_ns = 0;  // the parallel part of apply_ns (wall time)
+  uint64_t commit_parallel = 0;  // bulk-apply chunks committed per kind on threads
 } g_stats;
 
 struct Snapshot {
@@ -573,10 +577,10 @@ std::string okey(std::string_view ns, std::string_view name) {
   return k;
 }
 
-// The same key in a reused buffer (lookups only: no allocation once it has grown).  The
-// apply loop runs on the event-loop thread; the flush threads never look objects up.
+// The same key in a reused buffer (lookups only: no allocation once it has grown), one per
+// thread (the per-kind commit threads of a bulk apply look objects up too).
 const std::string& okey_scratch(std::string_view ns, std::string_view name) {
-  static std::string k;
+  thread_local std::string k;
   k.assign(ns.data(), ns.size());
   k += '\x01';
   k.append(name.data(), name.size());
@@ -935,12 +939,12 @@ std::shared_ptr<const Attrs> attrs_raw(const Raw& r) {
 
 // Store text for a raw-scanned object: server metadata spliced in (src = the line, the
 // object spans [ob, oe)).  Same edits as finish() without the DOM.
-Obj finish_raw(const Raw& r, std::string_view src, size_t ob, size_t oe, const Obj* prev) {
+Obj finish_raw(const Raw& r, std::string_view src, size_t ob, size_t oe, const Obj* prev, int64_t rv = 0) {
   Obj o;
   o.ns = std::string(r.ns);
   o.name = std::string(r.name);
   o.job = std::string(r.job);
-  o.rv = ++g_rv;
+  o.rv = rv > 0 ? rv : ++g_rv;
   std::string rvs = std::to_string(o.rv);
   std::string ins;  // inserted right after metadata's '{'
   if (r.uid.empty()) {
@@ -992,7 +996,8 @@ struct Prep {
   std::string_view line, type;
   int kind = -1;
   // 0: not raw (DOM path), 1: DELETED, 2: text prepared, 3: raw but needs the stored
-  // object (uid / creationTimestamp / resourceVersion to complete): built at commit
+  // object (uid / creationTimestamp / resourceVersion to complete): built at commit,
+  // 4: a bench LOG line (pods/log text; DOM path)
   int mode = 0;
   Raw r;
   size_t ob = 0, oe = 0;
@@ -1014,6 +1019,10 @@ void prepare(Prep& p, size_t width) {
   Raw& r = p.r;
   r.labels.reserve(8);
   if (!sc.envelope(p.type, p.ob, p.oe, r)) return;
+  if (p.type == "LOG") {
+    p.mode = 4;
+    return;
+  }
   if (!r.has_kind || !r.has_api || !r.has_md || r.md_keys == 0 || r.name.empty() || r.has_gen) return;
   p.kind = kind_by_name(r.kind);
   if (p.kind < 0) return;
@@ -1045,7 +1054,7 @@ void prepare(Prep& p, size_t width) {
 
 // false → the caller takes the DOM path
 bool commit(Prep& p) {
-  if (p.mode == 0) return false;
+  if (p.mode == 0 || p.mode == 4) return false;
   if (p.mode == 1) {
     remove(p.kind, p.r.ns, p.r.name, "Background");
     return true;
@@ -1054,13 +1063,14 @@ bool commit(Prep& p) {
   auto it = ks.objs.find(okey_scratch(p.r.ns, p.r.name));
   const Obj* prev = it == ks.objs.end() ? nullptr : &it->second;
   Obj o;
-  if (p.mode == 2 && digits(g_rv + 1) == p.o.rv_len) {
+  int64_t rv = ++g_rv;
+  if (p.mode == 2 && digits(rv) == p.o.rv_len) {
     o = std::move(p.o);
-    o.rv = ++g_rv;
+    o.rv = rv;
     std::to_chars(&(*p.text)[o.rv_off], &(*p.text)[o.rv_off] + o.rv_len, o.rv);
     o.json = std::move(p.text);
   } else {
-    o = finish_raw(p.r, p.line, p.ob, p.oe, prev);
+    o = finish_raw(p.r, p.line, p.ob, p.oe, prev, rv);
   }
   if (p.kind == K_POD && !(prev && prev->job == o.job)) {
     if (prev) index_pod(*prev, false);
@@ -1087,8 +1097,9 @@ class ParallelFor {
     for (auto& t : workers_) t.join();
     workers_.clear();
   }
-  void run(size_t n, const std::function<void(size_t)>& fn) {
-    if (workers_.empty() || n < 64) {
+  // blocks of `block` indexes; fewer than `min_n` run inline on the caller
+  void run(size_t n, const std::function<void(size_t)>& fn, size_t block = 16, size_t min_n = 64) {
+    if (workers_.empty() || n < min_n) {
       for (size_t i = 0; i < n; ++i) fn(i);
       return;
     }
@@ -1096,6 +1107,7 @@ class ParallelFor {
       std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn;
       n_ = n;
+      block_ = block;
       next_.store(0);
       pending_ = workers_.size();
       ++gen_;
@@ -1110,8 +1122,8 @@ class ParallelFor {
  private:
   void work() {
     size_t b;
-    while ((b = next_.fetch_add(16)) < n_)
-      for (size_t i = b; i < std::min(n_, b + 16); ++i) (*fn_)(i);
+    while ((b = next_.fetch_add(block_)) < n_)
+      for (size_t i = b; i < std::min(n_, b + block_); ++i) (*fn_)(i);
   }
   void loop() {
     uint64_t seen = 0;
@@ -1131,7 +1143,7 @@ class ParallelFor {
   std::mutex mu_;
   std::condition_variable cv_, done_;
   const std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0;
+  size_t n_ = 0, block_ = 16;
   std::atomic<size_t> next_{0};
   size_t pending_ = 0;
   uint64_t gen_ = 0;
@@ -1291,10 +1303,15 @@ void close_conn(int fd) {
   g_conns.erase(it);
 }
 
+std::mutex g_dirty_mu;  // a bulk apply's per-kind commit threads mark watch connections dirty
+
 void watch_push(Watch* w, const Line& line) {
   if (w->idle()) {
     auto it = g_conns.find(w->fd);
-    if (it != g_conns.end()) g_dirty.insert(it->second.get());
+    if (it != g_conns.end()) {
+      std::lock_guard<std::mutex> lk(g_dirty_mu);
+      g_dirty.insert(it->second.get());
+    }
   }
   w->lines_bytes += line.size();
   w->lines.push_back(line);
@@ -1754,9 +1771,31 @@ void h_apply(Conn& c, const Request& r) {
   size_t width = digits(g_rv + 1);
   g_apply_pool.run(preps.size(), [&](size_t i) { prepare(preps[i], width); });
   g_stats.prepare_ns += mono_ns() - t0;
+  // Kinds are independent stores with their own histories and watchers: when every line is
+  // a prepared object, an Event deletion or a LOG line, each kind's lines are committed in
+  // order on a thread of their own (the Events, half of a benchmark's lines, beside the Pods
+  // and Jobs).  Anything that crosses kinds or needs the serial helpers — a Job or Pod
+  // deletion (GC cascade, pod index, pod logs), a line for the DOM path, an object to
+  // complete from the stored one — keeps the whole chunk on the loop, in order.
+  bool by_kind = g_opt.apply_threads > 1;
+  std::vector<std::vector<Prep*>> kinds(NKINDS);
+  for (Prep& p : preps) {
+    if (!by_kind) break;
+    if (p.mode == 2 || (p.mode == 1 && p.kind != K_JOB && p.kind != K_POD)) kinds[p.kind].push_back(&p);
+    else if (p.mode != 4) by_kind = false;
+  }
+  if (by_kind) {
+    std::vector<int> busy;
+    for (int k = 0; k < NKINDS; ++k)
+      if (!kinds[k].empty()) busy.push_back(k);
+    g_apply_pool.run(busy.size(), [&](size_t i) {
+      for (Prep* p : kinds[busy[i]]) commit(*p);
+    }, 1, 2);
+    g_stats.commit_parallel += 1;
+  }
   for (Prep& p : preps) {
     std::string_view line = p.line;
-    if (commit(p)) {
+    if (by_kind ? p.mode != 4 : commit(p)) {
       ++n;
       continue;
     }
@@ -1864,7 +1903,7 @@ void handle(Conn& c, Request& r) {
                       ",\"throttled\":" + std::to_string(g_stats.throttled) + ",\"delayed\":" + std::to_string(g_stats.delayed) +
                       ",\"loops\":" + std::to_string(g_stats.loops) + ",\"sends\":" + std::to_string(g_stats.sends) +
                       ",\"send_bytes\":" + std::to_string(g_stats.send_bytes) + ",\"eagain\":" + std::to_string(g_stats.eagain) +
-                      ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"prepare_ns\":" + std::to_string(g_stats.prepare_ns) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
+                      ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"prepare_ns\":" + std::to_string(g_stats.prepare_ns) + ",\"commit_parallel\":" + std::to_string(g_stats.commit_parallel) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
                       ",\"flush_ns\":" + std::to_string(g_stats.flush_ns) + ",\"recv_ns\":" + std::to_string(g_stats.recv_ns) +
                       ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
                       ",\"objects\":{";

@@ -222,3 +222,63 @@ def test_inprocess_extensions_under_sanitizer(sanitize):
     assert "instrumented:" in out, out[-3000:]
     assert p.returncode == 0, out[-4000:]
     assert not any(r in out for r in _REPORTS), out[-4000:]
+
+
+@pytest.mark.parametrize("sanitize", ["thread", "address"])
+def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
+    """``nexus-kubesim`` with apply and fan-out threads: bulk applies of the lifecycle
+    workload (lines prepared on threads, kinds committed on threads) while three watches
+    stream and Job DELETEs cascade to their pods on another connection."""
+    from nexus_supervisor_amd.bench.workload import Workload
+    from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig
+    from nexus_supervisor_amd.testing.kubesim import KubeSim, SimControl, encode_events
+
+    _sanitized(sanitize)
+    os.environ["NEXUS_KUBESIM_BINARY"] = os.path.join(_build.BIN, f"nexus-kubesim-{sanitize}")
+    try:
+        sim = KubeSim(apply_threads=4, flush_threads=2, history=20_000).start(timeout=30)
+    finally:
+        os.environ.pop("NEXUS_KUBESIM_BINARY", None)
+    try:
+        async def go():
+            ctl = SimControl(sim.url)
+            wl = Workload(concurrent_jobs=300, hbm_shape="default-pod")
+            objs, _rows = wl.initial()
+            await ctl.apply([("ADDED", o) for o in objs])
+            rv = str((await ctl.stats())["rv"])
+            kc = KubeClient(KubeConfig(sim.url))
+            seen = {"Event": 0, "Pod": 0, "Job": 0}
+
+            async def watch(kind):
+                async for _t, _o in kc.watch(kind, "nexus", rv, timeout_seconds=30):
+                    seen[kind] += 1
+
+            tasks = [asyncio.ensure_future(watch(k)) for k in seen]
+            await asyncio.sleep(0.3)
+            lines = 0
+            for _ in range(8):
+                st = wl.step(60)
+                body = encode_events([(t, o) for t, o in st.traffic])
+                lines += body.count(b"\n")
+                await ctl.apply_raw(body)
+                await asyncio.gather(*(kc.delete_job("nexus", rid) for rid in st.failed))
+            for _ in range(200):
+                if seen["Event"] and seen["Pod"] and seen["Job"]:
+                    break
+                await asyncio.sleep(0.05)
+            await asyncio.sleep(0.5)
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+            stats = await ctl.stats()
+            await kc.close()
+            await ctl.close()
+            return seen, lines, stats
+
+        seen, lines, stats = arun(go(), timeout=240)
+    finally:
+        sim.stop()
+    log = sim.log()
+    assert not any(r in log for r in _REPORTS), log[-4000:]
+    assert all(seen.values()), seen
+    assert stats.get("commit_parallel", 0) > 0, stats  # the kinds were committed on threads
