@@ -462,17 +462,27 @@ def test_multi_rank_job_root_cause_from_a_real_hbm_oom(telemetry, stress_exe, tm
 
 def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, telemetry):
     """The GPU is filled by another tenant (``gpu_stress hbm-oom`` holding every chunk it
-    got, down to 8 MiB ones), then a fresh torch process needs a HIP context, a hipBLAS
-    handle and a 2 GiB buffer.  Whatever ROCm prints there — torch's ``C10_HIP_CHECK`` ``HIP error: out of
-    memory``, a hipBLAS / rocBLAS allocation status, or torch's ``OutOfMemoryError`` — is the
-    real text of a default pod's log tail, and it must be classified hbm-oom on GPU 0."""
+    got), then a fresh torch process needs a HIP context, a hipBLAS handle and a 2 GiB
+    buffer.  Two fill levels:
+
+    * 0.5 GiB chunks (under 0.5 GiB left): the context comes up and the allocation fails —
+      whatever ROCm / torch print (``HIP error: out of memory``, a hipBLAS / rocBLAS status,
+      torch's ``OutOfMemoryError``) is the real text of a default pod's log tail and must be
+      classified hbm-oom on GPU 0;
+    * then 8 MiB chunks into the rest (under 8 MiB left): the process may die while the HIP
+      runtime initialises.  If it printed an allocation failure that is hbm-oom as above; if
+      it printed none (a crash with nothing in the log) the row must NOT claim an HBM-OOM —
+      the other tenant's full GPU is no evidence about this pod."""
     import sys
 
-    # two fillers allocate chunks until HIP refuses one, write their termination logs and
-    # hold every chunk (--linger): 0.5 GiB chunks, then 8 MiB chunks into what is left, so
-    # the GPU keeps less than 8 MiB free — too little for a new process's HIP context and
-    # hipBLAS workspace, where ROCm's own "HIP error: out of memory" wording comes from
-    holders, hold_gib = [], []
+    from nexus_supervisor_amd.gpu import oom
+
+    code = ("import torch\n"
+            "a = torch.randn(256, 256, device='cuda')\n"
+            "b = a @ a\n"
+            "c = torch.empty(int(2 * 2**30), dtype=torch.uint8, device='cuda')\n"
+            "torch.cuda.synchronize()\n")
+    holders, fills, runs = [], [], []
     try:
         for i, chunk in enumerate(("0.5", "0.0078125")):
             done = tmp_path / f"filler{i}.termination"
@@ -483,13 +493,9 @@ def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, 
             while not done.exists() and holders[-1].poll() is None and time.time() < deadline:
                 time.sleep(0.2)
             assert done.exists() and holders[-1].poll() is None, f"filler {i} did not reach its OOM"
-            hold_gib.append(done.read_text()[:300])
-        code = ("import torch\n"
-                "a = torch.randn(256, 256, device='cuda')\n"
-                "b = a @ a\n"
-                "c = torch.empty(int(2 * 2**30), dtype=torch.uint8, device='cuda')\n"
-                "torch.cuda.synchronize()\n")
-        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+            fills.append(done.read_text()[:300])
+            p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+            runs.append({"fill_chunk_gib": float(chunk), "rc": p.returncode, "stderr": p.stderr})
     finally:
         for holder in holders:
             holder.terminate()
@@ -498,19 +504,25 @@ def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, 
             except subprocess.TimeoutExpired:
                 holder.kill()
                 holder.wait(30)
-    assert p.returncode != 0, (p.returncode, p.stderr[-800:])
-    from nexus_supervisor_amd.gpu import oom
-
-    sig = oom.hbm_signature(p.stderr)
-    assert sig, p.stderr[-1500:]
-    trace, _reqs = _supervise_default_pod(arun, tmp_path, p.stderr, p.returncode, agent=False)
-    assert trace["class"] == "hbm-oom", trace
-    assert trace["oom"].get("gpu_index", 0) == 0
+    out = []
+    for k, r in enumerate(runs):
+        assert r["rc"] != 0, (r["rc"], r["stderr"][-800:])
+        sig = oom.hbm_signature(r["stderr"])
+        exit_code = r["rc"] if r["rc"] > 0 else 128 - r["rc"]  # killed by a signal: 128 + signo
+        trace, _reqs = _supervise_default_pod(arun, tmp_path / f"run{k}", r["stderr"], exit_code,
+                                              agent=False)
+        if k == 0:
+            assert sig, r["stderr"][-1500:]
+        if sig:
+            assert trace["class"] == "hbm-oom" and trace["oom"].get("gpu_index", 0) == 0, trace
+        else:
+            assert trace["class"] != "hbm-oom", trace  # no text, a crash: no OOM is claimed
+        out.append({"fill_chunk_gib": r["fill_chunk_gib"], "rc": r["rc"], "signature": sig,
+                    "runtime_check_wording": "error: out of memory" in r["stderr"].lower(),
+                    "stderr_tail": r["stderr"][-1500:], "class": trace["class"], "trace": trace})
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/hip_runtime_oom.json", "w") as f:
-        json.dump({"filler": hold_gib, "rc": p.returncode, "signature": sig,
-                   "runtime_check_wording": "error: out of memory" in p.stderr.lower(),
-                   "stderr_tail": p.stderr[-1500:], "trace": trace}, f, indent=1)
+        json.dump({"fillers": fills, "runs": out}, f, indent=1)
 
 
 def test_node_agent_privileges_reported_on_the_box(stress_exe, tmp_path):
