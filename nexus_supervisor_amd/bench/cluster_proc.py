@@ -61,7 +61,7 @@ async def amain(args) -> None:
                       flush_threads=args.flush_threads, api_latency_us=args.api_latency_us,
                       write_qps=args.write_qps, write_burst=args.write_burst,
                       prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "768")),
-                      apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "4"))).start()
+                      apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "6"))).start()
         simctl = SimControl(sim.url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)
