@@ -40,8 +40,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dump")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--thread", choices=("all", "event-loop", "helper-thread"), default="all",
+                    help="only the samples of the event loop / the apply and fan-out threads")
     a = ap.parse_args()
     samples = [line.split() for line in open(a.dump) if line.strip()]
+    if a.thread != "all":
+        samples = [s for s in samples if s and s[-1] == f"[{a.thread}]+0x0"]
     names = symbolise({f for s in samples for f in s})
     flat, cum = collections.Counter(), collections.Counter()
     for s in samples:
