@@ -226,7 +226,7 @@ const KindInfo KINDS[] = {{"Event", "v1", "events"},
                           {"Lease", "coordination.k8s.io/v1", "leases"},
                           {"Node", "v1", "nodes"}};
 constexpr int NKINDS = sizeof(KINDS) / sizeof(KINDS[0]);
-constexpr int K_POD = 1, K_JOB = 2;
+constexpr int K_EVENT = 0, K_POD = 1, K_JOB = 2;
 
 int kind_by_plural(std::string_view p) {
   for (int i = 0; i < NKINDS; ++i)
@@ -1002,7 +1002,9 @@ struct Prep {
   int kind = -1;
   // 0: not raw (DOM path), 1: DELETED, 2: text prepared, 3: raw but needs the stored
   // object (uid / creationTimestamp / resourceVersion to complete): built at commit,
-  // 4: a bench LOG line (pods/log text; DOM path)
+  // 4: a bench LOG line (pods/log text; DOM path), 5: complete, built at commit (Pods and
+  // Jobs: the loop thread that commits them also frees them — Job DELETEs, pod GC — so
+  // their memory comes from that thread's heap cache, not a pool thread's)
   int mode = 0;
   Raw r;
   size_t ob = 0, oe = 0;
@@ -1037,6 +1039,10 @@ void prepare(Prep& p, size_t width) {
   }
   if (r.uid.empty() || !r.created.data() || !r.has_rv) {
     p.mode = 3;
+    return;
+  }
+  if (p.kind != K_EVENT) {
+    p.mode = 5;
     return;
   }
   Obj& o = p.o;
@@ -1119,6 +1125,28 @@ class ParallelFor {
     }
     cv_.notify_all();
     work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+  // fn(0) on the caller, fn(1..n-1) on the pool threads only (the caller waits for them)
+  void run_pinned(size_t n, const std::function<void(size_t)>& fn) {
+    if (workers_.empty() || n < 2) {
+      for (size_t i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      block_ = 1;
+      next_.store(1);
+      pending_ = workers_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [this] { return pending_ == 0; });
     fn_ = nullptr;
@@ -1786,16 +1814,23 @@ void h_apply(Conn& c, const Request& r) {
   std::vector<std::vector<Prep*>> kinds(NKINDS);
   for (Prep& p : preps) {
     if (!by_kind) break;
-    if (p.mode == 2 || (p.mode == 1 && p.kind != K_JOB && p.kind != K_POD)) kinds[p.kind].push_back(&p);
+    if (p.mode == 2 || p.mode == 5 || (p.mode == 1 && p.kind != K_JOB && p.kind != K_POD)) kinds[p.kind].push_back(&p);
     else if (p.mode != 4) by_kind = false;
   }
   if (by_kind) {
-    std::vector<int> busy;
-    for (int k = 0; k < NKINDS; ++k)
-      if (!kinds[k].empty()) busy.push_back(k);
-    g_apply_pool.run(busy.size(), [&](size_t i) {
-      for (Prep* p : kinds[busy[i]]) commit(*p);
-    }, 1, 2);
+    // the Events (most lines, and all the expiry deletions) on a pool thread; Pods and Jobs on
+    // the loop, which also deletes them (Job DELETE requests, GC) — their memory is freed by
+    // the thread that holds its heap's cache
+    std::vector<std::vector<int>> groups(1);
+    for (int k = 0; k < NKINDS; ++k) {
+      if (kinds[k].empty()) continue;
+      if (k == K_EVENT) groups.push_back({k});
+      else groups[0].push_back(k);
+    }
+    g_apply_pool.run_pinned(groups.size(), [&](size_t i) {
+      for (int k : groups[i])
+        for (Prep* p : kinds[k]) commit(*p);
+    });
     g_stats.commit_parallel += 1;
   }
   for (Prep& p : preps) {
