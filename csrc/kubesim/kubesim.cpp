@@ -723,7 +723,13 @@ struct Raw {
   std::string_view node, phase, ikind, iname, reason, type;
   bool has_kind = false, has_api = false, has_md = false, has_rv = false, has_gen = false;
   size_t md_open = 0, md_keys = 0, rv_off = 0, rv_len = 0;
-  std::vector<std::pair<std::string_view, std::string_view>> labels;
+  // labels inline (no heap: a bulk apply's lines are scanned on pool threads and dropped
+  // on the loop); an object with more goes the DOM path
+  static constexpr size_t kMaxLabels = 24;
+  std::pair<std::string_view, std::string_view> label_buf[kMaxLabels];
+  size_t nlabels = 0;
+  const std::pair<std::string_view, std::string_view>* labels_begin() const { return label_buf; }
+  const std::pair<std::string_view, std::string_view>* labels_end() const { return label_buf + nlabels; }
 };
 
 class RawScan {
@@ -897,7 +903,8 @@ class RawScan {
               std::string_view lv;
               field(lv, r);
               if (lv.data()) {
-                r.labels.emplace_back(lk, lv);
+                if (r.nlabels < Raw::kMaxLabels) r.label_buf[r.nlabels++] = {lk, lv};
+                else r.ok = false;
                 if (lk == "batch.kubernetes.io/job-name") r.job = lv;
               }
             });
@@ -929,9 +936,9 @@ class RawScan {
 std::shared_ptr<const Attrs> attrs_raw(const Raw& r) {
   auto a = std::make_shared<Attrs>();
   size_t bytes = 8 * 40;
-  for (auto& kv : r.labels) bytes += kv.first.size() + kv.second.size() + 8;
+  for (auto* kv = r.labels_begin(); kv != r.labels_end(); ++kv) bytes += kv->first.size() + kv->second.size() + 8;
   a->reserve(bytes + r.name.size() + r.ns.size() + r.node.size() + r.iname.size());
-  for (auto& kv : r.labels) a->add(kv.first, kv.second);
+  for (auto* kv = r.labels_begin(); kv != r.labels_end(); ++kv) a->add(kv->first, kv->second);
   const std::pair<const char*, std::string_view> fields[] = {
       {"\x01" "f:metadata.name", r.name},  {"\x01" "f:metadata.namespace", r.ns},
       {"\x01" "f:spec.nodeName", r.node},   {"\x01" "f:status.phase", r.phase},
@@ -1024,7 +1031,6 @@ size_t digits(int64_t v) {
 void prepare(Prep& p, size_t width) {
   RawScan sc(p.line.data(), p.line.size());
   Raw& r = p.r;
-  r.labels.reserve(8);
   if (!sc.envelope(p.type, p.ob, p.oe, r)) return;
   if (p.type == "LOG") {
     p.mode = 4;
