@@ -85,7 +85,7 @@ class WireHarness:
         self.proc = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd.bench.cluster_proc", "--cql",
                                       f"127.0.0.1:{self.cql.port}", "--ready-file", ready, "--history", str(history),
                                       # every rank's replica watches the shared namespace: fan out in parallel
-                                      "--flush-threads", str(min(8, cfg.world) if self.shared else 2),
+                                      "--flush-threads", str(min(8, cfg.world) if self.shared else 3),
                                       "--api-latency-us", str(int(cfg.api_latency_us)),
                                       "--write-qps", str(float(cfg.api_write_qps))],
                                      env=env, stdout=self._log, stderr=self._log, start_new_session=True,
