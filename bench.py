@@ -149,15 +149,16 @@ def auto_procs(local_world: int) -> int:
 
 def _harness_bound(cpu) -> dict:
     """Did a harness process limit the run?  The traffic generator by its CPU share, the
-    apiserver simulator by its event loop's busy share, the sharded CQL server by its
-    per-shard CPU."""
+    apiserver simulator by its busiest serial part (event loop, apply port, store lock), the
+    sharded CQL server by its per-shard CPU."""
     util = {k[:-5]: v for k, v in cpu.items() if k in ("kubesim_util", "cqlsrv_util", "cluster_util")}
     limit = dict(util)
     if "cqlsrv" in limit:
         limit["cqlsrv"] = util["cqlsrv"] / max(1, int(cpu.get("cqlsrv_shards") or 1))
-    if "kubesim" in limit and cpu.get("kubesim_loop_util") is not None:
-        # the simulator's event loop (its apply threads prepare lines off the loop): busy share
-        limit["kubesim"] = cpu["kubesim_loop_util"]
+    if "kubesim" in limit and cpu.get("kubesim_serial_util") is not None:
+        # the simulator is multi-threaded: its serial parts (event loop, apply port, store
+        # lock), not its process CPU, say whether it saturated
+        limit["kubesim"] = cpu["kubesim_serial_util"]
     bound = any(v >= 0.9 for v in limit.values())
     out = {"bound": bound, "util": util, "limit_util": {k: round(v, 3) for k, v in limit.items()}}
     if bound:

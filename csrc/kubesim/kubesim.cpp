@@ -55,6 +55,7 @@
 #include <pthread.h>
 #include <signal.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 #include <sys/uio.h>
@@ -557,6 +558,12 @@ std::unordered_map<std::string, std::unordered_map<std::string, std::string>> g_
 // the store's resourceVersion counter: per-kind commit threads take from it concurrently
 // (each kind's history stays increasing; rvs are unique, not contiguous per kind)
 std::atomic<int64_t> g_rv{1000};
+// The store (objects, histories, watchers' pending lines, the pod index and logs, the
+// connection table and the dirty set) is the event loop's, except while the apply thread
+// commits a bulk apply: both take g_store_mu for every touch.  The loop holds it while it
+// handles requests and timers, never across epoll_wait, recv or a watch's sendmsg.
+std::mutex g_store_mu;
+
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, applied = 0, throttled = 0, delayed = 0;
   std::atomic<uint64_t> deleted{0};  // also counted by per-kind commit threads
@@ -565,8 +572,18 @@ struct Stats {
   // wall time spent per phase of the event loop (ns): where a saturated simulator goes
   int64_t apply_ns = 0, request_ns = 0, flush_ns = 0, recv_ns = 0, busy_ns = 0;
   int64_t prepare_ns = 0;  // the parallel part of apply_ns (wall time)
+  int64_t store_ns = 0;    // time g_store_mu was held (loop + apply thread): the serial part
+  std::atomic<int64_t> apply_thread_ns{0};  // the apply port's busy time (reading, applying)
   uint64_t commit_parallel = 0;  // bulk-apply chunks committed per kind on threads
 } g_stats;
+
+// g_store_mu held for the scope; the hold time counts into g_stats.store_ns
+struct StoreLock {
+  std::unique_lock<std::mutex> lk;
+  int64_t t0;
+  StoreLock() : lk(g_store_mu), t0(mono_ns()) {}
+  ~StoreLock() { g_stats.store_ns += mono_ns() - t0; }
+};
 
 struct Snapshot {
   int64_t rv;
@@ -1028,7 +1045,7 @@ size_t digits(int64_t v) {
   return n;
 }
 
-void prepare(Prep& p, size_t width) {
+void prepare(Prep& p, size_t width, bool build_all) {
   RawScan sc(p.line.data(), p.line.size());
   Raw& r = p.r;
   if (!sc.envelope(p.type, p.ob, p.oe, r)) return;
@@ -1047,7 +1064,7 @@ void prepare(Prep& p, size_t width) {
     p.mode = 3;
     return;
   }
-  if (p.kind != K_EVENT) {
+  if (p.kind != K_EVENT && !build_all) {
     p.mode = 5;
     return;
   }
@@ -1361,24 +1378,42 @@ void watch_push(Watch* w, const Line& line) {
 // take is copied into c.out.  false = connection error.
 bool flush_watch(Conn& c) {
   Watch* w = c.watch;
+  // the committed lines are taken under the store lock (the apply thread may be appending)
+  // and sent without it; the taken Lines keep their texts alive
+  thread_local std::vector<Line> lines;
+  thread_local std::string pending;
+  size_t lines_bytes;
+  {
+    StoreLock lk;
+    if (w->idle()) return true;
+    lines.swap(w->lines);
+    pending.swap(w->pending);
+    lines_bytes = w->lines_bytes;
+    w->clear();
+    w->last_ms = mono_ms();
+  }
+  struct Done {
+    ~Done() {
+      lines.clear();
+      pending.clear();
+    }
+  } done;
   char hdr[24];
-  int hl = snprintf(hdr, sizeof hdr, "%zx\r\n", w->pending.size() + w->lines_bytes);
-  w->last_ms = mono_ms();
+  int hl = snprintf(hdr, sizeof hdr, "%zx\r\n", pending.size() + lines_bytes);
   if (!c.out.empty()) {  // keep the byte order: append behind what is queued
     c.out.append(hdr, static_cast<size_t>(hl));
-    c.out += w->pending;
-    for (auto& l : w->lines) append_line(c.out, l);
+    c.out += pending;
+    for (auto& l : lines) append_line(c.out, l);
     c.out += "\r\n";
-    w->clear();
     return true;
   }
   static char crlf[] = "\r\n";
   thread_local std::vector<iovec> iov;  // reused across flushes (one per fan-out thread)
   iov.clear();
-  iov.reserve(5 * w->lines.size() + 3);
+  iov.reserve(5 * lines.size() + 3);
   iov.push_back({hdr, static_cast<size_t>(hl)});
-  if (!w->pending.empty()) iov.push_back({w->pending.data(), w->pending.size()});
-  for (auto& l : w->lines) {  // pointers into w->lines stay valid until w->clear()
+  if (!pending.empty()) iov.push_back({pending.data(), pending.size()});
+  for (auto& l : lines) {  // pointers into the taken lines stay valid until they are cleared
     iov.push_back({const_cast<char*>(l.prefix->data()), l.prefix->size()});
     char* j = const_cast<char*>(l.json->data());
     if (l.rvn) {
@@ -1423,13 +1458,12 @@ bool flush_watch(Conn& c) {
     break;
   }
   for (; ok && i < iov.size(); ++i) c.out.append(static_cast<const char*>(iov[i].iov_base), iov[i].iov_len);
-  w->clear();
   return ok;
 }
 
 // write out a connection's queued bytes (and its watch's committed lines)
 bool flush(Conn& c) {
-  if (c.watch && !c.watch->idle() && !flush_watch(c)) return false;
+  if (c.watch && !flush_watch(c)) return false;
   size_t off = 0;
   while (off < c.out.size()) {
     ssize_t n = send(c.fd, c.out.data() + off, c.out.size() - off, MSG_NOSIGNAL);
@@ -1793,10 +1827,15 @@ void close_watches(int only_kind) {
   for (Conn* c : cs) end_watch(*c, true);
 }
 
-void h_apply(Conn& c, const Request& r) {
+std::mutex g_pool_mu;  // one bulk apply at a time uses the apply pool (loop port or apply port)
+
+// Applies an NDJSON body of watch events; returns the /sim/apply answer.  `locked`: the
+// caller (the event loop) holds g_store_mu.  Otherwise (the apply port) the lines are
+// prepared without it — every object's text built on the pool — and committed under it.
+std::string apply_body(std::string_view b, bool expire, bool locked) {
+  std::lock_guard<std::mutex> pool_lk(g_pool_mu);
   int64_t t0 = mono_ns();
   size_t pos = 0, n = 0;
-  std::string_view b = r.body;
   std::vector<Prep> preps;
   preps.reserve(b.size() / 512 + 16);  // a guess (objects are ~0.6-1.5 KB): no pass over the body
   while (pos < b.size()) {
@@ -1808,14 +1847,16 @@ void h_apply(Conn& c, const Request& r) {
     preps.emplace_back().line = line;
   }
   size_t width = digits(g_rv + 1);
-  g_apply_pool.run(preps.size(), [&](size_t i) { prepare(preps[i], width); });
-  g_stats.prepare_ns += mono_ns() - t0;
+  g_apply_pool.run(preps.size(), [&](size_t i) { prepare(preps[i], width, !locked); });
+  int64_t t_prep = mono_ns() - t0;
+  std::unique_ptr<StoreLock> lk;
+  if (!locked) lk = std::make_unique<StoreLock>();
   // Kinds are independent stores with their own histories and watchers: when every line is
   // a prepared object, an Event deletion or a LOG line, each kind's lines are committed in
   // order on a thread of their own (the Events, half of a benchmark's lines, beside the Pods
   // and Jobs).  Anything that crosses kinds or needs the serial helpers — a Job or Pod
   // deletion (GC cascade, pod index, pod logs), a line for the DOM path, an object to
-  // complete from the stored one — keeps the whole chunk on the loop, in order.
+  // complete from the stored one — keeps the whole chunk on one thread, in order.
   bool by_kind = g_opt.apply_threads > 1;
   std::vector<std::vector<Prep*>> kinds(NKINDS);
   for (Prep& p : preps) {
@@ -1825,8 +1866,8 @@ void h_apply(Conn& c, const Request& r) {
   }
   if (by_kind) {
     // the Events (most lines, and all the expiry deletions) on a pool thread; Pods and Jobs on
-    // the loop, which also deletes them (Job DELETE requests, GC) — their memory is freed by
-    // the thread that holds its heap's cache
+    // the calling thread (on the loop port: the loop, which also deletes them — Job DELETE
+    // requests, GC — so their memory is freed by the thread whose heap cache it came from)
     std::vector<std::vector<int>> groups(1);
     for (int k = 0; k < NKINDS; ++k) {
       if (kinds[k].empty()) continue;
@@ -1869,7 +1910,8 @@ void h_apply(Conn& c, const Request& r) {
     ++n;
   }
   g_stats.applied += n;
-  if (q(r, "expire") == "1") {
+  g_stats.prepare_ns += t_prep;
+  if (expire) {
     // compaction that overtakes the watchers: undelivered lines are lost, resuming
     // streams get 410 Gone and must re-list (exercises the informer's relist diff)
     for (auto& kv : g_conns)
@@ -1881,8 +1923,10 @@ void h_apply(Conn& c, const Request& r) {
   char buf[160];
   snprintf(buf, sizeof buf, "{\"applied\":%zu,\"rv\":%lld,\"t_push\":%.9f}", n, static_cast<long long>(g_rv),
            static_cast<double>(t0) / 1e9);
-  respond(c, 200, buf);
+  return buf;
 }
+
+void h_apply(Conn& c, const Request& r) { respond(c, 200, apply_body(r.body, q(r, "expire") == "1", true)); }
 
 // GET /api/v1/namespaces/{ns}/pods/{name}/log?container=&tailLines=&limitBytes= (kubelet-proxied
 // in a real cluster; priced like any object request with --api-latency-us)
@@ -1952,6 +1996,8 @@ void handle(Conn& c, Request& r) {
                       ",\"apply_ns\":" + std::to_string(g_stats.apply_ns) + ",\"prepare_ns\":" + std::to_string(g_stats.prepare_ns) + ",\"commit_parallel\":" + std::to_string(g_stats.commit_parallel) + ",\"request_ns\":" + std::to_string(g_stats.request_ns) +
                       ",\"flush_ns\":" + std::to_string(g_stats.flush_ns) + ",\"recv_ns\":" + std::to_string(g_stats.recv_ns) +
                       ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
+                      ",\"store_ns\":" + std::to_string(g_stats.store_ns) +
+                      ",\"apply_thread_ns\":" + std::to_string(g_stats.apply_thread_ns.load()) +
                       ",\"objects\":{";
       for (int k = 0; k < NKINDS; ++k) {
         if (k) s += ',';
@@ -2141,8 +2187,103 @@ bool on_input(Conn& c) {
   return true;
 }
 
-volatile sig_atomic_t g_stop = 0;
-void on_signal(int) { g_stop = 1; }
+std::atomic<int> g_stop{0};  // read by the apply threads too (lock-free: signal-safe)
+void on_signal(int) { g_stop.store(1); }
+
+// ------------------------------------------------------------ apply port
+// The benchmark's traffic generator posts its bulk applies to a port of their own, served
+// by their own threads: reading a multi-megabyte body and preparing its lines happen beside
+// the event loop, which keeps serving the supervisor's requests and watches; only the commit
+// takes the store lock.  The loop port still accepts /sim/apply (on the loop).
+int g_wake_fd = -1;  // eventfd: an apply committed watch lines the loop must send
+
+void apply_conn(int fd) {
+  std::string in;
+  std::vector<char> buf(1 << 16);
+  while (!g_stop) {
+    size_t he;
+    while ((he = in.find("\r\n\r\n")) == std::string::npos) {
+      ssize_t r = recv(fd, buf.data(), buf.size(), 0);
+      if (r <= 0) {
+        close(fd);
+        return;
+      }
+      in.append(buf.data(), static_cast<size_t>(r));
+    }
+    int64_t t0 = mono_ns();
+    std::string_view head(in.data(), he);
+    size_t le = head.find("\r\n");
+    std::string_view rl = head.substr(0, le);
+    size_t s1 = rl.find(' '), s2 = rl.rfind(' ');
+    // copies: reading the rest of the body may reallocate `in`
+    std::string method(rl.substr(0, s1));
+    std::string target(s1 == std::string_view::npos || s2 <= s1 ? std::string_view() : rl.substr(s1 + 1, s2 - s1 - 1));
+    size_t clen = 0;
+    size_t pos = le == std::string_view::npos ? head.size() : le + 2;
+    while (pos < head.size()) {
+      size_t e = head.find("\r\n", pos);
+      if (e == std::string_view::npos) e = head.size();
+      std::string_view line = head.substr(pos, e - pos);
+      pos = e + 2;
+      size_t colon = line.find(':');
+      if (colon != std::string_view::npos && iequals(line.substr(0, colon), "content-length"))
+        clen = static_cast<size_t>(strtoull(std::string(trim_view(line.substr(colon + 1))).c_str(), nullptr, 10));
+    }
+    if (in.capacity() < he + 4 + clen) in.reserve(he + 4 + clen);
+    while (in.size() < he + 4 + clen) {
+      ssize_t r = recv(fd, buf.data(), buf.size(), 0);
+      if (r <= 0) {
+        close(fd);
+        return;
+      }
+      in.append(buf.data(), static_cast<size_t>(r));
+    }
+    std::string_view body(in.data() + he + 4, clen);
+    int code = 200;
+    std::string out;
+    if (method == "POST" && target.substr(0, target.find('?')) == "/sim/apply" &&
+        target.find("expire=1") == std::string::npos) {
+      try {
+        out = apply_body(body, false, false);
+      } catch (const std::exception& e) {
+        code = 400;
+        out = status_body(400, "BadRequest", e.what());
+      }
+      uint64_t one = 1;
+      if (write(g_wake_fd, &one, sizeof one) < 0) { /* the loop wakes within 100 ms anyway */ }
+    } else {
+      code = 404;
+      out = status_body(404, "NotFound", "the apply port serves POST /sim/apply (without expire) only");
+    }
+    std::string resp = "HTTP/1.1 " + std::to_string(code) + " " + status_text(code) +
+                       "\r\nContent-Type: application/json\r\nContent-Length: " + std::to_string(out.size()) + "\r\n\r\n" + out;
+    size_t off = 0;
+    while (off < resp.size()) {
+      ssize_t w = send(fd, resp.data() + off, resp.size() - off, MSG_NOSIGNAL);
+      if (w <= 0) {
+        close(fd);
+        return;
+      }
+      off += static_cast<size_t>(w);
+    }
+    in.erase(0, he + 4 + clen);
+    g_stats.apply_thread_ns += mono_ns() - t0;
+  }
+  close(fd);
+}
+
+void apply_server(int afd) {
+  int one = 1;
+  while (!g_stop) {
+    int cfd = accept(afd, nullptr, nullptr);
+    if (cfd < 0) {
+      if (errno == EINTR) continue;
+      return;
+    }
+    setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    std::thread(apply_conn, cfd).detach();
+  }
+}
 
 void usage() {
   fprintf(stderr,
@@ -2241,8 +2382,27 @@ int main(int argc, char** argv) {
   lev.data.fd = lfd;
   epoll_ctl(g_ep, EPOLL_CTL_ADD, lfd, &lev);
 
-  char info[160];
-  snprintf(info, sizeof info, "{\"port\":%d,\"pid\":%d,\"url\":\"http://%s:%d\"}\n", port, getpid(), g_opt.host.c_str(), port);
+  // the apply port (bulk applies on their own threads) and the loop's wake-up eventfd
+  int afd = socket(AF_INET, SOCK_STREAM, 0);
+  setsockopt(afd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in aaddr = addr;
+  aaddr.sin_port = 0;
+  if (bind(afd, reinterpret_cast<sockaddr*>(&aaddr), sizeof aaddr) < 0 || listen(afd, 64) < 0) {
+    perror("bind/listen (apply port)");
+    return 1;
+  }
+  socklen_t aalen = sizeof aaddr;
+  getsockname(afd, reinterpret_cast<sockaddr*>(&aaddr), &aalen);
+  int aport = ntohs(aaddr.sin_port);
+  g_wake_fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  epoll_event wev{};
+  wev.events = EPOLLIN;
+  wev.data.fd = g_wake_fd;
+  epoll_ctl(g_ep, EPOLL_CTL_ADD, g_wake_fd, &wev);
+
+  char info[256];
+  snprintf(info, sizeof info, "{\"port\":%d,\"pid\":%d,\"url\":\"http://%s:%d\",\"apply_url\":\"http://%s:%d\"}\n", port,
+           getpid(), g_opt.host.c_str(), port, g_opt.host.c_str(), aport);
   if (!g_opt.ready_file.empty()) {
     std::string tmp = g_opt.ready_file + ".tmp";
     FILE* f = fopen(tmp.c_str(), "w");
@@ -2259,16 +2419,20 @@ int main(int argc, char** argv) {
 
   g_flush_pool.start(g_opt.flush_threads);
   g_apply_pool.start(g_opt.apply_threads);
+  std::thread(apply_server, afd).detach();
   std::vector<epoll_event> evs(512);
   int64_t last_tick = mono_ms();
   char buf[1 << 16];
   while (!g_stop) {
     int wait_ms = 100;
-    if (!g_delayed.empty()) {
-      int d = release_delayed();
-      if (d >= 0) wait_ms = std::min(wait_ms, d);
+    {
+      StoreLock lk;
+      if (!g_delayed.empty()) {
+        int d = release_delayed();
+        if (d >= 0) wait_ms = std::min(wait_ms, d);
+      }
+      if (!g_dirty.empty()) wait_ms = 0;
     }
-    if (!g_dirty.empty()) wait_ms = 0;
     int n = epoll_wait(g_ep, evs.data(), static_cast<int>(evs.size()), wait_ms);
     int64_t t_loop = mono_ns();
     ++g_stats.loops;
@@ -2278,6 +2442,11 @@ int main(int argc, char** argv) {
     }
     for (int i = 0; i < n; ++i) {
       int fd = evs[i].data.fd;
+      if (fd == g_wake_fd) {
+        uint64_t v;
+        if (read(g_wake_fd, &v, sizeof v) < 0) { /* drained */ }
+        continue;
+      }
       if (fd == lfd) {
         while (true) {
           int cfd = accept(lfd, nullptr, nullptr);
@@ -2290,13 +2459,19 @@ int main(int argc, char** argv) {
           ev.events = EPOLLIN | EPOLLRDHUP;
           ev.data.fd = cfd;
           epoll_ctl(g_ep, EPOLL_CTL_ADD, cfd, &ev);
+          StoreLock lk;
           g_conns[cfd] = std::move(c);
         }
         continue;
       }
-      auto it = g_conns.find(fd);
-      if (it == g_conns.end()) continue;
-      Conn& c = *it->second;
+      Conn* cp;
+      {
+        StoreLock lk;
+        auto it = g_conns.find(fd);
+        if (it == g_conns.end()) continue;
+        cp = it->second.get();
+      }
+      Conn& c = *cp;  // only the loop erases connections
       bool dead = false;
       if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
         int64_t tr = mono_ns();
@@ -2314,14 +2489,19 @@ int main(int argc, char** argv) {
           break;
         }
         g_stats.recv_ns += mono_ns() - tr;
-        if (!dead && !on_input(c)) dead = true;
+        if (!dead) {
+          StoreLock lk;
+          if (!on_input(c)) dead = true;
+        }
       }
+      StoreLock lk;
       if (dead) {
         close_conn(fd);
         continue;
       }
       if (evs[i].events & EPOLLOUT) g_dirty.insert(&c);
     }
+    StoreLock tick_lk;
     if (!g_delayed.empty()) release_delayed();
     int64_t now = mono_ms();
     if (now - last_tick >= 50) {
@@ -2341,15 +2521,23 @@ int main(int argc, char** argv) {
       }
       for (Conn* c : ended) end_watch(*c, true);
     }
-    if (!g_dirty.empty()) {
+    std::vector<Conn*> dirty(g_dirty.begin(), g_dirty.end());
+    g_dirty.clear();
+    tick_lk.lk.unlock();
+    g_stats.store_ns += mono_ns() - tick_lk.t0;
+    tick_lk.t0 = mono_ns();  // (the destructor adds the re-locked span below)
+    if (!dirty.empty()) {
       int64_t tf = mono_ns();
-      std::vector<Conn*> dirty(g_dirty.begin(), g_dirty.end());
-      g_dirty.clear();
       std::vector<uint8_t> ok(dirty.size(), 1);
       g_flush_pool.run(dirty, ok);
+      tick_lk.lk.lock();
+      tick_lk.t0 = mono_ns();
       for (size_t i = 0; i < dirty.size(); ++i)
         if (!ok[i]) close_conn(dirty[i]->fd);
       g_stats.flush_ns += mono_ns() - tf;
+    } else {
+      tick_lk.lk.lock();
+      tick_lk.t0 = mono_ns();
     }
     g_stats.busy_ns += mono_ns() - t_loop;
   }

@@ -62,7 +62,7 @@ async def amain(args) -> None:
                       write_qps=args.write_qps, write_burst=args.write_burst,
                       prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "768")),
                       apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "6"))).start()
-        simctl = SimControl(sim.url)
+        simctl = SimControl(sim.url, sim.apply_url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)
 

@@ -514,9 +514,15 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 if f"{k}_ns" in s1:
                     cpu[f"kubesim_{k}_us_per_event"] = round((s1[f"{k}_ns"] - s0.get(f"{k}_ns", 0)) / 1000.0 / n_ev, 2)
             if "busy_ns" in s1:
-                # the event loop's busy share of the timed region: the simulator's serial part
-                # (its apply threads only prepare lines for it), what saturates first
-                cpu["kubesim_loop_util"] = round((s1["busy_ns"] - s0.get("busy_ns", 0)) / 1e9 / elapsed, 3)
+                # the simulator's serial parts over the timed region: its event loop's busy share,
+                # its apply port's, and the store lock's hold time (the loop and the apply port
+                # both commit under it) — the largest is what saturates first
+                share = {k: round((s1.get(f"{k}_ns", 0) - s0.get(f"{k}_ns", 0)) / 1e9 / elapsed, 3)
+                         for k in ("busy", "apply_thread", "store")}
+                cpu["kubesim_loop_util"] = share["busy"]
+                cpu["kubesim_apply_port_util"] = share["apply_thread"]
+                cpu["kubesim_store_util"] = share["store"]
+                cpu["kubesim_serial_util"] = max(share.values())
         if getattr(harness, "cql_shards", None):
             cpu["cqlsrv_shards"] = harness.cql_shards
         workers = [v for k, v in cpu.items() if k.startswith("worker")]

@@ -54,6 +54,7 @@ class KubeSim:
         self.proc: Optional[subprocess.Popen] = None
         self.log_path = os.path.join(self.dir, "server.log")
         self.url = ""
+        self.apply_url = ""  # the bulk-apply port (its own threads beside the event loop)
 
     def start(self, timeout: float = 10.0) -> "KubeSim":
         ready = os.path.join(self.dir, "ready")
@@ -92,6 +93,7 @@ class KubeSim:
                     info = json.load(f)
                 self.port = info["port"]
                 self.url = info["url"]
+                self.apply_url = info.get("apply_url", "")
                 return self
             if self.proc.poll() is not None:
                 raise RuntimeError(f"nexus-kubesim exited rc={self.proc.returncode}: {self.log()}")
@@ -123,10 +125,13 @@ class KubeSim:
 
 
 class SimControl:
-    """Async client for the ``/sim/*`` control endpoints (one pooled aiohttp session)."""
+    """Async client for the ``/sim/*`` control endpoints (one pooled aiohttp session).
+    ``apply_url``: the simulator's apply port — bulk applies are read and prepared there
+    beside the event loop (``expire`` ones still go to the loop)."""
 
-    def __init__(self, url: str):
+    def __init__(self, url: str, apply_url: str = ""):
         self.url = url.rstrip("/")
+        self.apply_url = (apply_url or url).rstrip("/")
         self._s = None
 
     async def _session(self):
@@ -140,7 +145,8 @@ class SimControl:
         """Commit watch events; ``expire`` compacts history past them before any watcher
         reads them (resuming watches get 410 Gone)."""
         s = await self._session()
-        async with s.post(self.url + "/sim/apply", data=encode_events(events), params={"expire": "1"} if expire else None,
+        base = self.url if expire else self.apply_url
+        async with s.post(base + "/sim/apply", data=encode_events(events), params={"expire": "1"} if expire else None,
                           headers={"Content-Type": "application/x-ndjson"}) as r:
             doc = await r.json(content_type=None)
             if r.status != 200:
@@ -150,7 +156,7 @@ class SimControl:
     async def apply_raw(self, body: bytes) -> Dict[str, Any]:
         """``apply`` with a pre-encoded NDJSON body (:func:`encode_events`)."""
         s = await self._session()
-        async with s.post(self.url + "/sim/apply", data=body, headers={"Content-Type": "application/x-ndjson"}) as r:
+        async with s.post(self.apply_url + "/sim/apply", data=body, headers={"Content-Type": "application/x-ndjson"}) as r:
             doc = await r.json(content_type=None)
             if r.status != 200:
                 raise RuntimeError(f"/sim/apply: {r.status} {doc}")

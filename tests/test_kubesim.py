@@ -25,6 +25,51 @@ def _cfg(**over):
     return load_config(path=None, env={}, overrides=base)
 
 
+def test_apply_port_commits_beside_the_loop(arun):
+    """Bulk applies on the apply port (read and prepared on their own threads, committed
+    under the store lock) reach watches and REST like loop-port applies; the port serves
+    nothing else."""
+    import aiohttp
+
+    async def go():
+        labels = _cfg().labels
+        with KubeSim(apply_threads=4, flush_threads=2) as sim:
+            assert sim.apply_url and sim.apply_url != sim.url
+            ctl = SimControl(sim.url, sim.apply_url)
+            c = KubeClient(KubeConfig(sim.url))
+            rv = str((await ctl.stats())["rv"])
+            seen = []
+
+            async def watch():
+                async for t, o in c.watch("Pod", "nexus", rv, timeout_seconds=10):
+                    seen.append((t, o["metadata"]["name"]))
+
+            task = asyncio.ensure_future(watch())
+            await asyncio.sleep(0.2)
+            pods = [make_pod(f"a{i}", labels) for i in range(200)]
+            out = await ctl.apply([("ADDED", p) for p in pods])
+            assert out["applied"] == 200
+            await c.delete("Pod", "nexus", pods[0]["metadata"]["name"])
+            for _ in range(100):
+                if len(seen) >= 201:
+                    break
+                await asyncio.sleep(0.05)
+            task.cancel()
+            await asyncio.gather(task, return_exceptions=True)
+            assert len([s for s in seen if s[0] == "ADDED"]) == 200 and seen[-1] == ("DELETED", pods[0]["metadata"]["name"])
+            items, _ = await c.list("Pod", "nexus")
+            assert len(items) == 199
+            st = await ctl.stats()
+            assert st["apply_thread_ns"] > 0 and st["store_ns"] > 0
+            async with aiohttp.ClientSession() as s:
+                async with s.get(sim.apply_url + "/sim/stats") as r:
+                    assert r.status == 404
+            await c.close()
+            await ctl.close()
+
+    arun(go(), timeout=60)
+
+
 def test_rest_semantics(arun):
     async def go():
         labels = _cfg().labels

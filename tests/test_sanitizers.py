@@ -241,7 +241,7 @@ def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
         os.environ.pop("NEXUS_KUBESIM_BINARY", None)
     try:
         async def go():
-            ctl = SimControl(sim.url)
+            ctl = SimControl(sim.url, sim.apply_url)
             wl = Workload(concurrent_jobs=300, hbm_shape="default-pod")
             objs, _rows = wl.initial()
             await ctl.apply([("ADDED", o) for o in objs])

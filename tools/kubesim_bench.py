@@ -81,7 +81,7 @@ async def main(argv=None):
                  apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "1"))) as sim:
         host, port = sim.url.split("//")[1].split(":")
         port = int(port)
-        ctl = SimControl(sim.url)
+        ctl = SimControl(sim.url, sim.apply_url)
         await ctl.apply_raw(encode_events(("ADDED", o) for o in objs))
         stop, counter = threading.Event(), [0]
         ths = [threading.Thread(target=drain, args=(host, port, p, stop, counter), daemon=True)
