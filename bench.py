@@ -49,8 +49,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--jobs", type=int, default=10_000, help="concurrent live jobs per rank")
-    ap.add_argument("--events", type=int, default=5000,
-                    help="pod-fail events per step per rank (5000: the driver's 20 steps time at least 5 s on one MI355X box)")
+    ap.add_argument("--events", type=int, default=6000,
+                    help="pod-fail events per step per rank (6000: the driver's 20 steps time at least 5 s on one MI355X box)")
     ap.add_argument("--transport", choices=("wire", "inproc"), default="wire")
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
