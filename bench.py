@@ -48,9 +48,11 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--jobs", type=int, default=10_000, help="concurrent live jobs per rank")
-    ap.add_argument("--events", type=int, default=6000,
-                    help="pod-fail events per step per rank (6000: the driver's 20 steps time at least 5 s on one MI355X box)")
+    ap.add_argument("--jobs", type=int, default=None,
+                    help="concurrent live jobs per rank (default 10,000; node mode: 10,000 over the node's slots)")
+    ap.add_argument("--events", type=int, default=None,
+                    help="pod-fail events per step per rank (default 6,000: the driver's 20 steps time at least 5 s on "
+                         "one MI355X box; node mode: 6,000 over the node's slots)")
     ap.add_argument("--transport", choices=("wire", "inproc"), default="wire")
     ap.add_argument("--profile", choices=("uncapped", "reference"), default="uncapped",
                     help="reference = Helm defaults (10 eps, burst 100, 2 workers)")
@@ -215,6 +217,15 @@ def main(argv=None) -> int:
         if args.cluster == "shared" and world > 1:
             raise SystemExit("--gpu-evidence agent: one agent per apiserver (per-rank cluster or node mode)")
         args.hbm_shape = "termination-message"  # the agent's node-log reader has no /var/log/pods here
+    # Node mode is ONE replica and ONE simulator for the whole node: the north-star namespace
+    # (10k concurrent jobs, 6,000 failures a step) is split over the slots, so N slots measure
+    # the same supervisor on the same total work — strong scaling.  Replica mode keeps the
+    # per-slot work fixed (weak scaling: N replicas, N clusters).
+    node_split = slot_mode == "node" and world > 1
+    if args.jobs is None:
+        args.jobs = -(-10_000 // world) if node_split else 10_000
+    if args.events is None:
+        args.events = -(-6000 // world) if node_split else 6000
     if args.procs <= 0:
         # node mode: the one replica gets the node's CPU share (the other ranks only run GPU work)
         args.procs = auto_procs(1 if slot_mode == "node" else int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
@@ -361,7 +372,7 @@ def main(argv=None) -> int:
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * max_elapsed / max(args.steps, 1), 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if cluster == "node" else "weak",
             "vs_baseline": round(eps / REFERENCE_EPS, 2),
             "dtype": "n/a (control plane, no GPU compute)",
             "data": "synthetic pod-failure events, random job ids (no cluster / dataset)",

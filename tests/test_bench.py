@@ -22,7 +22,9 @@ def _check(out, n, steps, warmup, events):
         base = json.load(f)
     assert out["metric"] == base["metric"] or out["metric"].startswith("pod-fail")
     assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
-    assert out["scaling"] == "weak" and out["higher_is_better"] is True and out["errors"] == 0
+    # node mode: one replica over the node's slots on a split namespace (strong); else per-slot work (weak)
+    assert out["scaling"] == ("strong" if out["config"].get("cluster") == "node" else "weak")
+    assert out["higher_is_better"] is True and out["errors"] == 0
     assert out["value"] > 0 and out["config"]["global_batch"] == events * n
     assert abs(out["vs_baseline"] - out["value"] / 10.0) < 0.05
     assert out["p50_ms"] is not None and out["p99_ms"] >= out["p50_ms"]
