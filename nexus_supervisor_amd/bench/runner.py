@@ -627,6 +627,17 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     saved, tracker.latencies = tracker.latencies, []
     saved_parts, tracker.parts = tracker.parts, []
     saved_starts, tracker.start_latencies = tracker.start_latencies, []
+    if cfg.run_starts:
+        # the last timed step's new runs start now, before the first arrival: thousands of
+        # starts in one burst are the saturated workload's, not the north-star churn's
+        docs = await harness.step(0)
+        for d in (docs if isinstance(docs, list) else [docs]):
+            st = tracker.arm(d["rids"], d["t_push"], d.get("expected"), d.get("started"), d.get("start_expected"))
+            try:
+                await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
+            except asyncio.TimeoutError:
+                tracker.abandon(st)
+        tracker.latencies, tracker.parts, tracker.start_latencies = [], [], []
     rate = cfg.probe_rate_per_min / 60.0
     rng = random.Random(0x5EED + cfg.seed + cfg.rank)
     loop = asyncio.get_running_loop()
