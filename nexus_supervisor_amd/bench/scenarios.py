@@ -65,7 +65,8 @@ def _pct(xs: List[float], p: float) -> Optional[float]:
 
 
 class AckClock:
-    """First checkpoint ack per run (any replica), as a decision hook."""
+    """First checkpoint ack of each pushed failure (any replica), as a decision hook; a
+    run's start (ToRunning) is not its failure."""
 
     def __init__(self):
         self.pushed: Dict[str, float] = {}
@@ -76,6 +77,8 @@ class AckClock:
         rid = d.result.request_id
         if rid in self.acked or rid not in self.pushed:
             return
+        if d.result.action == "ToRunning":
+            return  # the run's start (lifecycle traffic), not the failure being timed
         if d.outcome in ("applied", "skipped-finished"):
             self.acked[rid] = d.result.stamps.get("ack_mono") or time.monotonic()
             self.outcomes[rid] = d.outcome

@@ -212,6 +212,8 @@ class Supervisor:
         self._gpu_waiters: Dict[str, asyncio.Future] = {}
         self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
         self._settle: Dict[str, asyncio.Future] = {}  # job name -> a Job decision waiting for its pod's failure
+        # shards just gained whose pods are being re-listed (set when the pod list is in)
+        self._pod_relist: Optional[Tuple[asyncio.Event, frozenset]] = None
         self._settle_wait = float(cfg.rules.job_pod_settle)
         self._job_label = cfg.labels.job_name_label
         # pod key -> (first receive, watch-batch delivery stamps) of a deferred pod failure:
@@ -417,25 +419,33 @@ class Supervisor:
         if lost:
             self.fence_shards(lost)
             if not gained and self._narrow_watches():
+                before = self.pod_informer.relists
                 for inf in (self.pod_informer, self.job_informer):
                     inf.relist()  # stop receiving the lost shards' objects
+                self._pod_list_pending(self.shards.owned or (), before)
         if gained:
             self.metrics.inc("shards_gained", len(gained))
             self.replay(lambda rid: self.shards.of(rid) in gained)
             infs = (self.event_informer, self.pod_informer, self.job_informer)
             before = [inf.relists for inf in infs]
             narrowed = self._narrow_watches()
+            relisted = False
             if self.worker_shard is not None and not self.hub_fed:
                 for inf in infs:
                     inf.relist()
+                relisted = True
             elif narrowed:
                 for inf in (self.pod_informer, self.job_informer):
                     inf.relist()
+                relisted = True
+            # the pod informer's own re-list takes its watch down for every shard it holds;
+            # the hub's upstream re-list only concerns the gained ones
+            relist = self._pod_list_pending(self.shards.owned if relisted else gained, None)
             # the three kinds re-list independently: an Event of a gained run can be applied
             # before its Job and parked; replay the gained shards once more after every
             # informer took its new list (or the hub's fresh snapshot), so no ordering of
             # the re-lists can strand a decision
-            t = asyncio.ensure_future(self._replay_after_relist(infs, before, gained))
+            t = asyncio.ensure_future(self._replay_after_relist(infs, before, gained, relist))
             self._bg.add(t)
             t.add_done_callback(self._bg.discard)
         self.metrics.set("shards_owned", float(len(self.shards.owned or ())))
@@ -444,10 +454,42 @@ class Supervisor:
                           lost=sorted(lost))
         return gained, lost
 
-    async def _replay_after_relist(self, infs, before, gained, timeout: float = 10.0) -> None:
+    def _pod_list_pending(self, shards, before: Optional[int]):
+        """The pod list of ``shards`` is being re-taken: until it lands, a cached pod of
+        theirs may be as old as this call (the pod watch is down while its informer
+        re-lists), so :meth:`_await_pod_failure` waits for the list instead of the settle
+        time alone.  ``before``: the pod informer's re-list count now, to clear the mark by
+        itself (else :meth:`_replay_after_relist` does)."""
+        prev = self._pod_relist
+        keep = prev[1] if prev is not None and not prev[0].is_set() else frozenset()
+        # an older mark's waiters are released by its own watcher: the re-list that replaced
+        # its list bumps the same counter when it lands
+        relist = self._pod_relist = (asyncio.Event(), frozenset(shards or ()) | keep)
+        if before is not None:
+            t = asyncio.ensure_future(self._pod_list_landed(relist, before))
+            self._bg.add(t)
+            t.add_done_callback(self._bg.discard)
+        return relist
+
+    async def _pod_list_landed(self, relist, before: int, timeout: float = 30.0) -> None:
+        deadline = time.monotonic() + timeout
+        while self.pod_informer.relists == before and time.monotonic() < deadline:
+            await asyncio.sleep(0.05)
+        self._end_pod_relist(relist)
+
+    def _end_pod_relist(self, relist) -> None:
+        relist[0].set()
+        if self._pod_relist is relist:
+            self._pod_relist = None
+
+    async def _replay_after_relist(self, infs, before, gained, relist=None, timeout: float = 30.0) -> None:
         deadline = time.monotonic() + timeout
         while any(inf.relists == b for inf, b in zip(infs, before)) and time.monotonic() < deadline:
+            if relist is not None and infs[1].relists != before[1] and not relist[0].is_set():
+                self._end_pod_relist(relist)  # the pods are in
             await asyncio.sleep(0.05)
+        if relist is not None:
+            self._end_pod_relist(relist)
         owned = self.shards.owned or frozenset()
         still = frozenset(gained) & owned
         if still and self.active:
@@ -1008,11 +1050,29 @@ class Supervisor:
         while True:
             # no pod cached at all counts as "not seen yet": a replica that just gained the
             # run's shard re-lists Jobs and Pods concurrently
-            if any(_pod_failed(p) for p in self.lookup.pods_of_job(r.request_id)):
+            pods = self.lookup.pods_of_job(r.request_id)
+            if any(_pod_failed(p) for p in pods):
                 break
+            relist = self._pod_relist
+            if relist is not None and not relist[0].is_set() and self.shards.of(r.request_id) in relist[1]:
+                # its shard was just gained and the pod list is not in yet: until it is, the
+                # pod watch is down and a cached pod may be as old as the gain (a 10k-pod list
+                # behind a kube-qps bucket shared with the replay's DELETEs took 18 s in
+                # config 5s) — wait for the list, not the settle time alone
+                waited = True
+                self.metrics.inc("job_pod_settle_relist_waits")
+                try:
+                    await asyncio.wait_for(relist[0].wait(), 30.0)
+                except asyncio.TimeoutError:
+                    pass
+                deadline = max(deadline, time.monotonic() + self._settle_wait)
+                continue
             left = deadline - time.monotonic()
             if left <= 0:
                 self.metrics.inc("job_pod_settle_expired")
+                self.log.info("no failed pod of the job seen within the settle time; deciding from the job",
+                              requestId=r.request_id, reason=r.reason,
+                              pods=[f"{kube.name_of(p)}:{(p.get('status') or {}).get('phase')}" for p in pods][:4])
                 break
             fut = self._settle.get(r.request_id)
             if fut is None or fut.done():

@@ -176,3 +176,62 @@ def test_kubesim_set_selectors(arun):
             await ctl.close()
 
     arun(go(), timeout=20)
+
+
+def test_job_decision_waits_for_the_pod_relist_of_a_shard_change(arun):
+    """Gaining a shard re-lists the Pod watch: until the list lands the cached pods of EVERY
+    owned shard are as old as the gain.  A Job's BackoffLimitExceeded seen meanwhile (its
+    own watch is back first) must wait for that list, not just ``rules.job-pod-settle``:
+    the cached pod still says Running, and deciding from the Job alone writes
+    DEADLINE_EXCEEDED without the pod's OOMKilled (config 5s at reference limits, where a
+    10k-pod list behind kube-qps 5 took 18 s)."""
+    async def go():
+        api = FakeApiServer(bookmark_interval=0.1)
+        url = await api.start()
+        cfg = _cfg(0, **{"sharding": {"shards": 2, "shard-label": LABEL, "mode": "lease"},
+                         "rules": {"job-pod-settle": "200ms"},
+                         "leader-election": {"lease-duration": "60s", "renew-deadline": "40s", "retry-period": "20s"}})
+        rid = next(f"relist-{i:02d}" for i in range(64) if shard_of(f"relist-{i:02d}", 2) == 1)
+        pod, job = _labelled(rid, cfg.labels)
+        api.create(pod)
+        api.create(job)
+        store = MemoryStore([CheckpointedRequest(algorithm=ALGORITHM, id=rid, lifecycle_stage="RUNNING")])
+        app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
+        sup = app.supervisor
+        sup.init()
+        await sup.start(wait_sync_timeout=5)
+        import time
+
+        sup.shards.set_deadlines({0: time.monotonic() + 60, 1: time.monotonic() + 60})
+        sup.set_shards({1})
+        for _ in range(200):
+            if sup.pod_informer.indexer.get_by_name("nexus", f"{rid}-acdey") is not None and sup._pod_relist is None:
+                break
+            await asyncio.sleep(0.02)
+        assert sup.pod_informer.indexer.get_by_name("nexus", f"{rid}-acdey") is not None
+        lw = sup.pod_informer.lw
+        slow_list = lw.list
+
+        async def list_late(*a, **kw):
+            await asyncio.sleep(1.5)  # the pod list queued behind a kube-qps bucket
+            return await slow_list(*a, **kw)
+
+        lw.list = list_late
+        sup.set_shards({0, 1})  # gains shard 0: the Pod watch is down until the list lands
+        await asyncio.sleep(0.1)
+        api.update(_oomkilled(api.get("Pod", "nexus", f"{rid}-acdey")))
+        from test_logtail import _job_failed
+
+        api.update(_job_failed(api.get("Job", "nexus", rid)))
+        for _ in range(250):
+            if store.get(ALGORITHM, rid).lifecycle_stage != "RUNNING":
+                break
+            await asyncio.sleep(0.02)
+        row = store.get(ALGORITHM, rid)
+        assert row.lifecycle_stage == "FAILED", (row.lifecycle_stage, row.algorithm_failure_details)
+        assert app.metrics.counter("job_pod_settle_relist_waits") >= 1
+        await sup.stop(drain=False)
+        await app.kube.close()
+        await api.stop()
+
+    arun(go(), timeout=30)
