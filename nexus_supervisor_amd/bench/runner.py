@@ -142,6 +142,7 @@ class Tracker:
         # frame), feed (→ decoded), dispatch (→ handler), classify (handler → enqueue, with any
         # log-tail wait), queue (→ dequeue), actuate (→ checkpoint ack)
         self.parts: List[Tuple[float, ...]] = []
+        self.pushed_at: List[float] = []  # push time of each entry of ``latencies``
 
     def __call__(self, d: Decision):
         s = d.result.stamps
@@ -246,6 +247,7 @@ class StepState:
                 else:
                     tr.failures += 1
                     tr.latencies.append(total)
+                    tr.pushed_at.append(self.t_push)
                     if x is not None and len(x) >= 6:
                         hub, feed, dec, cls, que, r2c = x[:6]
                         tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
@@ -627,6 +629,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     saved, tracker.latencies = tracker.latencies, []
     saved_parts, tracker.parts = tracker.parts, []
     saved_starts, tracker.start_latencies = tracker.start_latencies, []
+    saved_pushed, tracker.pushed_at = tracker.pushed_at, []
     if cfg.run_starts:
         # the last timed step's new runs start now, before the first arrival: thousands of
         # starts in one burst are the saturated workload's, not the north-star churn's
@@ -637,7 +640,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
                 await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
             except asyncio.TimeoutError:
                 tracker.abandon(st)
-        tracker.latencies, tracker.parts, tracker.start_latencies = [], [], []
+        tracker.latencies, tracker.parts, tracker.start_latencies, tracker.pushed_at = [], [], [], []
     rate = cfg.probe_rate_per_min / 60.0
     rng = random.Random(0x5EED + cfg.seed + cfg.rank)
     loop = asyncio.get_running_loop()
@@ -678,16 +681,22 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
             await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
         except asyncio.TimeoutError:
             tracker.abandon(st)
+    timed = list(zip(tracker.pushed_at, tracker.latencies))
     lat = sorted(tracker.latencies)
     starts = sorted(tracker.start_latencies)
     parts = tracker.parts
     tracker.latencies, tracker.parts, tracker.start_latencies = saved, saved_parts, saved_starts
+    tracker.pushed_at = saved_pushed
     if not lat:
         return {"events": 0}
     q = lambda p, v=lat: v[min(len(v) - 1, int(round(p * (len(v) - 1))))]  # noqa: E731
     out = {"rate_per_min": cfg.probe_rate_per_min, "arrivals": "poisson", "events": len(lat),
            "p50_ms": round(q(0.5), 3), "p90_ms": round(q(0.9), 3), "p99_ms": round(q(0.99), 3),
            "max_ms": round(lat[-1], 3)}
+    if timed:
+        # when the tail arrived: seconds from the first arrival of every failure at or over p99
+        t0 = min(t for t, _ in timed)
+        out["tail_arrival_s"] = sorted(round(t - t0, 2) for t, v in timed if v >= q(0.99))
     if starts:  # the replacement runs' Started → RUNNING at the same rate
         out["starts"] = len(starts)
         out["start_p50_ms"] = round(q(0.5, starts), 3)
