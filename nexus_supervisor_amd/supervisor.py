@@ -212,7 +212,7 @@ class Supervisor:
         self._gpu_waiters: Dict[str, asyncio.Future] = {}
         self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
         self._settle: Dict[str, asyncio.Future] = {}  # job name -> a Job decision waiting for its pod's failure
-        # shards just gained whose pods are being re-listed (set when the pod list is in)
+        # shards whose cached pods may be stale while the Pod informer re-lists (set when the list is in)
         self._pod_relist: Optional[Tuple[asyncio.Event, frozenset]] = None
         self._settle_wait = float(cfg.rules.job_pod_settle)
         self._job_label = cfg.labels.job_name_label
