@@ -89,6 +89,9 @@ def parse_args(argv=None):
                          "scheduled -> Running with the kubelet's Events (its Started is a ToRunning decision: "
                          "checkpoint read + RUNNING upsert), failures carry their Job / Event traffic and Events "
                          "expire; failures: the round-4 shape (failure traffic only, new runs never start)")
+    ap.add_argument("--diag-probe-timeline", action="store_true",
+                    help="diagnostic: every second of the probe, each bench process's CPU, the host's busy CPUs and the "
+                         "cgroup's CFS throttling (latency_at_rate.cpu_timeline)")
     ap.add_argument("--diag-slow-callback-ms", type=float, default=0.0,
                     help="diagnostic: count the event-loop callbacks (parent and workers) that run at least this "
                          "long and list the probe's in latency_at_rate.slow_callbacks (obs/loopwatch.py)")
@@ -297,7 +300,7 @@ def main(argv=None) -> int:
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster, run_starts=args.workload == "lifecycle",
                       pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz, slot_mode=slot_mode,
-                      gpu_evidence=args.gpu_evidence)
+                      gpu_evidence=args.gpu_evidence, probe_timeline=args.diag_probe_timeline)
     res = asyncio.run(run_rank(cfg, barrier_sync, share, oom_phase if slot_mode == "node" and world > 1 else None))
 
     elapsed = res["elapsed"]

@@ -49,6 +49,7 @@ class BenchConfig:
     inflight: int = 2
     probe_events: int = 600
     probe_rate_per_min: float = 1000.0
+    probe_timeline: bool = False  # diagnostic: CPU of every process (and the host) per second of the probe
     procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
     pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
     cluster: str = "per-rank"  # per-rank | shared (one apiserver + one CQL server for all ranks)
@@ -658,6 +659,9 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
                                   doc.get("start_expected")))
 
+    timeline = _CpuTimeline(harness) if cfg.probe_timeline and hasattr(harness, "external_cpu") else None
+    if timeline is not None:
+        timeline.start()
     played = getattr(harness, "probe", None)
     if played is not None:
         # the cluster process plays the schedule (same seed, same arrivals): one request for
@@ -681,6 +685,8 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
             await asyncio.wait_for(st.done.wait(), cfg.step_timeout)
         except asyncio.TimeoutError:
             tracker.abandon(st)
+    if timeline is not None:
+        await timeline.stop()
     timed = list(zip(tracker.pushed_at, tracker.latencies))
     lat = sorted(tracker.latencies)
     starts = sorted(tracker.start_latencies)
@@ -697,6 +703,8 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         # when the tail arrived: seconds from the first arrival of every failure at or over p99
         t0 = min(t for t, _ in timed)
         out["tail_arrival_s"] = sorted(round(t - t0, 2) for t, v in timed if v >= q(0.99))
+        if timeline is not None:
+            out["cpu_timeline"] = timeline.report(t0)
     if starts:  # the replacement runs' Started → RUNNING at the same rate
         out["starts"] = len(starts)
         out["start_p50_ms"] = round(q(0.5, starts), 3)
@@ -707,6 +715,83 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
 
 
 PART_NAMES = ("api", "hub", "feed", "dispatch", "classify", "queue", "actuate")
+
+
+class _CpuTimeline:
+    """``--diag-probe-timeline``: every second of the probe, the CPU share of each bench
+    process (simulator, CQL server, cluster process, shard workers, this replica parent),
+    the host's busy CPUs (``/proc/stat``: other tenants included) and the cgroup's CFS
+    throttling (``cpu.stat``) — to tell a stall of one process from contention for the box."""
+
+    def __init__(self, harness, interval: float = 1.0):
+        self.harness = harness
+        self.interval = interval
+        self.rows: List[Dict[str, Any]] = []
+        self._task: Optional[asyncio.Task] = None
+
+    @staticmethod
+    def _host() -> Tuple[float, float]:
+        try:
+            with open("/proc/stat") as f:
+                v = [int(x) for x in f.readline().split()[1:]]
+            return float(sum(v) - v[3] - (v[4] if len(v) > 4 else 0)), float(sum(v))
+        except (OSError, ValueError, IndexError):
+            return 0.0, 0.0
+
+    @staticmethod
+    def _throttled() -> Tuple[float, float]:
+        for path in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat"):
+            try:
+                with open(path) as f:
+                    kv = dict(line.split() for line in f if line.strip())
+                us = float(kv.get("throttled_usec", 0.0)) or float(kv.get("throttled_time", 0.0)) / 1000.0
+                return float(kv.get("nr_throttled", 0.0)), us
+            except (OSError, ValueError):
+                continue
+        return 0.0, 0.0
+
+    def _sample(self) -> Dict[str, Any]:
+        cpu = dict(self.harness.external_cpu())
+        t = os.times()
+        cpu["parent"] = t.user + t.system
+        busy, total = self._host()
+        n, us = self._throttled()
+        return {"t": time.monotonic(), "cpu": cpu, "host_busy": busy, "host_total": total, "thr_n": n, "thr_us": us}
+
+    async def _run(self) -> None:
+        while True:
+            self.rows.append(self._sample())
+            await asyncio.sleep(self.interval)
+
+    def start(self) -> None:
+        self._task = asyncio.ensure_future(self._run())
+
+    async def stop(self) -> None:
+        if self._task is not None:
+            self._task.cancel()
+            try:
+                await self._task
+            except asyncio.CancelledError:
+                pass
+        self.rows.append(self._sample())
+
+    def report(self, t0: float) -> List[Dict[str, Any]]:
+        """One entry per interval: seconds from ``t0`` (the first arrival), each process's
+        cores, the host's busy cores and the cgroup's throttled periods / milliseconds."""
+        ncpu = os.cpu_count() or 1
+        out = []
+        for a, b in zip(self.rows, self.rows[1:]):
+            dt = b["t"] - a["t"]
+            if dt <= 0:
+                continue
+            row = {"t": round(a["t"] - t0, 1)}
+            row.update({k: round((b["cpu"][k] - a["cpu"].get(k, 0.0)) / dt, 2) for k in b["cpu"] if not k.endswith("_sys")})
+            if b["host_total"] > a["host_total"]:
+                row["host_busy_cpus"] = round(ncpu * (b["host_busy"] - a["host_busy"]) / (b["host_total"] - a["host_total"]), 1)
+            row["throttled"] = int(b["thr_n"] - a["thr_n"])
+            row["throttled_ms"] = round((b["thr_us"] - a["thr_us"]) / 1000.0, 1)
+            out.append(row)
+        return out
 
 
 def _slow_callbacks(before: Dict[str, Dict[Any, float]], after: Dict[str, Dict[Any, float]],
