@@ -143,7 +143,7 @@ class Tracker:
         # frame), feed (→ decoded), dispatch (→ handler), classify (handler → enqueue, with any
         # log-tail wait), queue (→ dequeue), actuate (→ checkpoint ack)
         self.parts: List[Tuple[float, ...]] = []
-        self.pushed_at: List[float] = []  # push time of each entry of ``latencies``
+        self.pushed_at: List[Tuple[float, str]] = []  # (push time, run) of each entry of ``latencies``
 
     def __call__(self, d: Decision):
         s = d.result.stamps
@@ -248,7 +248,7 @@ class StepState:
                 else:
                     tr.failures += 1
                     tr.latencies.append(total)
-                    tr.pushed_at.append(self.t_push)
+                    tr.pushed_at.append((self.t_push, rid))
                     if x is not None and len(x) >= 6:
                         hub, feed, dec, cls, que, r2c = x[:6]
                         tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
@@ -651,11 +651,14 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     at = 0.0
     hold = getattr(harness, "probe_hold_ms", 0.0)
 
+    kinds: Dict[str, str] = {}  # probe run -> failure kind (the tail report)
+
     async def one():
         # the harness answers after the failure is delivered (hold): the driver's own work on
         # the answer stays out of the replica parent's loop while the line is in flight; the
         # decision's ack may arrive first (Tracker.report keeps it until the step is armed)
         doc = await (harness.step(1, hold) if hold else harness.step(1))
+        kinds.update(doc.get("kinds") or {})
         states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
                                   doc.get("start_expected")))
 
@@ -667,6 +670,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
         # the cluster process plays the schedule (same seed, same arrivals): one request for
         # the whole probe, every decision's ack kept by the tracker until its step is armed
         for doc in await played(cfg.probe_events, cfg.probe_rate_per_min, 0x5EED + cfg.seed + cfg.rank):
+            kinds.update(doc.get("kinds") or {})
             states.append(tracker.arm(doc["rids"], doc["t_push"], doc.get("expected"), doc.get("started"),
                                       doc.get("start_expected")))
     for i in range(cfg.probe_events if played is None else 0):
@@ -687,7 +691,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
             tracker.abandon(st)
     if timeline is not None:
         await timeline.stop()
-    timed = list(zip(tracker.pushed_at, tracker.latencies))
+    timed = [(t, rid, v) for (t, rid), v in zip(tracker.pushed_at, tracker.latencies)]
     lat = sorted(tracker.latencies)
     starts = sorted(tracker.start_latencies)
     parts = tracker.parts
@@ -701,8 +705,15 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
            "max_ms": round(lat[-1], 3)}
     if timed:
         # when the tail arrived: seconds from the first arrival of every failure at or over p99
-        t0 = min(t for t, _ in timed)
-        out["tail_arrival_s"] = sorted(round(t - t0, 2) for t, v in timed if v >= q(0.99))
+        t0 = min(t for t, _, _ in timed)
+        out["tail_arrival_s"] = sorted(round(t - t0, 2) for t, _, v in timed if v >= q(0.99))
+        if kinds:
+            # which failure kinds the tail is, against the probe's mix
+            out["tail_kinds"] = sorted(kinds.get(rid, "?") for _, rid, v in timed if v >= q(0.99))
+            mix: Dict[str, int] = {}
+            for _, rid, _ in timed:
+                mix[kinds.get(rid, "?")] = mix.get(kinds.get(rid, "?"), 0) + 1
+            out["kinds"] = mix
         if timeline is not None:
             out["cpu_timeline"] = timeline.report(t0)
     if starts:  # the replacement runs' Started → RUNNING at the same rate

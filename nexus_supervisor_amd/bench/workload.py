@@ -90,7 +90,7 @@ class StepTraffic:
     rows the receiver inserts first, and the stage each decision must write (fixed at
     generation: a run started here may fail in a later step)."""
 
-    __slots__ = ("failed", "started", "traffic", "rows", "expected", "start_expected")
+    __slots__ = ("failed", "started", "traffic", "rows", "expected", "start_expected", "kinds")
 
     def __init__(self):
         self.failed: List[str] = []
@@ -99,6 +99,7 @@ class StepTraffic:
         self.rows: List[CheckpointedRequest] = []
         self.expected: Dict[str, str] = {}
         self.start_expected: Dict[str, str] = {}
+        self.kinds: Dict[str, str] = {}  # failed run -> failure kind (MIX)
 
     def __iter__(self):
         """``failed, traffic, rows = workload.step(n)``."""
@@ -106,8 +107,11 @@ class StepTraffic:
 
     def doc(self, t_push: float) -> Dict[str, Any]:
         """The cluster's answer to a step (``/bench/step``)."""
-        return {"rids": self.failed, "t_push": t_push, "expected": self.expected, "started": self.started,
-                "start_expected": self.start_expected}
+        doc = {"rids": self.failed, "t_push": t_push, "expected": self.expected, "started": self.started,
+               "start_expected": self.start_expected}
+        if len(self.kinds) <= 8:  # a probe arrival: its failure's kind (the probe's tail report)
+            doc["kinds"] = self.kinds
+        return doc
 
 
 class Workload:
@@ -399,6 +403,7 @@ class Workload:
         st.failed.append(rid)
         st.expected[rid] = self.expected[rid] = self._stage[kind]
         self.kind_of[rid] = kind
+        st.kinds[rid] = kind
         # the supervisor's Job DELETE removes the Job and (GC) its pod; its Events expire later
         self.pods.pop(rid, None)
         self.jobs.pop(rid, None)
