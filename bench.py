@@ -89,6 +89,8 @@ def parse_args(argv=None):
                          "scheduled -> Running with the kubelet's Events (its Started is a ToRunning decision: "
                          "checkpoint read + RUNNING upsert), failures carry their Job / Event traffic and Events "
                          "expire; failures: the round-4 shape (failure traffic only, new runs never start)")
+    ap.add_argument("--diag-no-thp", action="store_true",
+                    help="diagnostic: disable transparent huge pages for the bench and every process it starts")
     ap.add_argument("--diag-probe-timeline", action="store_true",
                     help="diagnostic: every second of the probe, each bench process's CPU, the host's busy CPUs and the "
                          "cgroup's CFS throttling (latency_at_rate.cpu_timeline)")
@@ -207,6 +209,12 @@ def main(argv=None) -> int:
         pass
     if args.diag_slow_callback_ms > 0:  # read by the replica parent and inherited by its workers
         os.environ["NEXUS_SLOW_CALLBACK_MS"] = str(args.diag_slow_callback_ms)
+    if args.diag_no_thp:
+        # PR_SET_THP_DISABLE: no transparent huge pages for this process and every child
+        # (inherited over fork and exec) — khugepaged collapses take the address-space lock
+        import ctypes
+
+        ctypes.CDLL(None, use_errno=True).prctl(41, 1, 0, 0, 0)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
