@@ -203,6 +203,10 @@ async def amain(args) -> None:
                 # cluster must see them (their decisions are absorbed in the settle below)
                 stale = await nxt[1]
                 await apply(stale.traffic)
+            # the saturated steps' Events reach their TTL now, not in the first arrival's step
+            expired = sh.wl.expire_all()
+            if expired:
+                await apply(expired)
         await asyncio.sleep(float(p.get("settle_s", 2.0)))
 
         async def one(i):

@@ -411,6 +411,14 @@ class Workload:
         if evs:
             self._expiring[-1].extend(evs)
 
+    def expire_all(self) -> List[Tuple[str, Dict[str, Any]]]:
+        """Every Event still waiting for its TTL, as DELETED lines, now (the latency probe
+        lets the saturated steps' Events expire before its first arrival instead of in it)."""
+        out: List[Tuple[str, Dict[str, Any]]] = []
+        while self._expiring:
+            out.extend(("DELETED", ev) for ev in self._expiring.popleft())
+        return out
+
     def fail_with(self, kind: str, message: Optional[str] = None, rid: Optional[str] = None) -> StepTraffic:
         """One running run (``rid``, else a random one) fails as ``kind`` (``message``: the
         HIP text of an hbm-oom, e.g. a real OOM's); its replacement is created."""
