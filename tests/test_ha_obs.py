@@ -55,7 +55,7 @@ def test_exactly_one_leader_and_failover(arun):
         await b.stop(release=True)
         while not c.leader and time.monotonic() - t0 < 5:
             await asyncio.sleep(0.02)
-        assert c.leader and time.monotonic() - t0 < 0.5
+        assert c.leader and time.monotonic() - t0 < 1.0  # a few retry periods (CPU-loaded CI slack)
         await c.stop()
         for x in (ca, cb, cc):
             await x.close()
