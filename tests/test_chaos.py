@@ -100,7 +100,7 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
         await push(60)
         # round 3: eviction storm (pods evicted, Jobs then fail with BackoffLimitExceeded)
         await push(60, kinds=["evicted"])
-        missing = await _wait_stages(seed_store, wl.algorithm, expected, timeout=40)
+        missing = await _wait_stages(seed_store, wl.algorithm, expected, timeout=40 * TIME_SCALE)
         assert not missing, f"{len(missing)} runs never reached their stage, e.g. {list(missing.items())[:3]}"
         survivor = apps[0]
         assert survivor.supervisor.active
@@ -129,7 +129,7 @@ def test_two_replicas_survive_cql_restart_410_leader_crash_and_evictions(arun):
         await api.stop()
         srv.stop()
 
-    arun(go(), timeout=120)
+    arun(go(), timeout=120 * TIME_SCALE)
 
 
 def test_sharded_replicas_survive_cql_restart_storm_and_a_replica_crash(arun):
