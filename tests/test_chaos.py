@@ -151,4 +151,4 @@ def test_sharded_replicas_survive_cql_restart_storm_and_a_replica_crash(arun):
         back = ch["crashed"]["replica"]
         assert sum(1 for v in ch["rebalanced_owners"].values() if back in v) == 2, ch
 
-    arun(go(), timeout=120)
+    arun(go(), timeout=120 * TIME_SCALE)
