@@ -324,7 +324,9 @@ def test_late_replica_gets_its_share_back_by_rebalancing(arun):
         await asyncio.sleep(0.3)
         wrong, twice = _check_exactly_once(store, wl, expected)
         assert not wrong and not twice, (wrong, twice)
-        assert sum(a.shard_leases.rebalances for a in apps.values()) == 2  # 3+3 → 2+2+2 or 4+2 → 2+2+2
+        # 3+3 → 2+2+2 or 4+2 → 2+2+2: two hand-backs; one when a slow round (a loaded CI box,
+        # the coverage tracer) let a lease lapse and the newcomer took that shard unheld
+        assert 1 <= sum(a.shard_leases.rebalances for a in apps.values()) <= 2
         assert all(a.shard_leases.members == frozenset(apps) for a in apps.values())
         for a in apps.values():
             await a.stop(drain_timeout=1)
