@@ -734,7 +734,7 @@ class _CpuTimeline:
     the host's busy CPUs (``/proc/stat``: other tenants included) and the cgroup's CFS
     throttling (``cpu.stat``) — to tell a stall of one process from contention for the box."""
 
-    def __init__(self, harness, interval: float = 1.0):
+    def __init__(self, harness, interval: float = 0.25):
         self.harness = harness
         self.interval = interval
         self.rows: List[Dict[str, Any]] = []
@@ -761,13 +761,37 @@ class _CpuTimeline:
                 continue
         return 0.0, 0.0
 
+    def _pids(self) -> Dict[str, int]:
+        h = self.harness
+        out = {"parent": os.getpid()}
+        for name, proc in (("cluster", getattr(h, "proc", None)), ("cqlsrv", getattr(getattr(h, "cql", None), "proc", None))):
+            if proc is not None:
+                out[name] = proc.pid
+        if getattr(h, "sim_pid", None):
+            out["kubesim"] = h.sim_pid
+        pool = getattr(getattr(h, "app", None), "pool", None)
+        if pool is not None:
+            out.update({f"worker{w.index}": w.proc.pid for w in pool.workers})
+        return out
+
+    @staticmethod
+    def _faults(pid: int) -> Tuple[int, int]:
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                parts = f.read().rsplit(")", 1)[1].split()
+            return int(parts[7]), int(parts[9])  # minflt, majflt
+        except (OSError, ValueError, IndexError):
+            return 0, 0
+
     def _sample(self) -> Dict[str, Any]:
         cpu = dict(self.harness.external_cpu())
         t = os.times()
         cpu["parent"] = t.user + t.system
         busy, total = self._host()
         n, us = self._throttled()
-        return {"t": time.monotonic(), "cpu": cpu, "host_busy": busy, "host_total": total, "thr_n": n, "thr_us": us}
+        flt = {k: self._faults(pid) for k, pid in self._pids().items()}
+        return {"t": time.monotonic(), "cpu": cpu, "host_busy": busy, "host_total": total, "thr_n": n, "thr_us": us,
+                "flt": flt}
 
     async def _run(self) -> None:
         while True:
@@ -801,6 +825,9 @@ class _CpuTimeline:
                 row["host_busy_cpus"] = round(ncpu * (b["host_busy"] - a["host_busy"]) / (b["host_total"] - a["host_total"]), 1)
             row["throttled"] = int(b["thr_n"] - a["thr_n"])
             row["throttled_ms"] = round((b["thr_us"] - a["thr_us"]) / 1000.0, 1)
+            # page faults in the interval, all bench processes: minor, major
+            row["minflt"] = sum(v[0] - a["flt"].get(k, (0, 0))[0] for k, v in b["flt"].items())
+            row["majflt"] = sum(v[1] - a["flt"].get(k, (0, 0))[1] for k, v in b["flt"].items())
             out.append(row)
         return out
 
