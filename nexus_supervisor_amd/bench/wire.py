@@ -113,6 +113,11 @@ class WireHarness:
 
     async def start(self) -> None:
         info = await self._start_cluster() if self.owner else None
+        # diagnostic: start the replica this long after the harness (which of the two a
+        # time-since-start effect follows)
+        delay = float(os.environ.get("NEXUS_BENCH_DIAG_REPLICA_DELAY_S", "0") or 0)
+        if delay > 0:
+            await asyncio.sleep(delay)
         if self.shared:
             info = self.share(info)  # rank 0's harness addresses to every rank
         self.ctl = info["ctl"]
