@@ -706,6 +706,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
     if timed:
         # when the tail arrived: seconds from the first arrival of every failure at or over p99
         t0 = min(t for t, _, _ in timed)
+        out["t0_monotonic"] = round(t0, 4)  # the first arrival's push (CLOCK_MONOTONIC)
         out["tail_arrival_s"] = sorted(round(t - t0, 2) for t, _, v in timed if v >= q(0.99))
         if kinds:
             # which failure kinds the tail is, against the probe's mix

@@ -49,6 +49,9 @@ def install(metrics, threshold_ms: float, where: str = "") -> bool:
         return False
     threshold = threshold_ms / 1000.0
     orig = _events.Handle._run
+    # NEXUS_SLOW_CALLBACK_LOG=1: also one stderr line per slow callback, with its
+    # CLOCK_MONOTONIC end time (lines up with the bench's push stamps across processes)
+    log_each = os.environ.get("NEXUS_SLOW_CALLBACK_LOG", "") not in ("", "0")
     clock = time.perf_counter
     gc_s = [0.0, 0.0]  # [GC seconds so far, start of the running collection]
 
@@ -70,6 +73,11 @@ def install(metrics, threshold_ms: float, where: str = "") -> bool:
                 metrics.inc("slow_callback_seconds", d, labels=labels)
                 metrics.inc("slow_callback_gc_seconds", gc_s[0] - g0, labels=labels)
                 metrics.observe_seconds("slow_callback", d)
+                if log_each:
+                    import sys
+
+                    sys.stderr.write(f"SLOWCB {time.monotonic():.4f} {where} pid={os.getpid()} {labels['name']} "
+                                     f"{d * 1e3:.2f}ms gc={(gc_s[0] - g0) * 1e3:.2f}ms\n")
             except Exception:  # noqa: BLE001 - never let the watch break the loop it watches
                 pass
 
