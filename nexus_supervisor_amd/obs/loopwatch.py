@@ -76,8 +76,10 @@ def install(metrics, threshold_ms: float, where: str = "") -> bool:
                 if log_each:
                     import sys
 
+                    owner = getattr(self._callback, "__self__", None)
+                    task = owner.get_name() if hasattr(owner, "get_name") else ""
                     sys.stderr.write(f"SLOWCB {time.monotonic():.4f} {where} pid={os.getpid()} {labels['name']} "
-                                     f"{d * 1e3:.2f}ms gc={(gc_s[0] - g0) * 1e3:.2f}ms\n")
+                                     f"{task} {d * 1e3:.2f}ms gc={(gc_s[0] - g0) * 1e3:.2f}ms\n")
             except Exception:  # noqa: BLE001 - never let the watch break the loop it watches
                 pass
 
