@@ -33,7 +33,9 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import struct
+import sys
 import time
 from time import thread_time as _thread_time
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -50,6 +52,9 @@ SNAPSHOT, LINES, LINES_T = 1, 2, 3
 HEADER = struct.Struct("!BBI")
 STAMP = struct.Struct("!d")
 HIGH_WATER = 32 << 20
+
+
+_CHUNK_LOG = os.environ.get("NEXUS_SLOW_CALLBACK_LOG", "") not in ("", "0")
 
 
 class _Gone(Exception):
@@ -187,10 +192,18 @@ class WatchHub:
                         async for chunk in resp.content.iter_any():
                             t_read = time.monotonic()
                             outs, last, errors = splitter.feed(chunk)
+                            t_split = time.monotonic()
                             if last:
                                 rv = last
                             if any(outs):
                                 await self._route(ki, outs, LINES_T, STAMP.pack(t_read))
+                            if _CHUNK_LOG and time.monotonic() - t_read > 0.001:
+                                # diagnostic (NEXUS_SLOW_CALLBACK_LOG): a chunk that held the
+                                # loop: its size, the bytes routed to workers, split / route time
+                                sys.stderr.write(f"HUBCHUNK {t_read:.4f} {kind} in={len(chunk)} "
+                                                 f"out={sum(len(o) for o in outs if o)} "
+                                                 f"split={(t_split - t_read) * 1e3:.2f}ms "
+                                                 f"route={(time.monotonic() - t_split) * 1e3:.2f}ms\n")
                             if ki == 0 and self.metrics is not None:
                                 unread = self.router.stats["unread"]
                                 if unread != self._unread_seen:
