@@ -1122,11 +1122,17 @@ bool replica_owns_hash(const Router* r, uint32_t h) {
   return (*r->owned)[h % static_cast<uint32_t>(r->rcount)] != 0;
 }
 
+// At most `budget` entries per call: a saturated phase deletes ~20k pods a second, and
+// erasing all of them in the first call after their forget time held the hub's loop for
+// 1-5 ms per chunk for seconds (the open-loop probe's p99).  Spread over calls instead.
+constexpr size_t EXPIRE_BUDGET = 128;
+
 void expire_owners(Router* r) {
   auto& g = r->owners->gone;
   if (g.empty()) return;
   double now = mono_s();
-  while (!g.empty() && g.front().first <= now) {
+  size_t budget = EXPIRE_BUDGET;
+  while (budget-- > 0 && !g.empty() && g.front().first <= now) {
     r->owners->pod.erase(g.front().second);
     g.pop_front();
   }
