@@ -172,6 +172,14 @@ class Cluster:
             self.api.apply(etype, obj, copy_obj=False)
         return failed
 
+    async def prime(self, n: int) -> None:
+        """``n`` runs created and pending, so the next :meth:`push` can fail starting runs
+        (image-pull, gpu-admission: a start failure needs a run that has not started)."""
+        st = self.wl.create(n)
+        await self._write_rows(st.rows)
+        for etype, obj in st.traffic:
+            self.api.apply(etype, obj, copy_obj=False)
+
     async def final_stages(self, rids) -> Dict[str, Any]:
         bad = []
         for rid in rids:
@@ -227,12 +235,21 @@ async def cfg2_burst(profile: str, n: int = 100) -> Dict[str, Any]:
     c = Cluster(jobs=1000, profile=profile)
     await c.start()
     try:
+        # the start failures (image pulls, GPU admission rejections) need starting runs
+        await c.prime(n)
+        await asyncio.sleep(0.5)
         t0 = time.monotonic()
-        rids = await c.push(n, kinds=["host-oom", "image-pull"])
+        # OOMKilled and ImagePullBackOff as the config names them, plus a share of pods the
+        # kubelet refused because the device plugin could not allocate an amd.com/gpu
+        kinds = ["host-oom"] * 9 + ["image-pull"] * 9 + ["gpu-admission"] * 2
+        rids = await c.push(n, kinds=kinds)
         await c.clock.wait(rids, 120)
         dt = max(c.clock.acked.values()) - t0 if c.clock.acked else 0.0
-        return _summary("2: 100 failing pods (OOMKilled/ImagePullBackOff), 1 replica", profile, c.clock.latencies_ms(),
-                        n, dt, **(await c.final_stages(rids)))
+        mix: Dict[str, int] = {}
+        for r in rids:
+            mix[c.wl.kind_of.get(r, "?")] = mix.get(c.wl.kind_of.get(r, "?"), 0) + 1
+        return _summary("2: 100 failing pods (OOMKilled/ImagePullBackOff + GPU admission), 1 replica", profile,
+                        c.clock.latencies_ms(), n, dt, kinds=mix, **(await c.final_stages(rids)))
     finally:
         await c.stop()
 

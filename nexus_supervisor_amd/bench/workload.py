@@ -40,6 +40,11 @@ hbm-oom             Pod MODIFIED exit 1 + HIP OOM (termination message, or the  
 image-pull          (a starting run) Event Scheduled, Pod bound, Event Pulling,  SCHEDULING_FAILED
                     Event Failed (ErrImagePull), Pod waiting ErrImagePull,
                     Event BackOff (pulling image), Pod waiting ImagePullBackOff
+gpu-admission       (a starting run) Event Scheduled; Pod MODIFIED bound,        SCHEDULING_FAILED
+                    Failed/UnexpectedAdmissionError (device plugin "Allocate
+                    failed … amd.com/gpu"), no containers; Event (Pod)
+                    UnexpectedAdmissionError; Job MODIFIED Failed
+                    (BackoffLimitExceeded); Event (Job) BackoffLimitExceeded
 pod-failure-policy  Pod MODIFIED exit 255; Event (Job) PodFailurePolicy; Job    FAILED
                     MODIFIED Failed (PodFailurePolicy) — reference R-EVT path
 deadline            Event (Job) DeadlineExceeded; Job MODIFIED Failed           DEADLINE_EXCEEDED
@@ -69,12 +74,17 @@ DEFAULT_HIP_OOM = ("hipErrorOutOfMemory: HIP out of memory. Tried to allocate 4.
 MIX: Tuple[Tuple[str, float, str], ...] = (
     ("host-oom", 0.30, LifecycleStage.FAILED),
     ("hbm-oom", 0.20, LifecycleStage.FAILED),
-    ("image-pull", 0.20, LifecycleStage.SCHEDULING_FAILED),
+    ("image-pull", 0.17, LifecycleStage.SCHEDULING_FAILED),
+    ("gpu-admission", 0.03, LifecycleStage.SCHEDULING_FAILED),
     ("pod-failure-policy", 0.10, LifecycleStage.FAILED),
     ("deadline", 0.10, LifecycleStage.DEADLINE_EXCEEDED),
     ("evicted", 0.10, LifecycleStage.FAILED),
 )
-START_KINDS = ("image-pull",)  # failures of a starting run (the pod never ran)
+START_KINDS = ("image-pull", "gpu-admission")  # failures of a starting run (the pod never ran)
+# the AMD device plugin's allocation failure on a node whose GPU went unhealthy (kubelet
+# device manager wording)
+GPU_ADMISSION_MESSAGE = ("Allocate failed due to requested number of devices unavailable for amd.com/gpu. "
+                         "Requested: 1, Available: 0, which is unexpected")
 
 # what a running GPU pod's status / a started Job's status look like
 _T0 = "2026-01-01T00:00:00Z"
@@ -374,6 +384,20 @@ class Workload:
                 out.append(("MODIFIED", pod))
                 if reason == "ErrImagePull":
                     out.append(("ADDED", self._pod_event(rid, "BackOff", f'Back-off pulling image "{img}"', "Warning")))
+        elif kind == "gpu-admission":
+            # bound to a node whose GPU the device plugin marked unhealthy: the kubelet refuses
+            # the pod at admission (Failed, no container ever created), the Job controller
+            # counts the failure against backoffLimit 0
+            node = self._templates()[4]
+            out.append(("ADDED", self._pod_event(rid, "Scheduled", f"Successfully assigned {self.ns}/{pod_name} to {node}",
+                                                 component="default-scheduler")))
+            out.append(("MODIFIED", self._mod(self.pods[rid], {"phase": "Failed", "reason": "UnexpectedAdmissionError",
+                                                                "message": GPU_ADMISSION_MESSAGE},
+                                              spec={"nodeName": node})))
+            out.append(("ADDED", self._pod_event(rid, "UnexpectedAdmissionError", GPU_ADMISSION_MESSAGE, "Warning")))
+            msg = "Job has reached the specified backoff limit"
+            out.append(("MODIFIED", self._job_failed(rid, "BackoffLimitExceeded", msg)))
+            out.append(("ADDED", self._job_event(rid, "BackoffLimitExceeded", msg)))
         elif kind == "pod-failure-policy":
             out.append(("MODIFIED", self._terminated(rid, {"terminated": {"reason": "Error", "exitCode": 255,
                                                                           "message": ""}})))
@@ -437,6 +461,14 @@ class Workload:
         finally:
             self.hip_oom_message = saved
         self._create(st)
+        return st
+
+    def create(self, n: int) -> StepTraffic:
+        """``n`` new runs (Job + Pending Pod ADDED, rows BUFFERED) that start — or fail to
+        start (image-pull, gpu-admission) — in the next :meth:`step`."""
+        st = StepTraffic()
+        for _ in range(n):
+            self._create(st)
         return st
 
     def step(self, events: int, kinds: Optional[List[str]] = None) -> StepTraffic:

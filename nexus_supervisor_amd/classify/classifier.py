@@ -19,6 +19,7 @@ and never does I/O.
 from __future__ import annotations
 
 import json
+import re
 import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -49,11 +50,20 @@ MSG_CONFIG = "Unable to create the algorithm container - please review configura
 MSG_CRASH_LOOP = "Algorithm container is crash-looping."
 MSG_UNSCHEDULABLE = "Algorithm pod could not be scheduled on the target cluster."
 MSG_GPU_FAULT = "Algorithm hit a GPU fault."
+MSG_GPU_ADMISSION = "Algorithm pod was rejected by its node: no healthy AMD Instinct GPU could be allocated to it."
+MSG_ADMISSION = "Algorithm pod was rejected by its node at admission."
 
 IMAGE_PULL_WAITING = ("ErrImagePull", "ImagePullBackOff", "InvalidImageName", "ErrImageNeverPull")
 CONFIG_WAITING = ("CreateContainerConfigError", "CreateContainerError", "RunContainerError")
 EVICTION_EVENT_REASONS = ("Evicted", "Preempted", "Preempting", "TaintManagerEviction")
 NO_GPU_CLASSES = (F.IMAGE_PULL, F.CONFIG, F.SCHEDULING)
+ADMISSION_CLASSES = (F.GPU_ADMISSION, F.ADMISSION)
+# kubelet admission rejections recorded as pod Events (the OutOf<resource> ones are matched
+# by prefix; event_reasons_read() lists the common resources for the watch hub's filter)
+ADMISSION_EVENT_REASONS = ("UnexpectedAdmissionError", "TopologyAffinityError")
+# the device manager's / resource fit's numbers in an admission message
+_ALLOC_NUMS = re.compile(r"Requested:\s*(\d+),\s*Available:\s*(\d+)", re.I)
+_FIT_NUMS = re.compile(r"requested:\s*(\d+),\s*used:\s*(\d+),\s*capacity:\s*(\d+)", re.I)
 JOB_FAILED_CONDITION_REASONS = ("DeadlineExceeded", "BackoffLimitExceeded", "PodFailurePolicy",
                                 "MaxFailedIndexesExceeded", "FailedIndexes")
 
@@ -148,7 +158,7 @@ class Classifier:
         kind = inv.get("kind", "")
         if kind not in ("Job", "Pod"):
             return IGNORED, []
-        if event.get("reason", "") not in _EVENT_REASONS:
+        if event.get("reason", "") not in _EVENT_REASONS and not event.get("reason", "").startswith("OutOf"):
             # most of a namespace's Events (Scheduled, Pulling, Pulled, Created, Killing,
             # SuccessfulCreate, ...) decide nothing: no cache lookup, no stale-event parking
             return NOOP, []
@@ -195,7 +205,49 @@ class Classifier:
         if reason == "FailedScheduling":
             self.evidence.add((algorithm, request_id), {"kind": "unschedulable", "message": message})
             return EVIDENCE, []
+        if reason in ADMISSION_EVENT_REASONS or reason.startswith("OutOf"):
+            # the kubelet's rejection Event: the pod-status rule decides from the pod's own
+            # Failed status when it can wait for the node agent's GPU evidence (the kubelet
+            # always writes that status); otherwise the Event decides
+            det = self._admission_detail(reason, message, obj)
+            wait_for_status = (self.rules.pod_status_rules and det["gpu"] and self.gpu.evidence_wait > 0
+                               and not self.has_gpu_evidence(obj))
+            if self.rules.admission_policy == "observe" or wait_for_status:
+                self.evidence.add((algorithm, request_id), dict(det, kind="admission", message=message[-512:]))
+                return EVIDENCE, []
+            return DECIDED, [self._admission_result(obj, det, message, inv, request_id, algorithm, "event", ev_uid)]
         return NOOP, []
+
+    # ------------------------------------------------------------ kubelet admission
+    def _admission_detail(self, reason: str, message: str, pod: Optional[Dict[str, Any]]) -> Dict[str, Any]:
+        """What a kubelet admission rejection says: whether it is about the pod's GPUs (the
+        device plugin could not allocate — an unhealthy GPU after a reset or ECC storm, a
+        restarting device plugin —, OutOf<gpu resource>, or the topology manager could not
+        align the GPUs), the node, and the counts the message carries."""
+        res = self.gpu.gpu_resource_name
+        req = kube.gpu_request(pod, res) if pod else 0
+        gpu = (reason == "OutOf" + res or (bool(res) and res in message)
+               or (req > 0 and reason in ADMISSION_EVENT_REASONS))
+        d: Dict[str, Any] = {"reason": reason, "gpu": gpu, "node": ((pod or {}).get("spec") or {}).get("nodeName", "")}
+        if gpu:
+            d["resource"] = res
+            d["requested"] = req
+        m = _ALLOC_NUMS.search(message)
+        if m:
+            d["requested"], d["available"] = int(m.group(1)), int(m.group(2))
+        else:
+            m = _FIT_NUMS.search(message)
+            if m:
+                d["requested"], d["used"], d["capacity"] = int(m.group(1)), int(m.group(2)), int(m.group(3))
+        return d
+
+    def _admission_result(self, pod, det, message, inv, request_id, algorithm, source, ev_uid="") -> RunStatusAnalysisResult:
+        gpu = det["gpu"]
+        res = self._result(A.TO_FAIL_STUCK_IN_PENDING, MSG_GPU_ADMISSION if gpu else MSG_ADMISSION, message, inv,
+                           request_id, algorithm, det["reason"], F.GPU_ADMISSION if gpu else F.ADMISSION, source, ev_uid)
+        res.evidence["admission"] = det
+        self._enrich(res, pods=[pod])
+        return res
 
     # ------------------------------------------------------------ R-POD
     def has_gpu_evidence(self, pod: Dict[str, Any]) -> bool:
@@ -219,7 +271,8 @@ class Classifier:
             return []  # resync replay of an unchanged object
         status = pod.get("status") or {}
         if (not status.get("containerStatuses") and not status.get("initContainerStatuses")
-                and not status.get("conditions") and status.get("reason") != "Evicted"):
+                and not status.get("conditions") and status.get("reason") != "Evicted"
+                and status.get("phase") != "Failed"):
             return []  # freshly created / not yet scheduled: nothing any rule can match
         request_id = self._pod_request_id(pod)
         if not request_id:
@@ -227,7 +280,17 @@ class Classifier:
         algorithm = self._algorithm(pod)
         key = (algorithm, request_id)
         inv = {"kind": "Pod", "name": kube.name_of(pod), "uid": kube.uid_of(pod)}
-        status = pod.get("status") or {}
+        # 0. refused by the node's kubelet at admission (Failed, no container ever created)
+        rej = kube.admission_rejection(pod)
+        if rej is not None:
+            det = self._admission_detail(rej["reason"], rej["message"], pod)
+            if self.rules.admission_policy == "observe":
+                self.evidence.add(key, dict(det, kind="admission", message=rej["message"][-512:]))
+                return []
+            if det["gpu"] and allow_wait and not self.has_gpu_evidence(pod):
+                self.deferred = True  # the node agent's GPU-health record is on its way
+                return []
+            return [self._admission_result(pod, det, rej["message"], inv, request_id, algorithm, "pod-status")]
         current_terms = [t for t in kube.terminated_states(pod) if t["which"] == "state"]
         # 1. OOM (host cgroup OOMKilled or HIP OOM signature on a terminated container)
         failed_terms = [t for t in current_terms if t.get("exitCode", 0) != 0 or t.get("reason") == "OOMKilled"]
@@ -581,7 +644,7 @@ class Classifier:
             logs = [r for p in pods for r in self._cached_logs(p)] if self.log_cache else None
             if logs and want_gpu:
                 res.evidence["logs"] = logs
-            if verdict is None and res.action != A.TO_RUNNING:
+            if verdict is None and res.action != A.TO_RUNNING and res.failure_class not in ADMISSION_CLASSES:
                 terms = [t for p in pods for t in kube.terminated_states(p)]
                 ltexts = [x for p in pods for x in self._log_texts(p, gev if p is pod else self._pod_ctx(p)[1])]
                 verdict = oom_mod.analyze(list(texts) + ltexts, terms, gev,
@@ -607,20 +670,28 @@ class Classifier:
         prior = self.evidence.get(res.key)
         if prior:
             res.evidence["history"] = prior
-            if res.failure_class == F.BACKOFF_LIMIT and any(p.get("kind") == "evicted" for p in prior):
-                res.failure_class = F.EVICTED
+            if res.failure_class == F.BACKOFF_LIMIT:
+                adm = [p for p in prior if p.get("kind") == "admission"]
+                if adm:
+                    # its pods were refused by their nodes' kubelets: never ran, never retried
+                    # of their own doing (a GPU admission outranks any other rejection)
+                    a = next((p for p in adm if p.get("gpu")), adm[-1])
+                    res.failure_class = F.GPU_ADMISSION if a.get("gpu") else F.ADMISSION
+                    res.evidence.setdefault("admission", {k: v for k, v in a.items() if k not in ("kind", "message")})
+                elif any(p.get("kind") == "evicted" for p in prior):
+                    res.failure_class = F.EVICTED
         if (res.action == A.TO_FAIL_DEADLINE_EXCEEDED and res.reason == "BackoffLimitExceeded"
                 and self.rules.oom_fails_backoff_job):
-            # BackoffLimitExceeded of a run whose pods died of an OOM or were evicted: the run
-            # neither timed out nor ran out of retries of its own doing — write the row the
-            # pod-status OOM rule / ``evicted-policy: fail`` writes (FAILED with that cause).
+            # BackoffLimitExceeded of a run whose pods died of an OOM, were evicted or were
+            # refused at kubelet admission: the run neither timed out nor ran out of retries of
+            # its own doing — write the row the pod-status rule / ``evicted-policy: fail``
+            # writes (FAILED, or SCHEDULING_FAILED for an admission rejection, with that cause).
             # On by default; false keeps the reference's DEADLINE_EXCEEDED for
             # BackoffLimitExceeded (supervisor.go:183-193), the class and evidence then go into
             # the trace only (docs/PARITY.md)
-            msg = _BACKOFF_CAUSE.get(res.failure_class)
-            if msg is not None:
-                res.action = A.TO_FAIL_FATAL_ERROR
-                res.run_status_message = msg
+            cause = _BACKOFF_CAUSE.get(res.failure_class)
+            if cause is not None:
+                res.action, res.run_status_message = cause
 
     def late_enrich(self, res: RunStatusAnalysisResult, lookup: ObjectLookup) -> None:
         """Re-enrich a Job-level decision just before it is written.
@@ -637,6 +708,11 @@ class Classifier:
                 st = pod.get("status") or {}
                 if st.get("reason") == "Evicted" or self._disruption(pod):
                     self.evidence.add(res.key, {"kind": "evicted", "message": st.get("message", ""), "pod": kube.name_of(pod)})
+                else:
+                    rej = kube.admission_rejection(pod)
+                    if rej is not None:
+                        det = self._admission_detail(rej["reason"], rej["message"], pod)
+                        self.evidence.add(res.key, dict(det, kind="admission", message=rej["message"][-512:]))
             culprit = pods[-1] if pods else None
             if len(pods) > 1:
                 # the pods' last updates may have landed after the Job's: rank them again
@@ -658,13 +734,26 @@ class Classifier:
 
 
 _NO_EV: Dict[str, Any] = {}
-# Event reasons any rule reads (decisions and evidence)
+# Event reasons any rule reads (decisions and evidence); OutOf<resource> is matched by prefix
 _EVENT_REASONS = frozenset(R.JOB_EVENT_RULES) | frozenset(R.POD_EVENT_RULES) | frozenset(EVICTION_EVENT_REASONS) | {
-    "FailedScheduling"}
+    "FailedScheduling"} | frozenset(ADMISSION_EVENT_REASONS)
+# the kubelet's resource-fit rejections (OutOf<resource>) the watch hub lets through
+_OUT_OF = ("OutOfcpu", "OutOfmemory", "OutOfpods", "OutOfephemeral-storage")
+
+
+def event_reasons_read(gpu_resource: str = "amd.com/gpu") -> frozenset:
+    """Every Event reason a rule reads, for the watch hub's exact-match filter (the
+    OutOf<resource> rejections of the GPU resource and the common host resources)."""
+    return _EVENT_REASONS | frozenset(_OUT_OF) | frozenset(("OutOf" + gpu_resource,) if gpu_resource else ())
+
+
 # every Event reason a rule reads; the watch hub drops the others before decode
-EVENT_REASONS_READ = _EVENT_REASONS
-# BackoffLimitExceeded whose cause was found: the run's failure message per class
-_BACKOFF_CAUSE = {F.HBM_OOM: MSG_HBM_OOM, F.HOST_OOM: MSG_HOST_OOM, F.EVICTED: MSG_EVICTED}
+EVENT_REASONS_READ = event_reasons_read()
+# BackoffLimitExceeded whose cause was found: the run's (action, failure message) per class
+_BACKOFF_CAUSE = {F.HBM_OOM: (A.TO_FAIL_FATAL_ERROR, MSG_HBM_OOM), F.HOST_OOM: (A.TO_FAIL_FATAL_ERROR, MSG_HOST_OOM),
+                  F.EVICTED: (A.TO_FAIL_FATAL_ERROR, MSG_EVICTED),
+                  F.GPU_ADMISSION: (A.TO_FAIL_STUCK_IN_PENDING, MSG_GPU_ADMISSION),
+                  F.ADMISSION: (A.TO_FAIL_STUCK_IN_PENDING, MSG_ADMISSION)}
 
 
 def _running(pod) -> bool:

@@ -142,6 +142,11 @@ class RulesConfig:
     # Evicted pods: "fail" the run immediately, or "observe" (record evidence, let the
     # Job controller retry and enrich the terminal Job event)
     evicted_policy: str = field(default="observe", metadata=_k("evicted-policy"))
+    # a pod its node's kubelet refused at admission (UnexpectedAdmissionError — the GPU device
+    # plugin could not allocate —, OutOf<resource>, TopologyAffinityError, NodeAffinity…):
+    # "fail" the run (SCHEDULING_FAILED, class gpu-admission / admission), or "observe"
+    # (record it; the Job's BackoffLimitExceeded is then written with that cause)
+    admission_policy: str = field(default="fail", metadata=_k("admission-policy"))
     # FailedScheduling (e.g. insufficient amd.com/gpu): fail after this long unschedulable; 0 = never
     unschedulable_timeout: float = field(default=0.0, metadata=_k("unschedulable-timeout", "duration"))
     # keep events whose involved object is not cached yet this long before dropping as stale
@@ -408,6 +413,8 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("stages.finished cannot contain new / buffered / running")
     if cfg.rules.evicted_policy not in ("fail", "observe"):
         raise ConfigError("rules.evicted-policy must be fail|observe")
+    if cfg.rules.admission_policy not in ("fail", "observe"):
+        raise ConfigError("rules.admission-policy must be fail|observe")
     if cfg.rules.trace_format not in ("raw", "json", "auto"):
         raise ConfigError("rules.trace-format must be raw|json|auto")
     if cfg.rules.trace_max_bytes and cfg.rules.trace_max_bytes < 1024:

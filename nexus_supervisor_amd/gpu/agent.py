@@ -38,8 +38,8 @@ from typing import Any, Deque, Dict, List, Optional, Set, Tuple
 from ..informer import InformerFactory
 from ..models import kube
 from . import logtail
-from .podresources import PodResourcesClient, gpu_allocations, normalize_bdf
-from .telemetry import ATTRIBUTION_EVENTS, FAULT_EVENTS, GpuTelemetry, _pod_gpus, evidence_for
+from .podresources import PodResourcesClient, allocatable_ids, gpu_allocations, normalize_bdf
+from .telemetry import ATTRIBUTION_EVENTS, FAULT_EVENTS, GpuTelemetry, _pod_gpus, admission_evidence, evidence_for
 from .topology import topology_from_pod
 
 log = logging.getLogger("nexus_supervisor_amd.agent")
@@ -186,7 +186,24 @@ class NodeAgent:
         topo = topology_from_pod(pod, self.gpu_resource)
         return _pod_gpus(topo, self.tel.devices())
 
+    def allocatable_bdfs(self) -> Optional[List[str]]:
+        """PCI addresses of the GPUs the kubelet's device manager offers for allocation
+        (pod-resources ``GetAllocatableResources``), None when unknown."""
+        fn = getattr(self.podres, "allocatable", None)
+        if fn is None:
+            return None
+        try:
+            return allocatable_ids(fn(), self.gpu_resource)
+        except Exception as exc:  # noqa: BLE001 - kubelet socket optional / older kubelet
+            log.debug("pod-resources allocatable lookup failed: %s", exc)
+            return None
+
     def evidence(self, pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+        if kube.admission_rejection(pod) is not None:
+            # the kubelet refused the pod before allocating it a GPU: what the supervisor
+            # needs is which of this node's GPUs are unhealthy (classify: gpu-admission)
+            return admission_evidence(self.tel, pod, node=self.node, lookback=self.lookback,
+                                      allocatable_bdfs=self.allocatable_bdfs())
         alloc = self.allocation(pod)
         ev = evidence_for(self.tel, pod_uid=kube.uid_of(pod), gpu_indices=self.gpus_for(pod, alloc),
                           lookback=self.lookback, node=self.node, allocated=alloc)
@@ -308,7 +325,7 @@ class NodeAgent:
         if kube.annotations_of(pod).get(self.annotation):
             self.published[uid] = ("present", time.monotonic())
             return
-        self._spawn_publish(pod, "pod-failed")
+        self._spawn_publish(pod, "admission-rejected" if kube.admission_rejection(pod) is not None else "pod-failed")
 
     def _on_pod_delete(self, pod) -> None:
         uid = kube.uid_of(pod)

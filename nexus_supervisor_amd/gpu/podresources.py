@@ -109,6 +109,42 @@ def encode_list_response(pods: List[Dict[str, object]]) -> bytes:
     return out
 
 
+ALLOCATABLE_METHOD = "/v1.PodResourcesLister/GetAllocatableResources"
+
+
+def decode_allocatable_response(raw: bytes) -> List[Dict[str, object]]:
+    """``AllocatableResourcesResponse { repeated ContainerDevices devices = 1; … }`` →
+    ``[{"resource_name", "device_ids"}]`` (cpu_ids / memory are skipped)."""
+    out = []
+    for f, cv in _fields(raw):
+        if f != 1:
+            continue
+        d = {"resource_name": "", "device_ids": []}
+        for df, dv in _fields(cv):
+            if df == 1:
+                d["resource_name"] = dv.decode()
+            elif df == 2:
+                d["device_ids"].append(dv.decode())
+        out.append(d)
+    return out
+
+
+def encode_allocatable_response(devices: List[Dict[str, object]]) -> bytes:
+    """Inverse of :func:`decode_allocatable_response` (fake kubelet in tests)."""
+    out = b""
+    for d in devices:
+        db = _enc_bytes(1, d["resource_name"].encode())
+        for did in d["device_ids"]:
+            db += _enc_bytes(2, did.encode())
+        out += _enc_bytes(1, db)
+    return out
+
+
+def allocatable_ids(devices: List[Dict[str, object]], resource: str = "amd.com/gpu") -> List[str]:
+    """Device ids of one resource the kubelet's device manager offers for allocation."""
+    return [i for d in devices if d["resource_name"] == resource for i in d["device_ids"]]
+
+
 def gpu_allocations(pods: List[Dict[str, object]], resource: str = "amd.com/gpu") -> Dict[Tuple[str, str], List[str]]:
     """``(namespace, pod) -> [device ids]`` for one resource."""
     out: Dict[Tuple[str, str], List[str]] = {}
@@ -133,6 +169,17 @@ class PodResourcesClient:
         call = self._channel.unary_unary(LIST_METHOD, request_serializer=lambda _: b"",
                                          response_deserializer=lambda b: b)
         return decode_list_response(call(None, timeout=self.timeout))
+
+    def allocatable(self) -> List[Dict[str, object]]:
+        """``GetAllocatableResources`` (kubelet ≥ 1.23): the devices the device manager
+        offers — a GPU the AMD device plugin reported unhealthy is missing from it."""
+        import grpc
+
+        if self._channel is None:
+            self._channel = grpc.insecure_channel(self.target)
+        call = self._channel.unary_unary(ALLOCATABLE_METHOD, request_serializer=lambda _: b"",
+                                         response_deserializer=lambda b: b)
+        return decode_allocatable_response(call(None, timeout=self.timeout))
 
     def check(self) -> str:
         """``ok``, ``missing`` or ``denied``: can this process connect to the kubelet's

@@ -515,6 +515,71 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
     return out
 
 
+def node_gpu_health(telemetry: GpuTelemetry, lookback: float = 600.0, now: Optional[float] = None,
+                    snapshot: Optional[List[Dict[str, Any]]] = None,
+                    allocatable_bdfs: Optional[Iterable[str]] = None) -> Dict[str, Any]:
+    """Health of every GPU of the node, for a pod the kubelet refused at admission (it never
+    got a GPU, so no per-GPU record of its own exists): the GPUs amd-smi sees, and per
+    unhealthy GPU what is wrong — uncorrectable ECC errors, xGMI links down or in error,
+    resets / VM faults / ECC / xGMI events in the ``lookback`` window.  With the kubelet's
+    allocatable device set (pod-resources ``GetAllocatableResources``, by PCI BDF) the GPUs
+    amd-smi sees but the device plugin no longer offers are listed too
+    (``not_allocatable``): the usual shape of "the device plugin marked a GPU unhealthy"."""
+    from .podresources import normalize_bdf
+
+    snap = snapshot if snapshot is not None else telemetry.snapshot(False)
+    now = time.time() if now is None else now
+    alloc = None if allocatable_bdfs is None else {normalize_bdf(b) for b in allocatable_bdfs}
+    unhealthy: List[Dict[str, Any]] = []
+    not_alloc: List[int] = []
+    for g in snap:
+        problems: List[str] = []
+        if g.get("ecc_uncorrectable"):
+            problems.append(f"ecc_uncorrectable={g['ecc_uncorrectable']}")
+        if g.get("xgmi_links_down"):
+            problems.append(f"xgmi_links_down={g['xgmi_links_down']}/{g.get('xgmi_links_total')}")
+        if g.get("xgmi_error"):
+            problems.append(f"xgmi_error={g['xgmi_error']}")
+        evs = [{"type": e["type"], "t": round(e["t"], 3), "message": (e.get("message") or "")[:200]}
+               for e in g.get("events", ()) if e.get("type") in FAULT_EVENTS and e.get("t", 0) >= now - lookback]
+        if evs:
+            problems.append("events=" + ",".join(sorted({e["type"] for e in evs})))
+        if alloc is not None and g.get("bdf") and normalize_bdf(g["bdf"]) not in alloc:
+            not_alloc.append(g["index"])
+            problems.append("not in the kubelet's allocatable set")
+        if problems:
+            rec: Dict[str, Any] = {"index": g["index"], "uuid": g.get("hip_uuid") or g.get("uuid"), "bdf": g.get("bdf"),
+                                   "problems": problems}
+            if evs:
+                rec["events"] = evs[-TRACE_EVENTS:]
+            unhealthy.append(rec)
+    out: Dict[str, Any] = {"gpus_seen": len(snap), "healthy": sorted(g["index"] for g in snap
+                                                                      if g["index"] not in {u["index"] for u in unhealthy}),
+                           "unhealthy": unhealthy}
+    if alloc is not None:
+        out["allocatable"] = len(alloc)
+        out["not_allocatable"] = not_alloc
+    return out
+
+
+TRACE_EVENTS = 4  # fault events per unhealthy GPU in a node-health record
+
+
+def admission_evidence(telemetry: GpuTelemetry, pod: Dict[str, Any], node: str = "", lookback: float = 600.0,
+                       allocatable_bdfs: Optional[Iterable[str]] = None) -> Dict[str, Any]:
+    """Evidence record (same envelope as :func:`evidence_for`) for a pod refused at kubelet
+    admission: no per-GPU records, the node's GPU health instead."""
+    out: Dict[str, Any] = {"source": telemetry.name, "t": round(time.time(), 3), "gpus": [],
+                           "node_health": node_gpu_health(telemetry, lookback, allocatable_bdfs=allocatable_bdfs)}
+    n = node or (pod.get("spec") or {}).get("nodeName", "")
+    if n:
+        out["node"] = n
+    uid = kube.uid_of(pod)
+    if uid:
+        out["pod_uid"] = uid
+    return out
+
+
 def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/gpu", node: str = "",
                           lookback: float = 300.0):
     """Classifier hook (``Classifier.evidence_provider``): live evidence for a pod from a
@@ -540,6 +605,9 @@ def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/
                      links=_LazyLinks(snap), memo={})
 
     def provider(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+        if kube.admission_rejection(pod) is not None:
+            # refused by the kubelet before any GPU was allocated: the node's GPU health
+            return admission_evidence(telemetry, pod, node=node, lookback=lookback)
         topo = topology_from_pod(pod, gpu_resource)
         now = time.monotonic()
         if cache["snap"] is None or now - cache["t"] > ttl:

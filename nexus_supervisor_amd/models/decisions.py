@@ -37,6 +37,11 @@ class FailureClass:
     FATAL = "fatal"                      # PodFailurePolicy / other fatal exit
     CONFIG = "config"                    # CreateContainerConfigError
     COLLECTIVE = "collective"            # every failed rank shows only RCCL / collective errors
+    # the node's kubelet refused the pod at admission because of its GPUs: the device
+    # plugin could not allocate (UnexpectedAdmissionError), OutOf<gpu-resource>, or the
+    # topology manager could not align the GPUs (TopologyAffinityError)
+    GPU_ADMISSION = "gpu-admission"
+    ADMISSION = "admission"              # any other kubelet admission rejection (OutOfcpu, NodeAffinity, ...)
 
 
 @dataclass

@@ -214,6 +214,34 @@ def gpu_request(pod, resource: str = "amd.com/gpu") -> int:
     return total
 
 
+def admission_rejection(pod) -> Optional[Dict[str, str]]:
+    """``{"reason", "message"}`` of a pod the kubelet refused to admit, else None.
+
+    A pod bound to a node can still be rejected by that node's kubelet at admission
+    (``pkg/kubelet/lifecycle``): the pod goes straight to ``phase: Failed`` with
+    ``status.reason`` the admit handler's reason and no container statuses — the device
+    manager's ``UnexpectedAdmissionError`` ("Allocate failed due to …"), the resource fit
+    ``OutOf<resource>`` (``OutOfamd.com/gpu``, ``OutOfcpu``, …), or a node-side predicate
+    (``NodeAffinity``, ``NodeSelectorMismatching``, ``NodePorts``…)."""
+    st = pod.get("status") or _EMPTY
+    if st.get("phase") != "Failed":
+        return None
+    reason = st.get("reason") or ""
+    if not reason or reason == "Evicted" or st.get("containerStatuses") or st.get("initContainerStatuses"):
+        return None
+    if reason == "UnexpectedAdmissionError" or reason.startswith("OutOf") or reason in ADMISSION_PREDICATE_REASONS:
+        return {"reason": reason, "message": st.get("message") or ""}
+    return None
+
+
+# kubelet admit handlers' rejection reasons besides UnexpectedAdmissionError / OutOf<resource>
+ADMISSION_PREDICATE_REASONS = frozenset((
+    "NodeAffinity", "NodeSelectorMismatching", "NodePorts", "NodeName", "PodOSNotSupported",
+    "PodOSSelectorNodeLabelDoesNotMatch", "InvalidNodeInfo", "UnexpectedPredicateFailureType",
+    "SysctlForbidden", "AppArmor", "NodeShutdown", "NodeResourcesFit", "TopologyAffinityError",
+    "SMTAlignmentError", "UnsupportedHostNetwork"))
+
+
 def condition(obj, ctype: str) -> Optional[Dict[str, Any]]:
     for c in (obj.get("status") or {}).get("conditions") or []:
         if c.get("type") == ctype:

@@ -87,10 +87,10 @@ class WatchHub:
         self.drain = drain
         self.metrics = metrics
         self.router = _kube_native.ShardRouter(0, count, _SEED, cfg.labels.job_name_label, POD_FORGET_AFTER)
-        from ..classify.classifier import EVENT_REASONS_READ
+        from ..classify.classifier import event_reasons_read
 
         # an Event no rule reads decides nothing: no worker decodes, caches or dispatches it
-        self.router.set_event_reasons(sorted(EVENT_REASONS_READ))
+        self.router.set_event_reasons(sorted(event_reasons_read(cfg.gpu.gpu_resource_name)))
         self._unread_seen = 0
         from .sharding import ShardSet
 

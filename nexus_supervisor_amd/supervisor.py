@@ -55,7 +55,7 @@ STAGE_FOR_ACTION = {
 }
 
 
-_GPU_CLASSES = frozenset((F.HBM_OOM, F.GPU_FAULT, F.COLLECTIVE))
+_GPU_CLASSES = frozenset((F.HBM_OOM, F.GPU_FAULT, F.COLLECTIVE, F.GPU_ADMISSION))
 # Job event / condition reasons that imply one of the Job's pods has already failed
 _POD_FAILED_REASONS = frozenset(("BackoffLimitExceeded", "PodFailurePolicy"))
 
@@ -78,7 +78,13 @@ def failed_gpu(r: RunStatusAnalysisResult) -> Tuple[str, Optional[Any]]:
     ev = r.evidence
     topo = ev.get("topology") or {}
     gev = ev.get("gpu") or {}
-    node = topo.get("node") or gev.get("node") or ""
+    node = topo.get("node") or gev.get("node") or (ev.get("admission") or {}).get("node") or ""
+    health = gev.get("node_health")
+    if health is not None:
+        # refused at kubelet admission: no GPU was allocated — the one unhealthy GPU of the
+        # node, when the node agent's health record names exactly one
+        bad = health.get("unhealthy") or ()
+        return node, bad[0].get("index") if len(bad) == 1 else None
     oom = ev.get("oom") or {}
     if oom.get("gpu_index") is not None:
         return node, oom["gpu_index"]
@@ -619,7 +625,7 @@ class Supervisor:
                 fut.set_result(None)
         st = pod.get("status")
         if (not self._gpu_wait and (not st or not (st.get("containerStatuses") or st.get("initContainerStatuses")
-                                                   or st.get("conditions") or st.get("reason") == "Evicted"))):
+                                                   or st.get("conditions") or st.get("phase") == "Failed"))):
             return  # a new (pending, unscheduled) pod: no pod-status rule can match it yet
         recv = self.wall()
         wait = self.cfg.gpu.evidence_wait

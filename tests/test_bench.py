@@ -172,6 +172,8 @@ def test_baseline_scenarios_small(arun):
     assert r1["acked"] == 5 and r1["wrong_stage"] == 0 and r1["p50_ms"] < 1000
     r2 = arun(sc.cfg2_burst("reference", n=40), timeout=60)
     assert r2["acked"] == 40 and r2["wrong_stage"] == 0
+    # the mix really holds start failures (image pulls, GPU admission rejections)
+    assert r2["kinds"].get("image-pull") and r2["kinds"].get("gpu-admission") and r2["kinds"].get("host-oom")
     r4 = arun(sc.cfg4_rate("uncapped", seconds=2.0, rate=1200, jobs=300), timeout=60)
     assert r4["drained"] and r4["wrong_stage"] == 0 and r4["acked"] == r4["events"] == 40
     r5 = arun(sc.cfg5_chaos("uncapped", seconds=4.0, rate=1200, jobs=300), timeout=120)
