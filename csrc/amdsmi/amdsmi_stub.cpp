@@ -8,6 +8,7 @@
 #include <amd_smi/amdsmi.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -29,6 +30,7 @@ struct StubGpu {
   uint64_t ecc_uncorrectable = 0;
   int links_down = 0;
   std::vector<StubProc> procs;
+  std::vector<uint32_t> vanished;  // printed once by the next process-list call
 };
 
 struct StubEvent {
@@ -104,6 +106,12 @@ void nexus_stub_set_links_down(int gpu, int down) {
   std::lock_guard<std::mutex> lk(g_mu);
   ensure_gpus_locked();
   if (gpu >= 0 && gpu < static_cast<int>(g_gpus.size())) g_gpus[gpu].links_down = down;
+}
+
+void nexus_stub_add_vanished(int gpu, uint32_t pid) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  ensure_gpus_locked();
+  if (gpu >= 0 && gpu < static_cast<int>(g_gpus.size())) g_gpus[gpu].vanished.push_back(pid);
 }
 
 void nexus_stub_push_event(int gpu, int type, const char* message) {
@@ -249,6 +257,10 @@ amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle h, uint32_t*
   std::lock_guard<std::mutex> lk(g_mu);
   if (!valid(h)) return AMDSMI_STATUS_INVAL;
   auto& ps = g_gpus[handle_index(h)].procs;
+  // a process that exited while the real library listed it: its stderr line, once
+  for (uint32_t pid : g_gpus[handle_index(h)].vanished)
+    fprintf(stderr, "Unable to open queues directory for process %u: No such file or directory\n", pid);
+  g_gpus[handle_index(h)].vanished.clear();
   uint32_t n = static_cast<uint32_t>(ps.size());
   if (n > *max) {
     *max = n;

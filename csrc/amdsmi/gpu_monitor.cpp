@@ -200,6 +200,7 @@ void nexus_stub_set_vram(int gpu, uint32_t used_mb);
 void nexus_stub_set_proc(int gpu, uint32_t pid, uint64_t vram);
 void nexus_stub_end_proc(int gpu, uint32_t pid);
 void nexus_stub_set_links_down(int gpu, int down);
+void nexus_stub_add_vanished(int gpu, uint32_t pid);
 void nexus_stub_push_event(int gpu, int type, const char* message);
 }
 #endif
@@ -239,6 +240,20 @@ PYBIND11_MODULE(NEXUS_MONITOR_MODULE, m) {
       },
       "Zero the refusal counters");
   m.def(
+      "stderr_filter",
+      [](bool on) { Fd2Filter::instance().set_enabled(on); },
+      py::arg("enabled"),
+      "Keep libamd_smi's per-process stderr noise out of fd 2 (on by default; stderr_filter.hpp)");
+  m.def(
+      "stderr_filter_stats",
+      []() {
+        py::dict d;
+        d["noise_lines"] = Fd2Filter::instance().noise_lines();
+        d["forwarded_bytes"] = Fd2Filter::instance().forwarded_bytes();
+        return d;
+      },
+      "Noise lines dropped and other threads' stderr bytes forwarded so far");
+  m.def(
       "kfd_proc_usage",
       [](const std::string& sys_root) { return uses_list(kfd_proc_usage(sys_root, kfd_gpu_bdfs(sys_root))); },
       py::arg("sys_root") = "/sys", "Per-process VRAM from KFD sysfs (init-namespace PIDs)");
@@ -262,6 +277,7 @@ PYBIND11_MODULE(NEXUS_MONITOR_MODULE, m) {
       .def("peak_between", [](PyMonitor& s, int gpu, double t0, double t1) { return s.m_.peak_between(gpu, t0, t1); })
       .def("history", &PyMonitor::history, py::arg("gpu_index"), py::arg("since") = 0.0)
       .def_property_readonly("samples", [](PyMonitor& s) { return s.m_.samples(); })
+      .def_property_readonly("process_vanished", [](PyMonitor& s) { return s.m_.process_vanished(); })
       .def_property_readonly("last_sample", [](PyMonitor& s) { return s.m_.last_sample_seconds(); })
       .def_property_readonly("n_gpus", [](PyMonitor& s) { return s.m_.n_gpus(); })
       .def_property_readonly("proc_mode", [](PyMonitor& s) { return s.m_.proc_mode(); })
@@ -272,6 +288,7 @@ PYBIND11_MODULE(NEXUS_MONITOR_MODULE, m) {
   m.def("stub_set_proc", &nexus_stub_set_proc);
   m.def("stub_end_proc", &nexus_stub_end_proc);
   m.def("stub_set_links_down", &nexus_stub_set_links_down);
+  m.def("stub_add_vanished", &nexus_stub_add_vanished);
   m.def("stub_push_event", [](int gpu, const std::string& type, const std::string& msg) {
     int t = AMDSMI_EVT_NOTIF_VMFAULT;
     if (type == "GPU_PRE_RESET") t = AMDSMI_EVT_NOTIF_GPU_PRE_RESET;

@@ -47,6 +47,7 @@
 #include <vector>
 
 #include "procscan.hpp"
+#include "stderr_filter.hpp"
 
 namespace nexus_gpu {
 
@@ -325,6 +326,8 @@ class GpuMonitor {
   }
 
   uint64_t samples() const { return samples_.load(); }
+  // processes amd-smi could not read because they exited while it listed them
+  uint64_t process_vanished() const { return vanished_.load(); }
   double last_sample_seconds() const { return last_sample_s_.load(); }
   size_t n_gpus() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -503,11 +506,15 @@ class GpuMonitor {
       ecc_ok[i] = amdsmi_get_gpu_total_ecc_count(gs[i].h, &ecc[i]) == AMDSMI_STATUS_SUCCESS;
       if (mode == "kfd") continue;
       uint32_t n = static_cast<uint32_t>(buf.size());
-      amdsmi_status_t st = amdsmi_get_gpu_process_list(gs[i].h, &n, buf.data());
+      amdsmi_status_t st = AMDSMI_STATUS_SUCCESS;
+      // libamd_smi prints a line to stderr per process that exits mid-listing: counted
+      // (gpu_process_vanished), not printed (stderr_filter.hpp)
+      auto& fd2 = Fd2Filter::instance();
+      vanished_ += fd2.run([&] { st = amdsmi_get_gpu_process_list(gs[i].h, &n, buf.data()); });
       if (st == AMDSMI_STATUS_OUT_OF_RESOURCES || n > buf.size()) {
         buf.resize(std::min<uint32_t>(n, 4096) + 16);  // a count read while processes exit: bounded
         n = static_cast<uint32_t>(buf.size());
-        st = amdsmi_get_gpu_process_list(gs[i].h, &n, buf.data());
+        vanished_ += fd2.run([&] { st = amdsmi_get_gpu_process_list(gs[i].h, &n, buf.data()); });
       }
       if (st != AMDSMI_STATUS_SUCCESS) continue;
       for (uint32_t k = 0; k < n && k < buf.size(); ++k) {
@@ -703,6 +710,7 @@ class GpuMonitor {
   std::unordered_map<uint64_t, ProcRec> procs_;
   std::deque<EventRec> events_, pending_events_;
   std::atomic<uint64_t> samples_{0};
+  std::atomic<uint64_t> vanished_{0};
   std::atomic<uint64_t> sample_errors_{0};  // exceptions caught in the monitor threads
   std::atomic<double> last_sample_s_{0};
 };

@@ -63,7 +63,8 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
                if sanitize != "thread" else "-fno-omit-frame-pointer"]
     proto = os.path.join(CSRC, "cql", "cql_proto.hpp")
     amd = os.path.join(CSRC, "amdsmi")
-    mon_deps = [os.path.join(amd, "monitor_core.hpp"), os.path.join(amd, "procscan.hpp")]
+    mon_deps = [os.path.join(amd, "monitor_core.hpp"), os.path.join(amd, "procscan.hpp"),
+                os.path.join(amd, "stderr_filter.hpp")]
     ext_dir = os.path.join(SAN_DIR, sanitize) if sanitize else PKG
     sfx = f"-{sanitize}" if sanitize else ""
     return {

@@ -608,6 +608,9 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             agent.stop()
         await harness.stop()
         telemetry.stop()
+        if monitor is not None:
+            # libamd_smi's "Unable to open queues directory" lines, counted instead of printed
+            monitor["process_vanished"] = telemetry.process_vanished()
     return {"elapsed": elapsed, "events": cfg.events * cfg.steps * (cfg.world if cfg.node else 1), "errors": tracker.errors,
             "failures": timed[0], "starts": timed[1], "start_latencies_ms": timed[2],
             "starts_superseded": tracker.superseded,

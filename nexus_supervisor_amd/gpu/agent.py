@@ -128,6 +128,7 @@ class NodeAgent:
         # attribution that silently degrades for lack of privileges is counted and logged once
         self.metrics = Metrics("nexus_gpu_agent", {"node": node_name})
         self._denied_seen: Dict[str, int] = {}
+        self._vanished_seen = 0
         self._warned: Set[str] = set()
         self.privileges: Dict[str, Any] = {}
 
@@ -252,6 +253,11 @@ class NodeAgent:
             cur = self.tel.denials()
         except Exception:  # noqa: BLE001 - diagnostics only
             return {}
+        van = self.tel.process_vanished() if hasattr(self.tel, "process_vanished") else 0
+        if van > self._vanished_seen:
+            # processes that exited while amd-smi listed them (its stderr noise, counted)
+            self.metrics.inc("gpu_process_vanished", van - self._vanished_seen)
+            self._vanished_seen = van
         new = {}
         for src, n in cur.items():
             d = int(n) - self._denied_seen.get(src, 0)

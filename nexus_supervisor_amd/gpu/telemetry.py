@@ -66,6 +66,11 @@ class GpuTelemetry:
         degraded for lack of privileges."""
         return {}
 
+    def process_vanished(self) -> int:
+        """Processes that exited while amd-smi listed them (libamd_smi's "Unable to open
+        queues directory" — kept off stderr and counted, ``csrc/amdsmi/stderr_filter.hpp``)."""
+        return 0
+
 
 def native_monitor_module(stub: bool = False):
     """Import the native monitor (``stub``: the build over the stub amd-smi, for CPU
@@ -128,6 +133,9 @@ class AmdSmiTelemetry(GpuTelemetry):
     def denials(self) -> Dict[str, int]:
         fn = getattr(self._mod, "denials", None)
         return dict(fn()) if fn is not None else {}
+
+    def process_vanished(self) -> int:
+        return int(getattr(self._m, "process_vanished", 0))
 
     @property
     def samples(self) -> int:

@@ -210,3 +210,53 @@ def test_trim_ladder_is_deterministic():
     assert t["trimmed"][0] == "gpu.procs:1" and t["oom"]["kind"] == "hbm" and t["class"] == "hbm-oom"
     one = json.loads(render_trace(r, max_bytes=0))
     assert "trimmed" not in one and len(one["gpu"]["gpus"][0]["procs"]) == 4 and one["gpu"]["gpus"][0]["procs_total"] == 9
+
+
+_NOISE_CHILD = r"""
+import os, sys, threading, time
+sys.path.insert(0, {root!r})
+from nexus_supervisor_amd.testing.fakeprocfs import FakeProcFs
+from nexus_supervisor_amd.gpu.telemetry import AmdSmiTelemetry
+import nexus_supervisor_amd._amdsmi_monitor_stub as M
+fs = FakeProcFs({tmp!r}, n_gpus=2)
+t = AmdSmiTelemetry(interval=0.005, proc_source="amdsmi", proc_root=fs.proc, sys_root=fs.sys, stub=True)
+t.start()
+stop = False
+def chatter():  # another thread's stderr, written while samples swap fd 2
+    i = 0
+    while not stop:
+        os.write(2, b"other-thread line %d\n" % i)
+        i += 1
+        time.sleep(0.0005)
+    print("chatter", i, flush=True)
+th = threading.Thread(target=chatter)
+th.start()
+for k in range(6):
+    M.stub_add_vanished(k % 2, 4000 + k)
+    time.sleep(0.03)
+stop = True
+th.join()
+t.stop()
+print("vanished", t.process_vanished(), flush=True)
+print("stats", M.stderr_filter_stats()["noise_lines"], flush=True)
+"""
+
+
+def test_amdsmi_stderr_noise_is_counted_not_printed(tmp_path):
+    """libamd_smi prints "Unable to open queues directory for process N" to fd 2 for
+    each process that exits while it lists them (BENCH_r05's stderr was nothing else):
+    the sampler swaps fd 2 for a memfd around the call, counts those lines
+    (gpu_process_vanished) and forwards everything else another thread wrote meanwhile."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _NOISE_CHILD.format(root=root, tmp=str(tmp_path))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = dict(line.split(" ", 1) for line in p.stdout.splitlines() if " " in line)
+    assert int(out["vanished"]) == 6 and int(out["stats"]) == 6
+    assert "Unable to open queues directory" not in p.stderr
+    lines = [x for x in p.stderr.splitlines() if x.startswith("other-thread line")]
+    # nothing another thread wrote is lost, and its order is kept
+    assert len(lines) == int(out["chatter"]) and lines == sorted(lines, key=lambda x: int(x.split()[-1]))
