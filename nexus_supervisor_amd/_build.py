@@ -11,6 +11,7 @@ artefact               sources                                 toolchain
 ``bin/gpu_stress``     ``csrc/stress/gpu_stress.hip``          hipcc gfx950
 ``_amdsmi_monitor_stub`` monitor over ``amdsmi_stub.cpp``      g++ (CPU tests)
 ``bin/monitor_selftest`` monitor threads over the stub          g++ (TSan/ASan)
+``_certgen``           ``csrc/certgen/certgen.cpp``            g++ + libcrypto
 =====================  ======================================  ==================
 
 Every C++ target builds with ``-Wall -Wextra -Werror`` (the CI static-analysis gate).
@@ -83,6 +84,16 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
             "deps": [],
             "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, "-shared", "-fPIC",
                                       f"-I{sysconfig.get_paths()['include']}", *srcs, "-o", out],
+            "inproc": True,
+        },
+        # the shard-label webhook's self-signed CA + serving certificate (libcrypto)
+        "certgen": {
+            "out": os.path.join(ext_dir, "_certgen" + EXT),
+            "srcs": [os.path.join(CSRC, "certgen", "certgen.cpp")],
+            "deps": [],
+            "cmd": lambda out, srcs: [_cxx(), *common, *san, "-shared", "-fPIC", *_pybind_includes(), *srcs, "-lcrypto",
+                                      "-o", out],
+            "requires": "/usr/include/openssl/x509v3.h",
             "inproc": True,
         },
         "amdsmi_monitor": {

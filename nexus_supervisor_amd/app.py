@@ -68,44 +68,39 @@ def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
     return InformerFactory(lw, resync_period=cfg.resync_period)
 
 
-def _start_shard_audit(cfg, kube, metrics, log):
-    """The ``sharding.shard-label`` audit, in the process that owns the replica's API client
-    (a single-process replica, or a sharded replica's parent — not its shard workers)."""
-    if (not cfg.sharding.shard_label or cfg.sharding.shards <= 1 or kube is None or not hasattr(kube, "request")
-            or os.environ.get("NEXUS_WORKER_CONFIG")):
-        return None
-    from .parallel.sharding import audit_shard_labels
-
-    return asyncio.ensure_future(audit_shard_labels(cfg, kube, metrics, log))
-
-
-def _start_shard_relabel(cfg, kube, metrics, log, owned):
-    """``sharding.relabel``: re-stamp the shard label of the runs in ``owned`` (the process
-    that owns the replica's API client only)."""
+def _shard_label_keeper(cfg, kube, metrics, log, owned):
+    """The ``sharding.shard-label`` audit + repair and re-label passes
+    (:class:`~.admission.ShardLabelKeeper`), in the process that owns the replica's API
+    client (a single-process replica, or a sharded replica's parent — not its workers);
+    ``owned``: callable → the replica's current shards."""
     s = cfg.sharding
-    if (not s.shard_label or s.shards <= 1 or not s.relabel or kube is None or not hasattr(kube, "patch_merge")
-            or os.environ.get("NEXUS_WORKER_CONFIG") or not owned):
+    if (not s.shard_label or s.shards <= 1 or kube is None or not hasattr(kube, "request")
+            or not hasattr(kube, "patch_merge") or os.environ.get("NEXUS_WORKER_CONFIG")):
         return None
-    from .admission import relabel_owned
+    from .admission import ShardLabelKeeper
 
-    async def go():
-        try:
-            await relabel_owned(cfg, kube, frozenset(owned), metrics, log)
-        except asyncio.CancelledError:
-            raise
-        except Exception as exc:  # noqa: BLE001 - the audit keeps reporting unlabelled runs
-            log.error(exc, "shard re-label pass failed")
-
-    return asyncio.ensure_future(go())
+    keeper = ShardLabelKeeper(cfg, kube, metrics, log, owned)
+    keeper.start()
+    return keeper
 
 
-async def _start_webhook(cfg, metrics):
+async def _start_webhook(cfg, metrics, kube=None, log=None):
     if not cfg.sharding.webhook_port or os.environ.get("NEXUS_WORKER_CONFIG"):
         return None
     from .admission import WebhookServer
 
     ws = WebhookServer(cfg, metrics)
+    boot = None
+    if cfg.sharding.webhook_cert_bootstrap and kube is not None:
+        from .webhook_certs import WebhookCertBootstrap
+
+        # the serving pair exists before the server starts; renewals are picked up by its reload
+        boot = WebhookCertBootstrap.from_config(cfg, kube, metrics, log)
+        await boot.sync()
     await ws.start(cfg.observability.http_host, cfg.sharding.webhook_port, cfg.sharding.webhook_cert_dir)
+    if boot is not None:
+        boot.start(on_change=ws.check_cert)
+        ws.bootstrap = boot
     return ws
 
 
@@ -184,16 +179,16 @@ class Application:
         await self.supervisor.start()
         if self.elector is not None:
             self.elector.start()
-        self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
-        self.webhook = await _start_webhook(cfg, self.metrics)
-        if cfg.sharding.mode != "lease":
-            self._relabel = _start_shard_relabel(cfg, self.kube, self.metrics, self.log,
-                                                 self.supervisor.shards.owned)
+        self.labels = _shard_label_keeper(cfg, self.kube, self.metrics, self.log,
+                                          lambda: self.supervisor.shards.owned)
+        self.webhook = await _start_webhook(cfg, self.metrics, self.kube, self.log)
+        if cfg.sharding.mode != "lease" and self.labels is not None and self.supervisor.shards.owned:
+            self.labels.request_relabel(self.supervisor.shards.owned)
 
     def _set_shards(self, owned):
         gained, lost = self.supervisor.set_shards(owned)
-        if gained:  # their runs may carry labels of another shard count
-            _start_shard_relabel(self.cfg, self.kube, self.metrics, self.log, gained)
+        if gained and getattr(self, "labels", None) is not None:
+            self.labels.request_relabel(gained)  # their runs may carry labels of another shard count
         return gained, lost
 
     def ready(self) -> bool:
@@ -203,9 +198,8 @@ class Application:
         return await self.factory.wait_for_cache_sync(timeout)
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
-        for t in (getattr(self, "_audit", None), getattr(self, "_relabel", None)):
-            if t is not None:
-                t.cancel()
+        if getattr(self, "labels", None) is not None:
+            await self.labels.stop()
         if getattr(self, "webhook", None) is not None:
             await self.webhook.stop()
         if self.elector is not None:
@@ -383,10 +377,10 @@ class ShardedApplication:
             from .kube.client import KubeClient
 
             self.kube = KubeClient.for_config(cfg, self.metrics, schedule=self.pool.qps_schedule)
-        self._audit = _start_shard_audit(cfg, self.kube, self.metrics, self.log)
-        self.webhook = await _start_webhook(cfg, self.metrics)
-        if not lease_mode:
-            self._relabel = _start_shard_relabel(cfg, self.kube, self.metrics, self.log, self.shards.owned)
+        self.labels = _shard_label_keeper(cfg, self.kube, self.metrics, self.log, lambda: self.shards.owned)
+        self.webhook = await _start_webhook(cfg, self.metrics, self.kube, self.log)
+        if not lease_mode and self.labels is not None and self.shards.owned:
+            self.labels.request_relabel(self.shards.owned)
 
     def _shard_holds(self, until) -> None:
         """Shard hold deadlines renewed: the workers self-fence on them (no parent round trip)."""
@@ -397,8 +391,8 @@ class ShardedApplication:
         """Shard leases won / lost: the workers fence and replay, the hub re-routes and
         re-lists so the workers receive the runs of gained shards."""
         gained, lost = self.shards.update(owned)
-        if gained:
-            _start_shard_relabel(self.cfg, self.kube, self.metrics, self.log, gained)
+        if gained and getattr(self, "labels", None) is not None:
+            self.labels.request_relabel(gained)
         self.pool.set_shards(owned, self.shard_leases.deadlines() if self.shard_leases is not None else None)
         if self.hub is not None:
             self.hub.set_shards(self.shards)
@@ -418,9 +412,8 @@ class ShardedApplication:
         return self.merged_metrics
 
     async def stop(self, drain_timeout: float = 10.0) -> None:
-        for t in (getattr(self, "_audit", None), getattr(self, "_relabel", None)):
-            if t is not None:
-                t.cancel()
+        if getattr(self, "labels", None) is not None:
+            await self.labels.stop()
         if getattr(self, "webhook", None) is not None:
             await self.webhook.stop()
         if self.elector is not None:

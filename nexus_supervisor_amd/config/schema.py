@@ -273,17 +273,40 @@ class ShardingConfig:
     # (``<label> in (owned…)``, filtered by the API server's watch cache) instead of every
     # replica receiving the whole namespace.  Events carry no such label and stay a full
     # stream (dropped before decode by the native router).  Empty = off.  Jobs without the
-    # label are invisible with it on: /metrics shard_label_missing counts them (audit)
+    # label are invisible with it on: /metrics shard_label_missing counts them and the audit
+    # re-stamps them (audit-interval, repair-labels)
     shard_label: str = field(default="", metadata=_k("shard-label"))
     # serve the mutating admission webhook that stamps shard-label on Nexus Jobs (and their
     # pod templates) and Pods at CREATE (admission.py; the chart registers it with
     # failurePolicy: Ignore); 0 = off
     webhook_port: int = field(default=0, metadata=_k("webhook-port"))
-    # tls.crt / tls.key of the webhook's serving certificate (a Secret mounted here)
+    # tls.crt / tls.key of the webhook's serving certificate (a Secret mounted here; with
+    # webhook-cert-bootstrap a writable directory the replica writes its pair to)
     webhook_cert_dir: str = field(default="/etc/nexus/webhook-tls", metadata=_k("webhook-cert-dir"))
+    # no cert-manager: the replicas mint a self-signed CA + serving certificate into the
+    # Secret webhook-secret (compare-and-swap: one pair for all), renew it 30 days before
+    # expiry, and keep caBundle of webhook-config-name in step (webhook_certs.py)
+    webhook_cert_bootstrap: bool = field(default=False, metadata=_k("webhook-cert-bootstrap"))
+    webhook_secret: str = field(default="nexus-supervisor-webhook-tls", metadata=_k("webhook-secret"))
+    # the MutatingWebhookConfiguration whose caBundle the bootstrap sets; empty = leave it alone
+    webhook_config_name: str = field(default="", metadata=_k("webhook-config-name"))
+    # the webhook Service's name (the certificate's DNS names: <service>.<namespace>.svc…)
+    webhook_service: str = field(default="nexus-supervisor-webhook", metadata=_k("webhook-service"))
     # at startup (static mode) / on gaining a shard (lease mode): re-stamp the label of this
     # replica's runs whose label was computed for another shard count
     relabel: bool = field(default=True, metadata=_k("relabel"))
+    # the shard-label audit: every interval, LIST the Nexus Jobs / Pods whose label is missing
+    # or names no shard (shard_label_missing) — admitted while the webhook was unreachable
+    # (failurePolicy: Ignore) and invisible to every replica; 0 = off
+    audit_interval: float = field(default=60.0, metadata=_k("audit-interval", "duration"))
+    # the audit PATCHes the label of the runs of this replica's shards it finds (self-healing:
+    # a run submitted during a webhook outage is supervised within one audit interval);
+    # false = count and log only
+    repair_labels: bool = field(default=True, metadata=_k("repair-labels"))
+    # every this many audit passes, also re-check the runs labelled with this replica's shards
+    # and fix labels that disagree with shard_of(name, shards) (shard_label_wrong: a stale
+    # count stamped during a rolling change of shards)
+    relabel_every: int = field(default=5, metadata=_k("relabel-every"))
 
 
 @dataclass
@@ -425,6 +448,8 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("sharding.mode must be static|lease")
     if cfg.sharding.replicas < 0:
         raise ConfigError("sharding.replicas must be >= 0 (0 = greedy)")
+    if cfg.sharding.audit_interval < 0 or cfg.sharding.relabel_every < 1:
+        raise ConfigError("sharding.audit-interval must be >= 0 (0 = off) and sharding.relabel-every >= 1")
     rt = cfg.runtime
     if rt.worker_processes == 0:
         from ..utils.cpus import auto_worker_processes

@@ -76,6 +76,10 @@ RESOURCES: Dict[str, Tuple[str, str]] = {
     "Job": ("/apis/batch/v1", "jobs"),
     "Lease": ("/apis/coordination.k8s.io/v1", "leases"),
     "Node": ("/api/v1", "nodes"),
+    "Secret": ("/api/v1", "secrets"),
+    # cluster-scoped (namespace None): the shard-label webhook's registration, whose caBundle
+    # sharding.webhook-cert-bootstrap keeps in step with the certificate it minted
+    "MutatingWebhookConfiguration": ("/apis/admissionregistration.k8s.io/v1", "mutatingwebhookconfigurations"),
 }
 
 

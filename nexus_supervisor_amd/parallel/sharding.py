@@ -75,38 +75,6 @@ def watch_selector(cfg, kind: str, owned: Optional[Iterable[int]] = None) -> str
     return ",".join(parts)
 
 
-async def audit_shard_labels(cfg, kube, metrics, log, interval: float = 60.0) -> None:
-    """``sharding.shard-label`` safety net: with shard-narrowed watches a Nexus Job that
-    lacks the label is seen by no replica.  Every ``interval`` one LIST of Nexus Jobs
-    *without* the label (``!<label>``, at most 100) sets ``shard_label_missing`` and logs
-    their names, so an operator finds the submitter that does not stamp it."""
-    import asyncio
-
-    s = cfg.sharding
-    base = f"{cfg.labels.nexus_component_label}={cfg.labels.algorithm_run_value}"
-    warned = False
-    from ..kube.client import resource_path
-
-    path = resource_path("Job", cfg.resource_namespace)
-    while True:
-        try:
-            # one page: the audit needs a count and a few names, not every unlabelled Job
-            doc = await kube.request("GET", path, params={"labelSelector": f"{base},!{s.shard_label}", "limit": "100"})
-            items = doc.get("items") or []
-            n = len(items) + int((doc.get("metadata") or {}).get("remainingItemCount") or 0)
-            metrics.set("shard_label_missing", float(n))
-            if n and not warned:
-                names = sorted(kube_name(i) for i in items)[:5]
-                log.warning("Nexus Jobs without the shard label are invisible to every replica",
-                            label=s.shard_label, jobs=n, examples=names)
-            warned = bool(n)
-        except asyncio.CancelledError:
-            raise
-        except Exception as exc:  # noqa: BLE001 - an audit, never a reason to stop
-            log.v(1).info("shard label audit failed", error=str(exc))
-        await asyncio.sleep(interval)
-
-
 def kube_name(obj) -> str:
     return ((obj or {}).get("metadata") or {}).get("name", "")
 

@@ -32,7 +32,8 @@ from . import miniweb as web
 from ..kube.client import RESOURCES
 
 _PLURAL_TO_KIND = {plural: kind for kind, (_prefix, plural) in RESOURCES.items()}
-_API_VERSION = {"Event": "v1", "Pod": "v1", "Node": "v1", "Job": "batch/v1", "Lease": "coordination.k8s.io/v1"}
+_API_VERSION = {"Event": "v1", "Pod": "v1", "Node": "v1", "Job": "batch/v1", "Lease": "coordination.k8s.io/v1",
+                "Secret": "v1", "MutatingWebhookConfiguration": "admissionregistration.k8s.io/v1"}
 
 
 _ISO_CACHE = [0, ""]
@@ -276,6 +277,11 @@ class FakeApiServer:
             srv.add_route("PATCH", base + "/{name}", self._h_patch)
             srv.add_route("DELETE", base + "/{name}", self._h_delete)
             srv.add_route("GET", f"{prefix}/{plural}", self._h_collection)
+            # cluster-scoped objects (namespace ""): Nodes, MutatingWebhookConfigurations
+            srv.add_route("POST", f"{prefix}/{plural}", self._h_create)
+            srv.add_route("GET", f"{prefix}/{plural}/{{name}}", self._h_get)
+            srv.add_route("PUT", f"{prefix}/{plural}/{{name}}", self._h_replace)
+            srv.add_route("PATCH", f"{prefix}/{plural}/{{name}}", self._h_patch)
         srv.add_route("GET", "/api/v1/namespaces/{ns}/pods/{name}/log", self._h_pod_log)
         port = await srv.start(host, port, ssl_context=ssl_context)
         self._server = srv
@@ -615,7 +621,7 @@ class FakeApiServer:
         if bad is not None:
             return bad
         kind = self._kind(req)
-        obj = self.objects[kind].get((req.match_info["ns"], req.match_info["name"]))
+        obj = self.objects[kind].get((req.match_info.get("ns", ""), req.match_info["name"]))
         if obj is None:
             return self._status(404, "NotFound", f'{kind.lower()}s "{req.match_info["name"]}" not found')
         return web.json_response(obj)
@@ -657,7 +663,8 @@ class FakeApiServer:
         kind = self._kind(req)
         obj = await req.json()
         obj["kind"] = kind
-        obj.setdefault("metadata", {})["namespace"] = req.match_info["ns"]
+        if req.match_info.get("ns"):
+            obj.setdefault("metadata", {})["namespace"] = req.match_info["ns"]
         if self.mutating_webhooks:
             obj = await self._mutate(obj)
         try:
@@ -672,7 +679,9 @@ class FakeApiServer:
         kind = self._kind(req)
         obj = await req.json()
         obj["kind"] = kind
-        obj.setdefault("metadata", {}).update(namespace=req.match_info["ns"], name=req.match_info["name"])
+        obj.setdefault("metadata", {}).update(name=req.match_info["name"])
+        if req.match_info.get("ns"):
+            obj["metadata"]["namespace"] = req.match_info["ns"]
         try:
             return web.json_response(self.update(obj, check_rv=True))
         except KeyError:
@@ -685,12 +694,15 @@ class FakeApiServer:
         if bad is not None:
             return bad
         kind = self._kind(req)
-        key = (req.match_info["ns"], req.match_info["name"])
+        key = (req.match_info.get("ns", ""), req.match_info["name"])
         cur = self.objects[kind].get(key)
         if cur is None:
             return self._status(404, "NotFound", "not found")
         patch = await req.json()
-        new = _merge(copy.deepcopy(cur), patch)
+        if req.headers.get("Content-Type", "").startswith("application/json-patch+json"):
+            new = json_patch(copy.deepcopy(cur), patch)
+        else:
+            new = _merge(copy.deepcopy(cur), patch)
         return web.json_response(self.update(new))
 
     async def _h_delete(self, req: web.Request):
