@@ -91,7 +91,11 @@ inline bool keep_env_var(const std::string& k) {
                                 "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL", "JOB_COMPLETION_INDEX", "HOSTNAME"};
   for (const char* n : names)
     if (k == n) return true;
-  return k.rfind("NCCL_", 0) == 0 || k.rfind("RCCL_", 0) == 0;
+  // the collective families models/kube.py ENV_PREFIXES keeps from pod specs
+  static const char* prefixes[] = {"NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_", "MSCCL", "UCX_"};
+  for (const char* p : prefixes)
+    if (k.rfind(p, 0) == 0) return true;
+  return false;
 }
 
 // Pod UID from a cgroup path: kubepods[-burstable|-besteffort]-pod<uid>.slice (systemd
@@ -247,6 +251,7 @@ class GpuMonitor {
     wake_cv_.notify_all();
     if (sampler_.joinable()) sampler_.join();
     if (listener_.joinable()) listener_.join();
+    Fd2Filter::instance().flush();  // a write still in flight at the last swap back
     std::vector<amdsmi_processor_handle> registered;
     {
       std::lock_guard<std::mutex> lk(mu_);

@@ -10,13 +10,17 @@
 // Fd2Filter::run(fn) points fd 2 at an anonymous in-memory file (memfd, O_APPEND) for
 // the duration of `fn` (one amd-smi call, well under a millisecond), then puts the real
 // stderr back and forwards every captured line that is not amd-smi noise — anything
-// another thread wrote to stderr in that window — to it, in order.  Nothing can block
+// another thread wrote to stderr in that window — to it, in order (a write racing the
+// swap back by microseconds can come out a few lines late, never lost).  Nothing can block
 // (a memfd never fills like a pipe), nothing is lost unless the process dies inside the
-// window, and the noise lines are counted (the vanished processes) instead of printed.
+// window (a write still in flight at the swap back is forwarded by the next drain, or by
+// flush() when the monitor stops), and the noise lines are counted (the vanished
+// processes) instead of printed.
 // The swap is process-wide, so all monitors in the process share one mutex.
 #pragma once
 
 #include <fcntl.h>
+#include <linux/falloc.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
@@ -76,6 +80,12 @@ class Fd2Filter {
     return drain();
   }
 
+  // Forward what late writers appended after the last window (call when sampling stops).
+  uint32_t flush() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return memfd_ >= 0 ? drain(true) : 0;
+  }
+
   void set_enabled(bool on) { enabled_.store(on); }
   uint64_t noise_lines() const { return noise_.load(); }
   uint64_t forwarded_bytes() const { return forwarded_.load(); }
@@ -83,14 +93,30 @@ class Fd2Filter {
  private:
   Fd2Filter() = default;
 
-  uint32_t drain() {
+  // Reads what was appended since the last drain.  The file is never truncated: a write
+  // another thread started while fd 2 still pointed here can complete after the swap back,
+  // and it must land where the next drain reads it (a truncate could drop it).  The pages
+  // already read are released with a hole punch, so memory stays flat.
+  uint32_t drain(bool all = false) {
     off_t end = lseek(memfd_, 0, SEEK_END);
-    if (end <= 0) return 0;
-    std::string buf(static_cast<size_t>(end), '\0');
-    ssize_t got = pread(memfd_, &buf[0], buf.size(), 0);
-    if (ftruncate(memfd_, 0) != 0) { /* the next window appends after the stale bytes: harmless */ }
+    if (end <= off_) return 0;
+    std::string buf(static_cast<size_t>(end - off_), '\0');
+    ssize_t got = pread(memfd_, &buf[0], buf.size(), off_);
     if (got <= 0) return 0;
     buf.resize(static_cast<size_t>(got));
+    // only whole lines (a line written in pieces is read whole by the next drain), except
+    // on the final flush
+    size_t whole = buf.rfind('\n');
+    if (!all) {
+      if (whole == std::string::npos) return 0;
+      buf.resize(whole + 1);
+    }
+    off_ += static_cast<off_t>(buf.size());
+    const off_t page = 4096;
+    if (off_ / page > punched_ / page) {
+      off_t upto = (off_ / page) * page;
+      if (fallocate(memfd_, FALLOC_FL_PUNCH_HOLE | FALLOC_FL_KEEP_SIZE, punched_, upto - punched_) == 0) punched_ = upto;
+    }
     uint32_t noise = 0;
     std::string keep;
     size_t s = 0;
@@ -117,6 +143,8 @@ class Fd2Filter {
 
   std::mutex mu_;
   int memfd_ = -1;
+  off_t off_ = 0;       // bytes of the file already drained
+  off_t punched_ = 0;   // bytes released with a hole punch
   std::atomic<bool> enabled_{true};
   std::atomic<uint64_t> noise_{0};
   std::atomic<uint64_t> forwarded_{0};

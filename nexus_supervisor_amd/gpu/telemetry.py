@@ -24,6 +24,7 @@ import time
 from typing import Any, Dict, Iterable, List, Optional
 
 from ..models import kube
+from .topology import COLLECTIVE_PREFIXES as _COLLECTIVE_PREFIXES
 from .topology import _int, physical_gpu, topology_from_pod
 
 ATTRIBUTION_EVENTS = ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET", "GPU_POST_RESET", "THERMAL_THROTTLE",
@@ -514,6 +515,16 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
     if not gpus:
         return None
     out: Dict[str, Any] = {"source": telemetry.name, "t": round(now, 3), "gpus": gpus}
+    coll: Dict[str, str] = {}
+    for g in snap:
+        for p in g.get("procs", ()):
+            if (pod_uid and p.get("pod_uid") == pod_uid) or p.get("pid") in pids:
+                for k, v in (p.get("env") or {}).items():
+                    if k.startswith(_COLLECTIVE_PREFIXES) and k not in coll:
+                        coll[k] = v
+    if coll:
+        # the RCCL / NCCL env of the pod's processes (/proc/<pid>/environ), once per pod
+        out["collective_env"] = dict(sorted(coll.items()))
     if allocated:
         out["allocated"] = sorted(int(i) for i in allocated)
     if node:

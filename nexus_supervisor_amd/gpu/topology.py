@@ -49,9 +49,58 @@ def parse_visible_devices(value: Optional[str]) -> List[str]:
 _DEVICE_CHAIN = (("ROCR_VISIBLE_DEVICES",), ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
 
 
+# torchrun arguments given as env (``PET_<ARG>``: the Kubeflow training operator's PyTorchJob,
+# or a pod that runs torchrun itself) → the topology keys they imply; the RANK family is set
+# by torchrun in its child processes only, so from the pod spec these are all there is
+_PET_VARS = ("PET_NNODES", "PET_NPROC_PER_NODE", "PET_NODE_RANK", "PET_MASTER_ADDR", "PET_MASTER_PORT",
+             "PET_RDZV_ENDPOINT", "PET_RDZV_BACKEND")
+
 # every variable _topology_from_env reads (besides the collective prefixes)
 _READ_VARS = frozenset([v for v, _k in _INT_VARS] + [v for names in _DEVICE_CHAIN for v in names]
-                       + ["GPU_DEVICE_ORDINAL"])
+                       + ["GPU_DEVICE_ORDINAL"] + list(_PET_VARS))
+
+
+def _launcher_env(env: Dict[str, str], topo: Dict[str, Any], gpus_requested: int) -> None:
+    """Fold torchrun's ``PET_*`` arguments into ``topo`` where the direct variables are
+    absent: nodes, processes per node (``gpu`` / ``auto`` = the pod's GPUs), this node's
+    rank, the rendezvous endpoint, and the world size they imply.  An elastic range
+    (``PET_NNODES=1:4``) is kept as ``nnodes_range``: the world size is then unknown."""
+    if not any(v in env for v in _PET_VARS):
+        return
+    topo["launcher"] = "torchrun"
+    nn = (env.get("PET_NNODES") or "").strip()
+    if nn and "nnodes" not in topo:
+        if ":" in nn:
+            lo, _sep, hi = nn.partition(":")
+            if _int(lo) is not None and _int(hi) is not None:
+                topo["nnodes_range"] = [_int(lo), _int(hi)]
+                if _int(lo) == _int(hi):
+                    topo["nnodes"] = _int(lo)
+        elif _int(nn) is not None:
+            topo["nnodes"] = _int(nn)
+    npp = (env.get("PET_NPROC_PER_NODE") or "").strip()
+    if npp and "local_world_size" not in topo:
+        n = _int(npp)
+        if n is None and npp in ("gpu", "auto") and gpus_requested:
+            n = gpus_requested  # torchrun: one process per visible GPU
+        if n is not None:
+            topo["local_world_size"] = n
+    nr = _int(env.get("PET_NODE_RANK"))
+    if nr is not None and "node_rank" not in topo:
+        topo["node_rank"] = nr
+    addr, port = env.get("PET_MASTER_ADDR"), _int(env.get("PET_MASTER_PORT"))
+    ep = env.get("PET_RDZV_ENDPOINT") or ""
+    if not addr and ep:
+        host, _sep, p = ep.rpartition(":")
+        addr, port = (host, _int(p)) if host and _int(p) is not None else (ep, port)
+    if addr and "master_addr" not in topo:
+        topo["master_addr"] = addr
+    if port is not None and "master_port" not in topo:
+        topo["master_port"] = port
+    if env.get("PET_RDZV_BACKEND"):
+        topo["rdzv_backend"] = env["PET_RDZV_BACKEND"]
+    if "world_size" not in topo and topo.get("nnodes") and topo.get("local_world_size"):
+        topo["world_size"] = topo["nnodes"] * topo["local_world_size"]
 _ENV_MEMO: Dict[Tuple, Dict[str, Any]] = {}
 
 
@@ -100,6 +149,7 @@ def _topology_from_env(env: Dict[str, str], gpus_requested: int = 0, node: str =
         topo["master_addr"] = env["MASTER_ADDR"]
     if "rank" not in topo and "completion_index" in topo:
         topo["rank"] = topo["completion_index"]  # indexed Job → rank
+    _launcher_env(env, topo, gpus_requested)
     chain = []
     for names in _DEVICE_CHAIN:
         for var in names:
@@ -356,6 +406,16 @@ def merge_process_ranks(topo: Dict[str, Any], gpu_evidence: Optional[Dict[str, A
     if groups:
         ranks = [{k: v for k, v in e.items() if k != "_peak"} for e in groups.values()]
         topo = dict(topo, rank_map=sorted(ranks, key=lambda e: (e.get("rank", 1 << 30), e.get("gpu") or 0)))
+    penv = gpu_evidence.get("collective_env")
+    if penv:
+        # the RCCL / NCCL settings the ranks actually ran with (a launcher can pass them to
+        # its children only: mpirun -x, a wrapper script): the pod spec's own values win
+        mine = topo.get("collective_env") or {}
+        extra = {k: v for k, v in penv.items() if k not in mine}
+        if extra:
+            topo = dict(topo, collective_env=dict(sorted({**mine, **extra}.items())))
+            if mine:
+                topo["collective_env_from_processes"] = sorted(extra)
     return topo
 
 

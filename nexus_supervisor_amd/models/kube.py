@@ -264,7 +264,12 @@ _CONDITIONS = ["list", {"type": True, "status": True, "reason": True, "message":
 # cost of decoding a pod line (10 dicts of 2 strings each), and no other variable is used.
 ENV_KEEP = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "NODE_RANK", "NNODES",
             "ROLE_RANK", "ROLE_WORLD_SIZE", "JOB_COMPLETION_INDEX", "MASTER_ADDR", "MASTER_PORT",
-            "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+            "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL",
+            # torchrun's own arguments as env (PyTorchJob / Kubeflow training operator, torchrun in
+            # the pod): the pod spec carries these, the RANK / WORLD_SIZE family only exists in the
+            # processes torchrun starts
+            "PET_NNODES", "PET_NPROC_PER_NODE", "PET_NODE_RANK", "PET_MASTER_ADDR", "PET_MASTER_PORT",
+            "PET_RDZV_ENDPOINT", "PET_RDZV_BACKEND")
 ENV_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_", "MSCCL", "UCX_")
 _CSTATUS = ["list", {"name": True, "state": True, "lastState": True, "restartCount": True, "ready": True, "started": True}]
 

@@ -246,7 +246,8 @@ def test_amdsmi_stderr_noise_is_counted_not_printed(tmp_path):
     """libamd_smi prints "Unable to open queues directory for process N" to fd 2 for
     each process that exits while it lists them (BENCH_r05's stderr was nothing else):
     the sampler swaps fd 2 for a memfd around the call, counts those lines
-    (gpu_process_vanished) and forwards everything else another thread wrote meanwhile."""
+    (gpu_process_vanished) and forwards everything else another thread wrote meanwhile —
+    every line, none lost."""
     import subprocess
     import sys
 
@@ -258,5 +259,6 @@ def test_amdsmi_stderr_noise_is_counted_not_printed(tmp_path):
     assert int(out["vanished"]) == 6 and int(out["stats"]) == 6
     assert "Unable to open queues directory" not in p.stderr
     lines = [x for x in p.stderr.splitlines() if x.startswith("other-thread line")]
-    # nothing another thread wrote is lost, and its order is kept
-    assert len(lines) == int(out["chatter"]) and lines == sorted(lines, key=lambda x: int(x.split()[-1]))
+    # nothing another thread wrote is lost (a write racing the swap back by microseconds is
+    # forwarded by the next drain, so it can come out a few lines late)
+    assert sorted(lines) == sorted(f"other-thread line {i}" for i in range(int(out["chatter"])))
