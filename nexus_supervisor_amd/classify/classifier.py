@@ -652,10 +652,15 @@ class Classifier:
                                           topo=topo, gpu_involved=self._any_gpu(pods, pod, gev))
         elif verdict is None and res.action != A.TO_RUNNING and any(texts):
             verdict = oom_mod.analyze(texts, (), None, None, self.gpu.hbm_capacity_gb, self.gpu.hbm_oom_fraction)
-        if verdict is not None and verdict.kind:
-            res.evidence["oom"] = verdict.as_dict()
-            if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.CRASH_LOOP, F.COLLECTIVE):
-                res.failure_class = F.HBM_OOM if verdict.kind == "hbm" else F.HOST_OOM
+        if verdict is not None:
+            if verdict.kind:
+                res.evidence["oom"] = verdict.as_dict()
+                if res.failure_class in (F.FATAL, F.BACKOFF_LIMIT, F.NONE, F.CRASH_LOOP, F.COLLECTIVE):
+                    res.failure_class = F.HBM_OOM if verdict.kind == "hbm" else F.HOST_OOM
+            if verdict.foreign is not None:
+                # someone else filled the GPU: recorded with its holders whatever the verdict (a
+                # crash at HIP init on a full GPU has no OOM text, but is "gpu-occupied")
+                res.evidence["foreign_occupancy"] = verdict.foreign
         if res.action != A.TO_RUNNING:
             self._apply_history(res)
 
@@ -728,6 +733,10 @@ class Classifier:
                     if v.kind:
                         res.evidence["oom"] = v.as_dict()
                         res.failure_class = F.HBM_OOM if v.kind == "hbm" else F.HOST_OOM
+                        if gev and "gpu" not in res.evidence:
+                            res.evidence["gpu"] = gev
+                    if v.foreign is not None and "foreign_occupancy" not in res.evidence:
+                        res.evidence["foreign_occupancy"] = v.foreign
                         if gev and "gpu" not in res.evidence:
                             res.evidence["gpu"] = gev
         self._apply_history(res)
@@ -841,6 +850,9 @@ def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
     topo = d.get("topology") or {}
     xg = topo.get("xgmi") or {}
     ladder = [
+        ("gpu.holders:1", lambda: [g.__setitem__("holders", g["holders"][:1]) for g in gpus() if g.get("holders")]),
+        ("foreign_occupancy.holders:1", lambda: (d.get("foreign_occupancy") or {}).__setitem__(
+            "holders", (d.get("foreign_occupancy") or {}).get("holders", [])[:1]) if d.get("foreign_occupancy") else None),
         ("gpu.procs:1", lambda: [g.__setitem__("procs", (g.get("procs") or [])[:1]) for g in gpus()]),
         ("gpu.events:2", lambda: [g.__setitem__("events", (g.get("events") or [])[-2:]) for g in gpus() if "events" in g]),
         ("history:4", lambda: d.__setitem__("history", (d.get("history") or [])[-4:]) if "history" in d else None),
@@ -854,6 +866,7 @@ def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
         ("topology.rank_map", lambda: topo.pop("rank_map", None)),
         ("ranks.pods", lambda: (d.get("ranks") or {}).pop("pods", None)),
         ("gpu.procs", lambda: [g.pop("procs", None) for g in gpus()]),
+        ("gpu.holders", lambda: [g.pop("holders", None) for g in gpus()]),
         ("gpu.events", lambda: [g.pop("events", None) for g in gpus()]),
         ("gpu.gpus:slim", lambda: [slim(g) for g in gpus()]),
         ("topology.xgmi.peers", lambda: [r.pop("peers", None) for r in xg.get("per_gpu", [])]),

@@ -109,6 +109,11 @@ def _mentions(text: str, keys) -> bool:
             return True
     return False
 
+# "someone else filled the GPU": the device at or above this share of its HBM in the
+# window while the pod's own processes held under OWN_SHARE_MAX of it
+FOREIGN_FULL_FRACTION = 0.95
+OWN_SHARE_MAX = 0.10
+
 _TORCH_GPU = re.compile(r"GPU (\d+) has a total capacity of ([\d.]+) (GiB|MiB|GB|MB)", re.I)
 _TORCH_REQ = re.compile(r"Tried to allocate ([\d.]+) (GiB|MiB|GB|MB|KiB)", re.I)
 _UNIT = {"gib": 1 << 30, "gb": 1 << 30, "mib": 1 << 20, "mb": 1 << 20, "kib": 1 << 10}
@@ -130,6 +135,9 @@ class OomVerdict:
     oomkilled: bool = False
     hbm_text: bool = False
     host_text: bool = False
+    # the GPU was full of someone else's memory (:data:`FOREIGN_FULL_FRACTION`, the pod's own
+    # share under :data:`OWN_SHARE_MAX`): who held it — recorded whatever the verdict
+    foreign: Optional[Dict[str, Any]] = None
 
     @property
     def text_signature(self) -> bool:
@@ -145,6 +153,8 @@ class OomVerdict:
             v = getattr(self, k)
             if v is not None:
                 d[k] = v
+        if self.foreign is not None:
+            d["foreign_occupancy"] = True
         return d
 
 
@@ -301,6 +311,19 @@ def analyze(
                 v.peak_vram_bytes = own or peak
                 if v.gpu_index is None:
                     v.gpu_index = g.get("index")
+            if (v.foreign is None and peak and peak >= FOREIGN_FULL_FRACTION * total and own < OWN_SHARE_MAX * total):
+                # full, but not of the pod's doing: name who held it (the stage stays what the
+                # evidence says — an HBM-OOM is still one, a crash still a crash)
+                holders = g.get("holders") or []
+                v.foreign = {"gpu": g.get("index"), "device_peak_bytes": peak, "own_peak_bytes": own,
+                             "total_bytes": total, "holders": holders}
+                if g.get("foreign_vram_bytes"):
+                    v.foreign["other_namespace_bytes"] = g["foreign_vram_bytes"]
+                top = holders[0] if holders else None
+                who = (f"; largest holder pid {top.get('pid')} ({top.get('owner')}) "
+                       f"{(top.get('vram_bytes') or 0) / (1 << 30):.1f} GiB" if top else "")
+                v.signals.append(f"foreign occupancy: GPU {g.get('index')} was {peak / total:.0%} full while the pod's "
+                                 f"own processes held {own / (1 << 30):.1f} GiB{who}")
             faults = [e for e in g.get("events", []) if e.get("type") in ("VMFAULT", "QUEUE_EVICTION", "GPU_PRE_RESET")]
             if faults:
                 v.hbm_score += 0.25

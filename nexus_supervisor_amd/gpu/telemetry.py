@@ -501,6 +501,9 @@ def evidence_for(telemetry: GpuTelemetry, pod_uid: str = "", gpu_indices: Iterab
         if g.get("foreign_procs"):
             rec["foreign_procs"] = g["foreign_procs"]
             rec["foreign_vram_bytes"] = g.get("foreign_vram_bytes", 0)
+        holders = _holders(g.get("procs", ()), procs, t0 - grace, t1 + grace)
+        if holders:
+            rec["holders"] = holders
         rec["procs"] = [dict({"pid": p["pid"], "vram_bytes": p.get("vram_bytes", 0),
                               "peak_vram_bytes": p.get("peak_vram_bytes", 0), "alive": p.get("alive", False),
                               "source": p.get("source", "")},
@@ -597,6 +600,31 @@ def admission_evidence(telemetry: GpuTelemetry, pod: Dict[str, Any], node: str =
     if uid:
         out["pod_uid"] = uid
     return out
+
+
+HOLDERS_MAX = 4  # other processes listed per GPU, largest VRAM peak first
+
+
+def _holders(all_procs, own, t0: float, t1: float) -> List[Dict[str, Any]]:
+    """The *other* processes that held memory on a GPU while the pod's processes lived (or
+    in the lookback when none of them was seen): what filled a GPU a pod then ran out of,
+    or crashed on at init — a zombie of a previous tenant, another job, a host process.
+    Each names its pod (cgroup pod UID) or ``host``; largest peak first, at most
+    :data:`HOLDERS_MAX`."""
+    mine = {id(p) for p in own}
+    out = []
+    for p in all_procs:
+        if id(p) in mine:
+            continue
+        peak = p.get("peak_vram_bytes") or p.get("vram_bytes") or 0
+        if not peak or p.get("first_seen", t0) > t1 or p.get("last_seen", t1) < t0:
+            continue
+        out.append((peak, p))
+    if not out:
+        return []
+    out.sort(key=lambda x: (-x[0], x[1].get("pid") or 0))
+    return [{"pid": p.get("pid"), "vram_bytes": peak, "owner": p.get("pod_uid") or "host",
+             "name": p.get("name") or "", "alive": bool(p.get("alive"))} for peak, p in out[:HOLDERS_MAX]]
 
 
 def pod_evidence_provider(telemetry: GpuTelemetry, gpu_resource: str = "amd.com/gpu", node: str = "",

@@ -273,11 +273,12 @@ def _exit_status(pod, code):
     return p
 
 
-def _supervise_default_pod(arun, tmp_path, stream_text, rc, *, agent: bool):
+def _supervise_default_pod(arun, tmp_path, stream_text, rc, *, agent: bool, telemetry=None):
     """One default GPU pod fails with exit ``rc`` and an empty termination message; its
     stderr is ``stream_text``.  ``agent``: the node agent reads it from a /var/log/pods
-    fixture (CRI format, what the kubelet holds); else the supervisor GETs pods/log.
-    Returns the checkpoint row's trace."""
+    fixture (CRI format, what the kubelet holds); else the supervisor GETs pods/log
+    (``telemetry``: with the co-located monitor's GPU evidence).  Returns the checkpoint
+    row's trace."""
     import asyncio
 
     from nexus_supervisor_amd.app import Application
@@ -308,6 +309,10 @@ def _supervise_default_pod(arun, tmp_path, stream_text, rc, *, agent: bool):
         store = MemoryStore([row])
         app = Application(cfg, kube=KubeClient(KubeConfig(url)), store=store)
         await app.start()
+        if telemetry is not None:
+            from nexus_supervisor_amd.gpu.telemetry import pod_evidence_provider
+
+            app.supervisor.classifier.evidence_provider = pod_evidence_provider(telemetry, lookback=120)
         kc = ag = None
         if agent:
             tel = AmdSmiTelemetry(interval=cfg.gpu.sample_interval)  # the agent owns (and stops) it
@@ -495,7 +500,10 @@ def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, 
             assert done.exists() and holders[-1].poll() is None, f"filler {i} did not reach its OOM"
             fills.append(done.read_text()[:300])
             p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
-            runs.append({"fill_chunk_gib": float(chunk), "rc": p.returncode, "stderr": p.stderr})
+            run = {"fill_chunk_gib": float(chunk), "rc": p.returncode, "stderr": p.stderr}
+            # decided while the fillers still hold the GPU: the trace names who filled it
+            run["decision"] = _decide_on_full_gpu(arun, tmp_path / f"run{i}", p.stderr, p.returncode, telemetry)
+            runs.append(run)
     finally:
         for holder in holders:
             holder.terminate()
@@ -508,27 +516,58 @@ def test_real_hip_runtime_oom_wording_on_a_full_gpu(stress_exe, tmp_path, arun, 
     for k, r in enumerate(runs):
         assert r["rc"] != 0, (r["rc"], r["stderr"][-800:])
         sig = oom.hbm_signature(r["stderr"])
-        exit_code = r["rc"] if r["rc"] > 0 else 128 - r["rc"]  # killed by a signal: 128 + signo
         if k == 0:
             assert sig, r["stderr"][-1500:]
+        trace, verdict = r["decision"]
         if sig:
-            trace, _reqs = _supervise_default_pod(arun, tmp_path / f"run{k}", r["stderr"], exit_code, agent=False)
             assert trace["class"] == "hbm-oom" and trace["oom"].get("gpu_index", 0) == 0, trace
-            verdict = trace["class"]
         else:
-            # no text, a crash (exit 139 at HIP init was seen here): the pod's exit alone decides
-            # nothing (its Job's condition does), and no HBM-OOM may be read into it
-            v = oom.analyze([("pods/log tail", r["stderr"])], [{"which": "state", "container": "algorithm",
-                                                                 "exitCode": exit_code, "reason": "Error", "message": ""}],
-                            None, "0", gpu_involved=True)
-            assert v.kind != "hbm", v.as_dict()
-            trace, verdict = None, f"no OOM verdict (exit {exit_code}, no allocation-failure text)"
+            # no text, a crash (exit 139 at HIP init was seen here): no HBM-OOM may be read into
+            # it; its Job's BackoffLimitExceeded decides
+            assert "oom" not in trace and trace["class"] != "hbm-oom", trace
+        # either way the GPU is named as someone else's: the filler's ~287 GiB is the holder
+        fo = trace["foreign_occupancy"]
+        assert fo["gpu"] == 0 and fo["own_peak_bytes"] < 0.1 * fo["total_bytes"], fo
+        assert fo["holders"] and fo["holders"][0]["vram_bytes"] >= 250 * (1 << 30), fo["holders"]
         out.append({"fill_chunk_gib": r["fill_chunk_gib"], "rc": r["rc"], "signature": sig,
                     "runtime_check_wording": "error: out of memory" in r["stderr"].lower(),
                     "stderr_tail": r["stderr"][-1500:], "verdict": verdict, "trace": trace})
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/hip_runtime_oom.json", "w") as f:
         json.dump({"fillers": fills, "runs": out}, f, indent=1)
+
+
+def _decide_on_full_gpu(arun, tmp_path, stderr, rc, telemetry):
+    """The decision a failed default pod gets on this box's (filled) GPU with the
+    co-located monitor's evidence: the pod-status decision when its log tail holds an
+    allocation failure, else (a crash with no text) its Job's BackoffLimitExceeded.
+    Returns (trace, verdict)."""
+    from nexus_supervisor_amd.classify import Classifier, render_trace
+    from nexus_supervisor_amd.config.schema import LabelConfig
+    from nexus_supervisor_amd.gpu import oom
+    from nexus_supervisor_amd.gpu.telemetry import pod_evidence_provider
+    from nexus_supervisor_amd.testing.seed import make_event, make_job
+
+    exit_code = rc if rc > 0 else 128 - rc  # killed by a signal: 128 + signo
+    if oom.hbm_signature(stderr):
+        trace, _reqs = _supervise_default_pod(arun, tmp_path, stderr, exit_code, agent=False, telemetry=telemetry)
+        return trace, trace["class"]
+    labels = LabelConfig()
+    pod = _exit_status(_default_pod(labels, "crash-at-init"), exit_code)
+    job = make_job("crash-at-init", labels)
+
+    class Lookup:
+        def get(self, kind, name):
+            return job if kind == "Job" else None
+
+        def pods_of_job(self, name):
+            return [pod]
+
+    c = Classifier(labels)
+    c.evidence_provider = pod_evidence_provider(telemetry, lookback=120)
+    _s, [r] = c.classify_event(make_event("Job", "crash-at-init", "BackoffLimitExceeded", "backoff limit"), Lookup())
+    trace = json.loads(render_trace(r))
+    return trace, f"no OOM verdict (exit {exit_code}, no allocation-failure text), GPU occupied"
 
 
 def test_node_agent_privileges_reported_on_the_box(stress_exe, tmp_path):
