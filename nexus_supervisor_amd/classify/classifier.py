@@ -378,12 +378,28 @@ class Classifier:
         # 7. running (backup for a lost "Started" event): only the pod's transition to Running
         # is a start — a pod already running when it is first listed (a restart's initial LIST
         # of 10k live runs) is not, and its Started Event is replayed from the Event list; a
-        # pod being deleted is not starting either
+        # pod being deleted is not starting either.  A run whose Started Event expired while
+        # the supervisor was down is caught by the supervisor's running sweep
+        # (rules.running-sweep-rate, :meth:`running_result`)
         if (old is not None and status.get("phase") == "Running" and not _running(old)
                 and not kube.meta(pod).get("deletionTimestamp") and _running(pod)):
             res = self._result(A.TO_RUNNING, "Started", "", inv, request_id, algorithm, "Running", F.NONE, "pod-status")
             return [res]
         return []
+
+    def running_result(self, pod: Dict[str, Any]) -> Optional[RunStatusAnalysisResult]:
+        """``ToRunning`` for a Nexus pod that is running now (not being deleted), else None:
+        the running sweep's decision for a run whose Started Event is gone (event TTL)."""
+        if not self.is_nexus(pod) or kube.meta(pod).get("deletionTimestamp"):
+            return None
+        if (pod.get("status") or {}).get("phase") != "Running" or not _running(pod):
+            return None
+        request_id = self._pod_request_id(pod)
+        if not request_id:
+            return None
+        inv = {"kind": "Pod", "name": kube.name_of(pod), "uid": kube.uid_of(pod)}
+        return self._result(A.TO_RUNNING, "Started", "", inv, request_id, self._algorithm(pod), "Running", F.NONE,
+                            "running-sweep")
 
     def _disruption(self, pod) -> Optional[Dict[str, Any]]:
         c = kube.condition(pod, "DisruptionTarget")
@@ -850,9 +866,12 @@ def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
     topo = d.get("topology") or {}
     xg = topo.get("xgmi") or {}
     ladder = [
-        ("gpu.holders:1", lambda: [g.__setitem__("holders", g["holders"][:1]) for g in gpus() if g.get("holders")]),
-        ("foreign_occupancy.holders:1", lambda: (d.get("foreign_occupancy") or {}).__setitem__(
-            "holders", (d.get("foreign_occupancy") or {}).get("holders", [])[:1]) if d.get("foreign_occupancy") else None),
+        # (a step returning False had nothing to trim and is not listed)
+        ("gpu.holders:1", lambda: [g.__setitem__("holders", g["holders"][:1]) for g in gpus()
+                                   if len(g.get("holders") or ()) > 1] or False),
+        ("foreign_occupancy.holders:1", lambda: d["foreign_occupancy"].__setitem__(
+            "holders", d["foreign_occupancy"]["holders"][:1])
+         if len((d.get("foreign_occupancy") or {}).get("holders") or ()) > 1 else False),
         ("gpu.procs:1", lambda: [g.__setitem__("procs", (g.get("procs") or [])[:1]) for g in gpus()]),
         ("gpu.events:2", lambda: [g.__setitem__("events", (g.get("events") or [])[-2:]) for g in gpus() if "events" in g]),
         ("history:4", lambda: d.__setitem__("history", (d.get("history") or [])[-4:]) if "history" in d else None),
@@ -866,7 +885,7 @@ def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
         ("topology.rank_map", lambda: topo.pop("rank_map", None)),
         ("ranks.pods", lambda: (d.get("ranks") or {}).pop("pods", None)),
         ("gpu.procs", lambda: [g.pop("procs", None) for g in gpus()]),
-        ("gpu.holders", lambda: [g.pop("holders", None) for g in gpus()]),
+        ("gpu.holders", lambda: [g.pop("holders") for g in gpus() if "holders" in g] or False),
         ("gpu.events", lambda: [g.pop("events", None) for g in gpus()]),
         ("gpu.gpus:slim", lambda: [slim(g) for g in gpus()]),
         ("topology.xgmi.peers", lambda: [r.pop("peers", None) for r in xg.get("per_gpu", [])]),
@@ -877,7 +896,8 @@ def _trim_trace(doc: Dict[str, Any], max_bytes: int) -> str:
     for name, step in ladder:
         if size() <= max_bytes:
             break
-        step()
+        if step() is False:
+            continue
         steps.append(name)
     if size() > max_bytes:
         # last resort: the decision's essentials only

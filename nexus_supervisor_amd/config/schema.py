@@ -147,6 +147,13 @@ class RulesConfig:
     # "fail" the run (SCHEDULING_FAILED, class gpu-admission / admission), or "observe"
     # (record it; the Job's BackoffLimitExceeded is then written with that cause)
     admission_policy: str = field(default="fail", metadata=_k("admission-policy"))
+    # after a restart: runs whose pod is running but whose Started Event is not in the Event
+    # list (it expired — the API server keeps Events ~1 h — while the supervisor was down)
+    # get a ToRunning decision, at most this many per second and only while no decision is
+    # queued (a backlog of failures is never delayed); 0 = off (the reference: never)
+    running_sweep_rate: float = field(default=5.0, metadata=_k("running-sweep-rate", "number"))
+    # wait this long after the caches synced before sweeping (the replayed Events decide first)
+    running_sweep_delay: float = field(default=30.0, metadata=_k("running-sweep-delay", "duration"))
     # FailedScheduling (e.g. insufficient amd.com/gpu): fail after this long unschedulable; 0 = never
     unschedulable_timeout: float = field(default=0.0, metadata=_k("unschedulable-timeout", "duration"))
     # keep events whose involved object is not cached yet this long before dropping as stale
@@ -436,6 +443,8 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         raise ConfigError("stages.finished cannot contain new / buffered / running")
     if cfg.rules.evicted_policy not in ("fail", "observe"):
         raise ConfigError("rules.evicted-policy must be fail|observe")
+    if cfg.rules.running_sweep_rate < 0 or cfg.rules.running_sweep_delay < 0:
+        raise ConfigError("rules.running-sweep-rate and rules.running-sweep-delay must be >= 0")
     if cfg.rules.admission_policy not in ("fail", "observe"):
         raise ConfigError("rules.admission-policy must be fail|observe")
     if cfg.rules.trace_format not in ("raw", "json", "auto"):

@@ -196,18 +196,20 @@ class TokenBucket:
         self._queues[cls].append((t0, fut))
         self._nq += 1
         self._kick()
-        if timeout is None:
-            await fut
-        else:
-            try:
+        try:
+            if timeout is None:
+                await fut
+            else:
                 await asyncio.wait_for(asyncio.shield(fut), timeout)
-            except asyncio.TimeoutError:
-                if fut.done() and not fut.cancelled():
-                    # released in the same tick as the timeout: the token is ours, return it
-                    self.give_back()
-                else:
-                    fut.cancel()
-                raise
+        except (asyncio.TimeoutError, asyncio.CancelledError):
+            # timed out, or the caller was cancelled (a log fetch on fence or shard loss): a
+            # token released to us in the same tick goes back, a queued wait is withdrawn —
+            # in shared mode a stranded token is the whole replica's budget
+            if fut.done() and not fut.cancelled():
+                self.give_back()
+            else:
+                fut.cancel()
+            raise
         d = self.clock() - t0
         self.waits += 1
         self.waited_s += d

@@ -155,6 +155,10 @@ class PipelineStage:
                     self._signal()  # woken, then cancelled: hand the wakeup on
                 raise
 
+    def busy(self) -> bool:
+        """Any decision queued, waiting out a backoff or being processed."""
+        return bool(self._pending or self._active or self._ready)
+
     def _check_idle(self):
         if self._idle is not None and not self._pending and not self._active and not self._ready:
             self._idle.set()

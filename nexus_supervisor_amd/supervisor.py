@@ -317,9 +317,51 @@ class Supervisor:
                 raise RuntimeError("failed to wait for pod informer caches to sync")
             self.log.info("resource informers synced")
             self.gc_tuner.after_sync()
+            if self.cfg.rules.running_sweep_rate > 0:
+                t = asyncio.ensure_future(self._running_sweep())
+                self._bg.add(t)
+                t.add_done_callback(self._bg.discard)
 
         await self.pipeline.start(post_start)
         self._sweeper = asyncio.create_task(self._sweep_parked(), name="stale-event-sweeper")
+
+    async def _running_sweep(self) -> None:
+        """After a restart, a run whose Started Event expired while the supervisor was down
+        (the API server keeps Events about an hour) and whose pod was already running at the
+        initial LIST would never be moved to RUNNING: the pod-status backup rule fires only
+        on a transition to Running.  Once, ``rules.running-sweep-delay`` after the caches
+        synced, every running Nexus pod of this replica with no Started Event in the Event
+        cache gets a ``ToRunning`` decision — at most ``running-sweep-rate`` a second and
+        only while no decision is queued, so a failure backlog is never held up.  A row
+        already RUNNING or finished costs a read (the conditional ToRunning writes nothing)."""
+        r = self.cfg.rules
+        await asyncio.sleep(r.running_sweep_delay)
+        started = set()
+        for ev in list(self.event_informer.indexer.values()):
+            if ev.get("reason") == "Started":
+                inv = ev.get("involvedObject") or {}
+                if inv.get("kind") == "Pod":
+                    started.add(inv.get("name", ""))
+        keys = [kube.object_key(p) for p in list(self.pod_informer.indexer.values())
+                if kube.name_of(p) not in started and (p.get("status") or {}).get("phase") == "Running"]
+        interval = 1.0 / r.running_sweep_rate
+        n = 0
+        for key in keys:
+            while self.pipeline.busy():
+                await asyncio.sleep(interval)
+            pod = self.pod_informer.indexer.get(key)
+            if pod is None or not self.active:
+                continue
+            res = self.classifier.running_result(pod)
+            if res is None:
+                continue
+            now = self.wall()
+            self._submit(res, now, now, "Pod")
+            n += 1
+            self.metrics.inc("running_sweep_decisions")
+            await asyncio.sleep(interval)
+        if n:
+            self.log.info("running sweep: runs without a Started Event re-checked", runs=n)
 
     async def stop(self, drain: bool = True, timeout: float = 10.0) -> None:
         self.gc_tuner.stop()

@@ -357,6 +357,26 @@ def test_bucket_wait_timeout_takes_no_token(arun):
     arun(go(), timeout=10)
 
 
+def test_cancelled_wait_strands_no_token(arun):
+    """a log fetch cancelled (fence, shard loss) while it waits with a timeout:
+    its queued wait is withdrawn, so the next token goes to the next waiter instead of to
+    nobody."""
+    async def go():
+        b = TokenBucket(10, 1)
+        assert b.try_accept()
+        t = asyncio.ensure_future(b.wait(0, timeout=5.0))
+        await asyncio.sleep(0.01)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        await asyncio.sleep(0)
+        assert b.queued == 0
+        d = await asyncio.wait_for(b.wait(0), 1.0)  # the token the cancelled wait would have had
+        assert d < 0.15
+
+    arun(go(), timeout=10)
+
+
 def test_give_back_refunds_try_accept():
     b = TokenBucket(1, 1)
     assert b.try_accept() and not b.try_accept()

@@ -228,3 +228,53 @@ def test_event_repeat_count_update_is_handled(arun):
     store2, _ = arun(_run(_cfg(**{"rules": {"handle-event-updates": False}}), [make_job(RID, cfg.labels)],
                           [("ADDED", ev), ("MODIFIED", ev2)]))
     assert store2.get(ALGORITHM, RID).lifecycle_stage == S.RUNNING  # reference behaviour: AddFunc only
+
+
+def test_running_sweep_after_restart_when_started_event_expired(arun):
+    """a pod already running at the initial LIST whose Started Event expired
+    while the supervisor was down (Event TTL) never produced ToRunning; the running sweep
+    decides it after the caches synced — but not runs whose Started Event is cached (the
+    replay decides those), pods being deleted, or pending pods."""
+    cfg = _cfg(**{"rules": {"running-sweep-rate": 50, "running-sweep-delay": "0s"}})
+    running = _status({"running": {"startedAt": "2026-01-01T00:00:00Z"}}, phase="Running")
+    expired = make_pod(BID, cfg.labels, status=running)                       # no Started Event left
+    rows = [BUFFERED_ROW] + [type(BUFFERED_ROW)(algorithm=ALGORITHM, id=f"sweep-{i}", lifecycle_stage="BUFFERED")
+                             for i in range(3)]
+    replayed = make_pod("sweep-0", cfg.labels, status=running)
+    deleting = make_pod("sweep-1", cfg.labels, status=running)
+    deleting["metadata"]["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+    pending = make_pod("sweep-2", cfg.labels, status={"phase": "Pending"})
+    started_ev = make_event("Pod", replayed["metadata"]["name"], "Started", "Started container algorithm")
+
+    async def go():
+        store = MemoryStore(rows)
+        c = InProcCluster(cfg, store, [expired, replayed, deleting, pending, started_ev])
+        await c.start()
+        for _ in range(100):
+            if store.get(ALGORITHM, BID).lifecycle_stage == S.RUNNING:
+                break
+            await asyncio.sleep(0.02)
+        await asyncio.sleep(0.2)
+        await c.stop()
+        return store, c
+
+    import asyncio
+
+    store, c = arun(go())
+    assert store.get(ALGORITHM, BID).lifecycle_stage == S.RUNNING          # the sweep
+    assert store.get(ALGORITHM, "sweep-0").lifecycle_stage == S.RUNNING    # the replayed Started Event
+    assert store.get(ALGORITHM, "sweep-1").lifecycle_stage == "BUFFERED"   # being deleted
+    assert store.get(ALGORITHM, "sweep-2").lifecycle_stage == "BUFFERED"   # not running
+    assert c.supervisor.metrics.counter("running_sweep_decisions") == 1
+    # off: the reference's behaviour (nothing moves the expired run)
+    cfg0 = _cfg(**{"rules": {"running-sweep-rate": 0}})
+    store0 = MemoryStore([BUFFERED_ROW])
+
+    async def go0():
+        c0 = InProcCluster(cfg0, store0, [make_pod(BID, cfg0.labels, status=running)])
+        await c0.start()
+        await asyncio.sleep(0.2)
+        await c0.stop()
+
+    arun(go0())
+    assert store0.get(ALGORITHM, BID).lifecycle_stage == "BUFFERED"
