@@ -144,6 +144,8 @@ class Tracker:
         # log-tail wait), queue (→ dequeue), actuate (→ checkpoint ack)
         self.parts: List[Tuple[float, ...]] = []
         self.pushed_at: List[Tuple[float, str]] = []  # (push time, run) of each entry of ``latencies``
+        self.part_of: Dict[str, Tuple[float, ...]] = {}  # run -> its entry of ``parts`` (by-kind report)
+        self.by_rid = False  # fill part_of (the latency probe only)
 
     def __call__(self, d: Decision):
         s = d.result.stamps
@@ -251,8 +253,11 @@ class StepState:
                     tr.pushed_at.append((self.t_push, rid))
                     if x is not None and len(x) >= 6:
                         hub, feed, dec, cls, que, r2c = x[:6]
-                        tr.parts.append((total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
-                                         (t - r2c - dec) * 1e3, cls * 1e3, que * 1e3, (r2c - cls - que) * 1e3))
+                        part = (total, (hub - self.t_push) * 1e3, (feed - hub) * 1e3, (dec - feed) * 1e3,
+                                (t - r2c - dec) * 1e3, cls * 1e3, que * 1e3, (r2c - cls - que) * 1e3)
+                        tr.parts.append(part)
+                        if tr.by_rid:
+                            tr.part_of[rid] = part
         if not self.waiting:
             self.done.set()
 
@@ -645,6 +650,7 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
             except asyncio.TimeoutError:
                 tracker.abandon(st)
         tracker.latencies, tracker.parts, tracker.start_latencies, tracker.pushed_at = [], [], [], []
+    tracker.by_rid, tracker.part_of = True, {}
     rate = cfg.probe_rate_per_min / 60.0
     rng = random.Random(0x5EED + cfg.seed + cfg.rank)
     loop = asyncio.get_running_loop()
@@ -718,8 +724,10 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
             for _, rid, _ in timed:
                 mix[kinds.get(rid, "?")] = mix.get(kinds.get(rid, "?"), 0) + 1
             out["kinds"] = mix
+            out["by_kind"] = _by_kind(timed, kinds, tracker.part_of)
         if timeline is not None:
             out["cpu_timeline"] = timeline.report(t0)
+    tracker.by_rid, tracker.part_of = False, {}
     if starts:  # the replacement runs' Started → RUNNING at the same rate
         out["starts"] = len(starts)
         out["start_p50_ms"] = round(q(0.5, starts), 3)
@@ -730,6 +738,27 @@ async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dic
 
 
 PART_NAMES = ("api", "hub", "feed", "dispatch", "classify", "queue", "actuate")
+
+
+def _by_kind(timed, kinds: Dict[str, str], part_of: Dict[str, Tuple[float, ...]]) -> Dict[str, Any]:
+    """Probe latency per failure kind: count, p50 / p99 / max, and the mean of each
+    delivery stage — does one kind (an hbm-oom's log-tail read, an eviction's Job settle)
+    carry the tail?"""
+    by: Dict[str, List[Tuple[float, str]]] = {}
+    for _t, rid, v in timed:
+        by.setdefault(kinds.get(rid, "?"), []).append((v, rid))
+    out: Dict[str, Any] = {}
+    for kind, vs in sorted(by.items()):
+        lat = sorted(v for v, _ in vs)
+        q = lambda p: lat[min(len(lat) - 1, int(round(p * (len(lat) - 1))))]  # noqa: E731
+        rec: Dict[str, Any] = {"n": len(lat), "p50_ms": round(q(0.5), 3), "p99_ms": round(q(0.99), 3),
+                               "max_ms": round(lat[-1], 3)}
+        parts = [part_of[rid] for _, rid in vs if rid in part_of]
+        if parts:
+            rec["stage_mean_ms"] = {name: round(sum(p[i + 1] for p in parts) / len(parts), 3)
+                                    for i, name in enumerate(PART_NAMES)}
+        out[kind] = rec
+    return out
 
 
 class _CpuTimeline:
