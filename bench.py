@@ -227,7 +227,6 @@ def main(argv=None) -> int:
             raise SystemExit("--gpu-evidence agent needs --transport wire")
         if args.cluster == "shared" and world > 1:
             raise SystemExit("--gpu-evidence agent: one agent per apiserver (per-rank cluster or node mode)")
-        args.hbm_shape = "termination-message"  # the agent's node-log reader has no /var/log/pods here
     # Node mode is ONE replica and ONE simulator for the whole node: the north-star namespace
     # (10k concurrent jobs, 6,000 failures a step) is split over the slots, so N slots measure
     # the same supervisor on the same total work — strong scaling.  Replica mode keeps the

@@ -46,6 +46,7 @@
 //               [--bookmark-ms 1000] [--token T] [--api-latency-us US] [--write-qps Q]
 //               [--write-burst B] [--throttle-deletes N] [--retry-after S]
 #include <arpa/inet.h>
+#include <dirent.h>
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <fcntl.h>
@@ -57,6 +58,7 @@
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/time.h>
 #include <sys/uio.h>
 #include <time.h>
@@ -171,6 +173,10 @@ struct Options {
   int64_t throttle_deletes = 0; // answer this many first Job DELETEs 429
   int retry_after_s = 1;        // Retry-After of every 429
   size_t prefault_mb = 0;       // heap pages touched at startup (kept: trim threshold 1 GiB)
+  // a kubelet's /var/log/pods: every bench LOG line (with the pod's uid) is also written as
+  // <root>/<ns>_<pod>_<uid>/<container>/<restart>.log in the CRI format, for a node agent
+  // process reading the node's logs (the deployed default-pod path); empty = off
+  std::string log_root;
 } g_opt;
 
 int64_t mono_ns() {
@@ -553,6 +559,79 @@ struct KindStore {
 
 KindStore g_store[NKINDS];
 std::unordered_map<std::string, std::set<std::string>> g_pods_by_job;  // ns \x01 job → pod names
+// A LOG line's text as the container runtime would have written it (--log-root): one CRI
+// record per line, "<RFC3339Nano> stderr F <text>", into the instance's file.  The
+// directory of a deleted pod is removed with it (the kubelet's log GC).
+bool plain_component(std::string_view s) {
+  return !s.empty() && s != "." && s != ".." && s.find('/') == std::string_view::npos;
+}
+
+std::string pod_log_dir(std::string_view ns, std::string_view pod, std::string_view uid) {
+  std::string d = g_opt.log_root;
+  d += '/';
+  d.append(ns);
+  d += '_';
+  d.append(pod);
+  d += '_';
+  d.append(uid);
+  return d;
+}
+
+void write_cri_log(std::string_view ns, std::string_view pod, std::string_view uid, std::string_view container,
+                   long restart, std::string_view text) {
+  if (!plain_component(ns) || !plain_component(pod) || !plain_component(uid) || !plain_component(container)) return;
+  std::string dir = pod_log_dir(ns, pod, uid);
+  mkdir(dir.c_str(), 0755);
+  dir += '/';
+  dir.append(container);
+  mkdir(dir.c_str(), 0755);
+  std::string path = dir + "/" + std::to_string(restart) + ".log";
+  std::string out;
+  size_t s = 0;
+  while (s < text.size()) {
+    size_t e = text.find('\n', s);
+    if (e == std::string_view::npos) e = text.size();
+    out += "2026-01-01T00:00:00.000000000Z stderr F ";
+    out.append(text.substr(s, e - s));
+    out += '\n';
+    s = e + 1;
+  }
+  int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+  if (fd < 0) return;
+  size_t off = 0;
+  while (off < out.size()) {
+    ssize_t w = write(fd, out.data() + off, out.size() - off);
+    if (w <= 0) break;
+    off += static_cast<size_t>(w);
+  }
+  close(fd);
+}
+
+// ns \x01 pod → pod uid of the log directories written (--log-root), for their removal
+std::unordered_map<std::string, std::string> g_log_dirs;
+
+void remove_pod_logs(std::string_view ns, std::string_view pod) {
+  auto it = g_log_dirs.find(std::string(ns) + '\x01' + std::string(pod));
+  if (it == g_log_dirs.end()) return;
+  std::string dir = pod_log_dir(ns, pod, it->second);
+  g_log_dirs.erase(it);
+  // <dir>/<container>/<n>.log: two levels
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* c = readdir(d)) {
+      if (!strcmp(c->d_name, ".") || !strcmp(c->d_name, "..")) continue;
+      std::string sub = dir + "/" + c->d_name;
+      if (DIR* f = opendir(sub.c_str())) {
+        while (dirent* x = readdir(f))
+          if (strcmp(x->d_name, ".") && strcmp(x->d_name, "..")) unlink((sub + "/" + x->d_name).c_str());
+        closedir(f);
+      }
+      rmdir(sub.c_str());
+    }
+    closedir(d);
+  }
+  rmdir(dir.c_str());
+}
+
 // ns \x01 pod → container → log text (bench LOG lines; pods/log answers from it)
 std::unordered_map<std::string, std::unordered_map<std::string, std::string>> g_pod_logs;
 // the store's resourceVersion counter: per-kind commit threads take from it concurrently
@@ -1268,6 +1347,7 @@ bool remove(int kind, std::string_view ns, std::string_view name, std::string_vi
   if (kind == K_POD) {
     index_pod(o, false);
     if (!g_pod_logs.empty()) g_pod_logs.erase(okey_scratch(o.ns, o.name));
+    if (!g_log_dirs.empty()) remove_pod_logs(o.ns, o.name);
   }
   if (o.rv_off != std::string::npos) {
     record(kind, "DELETED", o, ++g_rv);  // new resourceVersion spliced in on send
@@ -1894,6 +1974,11 @@ std::string apply_body(std::string_view b, bool expire, bool locked) {
     if (type == "LOG") {
       g_pod_logs[okey(obj->path({"namespace"}), obj->path({"pod"}))][std::string(obj->path({"container"}))] =
           std::string(obj->path({"text"}));
+      if (!g_opt.log_root.empty() && !obj->path({"uid"}).empty()) {
+        std::string_view ns = obj->path({"namespace"}), pod = obj->path({"pod"}), uid = obj->path({"uid"});
+        write_cri_log(ns, pod, uid, obj->path({"container"}), 0, obj->path({"text"}));
+        g_log_dirs[std::string(ns) + '\x01' + std::string(pod)] = std::string(uid);
+      }
       ++n;
       continue;
     }
@@ -2289,7 +2374,7 @@ void usage() {
   fprintf(stderr,
           "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n"
           "              [--flush-threads N] [--apply-threads N] [--api-latency-us US] [--write-qps Q] [--write-burst B]\n"
-          "              [--throttle-deletes N] [--retry-after S]\n");
+          "              [--throttle-deletes N] [--retry-after S] [--log-root DIR]\n");
 }
 
 }  // namespace
@@ -2318,6 +2403,7 @@ int main(int argc, char** argv) {
     else if (a == "--write-burst") g_opt.write_burst = atoi(next().c_str());
     else if (a == "--throttle-deletes") g_opt.throttle_deletes = atol(next().c_str());
     else if (a == "--retry-after") g_opt.retry_after_s = std::max(0, atoi(next().c_str()));
+    else if (a == "--log-root") g_opt.log_root = next();
     else {
       usage();
       return 2;

@@ -61,7 +61,8 @@ async def amain(args) -> None:
                       flush_threads=args.flush_threads, api_latency_us=args.api_latency_us,
                       write_qps=args.write_qps, write_burst=args.write_burst,
                       prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "768")),
-                      apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "6"))).start()
+                      apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "6")),
+                      log_root=args.log_root).start()
         simctl = SimControl(sim.url, sim.apply_url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)
@@ -347,6 +348,7 @@ def main(argv=None) -> int:
     ap.add_argument("--api-latency-us", type=int, default=0, help="simulated API answer latency (kubesim)")
     ap.add_argument("--write-qps", type=float, default=0.0, help="APF-like cap on mutating requests (kubesim)")
     ap.add_argument("--write-burst", type=int, default=0)
+    ap.add_argument("--log-root", default="", help="kubesim: write LOG lines as CRI files here (/var/log/pods)")
     ap.add_argument("--api", choices=("kubesim", "python"), default="kubesim",
                     help="native apiserver simulator (default) or the Python fake")
     args = ap.parse_args(argv)

@@ -433,7 +433,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
 
             agent = await AgentProcess(harness.api, cfg.workdir, f"mi355x-{cfg.rank // 8:03d}", namespace=sc.resource_namespace,
                                        backend="amdsmi" if cfg.telemetry == "amdsmi" else "fake",
-                                       kube_qps=sc.kube_qps, kube_burst=sc.kube_burst).start()
+                                       kube_qps=sc.kube_qps, kube_burst=sc.kube_burst,
+                                       log_root=getattr(harness, "log_root", "") or None).start()
             ev0 = {k: sup.metrics.counter(k) for k in _EVIDENCE_COUNTERS}
         else:
             sup.classifier.evidence_provider = pod_evidence_provider(telemetry)
@@ -587,7 +588,10 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                             "agent_util": cpu.get("agent_util"), "agent_cpu_us_per_event": cpu.get("agent_cpu_us_per_event"),
                             "deferred": deferred, "wait_expired": ev["gpu_evidence_wait_expired"],
                             "wait_expired_share": round(ev["gpu_evidence_wait_expired"] / deferred, 4) if deferred else None,
-                            "job_decisions_awaited": ev["decisions_awaited_gpu_evidence"]}
+                            "job_decisions_awaited": ev["decisions_awaited_gpu_evidence"],
+                            # default pods: the agent read their OOM text from the node's logs
+                            "agent_log_reads": int(sum(v for k, v in am.items() if k.endswith("agent_log_reads_total"))),
+                            "supervisor_log_fetches": int(sup.metrics.counter("decisions_deferred_for_log_tail"))}
         readback = await _read_back(harness, tracker)
         attribution = None
         if cfg.node and oom_phase is not None:

@@ -82,12 +82,19 @@ class WireHarness:
         self._log = open(os.path.join(self.workdir, "cluster.log"), "ab")
         # the apiserver's watch cache scales with the traffic it must hold (every shard's)
         history = 50_000 * (cfg.world if self.shared or self.node else 1)
+        # the node agent process reads default pods' HIP OOM text from a kubelet-style
+        # /var/log/pods the simulator writes (its LOG lines as CRI files)
+        self.log_root = ""
+        if cfg.gpu_evidence == "agent" and cfg.hbm_shape == "default-pod":
+            self.log_root = os.path.join(self.workdir, "var-log-pods")
+            os.makedirs(self.log_root, exist_ok=True)
         self.proc = subprocess.Popen([sys.executable, "-m", "nexus_supervisor_amd.bench.cluster_proc", "--cql",
                                       f"127.0.0.1:{self.cql.port}", "--ready-file", ready, "--history", str(history),
                                       # every rank's replica watches the shared namespace: fan out in parallel
                                       "--flush-threads", str(min(8, cfg.world) if self.shared else 3),
                                       "--api-latency-us", str(int(cfg.api_latency_us)),
-                                      "--write-qps", str(float(cfg.api_write_qps))],
+                                      "--write-qps", str(float(cfg.api_write_qps)),
+                                      "--log-root", self.log_root],
                                      env=env, stdout=self._log, stderr=self._log, start_new_session=True,
                                      preexec_fn=die_with_parent())
         deadline = time.monotonic() + 120

@@ -35,8 +35,11 @@ kind                watch traffic                                               
 host-oom            Pod MODIFIED terminated OOMKilled 137; Job MODIFIED Failed  FAILED
                     (PodFailurePolicy); Event (Job) PodFailurePolicy
 hbm-oom             Pod MODIFIED exit 1 + HIP OOM (termination message, or the  FAILED
-                    container log of a default pod); Job MODIFIED Failed
-                    (BackoffLimitExceeded); Event (Job) BackoffLimitExceeded
+                    container log of a default pod — LOG, written before the
+                    termination: pods/log, and with the simulator's --log-root a
+                    kubelet-style /var/log/pods the node agent reads); Job
+                    MODIFIED Failed (BackoffLimitExceeded); Event (Job)
+                    BackoffLimitExceeded
 image-pull          (a starting run) Event Scheduled, Pod bound, Event Pulling,  SCHEDULING_FAILED
                     Event Failed (ErrImagePull), Pod waiting ErrImagePull,
                     Event BackOff (pulling image), Pod waiting ImagePullBackOff
@@ -45,8 +48,9 @@ gpu-admission       (a starting run) Event Scheduled; Pod MODIFIED bound,       
                     failed … amd.com/gpu"), no containers; Event (Pod)
                     UnexpectedAdmissionError; Job MODIFIED Failed
                     (BackoffLimitExceeded); Event (Job) BackoffLimitExceeded
-pod-failure-policy  Pod MODIFIED exit 255; Event (Job) PodFailurePolicy; Job    FAILED
-                    MODIFIED Failed (PodFailurePolicy) — reference R-EVT path
+pod-failure-policy  Pod MODIFIED exit 255 (a default pod: its log holds a plain     FAILED
+                    traceback); Event (Job) PodFailurePolicy; Job MODIFIED Failed
+                    (PodFailurePolicy) — reference R-EVT path
 deadline            Event (Job) DeadlineExceeded; Job MODIFIED Failed           DEADLINE_EXCEEDED
                     (DeadlineExceeded); Event (Pod) Killing; Pod MODIFIED
                     (deletionTimestamp) — reference R-EVT path
@@ -362,11 +366,14 @@ class Workload:
             out.append(("ADDED", self._job_event(rid, "PodFailurePolicy", msg)))
         elif kind == "hbm-oom":
             default_pod = self.hbm_shape == "default-pod"
+            if default_pod:
+                # the container runtime has the process's stderr in the log before the kubelet
+                # reports the container terminated
+                out.append(("LOG", {"namespace": self.ns, "pod": pod_name, "container": "algorithm",
+                                    "uid": self.pods[rid]["metadata"]["uid"],
+                                    "text": f"epoch 3 step 1200 loss 0.412\n{self.hip_oom_message}\n"}))
             out.append(("MODIFIED", self._terminated(rid, {"terminated": {
                 "reason": "Error", "exitCode": 1, "message": "" if default_pod else self.hip_oom_message}})))
-            if default_pod:
-                out.append(("LOG", {"namespace": self.ns, "pod": pod_name, "container": "algorithm",
-                                    "text": f"epoch 3 step 1200 loss 0.412\n{self.hip_oom_message}\n"}))
             msg = "Job has reached the specified backoff limit"
             out.append(("MODIFIED", self._job_failed(rid, "BackoffLimitExceeded", msg)))
             out.append(("ADDED", self._job_event(rid, "BackoffLimitExceeded", msg)))
@@ -399,6 +406,12 @@ class Workload:
             out.append(("MODIFIED", self._job_failed(rid, "BackoffLimitExceeded", msg)))
             out.append(("ADDED", self._job_event(rid, "BackoffLimitExceeded", msg)))
         elif kind == "pod-failure-policy":
+            if self.hbm_shape == "default-pod":
+                # a default pod's log always exists: here a plain crash, nothing an OOM rule reads
+                out.append(("LOG", {"namespace": self.ns, "pod": pod_name, "container": "algorithm",
+                                    "uid": self.pods[rid]["metadata"]["uid"],
+                                    "text": "Traceback (most recent call last):\n  File \"train.py\", line 212, in <module>\n"
+                                            "RuntimeError: invalid dataset shard index\n"}))
             out.append(("MODIFIED", self._terminated(rid, {"terminated": {"reason": "Error", "exitCode": 255,
                                                                           "message": ""}})))
             msg = (f"Container algorithm for pod {self.ns}/{pod_name} failed with exit code 255 matching FailJob rule "

@@ -228,6 +228,9 @@ class NodeAgent:
         for r in recs:
             if r.get("denied"):
                 self._denied("log")
+            elif not r.get("error"):
+                # agent_log_reads{match}: container log tails read from the node's /var/log/pods
+                self.metrics.inc("agent_log_reads", labels={"match": r.get("match") or "none"})
         return recs
 
     # ------------------------------------------------------------ privileges

@@ -68,8 +68,9 @@ def test_bench_wire_in_process(tmp_path, capsys):
 @pytest.mark.slow
 def test_bench_gpu_evidence_through_the_node_agent(capsys):
     """``--gpu-evidence agent``: the node agent as its own process annotates every failed GPU
-    pod, the supervisor (no local telemetry) holds each decision for it; the line reports the
-    agent's cost and how many waits expired, and every row still reads back correct."""
+    pod (default pods: their logs read from a kubelet-style /var/log/pods the simulator
+    writes), the supervisor (no local telemetry) holds each decision for it; the line reports
+    the agent's cost and how many waits expired, and every row still reads back correct."""
     import bench
 
     rc = bench.main(["--steps", "2", "--warmup", "1", "--jobs", "300", "--events", "40", "--probe-events", "5",
@@ -80,7 +81,10 @@ def test_bench_gpu_evidence_through_the_node_agent(capsys):
     ev = out["config"]["gpu_evidence"]
     assert ev["via"] == "node-agent" and ev["deferred"] > 0 and ev["agent_annotations"] >= ev["deferred"] * 0.9, ev
     assert ev["wait_expired"] == 0 and ev["agent_util"] > 0, ev
-    assert out["config"]["hbm_oom_shape"] == "termination-message"
+    # default pods: the agent reads their OOM text from the simulator's /var/log/pods, the
+    # supervisor never has to fetch a tail over pods/log
+    assert out["config"]["hbm_oom_shape"] == "default-pod"
+    assert ev["agent_log_reads"] > 0 and ev["supervisor_log_fetches"] == 0, ev
 
 
 @pytest.mark.slow
