@@ -941,7 +941,8 @@ def _actuation(sc: SupervisorConfig) -> str:
     if fused_actuation(sc):
         return "fused conditional write"
     cu = sc.compat.conditional_update
-    return "read+write" + (" (ToRunning conditional)" if cu == "auto" else " (conditional)" if cu == "always" else "")
+    return "read+write" + (" (ToRunning: one conditional write)" if cu == "auto" else " (conditional)" if cu == "always"
+                           else "")
 
 
 STAGES = ("receive_to_checkpoint", "stage_classify", "stage_queue", "stage_read", "stage_prepare", "stage_write",

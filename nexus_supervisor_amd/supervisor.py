@@ -94,6 +94,14 @@ def failed_gpu(r: RunStatusAnalysisResult) -> Tuple[str, Optional[Any]]:
     return node, topo.get("expected_gpu")
 
 
+def running_fused_actuation(cfg: SupervisorConfig) -> bool:
+    """Is a ``ToRunning`` decision ONE conditional write (no read first)?  Whenever its write
+    is conditional anyway (``compat.conditional-update`` auto / always) and the write is the
+    owned-columns UPDATE (the full-row upsert needs the row read)."""
+    c = cfg.compat
+    return not c.full_row_upsert and c.conditional_update != "never"
+
+
 def fused_actuation(cfg: SupervisorConfig) -> bool:
     """Is a decision ONE conditional write (``compat.fused-write``)?  ``auto``: only when
     a deposed owner may still hold decisions — leader election or shard leases — where
@@ -211,6 +219,11 @@ class Supervisor:
         # one conditional write per decision instead of read + write (compat.fused-write);
         # conditional-update: never (the reference's unconditional writes) turns it off
         self._fused = fused_actuation(cfg)
+        # ToRunning is a conditional write whenever conditional-update is not "never": its
+        # not-applied answer already says "no row" / "finished" / "already RUNNING", so the
+        # reference's read before it (supervisor.go:264) is one round trip that decides
+        # nothing — the one-call path serves it even when failures take the read + write
+        self._fused_running = self._fused or (running_fused_actuation(cfg))
         self._guards: Dict[Any, Any] = {}
         self._parked: Dict[Tuple[str, str], List[Tuple[float, Dict[str, Any], float]]] = {}
         self._gpu_wait: Dict[str, float] = {}  # pod key -> deadline (waiting for node-agent GPU evidence)
@@ -1004,7 +1017,7 @@ class Supervisor:
             if self._log_fetches and r.object_kind == "Job":
                 await self._await_pod_logs(r)
             self.classifier.finish(r, self.lookup)
-        if self._fused:
+        if self._fused or (self._fused_running and not failing):
             d = await self._fused_action(r, epoch, failing)
             if d is not None:
                 return d

@@ -57,11 +57,15 @@ def test_bench_wire_in_process(tmp_path, capsys):
     _check(out, 1, 2, 1, 60)
     cfg = out["config"]
     assert cfg["transport"] == "wire" and cfg["store"].startswith("cql")
-    assert cfg["actuation"] == "read+write (ToRunning conditional)"  # one replica, no HA: no LWT per decision
+    # one replica, no HA: failures read then write plainly; a ToRunning is one conditional write
+    assert cfg["actuation"] == "read+write (ToRunning: one conditional write)"
     st = cfg["stages_ms"]
     assert st["receive_to_checkpoint"]["count"] >= 120
-    for k in ("stage_classify", "stage_queue", "stage_read", "stage_write"):
+    for k in ("stage_classify", "stage_queue", "stage_write"):
         assert st[k]["count"] == st["receive_to_checkpoint"]["count"]
+    # the reads are the failures' only: no ToRunning reads its row first
+    assert 0 < st["stage_read"]["count"] < st["receive_to_checkpoint"]["count"]
+    assert st["stage_read"]["count"] + st["stage_prepare"]["count"] == st["receive_to_checkpoint"]["count"]
     assert out["latency_at_rate"]["events"] == 3
 
 
