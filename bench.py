@@ -94,6 +94,9 @@ def parse_args(argv=None):
     ap.add_argument("--diag-probe-timeline", action="store_true",
                     help="diagnostic: every second of the probe, each bench process's CPU, the host's busy CPUs and the "
                          "cgroup's CFS throttling (latency_at_rate.cpu_timeline)")
+    ap.add_argument("--diag-step-timeline", action="store_true",
+                    help="diagnostic: each bench process's CPU every 0.2 s of the timed steps, and which one was "
+                         "closest to a full core in their steady part (config.step_timeline)")
     ap.add_argument("--diag-slow-callback-ms", type=float, default=0.0,
                     help="diagnostic: count the event-loop callbacks (parent and workers) that run at least this "
                          "long and list the probe's in latency_at_rate.slow_callbacks (obs/loopwatch.py)")
@@ -307,7 +310,8 @@ def main(argv=None) -> int:
                       probe_rate_per_min=args.probe_rate, procs=args.procs if args.transport == "wire" else 1,
                       pregen=not args.no_pregen, cluster=cluster, run_starts=args.workload == "lifecycle",
                       pprof_out=args.pprof_out if rank == 0 else "", pprof_hz=args.pprof_hz, slot_mode=slot_mode,
-                      gpu_evidence=args.gpu_evidence, probe_timeline=args.diag_probe_timeline)
+                      gpu_evidence=args.gpu_evidence, probe_timeline=args.diag_probe_timeline,
+                      step_timeline=args.diag_step_timeline)
     res = asyncio.run(run_rank(cfg, barrier_sync, share, oom_phase if slot_mode == "node" and world > 1 else None))
 
     elapsed = res["elapsed"]
@@ -456,6 +460,7 @@ def main(argv=None) -> int:
                 "stages_ms": res.get("stages"),
                 "cpu_util_rank0": res.get("cpu"),
                 "step_done_ms_rank0": res.get("step_done_ms"),
+                **({"step_timeline": res["step_timeline"]} if res.get("step_timeline") else {}),
                 "baseline": "reference derived ceiling 10 decisions/s (Helm defaults; BASELINE.md)",
             },
         }

@@ -29,6 +29,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <memory_resource>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -1067,11 +1068,140 @@ struct PodOwner {
   bool labeled;
 };
 
+// Deleted pods are remembered (for Pod Events still in flight) in two generations, each
+// a hash map living in a bump arena: a generation is dropped by handing its arena's blocks
+// back to a shared pool — never by erasing its entries one by one.  Erasing them (a budget
+// per pod line, before) touched every cold entry once more: a saturated phase deletes ~20k
+// pods a second, and 30 s later the hub's pump spent ~1 ms per chunk for seconds erasing
+// them (the open-loop probe's recurring tail window, profiles/r6/README.md).  Blocks are
+// kept for the next generation (up to POOL_KEEP bytes), so a rotation makes no syscall.
+constexpr size_t ARENA_BLOCK = 1 << 20;
+constexpr size_t POOL_KEEP = size_t(96) << 20;
+
+struct BlockPool {
+  std::vector<char*> blocks;                    // free ARENA_BLOCK blocks
+  std::vector<std::pair<char*, size_t>> large;  // free oversized blocks (hash bucket arrays)
+  size_t kept = 0;
+  char* take(size_t n, size_t& got) {
+    if (n <= ARENA_BLOCK) {
+      got = ARENA_BLOCK;
+      if (!blocks.empty()) {
+        char* b = blocks.back();
+        blocks.pop_back();
+        kept -= ARENA_BLOCK;
+        return b;
+      }
+      return static_cast<char*>(::operator new(ARENA_BLOCK));
+    }
+    for (size_t i = 0; i < large.size(); ++i)
+      if (large[i].second >= n) {
+        auto b = large[i];
+        large[i] = large.back();
+        large.pop_back();
+        kept -= b.second;
+        got = b.second;
+        return b.first;
+      }
+    got = n;
+    return static_cast<char*>(::operator new(n));
+  }
+  void give(char* b, size_t n) {
+    if (kept + n > POOL_KEEP) {
+      ::operator delete(b);
+      return;
+    }
+    kept += n;
+    if (n == ARENA_BLOCK) blocks.push_back(b);
+    else large.emplace_back(b, n);
+  }
+  ~BlockPool() {
+    for (char* b : blocks) ::operator delete(b);
+    for (auto& b : large) ::operator delete(b.first);
+  }
+};
+
+class GenArena : public std::pmr::memory_resource {
+ public:
+  explicit GenArena(BlockPool* pool) : pool_(pool) {}
+  ~GenArena() override { reset(); }
+  // hand every block back to the pool: the objects in them are simply forgotten (their
+  // types own nothing outside this arena)
+  void reset() {
+    for (auto& b : used_) pool_->give(b.first, b.second);
+    used_.clear();
+    cur_ = end_ = nullptr;
+  }
+
+ private:
+  static char* align_up(char* p, size_t align) {
+    return reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(p) + align - 1) & ~(uintptr_t(align) - 1));
+  }
+  void* do_allocate(size_t n, size_t align) override {
+    size_t got = 0;
+    if (n + align > ARENA_BLOCK / 4) {  // a big object (a bucket array) gets a block of its own
+      char* b = pool_->take(n + align, got);
+      used_.emplace_back(b, got);
+      return align_up(b, align);
+    }
+    char* p = cur_ ? align_up(cur_, align) : nullptr;
+    if (p == nullptr || p + n > end_) {
+      char* b = pool_->take(ARENA_BLOCK, got);
+      used_.emplace_back(b, got);
+      cur_ = b;
+      end_ = b + got;
+      p = align_up(cur_, align);
+    }
+    cur_ = p + n;
+    return p;
+  }
+  void do_deallocate(void*, size_t, size_t) override {}  // freed wholesale by reset()
+  bool do_is_equal(const std::pmr::memory_resource& o) const noexcept override { return this == &o; }
+
+  BlockPool* pool_;
+  std::vector<std::pair<char*, size_t>> used_;
+  char* cur_ = nullptr;
+  char* end_ = nullptr;
+};
+
+struct GoneGen {
+  using Map = std::pmr::unordered_map<std::string_view, PodOwner>;
+  GenArena arena;
+  Map* map = nullptr;  // constructed in the arena, never destructed: dropped with it
+  explicit GoneGen(BlockPool* pool) : arena(pool) { fresh(); }
+  void fresh() {
+    arena.reset();
+    map = new (arena.allocate(sizeof(Map), alignof(Map))) Map(&arena);
+  }
+  const PodOwner* find(std::string_view k) const;
+  void put(std::string_view k, const PodOwner& po);
+  size_t size() const { return map->size(); }
+};
+
 struct Owners {
-  std::unordered_map<std::string, PodOwner> pod;
-  std::deque<std::pair<double, std::string>> gone;
+  std::unordered_map<std::string, PodOwner> pod;  // pods not deleted (yet)
+  BlockPool pool;                                 // outlives the generations below
+  std::unique_ptr<GoneGen> gone_cur = std::make_unique<GoneGen>(&pool);
+  std::unique_ptr<GoneGen> gone_prev = std::make_unique<GoneGen>(&pool);
+  double rotate_at = 0.0;
   std::string tmp;  // lookup key buffer
 };
+
+const PodOwner* GoneGen::find(std::string_view k) const {
+  auto it = map->find(k);
+  return it == map->end() ? nullptr : &it->second;
+}
+
+void GoneGen::put(std::string_view k, const PodOwner& po) {
+  auto it = map->find(k);
+  if (it != map->end()) {
+    it->second = po;
+    return;
+  }
+  char* c = static_cast<char*>(arena.allocate(k.size() ? k.size() : 1, 1));
+  std::memcpy(c, k.data(), k.size());
+  map->emplace(std::string_view(c, k.size()), po);
+}
+
 
 typedef struct {
   PyObject_HEAD
@@ -1122,20 +1252,26 @@ bool replica_owns_hash(const Router* r, uint32_t h) {
   return (*r->owned)[h % static_cast<uint32_t>(r->rcount)] != 0;
 }
 
-// At most `budget` entries per call: a saturated phase deletes ~20k pods a second, and
-// erasing all of them in the first call after their forget time held the hub's loop for
-// 1-5 ms per chunk for seconds (the open-loop probe's p99).  Spread over calls instead.
-constexpr size_t EXPIRE_BUDGET = 128;
-
-void expire_owners(Router* r) {
-  auto& g = r->owners->gone;
-  if (g.empty()) return;
+// A deleted pod leaves the live map (its entry was just touched: a cheap erase) for the
+// current generation; generations rotate every forget_after seconds, so a deleted pod is
+// remembered for forget_after to twice that.
+void note_deleted(Router* r, const std::string& name, const PodOwner& po) {
+  Owners& ow = *r->owners;
   double now = mono_s();
-  size_t budget = EXPIRE_BUDGET;
-  while (budget-- > 0 && !g.empty() && g.front().first <= now) {
-    r->owners->pod.erase(g.front().second);
-    g.pop_front();
+  if (now >= ow.rotate_at) {
+    ow.gone_prev->fresh();
+    std::swap(ow.gone_prev, ow.gone_cur);
+    ow.rotate_at = now + r->forget_after;
   }
+  ow.pod.erase(name);
+  ow.gone_cur->put(name, po);
+}
+
+const PodOwner* find_pod(const Owners& ow, const std::string& name) {
+  auto it = ow.pod.find(name);
+  if (it != ow.pod.end()) return &it->second;
+  if (const PodOwner* g = ow.gone_cur->find(name)) return g;
+  return ow.gone_prev->find(name);
 }
 
 // Owner worker of one object: a watch line ({"type", "object"} envelope) or a bare LIST
@@ -1168,11 +1304,13 @@ int route_info(Router* r, int role, const Scan::Info& in, bool envelope) {
     if (in.has_job) po = PodOwner{owner_of(r, in.job), replica_hash(r, in.job), true};
     Owners& ow = *r->owners;
     ow.tmp.assign(in.name.data(), in.name.size());  // reused buffer: no allocation for a known pod
-    auto it = ow.pod.find(ow.tmp);
-    if (it == ow.pod.end()) ow.pod.emplace(ow.tmp, po);
-    else it->second = po;
-    if (envelope && in.has_type && in.type == "DELETED") ow.gone.emplace_back(mono_s() + r->forget_after, ow.tmp);
-    expire_owners(r);
+    if (envelope && in.has_type && in.type == "DELETED") {
+      note_deleted(r, ow.tmp, po);
+    } else {
+      auto it = ow.pod.find(ow.tmp);
+      if (it == ow.pod.end()) ow.pod.emplace(ow.tmp, po);
+      else it->second = po;
+    }
     return pod_owner_now(r, po);
   }
   if (role == ROLE_EVENT) {
@@ -1185,9 +1323,9 @@ int route_info(Router* r, int role, const Scan::Info& in, bool envelope) {
     if (in.ikind == "Pod") {
       Owners& ow = *r->owners;
       ow.tmp.assign(in.iname.data(), in.iname.size());
-      auto it = ow.pod.find(ow.tmp);
+      const PodOwner* po = find_pod(ow, ow.tmp);
       // unknown pod: everyone parks it until the pod shows up
-      return it == ow.pod.end() ? OWNER_ALL : pod_owner_now(r, it->second);
+      return po == nullptr ? OWNER_ALL : pod_owner_now(r, *po);
     }
     return 0;
   }
@@ -1266,9 +1404,9 @@ PyObject* Router_pod_owner(Router* self, PyObject* arg) {
   Py_ssize_t n;
   const char* s = PyUnicode_AsUTF8AndSize(arg, &n);
   if (!s) return nullptr;
-  auto it = self->owners->pod.find(std::string(s, static_cast<size_t>(n)));
-  if (it == self->owners->pod.end()) Py_RETURN_NONE;
-  return PyLong_FromLong(pod_owner_now(self, it->second));
+  const PodOwner* po = find_pod(*self->owners, std::string(s, static_cast<size_t>(n)));
+  if (po == nullptr) Py_RETURN_NONE;
+  return PyLong_FromLong(pod_owner_now(self, *po));
 }
 
 // note_pod(name, owner[, deleted[, job]]) — job: the pod's run (job name) for replica sharding
@@ -1281,9 +1419,8 @@ PyObject* Router_note_pod(Router* self, PyObject* args) {
   if (!PyArg_ParseTuple(args, "si|pz#", &name, &owner, &deleted, &job, &job_n)) return nullptr;
   PodOwner po{owner, 0, false};
   if (job) po = PodOwner{owner, replica_hash(self, std::string_view(job, static_cast<size_t>(job_n))), true};
-  self->owners->pod[name] = po;
-  if (deleted) self->owners->gone.emplace_back(mono_s() + self->forget_after, name);
-  expire_owners(self);
+  if (deleted) note_deleted(self, name, po);
+  else self->owners->pod[name] = po;
   Py_RETURN_NONE;
 }
 
@@ -1341,8 +1478,11 @@ PyObject* Router_set_event_reasons(Router* self, PyObject* arg) {
 }
 
 PyObject* Router_stats(Router* self, void*) {
-  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:n}", "passed", self->passed, "dropped", self->dropped, "foreign",
-                       self->foreign, "unread", self->unread, "pods", static_cast<Py_ssize_t>(self->owners->pod.size()));
+  const Owners& ow = *self->owners;
+  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:n,s:n,s:n}", "passed", self->passed, "dropped", self->dropped, "foreign",
+                       self->foreign, "unread", self->unread, "pods", static_cast<Py_ssize_t>(ow.pod.size()),
+                       "gone", static_cast<Py_ssize_t>(ow.gone_cur->size() + ow.gone_prev->size()), "pool_bytes",
+                       static_cast<Py_ssize_t>(ow.pool.kept));
 }
 
 PyMethodDef Router_methods[] = {

@@ -52,10 +52,12 @@ def _cxx() -> str:
     return os.environ.get("CXX", "g++")
 
 
-def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
+def targets(sanitize: Optional[str] = None, out_root: Optional[str] = None) -> Dict[str, Dict]:
     """Every native artefact.  With ``sanitize`` the in-process extensions are built into
     ``SAN_DIR/<sanitizer>/`` (loaded in a subprocess through ``NEXUS_NATIVE_DIR``) and the
-    executables get a ``-<sanitizer>`` suffix."""
+    executables get a ``-<sanitizer>`` suffix.  ``out_root``: extensions and executables
+    all go there instead (a from-source rebuild beside the in-tree artefacts, loaded the
+    same way — ``tests/test_gpu_box.py`` rebuilds on the GPU box itself)."""
     common = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter", "-fvisibility=hidden"]
     san = []
     if sanitize:
@@ -66,7 +68,8 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
     amd = os.path.join(CSRC, "amdsmi")
     mon_deps = [os.path.join(amd, "monitor_core.hpp"), os.path.join(amd, "procscan.hpp"),
                 os.path.join(amd, "stderr_filter.hpp")]
-    ext_dir = os.path.join(SAN_DIR, sanitize) if sanitize else PKG
+    ext_dir = out_root or (os.path.join(SAN_DIR, sanitize) if sanitize else PKG)
+    bin_dir = out_root or BIN
     sfx = f"-{sanitize}" if sanitize else ""
     return {
         "cql_native": {
@@ -116,7 +119,7 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
             "inproc": True,
         },
         "monitor_selftest": {
-            "out": os.path.join(BIN, "monitor_selftest" + sfx),
+            "out": os.path.join(bin_dir, "monitor_selftest" + sfx),
             "srcs": [os.path.join(amd, "monitor_selftest.cpp"), os.path.join(amd, "amdsmi_stub.cpp")],
             "deps": mon_deps,
             "cmd": lambda out, srcs: [_cxx(), *common, *san, f"-I{ROCM}/include", *srcs, "-pthread", "-o", out],
@@ -124,21 +127,21 @@ def targets(sanitize: Optional[str] = None) -> Dict[str, Dict]:
             "exe": True,
         },
         "cqlsrv": {
-            "out": os.path.join(BIN, "nexus-cqlsrv" + sfx),
+            "out": os.path.join(bin_dir, "nexus-cqlsrv" + sfx),
             "srcs": [os.path.join(CSRC, "cqlsrv", "cqlsrv.cpp")],
             "deps": [proto],
             "cmd": lambda out, srcs: [_cxx(), *common, *san, "-pthread", f"-I{os.path.join(CSRC, 'cql')}", *srcs, "-o", out],
             "exe": True,
         },
         "kubesim": {
-            "out": os.path.join(BIN, "nexus-kubesim" + sfx),
+            "out": os.path.join(bin_dir, "nexus-kubesim" + sfx),
             "srcs": [os.path.join(CSRC, "kubesim", "kubesim.cpp")],
             "deps": [os.path.join(CSRC, "kubesim", "json.hpp")],
             "cmd": lambda out, srcs: [_cxx(), *common, "-O3", *san, "-pthread", *srcs, "-o", out],
             "exe": True,
         },
         "gpu_stress": {
-            "out": os.path.join(BIN, "gpu_stress"),
+            "out": os.path.join(bin_dir, "gpu_stress"),
             "srcs": [os.path.join(CSRC, "stress", "gpu_stress.hip")],
             "deps": [],
             "cmd": lambda out, srcs: [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17",
@@ -244,15 +247,16 @@ def build_compiled(force: bool = False, verbose: bool = False) -> str:
     return f"compiled: {len(done)} built, {len(compiled.MODULES) - len(done)} up to date"
 
 
-def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optional[str] = None, verbose: bool = False) -> List[str]:
-    ts = targets(sanitize)
+def build(force: bool = False, only: Optional[List[str]] = None, sanitize: Optional[str] = None, verbose: bool = False,
+          out_root: Optional[str] = None) -> List[str]:
+    ts = targets(sanitize, out_root)
     names = [n for n in ts if not only or n in only]
     if sanitize:
         names = [n for n in names if ts[n].get("exe") or ts[n].get("inproc")]
     with cf.ThreadPoolExecutor(max_workers=min(4, len(names) or 1)) as ex:
         futs = {ex.submit(build_one, n, ts[n], force, verbose): n for n in names}
         out = [f.result() for f in cf.as_completed(futs)]
-    if not sanitize and (not only or "compiled" in only):
+    if not sanitize and not out_root and (not only or "compiled" in only):
         out.append(build_compiled(force, verbose))
     return out
 

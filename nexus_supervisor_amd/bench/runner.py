@@ -50,6 +50,7 @@ class BenchConfig:
     probe_events: int = 600
     probe_rate_per_min: float = 1000.0
     probe_timeline: bool = False  # diagnostic: CPU of every process (and the host) per second of the probe
+    step_timeline: bool = False  # diagnostic: the same over the timed steps, and which process paced them
     procs: int = 1  # supervisor shard-worker processes (runtime.worker-processes)
     pregen: bool = True  # cluster pre-generates the synthetic steps' traffic before the timed region
     cluster: str = "per-rank"  # per-rank | shared (one apiserver + one CQL server for all ranks)
@@ -489,11 +490,23 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         x0 = harness.external_cpu()
         sim_stats = getattr(harness, "sim_stats", None)
         s0 = await sim_stats() if sim_stats is not None else None
+        step_tl = (_CpuTimeline(harness, interval=0.2)
+                   if cfg.step_timeline and hasattr(harness, "external_cpu") else None)
+        if step_tl is not None:
+            step_tl.start()
         await run_steps(cfg.steps)
+        if step_tl is not None:
+            await step_tl.stop()
         barrier_sync()
         elapsed = time.perf_counter() - t0
         timed = (tracker.failures, tracker.starts, list(tracker.start_latencies))
         step_done_ms = [round(1000.0 * (t - t0), 1) for t in done_at]
+        step_timeline = None
+        if step_tl is not None:
+            # t0 of the rows: the timed region's start on the monotonic clock
+            mono0 = time.monotonic() - (time.perf_counter() - t0)
+            rows = step_tl.report(mono0)
+            step_timeline = {"rows": rows, "steady": steady_util(rows, step_done_ms)}
         cpu = {"supervisor_util": round((time.process_time() - c0) / elapsed, 3),
                "supervisor_max_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1)}
         x1 = harness.external_cpu()
@@ -629,7 +642,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
             "actuation": _actuation(sc),
             "eps": sc.rate_limit_elements_per_second, "kube_qps": sc.kube_qps, "telemetry": telemetry.name, "stages": stages, "cpu": cpu,
             "probe": probe, "step_done_ms": step_done_ms, "monitor": monitor, "attribution": attribution,
-            "gpu_evidence": gpu_evidence}
+            "gpu_evidence": gpu_evidence, "step_timeline": step_timeline}
 
 
 async def _latency_probe(harness, tracker: "Tracker", cfg: "BenchConfig") -> Dict[str, Any]:
@@ -762,6 +775,36 @@ def _by_kind(timed, kinds: Dict[str, str], part_of: Dict[str, Tuple[float, ...]]
             rec["stage_mean_ms"] = {name: round(sum(p[i + 1] for p in parts) / len(parts), 3)
                                     for i, name in enumerate(PART_NAMES)}
         out[kind] = rec
+    return out
+
+
+_PACING_KEYS = ("parent", "cluster", "cqlsrv", "kubesim")
+
+
+def steady_util(rows: List[Dict[str, Any]], step_done_ms: List[float]) -> Dict[str, Any]:
+    """Each process's CPU (cores) over the *steady* part of the timed steps — from the
+    second step's completion to the second-to-last's, when every in-flight slot is full —
+    as its median and 90th percentile over the timeline's intervals, and the process closest
+    to a full core there (``pacing``: the stage the line waits on; the simulator's figure
+    is its whole CPU, threads included, its serial loop is ``kubesim_loop_util``)."""
+    if len(step_done_ms) >= 4:
+        lo, hi = step_done_ms[1] / 1000.0, step_done_ms[-2] / 1000.0
+    else:
+        lo, hi = float("-inf"), float("inf")
+    sel = [r for r in rows if lo <= r["t"] <= hi] or rows
+    if not sel:
+        return {}
+    keys = [k for k in sel[0] if k.startswith("worker") or k in _PACING_KEYS]
+    out: Dict[str, Any] = {"window_s": [round(lo, 2), round(hi, 2)] if lo != float("-inf") else None,
+                           "intervals": len(sel), "median": {}, "p90": {}}
+    for k in keys:
+        v = sorted(r.get(k, 0.0) for r in sel)
+        out["median"][k] = v[len(v) // 2]
+        out["p90"][k] = v[min(len(v) - 1, int(0.9 * len(v)))]
+    single = {k: v for k, v in out["median"].items() if k != "kubesim"}  # one-thread processes
+    if single:
+        top = max(single, key=single.get)
+        out["pacing"] = {"process": top, "median_util": single[top]}
     return out
 
 

@@ -180,9 +180,11 @@ class PipelineStage:
             if delay > 0:
                 await asyncio.sleep(delay)
             gate = self.gate
+            gated = False
             try:
                 if gate is not None and not gate.is_closed():
                     await gate.wait()
+                    gated = True
                 out = await self.processor(entry.item)
             except asyncio.CancelledError:
                 self._running.discard(key)
@@ -190,6 +192,13 @@ class PipelineStage:
             except BaseException as exc:  # noqa: BLE001 - every failure is retried / dead-lettered
                 self._running.discard(key)
                 self.stats.failed_attempts += 1
+                if gated and getattr(gate, "state", None) == "open":
+                    # a probe through the open gate failed and the gate is shut again: that is
+                    # the store's verdict, not this item's — it keeps its retry budget and
+                    # waits at the gate again (which item probes is the scheduler's choice)
+                    self.stats.retries += 1
+                    self._schedule_retry(key, 0.0)
+                    continue
                 nfail = self.backoff.failures(key) + 1
                 if self.max_retries and nfail > self.max_retries:
                     self.stats.dead_lettered += 1

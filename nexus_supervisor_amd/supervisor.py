@@ -94,6 +94,12 @@ def failed_gpu(r: RunStatusAnalysisResult) -> Tuple[str, Optional[Any]]:
     return node, topo.get("expected_gpu")
 
 
+def _consume_exception(fut: asyncio.Future) -> None:
+    """A prefetched read that failed or was dropped: the decision reads on its own."""
+    if not fut.cancelled():
+        fut.exception()
+
+
 def running_fused_actuation(cfg: SupervisorConfig) -> bool:
     """Is a ``ToRunning`` decision ONE conditional write (no read first)?  Whenever its write
     is conditional anyway (``compat.conditional-update`` auto / always) and the write is the
@@ -230,6 +236,11 @@ class Supervisor:
         # pod key -> a Job decision waiting for that pod's GPU evidence wait to end
         self._gpu_waiters: Dict[str, asyncio.Future] = {}
         self._log_fetches: Dict[str, asyncio.Future] = {}  # pod key -> in-flight pods/log tail fetch
+        # run -> checkpoint stage read started while its deferred GPU failure waits (for its
+        # log tail or the node agent's evidence): the decision that follows takes it instead
+        # of a round trip of its own (two-step owned-columns actuation only)
+        self._prefetch: "OrderedDict[Tuple[str, str], asyncio.Future]" = OrderedDict()
+        self._prefetch_reads = not self._fused and not cfg.compat.full_row_upsert
         self._settle: Dict[str, asyncio.Future] = {}  # job name -> a Job decision waiting for its pod's failure
         # shards whose cached pods may be stale while the Pod informer re-lists (set when the list is in)
         self._pod_relist: Optional[Tuple[asyncio.Event, frozenset]] = None
@@ -429,6 +440,7 @@ class Supervisor:
             self._gpu_wait_over(key)
         self._parked.clear()
         self._applied.clear()
+        self._drop_prefetch(lambda rid: True)
         self.metrics.inc("fenced_decisions_dropped", dropped)
         self.metrics.inc("fencings")
         self.log.info("leadership lost: fenced in-flight work", dropped=dropped, epoch=self.epoch)
@@ -566,6 +578,7 @@ class Supervisor:
                 self._deletes.pop(t, None)
         for key in [k for k in self._applied if of(k[1]) in lost]:
             del self._applied[key]
+        self._drop_prefetch(lambda rid: of(rid) in lost)
         self._purge(lambda rid: of(rid) in lost)
         self.metrics.inc("fenced_decisions_dropped", dropped)
         self.metrics.inc("shards_lost", len(lost))
@@ -705,6 +718,8 @@ class Supervisor:
             if key not in self._gpu_wait:
                 self._gpu_wait[key] = time.monotonic() + wait
                 self.metrics.inc("decisions_deferred_for_gpu_evidence")
+                if self._prefetch_reads:
+                    self._prefetch_read(pod)
             return
         if self._gpu_wait.pop(key, None) is not None and self._gpu_waiters:
             self._gpu_wait_over(key)
@@ -723,6 +738,31 @@ class Supervisor:
         self.metrics.inc("decisions_deferred_for_log_tail")
         t = asyncio.ensure_future(self._fetch_log_tail(key, pod, want, waited))
         self._log_fetches[key] = t
+        if self._prefetch_reads:
+            self._prefetch_read(pod)
+
+    def _prefetch_read(self, pod: Dict[str, Any]) -> None:
+        """Start the checkpoint stage read of a deferred GPU failure's run now, overlapped
+        with the wait (the log tail's GET, the agent's annotation).  Only the finished /
+        missing checks read it: a decision of this process that wrote the row since is
+        caught by ``_applied`` before the read is taken, as with a read of its own."""
+        labels = kube.labels_of(pod)
+        rid = labels.get(self._job_label)
+        if not rid:
+            return
+        key = (labels.get(self.cfg.labels.job_template_name_key, ""), rid)
+        if key in self._prefetch or key in self._applied:
+            return
+        if len(self._prefetch) >= 4096:  # deferrals that never became a decision
+            self._prefetch.popitem(last=False)[1].cancel()
+        fut = asyncio.ensure_future(self.store.read_status(*key))
+        fut.add_done_callback(_consume_exception)
+        self._prefetch[key] = fut
+        self.metrics.inc("checkpoint_reads_prefetched")
+
+    def _drop_prefetch(self, lost: Callable[[str], bool]) -> None:
+        for key in [k for k in self._prefetch if lost(k[1])]:
+            self._prefetch.pop(key).cancel()
 
     async def _fetch_log_tail(self, key: str, pod: Dict[str, Any], want: List[Dict[str, Any]], waited: bool) -> None:
         from .gpu.logtail import fetch_api_tail
@@ -1024,8 +1064,13 @@ class Supervisor:
         try:
             # the owned-columns write needs only the stage; the full-row upsert (reference
             # UpsertCheckpoint of the deep copy) needs every column
-            read = self.store.read_checkpoint if compat.full_row_upsert else self.store.read_status
-            cp = await read(r.algorithm, r.request_id)
+            pre = self._prefetch.pop((r.algorithm, r.request_id), None) if self._prefetch else None
+            if pre is not None and not pre.cancelled() and (not pre.done() or pre.exception() is None):
+                cp = await pre  # started while the failure waited for its log tail / evidence
+                self.metrics.inc("checkpoint_reads_prefetch_used")
+            else:
+                read = self.store.read_checkpoint if compat.full_row_upsert else self.store.read_status
+                cp = await read(r.algorithm, r.request_id)
             r.answered = r.attempts
         except Exception as exc:
             self.log.error(exc, "no checkpoint exists for the provided request, job will be deleted without metadata saved",
@@ -1253,6 +1298,8 @@ class Supervisor:
             raise
         key = (r.algorithm, rid)
         if not applied:
+            if current is not None:
+                self.metrics.inc("conditional_write_rejected")
             if current is None:
                 return await self._skip_missing(r, failing)
             if current in _cp.FINISHED_STAGES:

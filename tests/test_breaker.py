@@ -56,10 +56,10 @@ class FlakyStore(MemoryStore):
         await super()._io()
 
 
-def _scenario(breaker: bool, n: int = 12, outage: float = 0.6):
+def _scenario(breaker: bool, n: int = 12, outage: float = 0.6, max_retries: int = 3):
     cfg = load_config(path=None, env={}, overrides={
         "cql-store-type": "memory", "workers": 16, "rate-limit-elements-per-second": 0, "resync-period": "0s",
-        "failure-rate-base-delay": "10ms", "failure-rate-max-delay": "40ms", "max-retries": 3,
+        "failure-rate-base-delay": "10ms", "failure-rate-max-delay": "40ms", "max-retries": max_retries,
         "circuit-breaker": {"enabled": breaker, "failure-threshold": 3, "open-duration": "50ms",
                             "max-open-duration": "100ms"}})
     rids = [f"outage-run-{i}" for i in range(n)]
@@ -85,6 +85,14 @@ def _scenario(breaker: bool, n: int = 12, outage: float = 0.6):
         return failed, c.supervisor.pipeline.stats.dead_lettered, during, c.supervisor
 
     return go()
+
+
+def test_failed_probes_do_not_spend_the_retry_budget(arun):
+    """Whichever decision the scheduler lets through as the probe, a probe that fails and
+    re-opens the circuit is the store's verdict: with one retry allowed and a 0.8 s outage
+    (several failed probes), nothing is dead-lettered."""
+    failed, dead, _during, sup = arun(_scenario(breaker=True, outage=0.8, max_retries=1), timeout=30)
+    assert failed == 12 and dead == 0 and sup.breaker.trips >= 2
 
 
 def test_outage_longer_than_the_retry_budget_loses_nothing(arun):

@@ -45,6 +45,12 @@ class GatedStore(MemoryStore):
             await self.write_gate.wait()
         return await super().update_status(*a, **kw)
 
+    async def cas_update(self, *a, **kw):  # a ToRunning is one conditional write (no read first)
+        if self.write_gate is not None:
+            self.at_write.set()
+            await self.write_gate.wait()
+        return await super().cas_update(*a, **kw)
+
 
 def _cfg(**over):
     """These tests pin the two-step (read, then write) actuation: the fused single-write path

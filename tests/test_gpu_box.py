@@ -640,3 +640,67 @@ def test_cfg3a_agent_path_real_hbm_oom(arun):
     assert r["supervisor_pod_log_reads"] == 0 and r["evidence_wait_expired"] == 0, r
     assert r["rows_with_gpu_record"] == 10 and r["vram_total_mb"] > 250_000, r
     assert r["vram_peak_mb"] >= 0.9 * r["vram_total_mb"], r
+
+
+_REBUILT_CHECK = r"""
+import json, os, subprocess, sys, time
+tmp = os.environ["NEXUS_NATIVE_DIR"]
+from nexus_supervisor_amd import _amdsmi_monitor, _cql_native, _kube_native
+mods = {m.__name__: m.__file__ for m in (_amdsmi_monitor, _cql_native, _kube_native)}
+assert all(f.startswith(tmp) for f in mods.values()), mods
+assert _cql_native.murmur3_token(b"123") == -7468325962851647638
+router = _kube_native.ShardRouter(0, 2, 7, "app.kubernetes.io/name", 30.0)
+from nexus_supervisor_amd.gpu.telemetry import AmdSmiTelemetry
+tel = AmdSmiTelemetry(interval=0.05)
+tel.start()
+try:
+    t0 = time.time()
+    p = subprocess.run([os.path.join(tmp, "gpu_stress"), "hold", "--gib", "4", "--seconds", "0.6"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    time.sleep(0.2)
+    gi = tel.devices()[0]["index"]
+    peak = tel.peak_between(gi, t0, time.time())
+finally:
+    tel.stop()
+print(json.dumps({"modules": mods, "peak_mb": peak}))
+"""
+
+
+def test_native_code_rebuilt_from_source_on_the_box(tmp_path):
+    """The pushed tree carries container-built ``.so`` files; this rebuilds the native
+    extensions and the gfx950 HIP workload from source *on the box* (its own hipcc and
+    g++), loads the rebuilt extensions in a fresh interpreter (``NEXUS_NATIVE_DIR``) and
+    has the rebuilt amd-smi monitor see the rebuilt HIP workload's 4 GiB on the MI355X."""
+    import hashlib
+    import sys
+
+    from nexus_supervisor_amd import _build
+
+    only = ["cql_native", "kube_native", "amdsmi_monitor", "gpu_stress"]
+    t0 = time.time()
+    lines = _build.build(force=True, only=only, out_root=str(tmp_path))
+    build_s = time.time() - t0
+    assert all(": built " in ln for ln in lines), lines
+    ts, intree = _build.targets(out_root=str(tmp_path)), _build.targets()
+
+    def sha(path):
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+
+    env = dict(os.environ, NEXUS_NATIVE_DIR=str(tmp_path))
+    p = subprocess.run([sys.executable, "-c", _REBUILT_CHECK], capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res["peak_mb"] >= 4000, res
+    tools = {}
+    for name, cmd in (("hipcc", [os.path.join(_build.ROCM, "bin", "hipcc"), "--version"]), ("cxx", [_build._cxx(), "--version"])):
+        out = subprocess.run(cmd, capture_output=True, text=True).stdout.strip().splitlines()
+        tools[name] = out[0] if out else ""
+    rec = {"build_s": round(build_s, 1), "built": lines, "tools": tools, "loaded": res["modules"],
+           "peak_mb": res["peak_mb"],
+           "sha16": {n: {"in_tree": sha(intree[n]["out"]) if os.path.exists(intree[n]["out"]) else None,
+                         "rebuilt": sha(ts[n]["out"])} for n in only}}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/box_rebuild.json", "w") as f:
+        json.dump(rec, f, indent=1)

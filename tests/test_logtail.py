@@ -246,6 +246,9 @@ def test_supervisor_fetches_pods_log_for_a_default_pod(arun):
         assert sorted(q["pod"] for q in api.log_requests) == sorted(f"{r.id}-acdey" for r in (oom_row, crash_row))
         assert all(q["container"] == "algorithm" and q["tailLines"] and q["limitBytes"] for q in api.log_requests)
         assert app.metrics.counter("log_tail_fetches") == 2
+        # each run's checkpoint read went out beside its log GET; the decisions took them
+        assert app.metrics.counter("checkpoint_reads_prefetched") == 2
+        assert app.metrics.counter("checkpoint_reads_prefetch_used") == 2
         await asyncio.sleep(0.2)
         assert len(api.log_requests) == 2  # one fetch per pod
         await app.stop()
@@ -281,6 +284,7 @@ def test_job_failure_waits_for_the_pods_log_read(arun):
         assert trace["class"] == "hbm-oom", trace
         assert out.algorithm_failure_cause.endswith("Algorithm ran out of GPU memory (HBM) on an AMD Instinct GPU.")
         assert app.metrics.counter("decisions_awaited_log_tail") >= 1
+        assert app.metrics.counter("checkpoint_reads_prefetch_used") == 1  # by whichever decision came first
         await app.stop()
         await api.stop()
 

@@ -206,7 +206,9 @@ def test_inprocess_extensions_under_sanitizer(sanitize):
     if sanitize == "address":
         tests = ["tests/test_sanitizers.py::test_frame_reader_fuzz", "tests/test_sanitizers.py::test_projected_decoder_fuzz",
                  "tests/test_native_json.py", "tests/test_gpu_monitor_native.py",
-                 "tests/test_kube_wire.py::test_reference_parity_over_http_and_cql", "tests/test_cql.py"]
+                 "tests/test_kube_wire.py::test_reference_parity_over_http_and_cql", "tests/test_cql.py",
+                 "tests/test_workers.py::test_router_forgets_deleted_pods_by_generation",
+                 "tests/test_workers.py::test_watch_splitter_routes_lines_and_list_items"]
     else:
         tests = ["tests/test_gpu_monitor_native.py"]
     env = dict(os.environ, NEXUS_NATIVE_DIR=os.path.join(_build.SAN_DIR, sanitize), LD_PRELOAD=rt,

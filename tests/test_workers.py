@@ -583,3 +583,34 @@ def test_hub_feed_protocol_split_reads_join_lines_and_keep_order():
         assert all(q.get_nowait() == (0, b"") for q in proto_feed.queues.values())
 
     asyncio.run(go())
+
+
+def test_router_forgets_deleted_pods_by_generation():
+    """A deleted pod's owner stays known for Pod Events still in flight, for forget_after
+    to twice that, then is forgotten wholesale with its generation (no per-entry erase on
+    the hub's hot path); a live pod is never forgotten, and arena blocks are reused."""
+    import time
+
+    labels = LabelConfig()
+    router = _kube_native.ShardRouter(0, 3, _SEED, JOB_LABEL, 0.2)
+    sp_pod = _kube_native.WatchSplitter(router, "pod")
+    pods = [make_pod(f"gen-{i}", labels) for i in range(2000)]
+    sp_pod.feed(b"".join(_line("ADDED", p) for p in pods))
+    assert router.stats["pods"] == 2000 and router.stats["gone"] == 0
+    sp_pod.feed(b"".join(_line("DELETED", p) for p in pods[:1500]))
+    st = router.stats
+    assert st["pods"] == 500 and st["gone"] == 1500
+    name = pods[0]["metadata"]["name"]
+    assert router.pod_owner(name) == worker_of("gen-0", 3)  # remembered after its DELETE
+    time.sleep(0.25)
+    router.note_pod("other-a", 1, True)  # next deletion rotates: the 1500 move to the old generation
+    assert router.pod_owner(name) == worker_of("gen-0", 3) and router.stats["gone"] == 1501
+    time.sleep(0.25)
+    router.note_pod("other-b", 2, True)  # second rotation: the first generation is dropped
+    assert router.pod_owner(name) is None
+    assert router.pod_owner("other-a") == 1 and router.pod_owner("other-b") == 2
+    assert router.stats["gone"] == 2 and router.stats["pool_bytes"] >= 0  # freed blocks are pooled for reuse
+    assert router.pod_owner(pods[1999]["metadata"]["name"]) == worker_of("gen-1999", 3)  # live: kept
+    # a re-created pod of the same name is live again
+    sp_pod.feed(_line("ADDED", pods[1]))
+    assert router.pod_owner(pods[1]["metadata"]["name"]) == worker_of("gen-1", 3)
