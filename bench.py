@@ -89,6 +89,10 @@ def parse_args(argv=None):
                          "scheduled -> Running with the kubelet's Events (its Started is a ToRunning decision: "
                          "checkpoint read + RUNNING upsert), failures carry their Job / Event traffic and Events "
                          "expire; failures: the round-4 shape (failure traffic only, new runs never start)")
+    ap.add_argument("--cpu-affinity", default="auto", choices=("auto", "none", "numa", "numa-cores"),
+                    help="CPU placement of the bench's processes (utils/affinity.py): auto = the rank GPU's NUMA "
+                         "node, one hardware thread per core (numa-cores) when that leaves >= 16 CPUs; none = "
+                         "the scheduler's")
     ap.add_argument("--diag-no-thp", action="store_true",
                     help="diagnostic: disable transparent huge pages for the bench and every process it starts")
     ap.add_argument("--diag-probe-timeline", action="store_true",
@@ -221,6 +225,16 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # before anything touches the GPU or starts a process: every child inherits the placement
+    from nexus_supervisor_amd.utils import affinity
+
+    visible = [v for v in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if v.strip().isdigit()]
+    gpu_index = int(visible[local_rank]) if local_rank < len(visible) else local_rank
+    try:
+        placed = affinity.apply(affinity.plan(args.cpu_affinity, gpu_index))
+    except OSError as exc:  # a restricted sandbox: keep the scheduler's placement
+        print(f"[bench] cpu affinity not applied: {exc}", file=sys.stderr)
+        placed = None
     slot_mode = args.slot_mode if args.slot_mode != "auto" else (
         "node" if world > 1 and args.transport == "wire" else "replica")
     if slot_mode == "node" and args.transport != "wire":
@@ -424,6 +438,7 @@ def main(argv=None) -> int:
                 "parallelism": (f"node{world}slots:1replica:{args.procs}proc" if cluster == "node" else
                                 f"shard{world}x{args.procs if args.transport == 'wire' else 1}proc"),
                 "slot_mode": slot_mode,
+                "cpu_affinity": placed,
                 # GPU monitors over the node's GPUs: one (rank 0's, the node agent's role) in
                 # node mode, one per rank otherwise
                 "gpu_monitors": 1 if cluster == "node" or world == 1 else world,

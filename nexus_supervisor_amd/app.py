@@ -462,6 +462,16 @@ def main(argv=None) -> int:
     metrics = Metrics(cfg.observability.statsd_name, {"version": __version__})
     metrics.statsd = DogStatsd.from_env(cfg.observability.statsd_name)
     log.v(1).info("configuration", config=redacted(cfg))
+    rt = cfg.runtime
+    if rt.cpu_affinity != "none":
+        from .utils import affinity
+
+        try:  # before any worker process starts: they inherit it
+            placed = affinity.apply(affinity.plan(rt.cpu_affinity, 0, min_cpus=rt.worker_processes + 1))
+        except OSError as exc:
+            log.error(exc, "cpu placement not applied")
+        else:
+            log.info("cpu placement", **(placed or {"mode": "none (too few CPUs allowed)"}))
 
     async def amain() -> int:
         stop = asyncio.Event()

@@ -490,7 +490,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         x0 = harness.external_cpu()
         sim_stats = getattr(harness, "sim_stats", None)
         s0 = await sim_stats() if sim_stats is not None else None
-        step_tl = (_CpuTimeline(harness, interval=0.2)
+        step_tl = (_CpuTimeline(harness, interval=0.2, sim=True)
                    if cfg.step_timeline and hasattr(harness, "external_cpu") else None)
         if step_tl is not None:
             step_tl.start()
@@ -778,15 +778,18 @@ def _by_kind(timed, kinds: Dict[str, str], part_of: Dict[str, Tuple[float, ...]]
     return out
 
 
-_PACING_KEYS = ("parent", "cluster", "cqlsrv", "kubesim")
+_SIM_SERIAL = ("busy", "apply_thread", "store")  # the simulator's single-thread parts (/sim/stats)
+_PACING_KEYS = ("parent", "cluster", "cqlsrv", "kubesim") + tuple(f"kubesim_{k}" for k in _SIM_SERIAL)
 
 
 def steady_util(rows: List[Dict[str, Any]], step_done_ms: List[float]) -> Dict[str, Any]:
     """Each process's CPU (cores) over the *steady* part of the timed steps — from the
     second step's completion to the second-to-last's, when every in-flight slot is full —
     as its median and 90th percentile over the timeline's intervals, and the process closest
-    to a full core there (``pacing``: the stage the line waits on; the simulator's figure
-    is its whole CPU, threads included, its serial loop is ``kubesim_loop_util``)."""
+    to a full core there (``pacing``: the stage the line waits on).  ``kubesim`` is the
+    simulator's whole CPU, threads included; its single-thread parts are ``kubesim_busy``
+    (event loop), ``kubesim_apply_thread`` (apply port) and ``kubesim_store`` (store lock
+    held)."""
     if len(step_done_ms) >= 4:
         lo, hi = step_done_ms[1] / 1000.0, step_done_ms[-2] / 1000.0
     else:
@@ -801,7 +804,7 @@ def steady_util(rows: List[Dict[str, Any]], step_done_ms: List[float]) -> Dict[s
         v = sorted(r.get(k, 0.0) for r in sel)
         out["median"][k] = v[len(v) // 2]
         out["p90"][k] = v[min(len(v) - 1, int(0.9 * len(v)))]
-    single = {k: v for k, v in out["median"].items() if k != "kubesim"}  # one-thread processes
+    single = {k: v for k, v in out["median"].items() if k != "kubesim"}  # one-thread processes / parts
     if single:
         top = max(single, key=single.get)
         out["pacing"] = {"process": top, "median_util": single[top]}
@@ -814,11 +817,14 @@ class _CpuTimeline:
     the host's busy CPUs (``/proc/stat``: other tenants included) and the cgroup's CFS
     throttling (``cpu.stat``) — to tell a stall of one process from contention for the box."""
 
-    def __init__(self, harness, interval: float = 0.25):
+    def __init__(self, harness, interval: float = 0.25, sim: bool = False):
         self.harness = harness
         self.interval = interval
         self.rows: List[Dict[str, Any]] = []
         self._task: Optional[asyncio.Task] = None
+        # the simulator's serial parts too (its /sim/stats busy counters): event loop, apply
+        # port, store lock — each a single thread of the multi-threaded process
+        self.sim = getattr(harness, "sim_stats", None) if sim else None
 
     @staticmethod
     def _host() -> Tuple[float, float]:
@@ -873,9 +879,20 @@ class _CpuTimeline:
         return {"t": time.monotonic(), "cpu": cpu, "host_busy": busy, "host_total": total, "thr_n": n, "thr_us": us,
                 "flt": flt}
 
+    async def _sim(self, row: Dict[str, Any]) -> None:
+        try:
+            st = await self.sim()
+        except Exception:  # noqa: BLE001 - a diagnostic: a missed sample is a gap
+            return
+        if st:
+            row["cpu"].update({f"kubesim_{k}": st.get(f"{k}_ns", 0) / 1e9 for k in _SIM_SERIAL})
+
     async def _run(self) -> None:
         while True:
-            self.rows.append(self._sample())
+            row = self._sample()
+            if self.sim is not None:
+                await self._sim(row)
+            self.rows.append(row)
             await asyncio.sleep(self.interval)
 
     def start(self) -> None:
@@ -888,7 +905,10 @@ class _CpuTimeline:
                 await self._task
             except asyncio.CancelledError:
                 pass
-        self.rows.append(self._sample())
+        row = self._sample()
+        if self.sim is not None:
+            await self._sim(row)
+        self.rows.append(row)
 
     def report(self, t0: float) -> List[Dict[str, Any]]:
         """One entry per interval: seconds from ``t0`` (the first arrival), each process's
@@ -900,7 +920,8 @@ class _CpuTimeline:
             if dt <= 0:
                 continue
             row = {"t": round(a["t"] - t0, 1)}
-            row.update({k: round((b["cpu"][k] - a["cpu"].get(k, 0.0)) / dt, 2) for k in b["cpu"] if not k.endswith("_sys")})
+            row.update({k: round((b["cpu"][k] - a["cpu"].get(k, 0.0)) / dt, 2) for k in b["cpu"]
+                        if not k.endswith("_sys") and k in a["cpu"]})
             if b["host_total"] > a["host_total"]:
                 row["host_busy_cpus"] = round(ncpu * (b["host_busy"] - a["host_busy"]) / (b["host_total"] - a["host_total"]), 1)
             row["throttled"] = int(b["thr_n"] - a["thr_n"])

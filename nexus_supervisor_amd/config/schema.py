@@ -337,6 +337,12 @@ class RuntimeConfig:
     # with worker processes: the parent holds one LIST+WATCH per kind and routes each object
     # to its owner worker (parallel/watchhub.py) instead of every worker watching everything
     watch_hub: bool = field(default=True, metadata=_k("watch-hub"))
+    # CPU placement of the supervisor's processes (utils/affinity.py), set at start-up and
+    # inherited by the shard workers: none = the scheduler's (or the pod cpuset's); numa =
+    # the NUMA node of the host's first GPU (node 0 without one); numa-cores = that node,
+    # one hardware thread per physical core; auto = numa-cores, else numa, when either
+    # leaves at least worker-processes + 1 CPUs of the allowed set
+    cpu_affinity: str = field(default="none", metadata=_k("cpu-affinity"))
 
 
 @dataclass
@@ -466,6 +472,8 @@ def validate(cfg: SupervisorConfig) -> SupervisorConfig:
         rt.worker_processes = auto_worker_processes()
     if rt.worker_processes < 1 or not 0 <= rt.worker_index < rt.worker_processes:
         raise ConfigError("runtime.worker-processes must be >= 0 (0 = auto) and runtime.worker-index in [0, worker-processes)")
+    if rt.cpu_affinity not in ("none", "numa", "numa-cores", "auto"):
+        raise ConfigError("runtime.cpu-affinity must be none|numa|numa-cores|auto")
     if not 0 < cfg.gpu.hbm_oom_fraction <= 1:
         raise ConfigError("gpu.hbm-oom-fraction must be in (0, 1]")
     if cfg.gpu.log_tail not in ("auto", "api", "node", "off"):

@@ -41,20 +41,26 @@ class JsonFormatter(logging.Formatter):
     _sec_text = ""
 
     def format(self, record: logging.LogRecord) -> str:
-        sec = int(record.created)
+        error = self.formatException(record.exc_info) if record.exc_info else None
+        return self.line(record.created, record.msecs, record.levelname, record.name, record.getMessage(),
+                         getattr(record, "v", None), getattr(record, "kv", None), error)
+
+    def line(self, created: float, msecs: float, levelname: str, name: str, msg: str, v=None, kv=None,
+             error: Optional[str] = None) -> str:
+        """One JSON line (also :meth:`KLogger._emit`'s direct path, which has no record)."""
+        sec = int(created)
         if sec != self._sec:  # one strftime per second, not per line
             self._sec, self._sec_text = sec, time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(sec))
-        doc: Dict[str, Any] = {"time": f"{self._sec_text}.{int(record.msecs):03d}Z",
-                               "level": record.levelname, "logger": record.name, "msg": record.getMessage()}
-        v = getattr(record, "v", None)
+        doc: Dict[str, Any] = {"time": f"{self._sec_text}.{int(msecs):03d}Z",
+                               "level": levelname, "logger": name, "msg": msg}
         if v:
             doc["v"] = v
-        kv = getattr(record, "kv", None)
         if kv:
             doc.update(kv)
-        if record.exc_info:
-            doc["error"] = self.formatException(record.exc_info)
-        doc.update(self.static)
+        if error is not None:
+            doc["error"] = error
+        if self.static:
+            doc.update(self.static)
         if _dumps is not None:  # one log line per decision (reference V(0)): native encoder
             return _dumps(doc, default=str).decode()
         return json.dumps(doc, default=str, separators=(",", ":"), ensure_ascii=False)
@@ -112,6 +118,19 @@ class KLogger:
     def _emit(self, level: int, msg: str, extra: Dict[str, Any]) -> None:
         lg = self._log
         if lg.isEnabledFor(level):
+            hs = lg.handlers
+            if len(hs) == 1 and not lg.filters and not lg.propagate:
+                h = hs[0]
+                if type(h) is BufferedStreamHandler and not h.filters and type(h.formatter) is JsonFormatter \
+                        and level >= h.level:
+                    # the deployed configuration (configure_logging without a Datadog sink): the
+                    # line straight into the handler's buffer — no LogRecord, no handler lock
+                    # (one event-loop thread writes; the flusher only flushes)
+                    ct = time.time()
+                    h.write_line(h.formatter.line(ct, (ct - int(ct)) * 1000, _LEVEL_NAMES.get(level) or
+                                                  logging.getLevelName(level), lg.name, msg, extra.get("v"),
+                                                  extra.get("kv")), level)
+                    return
             lg.handle(_Record(lg.name, level, msg, extra))
 
     def info(self, msg: str, **kv) -> None:
@@ -183,7 +202,18 @@ class BufferedStreamHandler(logging.StreamHandler):
         except Exception:  # pragma: no cover
             self.handleError(record)
             return
-        if record.levelno >= logging.WARNING or self.interval <= 0:
+        self._written(record.levelno)
+
+    def write_line(self, line: str, levelno: int) -> None:
+        """A formatted line from :meth:`KLogger._emit`'s direct path."""
+        try:
+            self.stream.write(line + self.terminator)
+        except Exception:  # pragma: no cover - a closed stream: as handleError, say nothing
+            return
+        self._written(levelno)
+
+    def _written(self, levelno: int) -> None:
+        if levelno >= logging.WARNING or self.interval <= 0:
             self.flush()
         elif not self._dirty:
             self._dirty = True

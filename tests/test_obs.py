@@ -318,3 +318,35 @@ def test_buffered_log_handler_flushes_late_without_a_thread_per_window(arun):
     finally:
         lg.removeHandler(h)
         h.close()
+
+
+def test_direct_log_path_writes_the_record_paths_line():
+    """KLogger's direct path (one BufferedStreamHandler, no filters: the deployed setup)
+    writes the same JSON line the LogRecord path does; a filter or a second handler puts
+    every line back on the record path."""
+    import io
+    import json as _json
+    import logging as _logging
+
+    from nexus_supervisor_amd.obs.logging import configure_logging, shutdown_logging
+
+    def lines(extra_handler):
+        buf = io.StringIO()
+        log = configure_logging("DEBUG", stream=buf, static={"service": "s"})
+        root = _logging.getLogger("nexus_supervisor_amd")
+        if extra_handler:
+            root.addHandler(_logging.NullHandler())
+        log.info("Algorithm run failed", requestId="r1", reason="OOMKilled")
+        log.v(4).info("event received", object="ns/e")
+        root.handlers[0].flush()
+        shutdown_logging()
+        out = [_json.loads(x) for x in buf.getvalue().splitlines()]
+        for d in out:
+            d.pop("time")
+        return out
+
+    direct, via_record = lines(False), lines(True)
+    assert direct == via_record
+    assert direct[0] == {"level": "INFO", "logger": "nexus_supervisor_amd", "msg": "Algorithm run failed",
+                         "requestId": "r1", "reason": "OOMKilled", "service": "s"}
+    assert direct[1]["v"] == 4
