@@ -124,8 +124,8 @@ class KLogger:
                 if type(h) is BufferedStreamHandler and not h.filters and type(h.formatter) is JsonFormatter \
                         and level >= h.level:
                     # the deployed configuration (configure_logging without a Datadog sink): the
-                    # line straight into the handler's buffer — no LogRecord, no handler lock
-                    # (one event-loop thread writes; the flusher only flushes)
+                    # line straight into the handler's buffer — no LogRecord, no filter or
+                    # handler-chain walk
                     ct = time.time()
                     h.write_line(h.formatter.line(ct, (ct - int(ct)) * 1000, _LEVEL_NAMES.get(level) or
                                                   logging.getLevelName(level), lg.name, msg, extra.get("v"),
@@ -205,11 +205,18 @@ class BufferedStreamHandler(logging.StreamHandler):
         self._written(record.levelno)
 
     def write_line(self, line: str, levelno: int) -> None:
-        """A formatted line from :meth:`KLogger._emit`'s direct path."""
+        """A formatted line from :meth:`KLogger._emit`'s direct path (under the handler's
+        lock, as ``Handler.handle`` would take it: a flusher thread may flush meanwhile)."""
+        lock = self.lock
+        if lock is not None:
+            lock.acquire()
         try:
             self.stream.write(line + self.terminator)
         except Exception:  # pragma: no cover - a closed stream: as handleError, say nothing
             return
+        finally:
+            if lock is not None:
+                lock.release()
         self._written(levelno)
 
     def _written(self, levelno: int) -> None:
