@@ -652,9 +652,16 @@ struct Stats {
   int64_t apply_ns = 0, request_ns = 0, flush_ns = 0, recv_ns = 0, busy_ns = 0;
   int64_t prepare_ns = 0;  // the parallel part of apply_ns (wall time)
   int64_t store_ns = 0;    // time g_store_mu was held (loop + apply thread): the serial part
-  std::atomic<int64_t> apply_thread_ns{0};  // the apply port's busy time (reading, applying)
+  std::atomic<int64_t> apply_thread_ns{0};  // the apply port's busy time (reading, applying), all connections
   uint64_t commit_parallel = 0;  // bulk-apply chunks committed per kind on threads
 } g_stats;
+
+// busy time per apply connection: each connection is served by one thread, so each is a
+// serial part of its own; with several generators (node mode: one per slot) the sum over
+// connections is not any one thread's load
+std::mutex g_apply_conn_mu;
+std::map<int, int64_t> g_apply_conn_ns;
+std::atomic<int> g_apply_conn_seq{0};
 
 // g_store_mu held for the scope; the hold time counts into g_stats.store_ns
 struct StoreLock {
@@ -2083,7 +2090,17 @@ void handle(Conn& c, Request& r) {
                       ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
                       ",\"store_ns\":" + std::to_string(g_stats.store_ns) +
                       ",\"apply_thread_ns\":" + std::to_string(g_stats.apply_thread_ns.load()) +
-                      ",\"objects\":{";
+                      ",\"apply_conn_ns\":{";
+      {
+        std::lock_guard<std::mutex> lk(g_apply_conn_mu);
+        bool first = true;
+        for (const auto& [id, ns] : g_apply_conn_ns) {
+          if (!first) s += ',';
+          first = false;
+          s += "\"" + std::to_string(id) + "\":" + std::to_string(ns);
+        }
+      }
+      s += "},\"objects\":{";
       for (int k = 0; k < NKINDS; ++k) {
         if (k) s += ',';
         s += "\"" + std::string(KINDS[k].kind) + "\":" + std::to_string(g_store[k].objs.size());
@@ -2283,6 +2300,7 @@ void on_signal(int) { g_stop.store(1); }
 int g_wake_fd = -1;  // eventfd: an apply committed watch lines the loop must send
 
 void apply_conn(int fd) {
+  const int conn_id = ++g_apply_conn_seq;
   std::string in;
   std::vector<char> buf(1 << 16);
   while (!g_stop) {
@@ -2352,7 +2370,12 @@ void apply_conn(int fd) {
       off += static_cast<size_t>(w);
     }
     in.erase(0, he + 4 + clen);
-    g_stats.apply_thread_ns += mono_ns() - t0;
+    int64_t dt = mono_ns() - t0;
+    g_stats.apply_thread_ns += dt;
+    {
+      std::lock_guard<std::mutex> lk(g_apply_conn_mu);
+      g_apply_conn_ns[conn_id] += dt;
+    }
   }
   close(fd);
 }

@@ -541,6 +541,11 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 # both commit under it) — the largest is what saturates first
                 share = {k: round((s1.get(f"{k}_ns", 0) - s0.get(f"{k}_ns", 0)) / 1e9 / elapsed, 3)
                          for k in ("busy", "apply_thread", "store")}
+                c0, c1 = s0.get("apply_conn_ns"), s1.get("apply_conn_ns")
+                if c1:
+                    # each apply connection is one thread: the busiest one is the serial part
+                    # (node mode has one generator connection per slot; their sum is not)
+                    share["apply_thread"] = round(max(v - (c0 or {}).get(k, 0) for k, v in c1.items()) / 1e9 / elapsed, 3)
                 cpu["kubesim_loop_util"] = share["busy"]
                 cpu["kubesim_apply_port_util"] = share["apply_thread"]
                 cpu["kubesim_store_util"] = share["store"]
@@ -886,6 +891,9 @@ class _CpuTimeline:
             return
         if st:
             row["cpu"].update({f"kubesim_{k}": st.get(f"{k}_ns", 0) / 1e9 for k in _SIM_SERIAL})
+            conns = st.get("apply_conn_ns")
+            if conns:  # one thread per apply connection: the busiest one (see run_rank)
+                row["cpu"]["kubesim_apply_thread"] = max(conns.values()) / 1e9
 
     async def _run(self) -> None:
         while True:

@@ -61,6 +61,14 @@ def test_apply_port_commits_beside_the_loop(arun):
             assert len(items) == 199
             st = await ctl.stats()
             assert st["apply_thread_ns"] > 0 and st["store_ns"] > 0
+            # busy time per apply connection (one thread each): a second generator connection
+            # is a second serial part, not more load on the first
+            ctl2 = SimControl(sim.url, sim.apply_url)
+            await ctl2.apply([("ADDED", make_pod("b0", labels))])
+            conns = (await ctl.stats())["apply_conn_ns"]
+            assert len(conns) == 2 and all(v > 0 for v in conns.values())
+            assert sum(conns.values()) == (await ctl.stats())["apply_thread_ns"]
+            await ctl2.close()
             async with aiohttp.ClientSession() as s:
                 async with s.get(sim.apply_url + "/sim/stats") as r:
                     assert r.status == 404
