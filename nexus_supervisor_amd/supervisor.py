@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import asyncio
 import datetime as _dt
+import functools
 import time
 from collections import OrderedDict
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -92,6 +93,11 @@ def failed_gpu(r: RunStatusAnalysisResult) -> Tuple[str, Optional[Any]]:
         if any(e.get("type") in FAULT_EVENTS for e in g.get("events") or ()):
             return node, g.get("index")
     return node, topo.get("expected_gpu")
+
+
+def _wake(waiter: asyncio.Future, *_args) -> None:
+    if not waiter.done():
+        waiter.set_result(None)
 
 
 def _consume_exception(fut: asyncio.Future) -> None:
@@ -1180,14 +1186,23 @@ class Supervisor:
                               requestId=r.request_id, reason=r.reason,
                               pods=[f"{kube.name_of(p)}:{(p.get('status') or {}).get('phase')}" for p in pods][:4])
                 break
+            loop = asyncio.get_running_loop()
             fut = self._settle.get(r.request_id)
             if fut is None or fut.done():
-                fut = self._settle[r.request_id] = asyncio.get_running_loop().create_future()
+                fut = self._settle[r.request_id] = loop.create_future()
             waited = True
+            # a plain waiter woken by the pod's update or the settle timer: most Job
+            # decisions of a pod failure wait here once (the two watch streams race), and
+            # wait_for(shield(...)) costs a Task and two futures per wait
+            waiter = loop.create_future()
+            wake = functools.partial(_wake, waiter)
+            fut.add_done_callback(wake)
+            timer = loop.call_later(left, wake)
             try:
-                await asyncio.wait_for(asyncio.shield(fut), left)
-            except asyncio.TimeoutError:
-                pass
+                await waiter
+            finally:
+                timer.cancel()
+                fut.remove_done_callback(wake)
         if waited:
             self.metrics.inc("job_pod_settle_waits")
 

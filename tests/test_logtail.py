@@ -553,3 +553,33 @@ def test_a_log_read_without_a_decision_forgets_the_arrival_stamps(arun):
         await sup.stop(drain=False)
 
     arun(go(), timeout=20)
+
+
+def test_prefetched_reads_are_dropped_when_fenced(arun):
+    """A checkpoint read prefetched for a deferred GPU failure belongs to the current lease:
+    losing it (or the run's shard) cancels the read, so a new leader's decision never takes
+    a row read under the old one."""
+    from nexus_supervisor_amd.testing.inproc import InProcCluster
+
+    async def go():
+        cfg = _app_cfg()
+        rows = seed_rows()
+        store = MemoryStore(rows)
+        pods = [make_pod(r.id, cfg.labels, gpus=1) for r in rows[:2]]
+        c = InProcCluster(cfg, store, pods)
+        await c.start()
+        sup = c.supervisor
+        sup.set_active(True)
+        assert sup._prefetch_reads
+        for p in pods:
+            sup._prefetch_read(p)
+        sup._prefetch_read(pods[0])  # one read per run
+        assert len(sup._prefetch) == 2 and sup.metrics.counter("checkpoint_reads_prefetched") == 2
+        futs = list(sup._prefetch.values())
+        sup.fence()
+        assert not sup._prefetch
+        await asyncio.sleep(0)
+        assert all(f.cancelled() or f.done() for f in futs)
+        await c.stop()
+
+    arun(go(), timeout=30)
