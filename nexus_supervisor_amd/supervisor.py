@@ -245,8 +245,12 @@ class Supervisor:
         # run -> checkpoint stage read started while its deferred GPU failure waits (for its
         # log tail or the node agent's evidence): the decision that follows takes it instead
         # of a round trip of its own (two-step owned-columns actuation only)
-        self._prefetch: "OrderedDict[Tuple[str, str], asyncio.Future]" = OrderedDict()
+        self._prefetch: "OrderedDict[Tuple[str, str], Tuple[asyncio.Future, float]]" = OrderedDict()
         self._prefetch_reads = not self._fused and not cfg.compat.full_row_upsert
+        # a prefetched read is taken only by a decision that follows its wait: one that
+        # outlived the longest wait it can overlap (a deferral that decided nothing) is
+        # dropped, never used for a later decision of the run
+        self._prefetch_ttl = max(cfg.gpu.log_tail_timeout, cfg.gpu.evidence_wait) + 2.0
         self._settle: Dict[str, asyncio.Future] = {}  # job name -> a Job decision waiting for its pod's failure
         # shards whose cached pods may be stale while the Pod informer re-lists (set when the list is in)
         self._pod_relist: Optional[Tuple[asyncio.Event, frozenset]] = None
@@ -757,18 +761,40 @@ class Supervisor:
         if not rid:
             return
         key = (labels.get(self.cfg.labels.job_template_name_key, ""), rid)
-        if key in self._prefetch or key in self._applied:
+        if key in self._applied:
             return
-        if len(self._prefetch) >= 4096:  # deferrals that never became a decision
-            self._prefetch.popitem(last=False)[1].cancel()
+        now = time.monotonic()
+        old = self._prefetch.get(key)
+        if old is not None:
+            if now - old[1] <= self._prefetch_ttl:
+                return
+            del self._prefetch[key]  # a stale one: read again
+            old[0].cancel()
+        while self._prefetch:  # deferrals that never became a decision (oldest first)
+            k0, (f0, t0) = next(iter(self._prefetch.items()))
+            if now - t0 <= self._prefetch_ttl and len(self._prefetch) < 4096:
+                break
+            del self._prefetch[k0]
+            f0.cancel()
         fut = asyncio.ensure_future(self.store.read_status(*key))
         fut.add_done_callback(_consume_exception)
-        self._prefetch[key] = fut
+        self._prefetch[key] = (fut, now)
         self.metrics.inc("checkpoint_reads_prefetched")
+
+    def _take_prefetch(self, key: Tuple[str, str]) -> Optional[asyncio.Future]:
+        """The prefetched read of ``key`` if it is fresh and did not fail, else None."""
+        entry = self._prefetch.pop(key, None)
+        if entry is None:
+            return None
+        fut, t0 = entry
+        if time.monotonic() - t0 > self._prefetch_ttl or fut.cancelled() or (fut.done() and fut.exception() is not None):
+            fut.cancel()
+            return None
+        return fut
 
     def _drop_prefetch(self, lost: Callable[[str], bool]) -> None:
         for key in [k for k in self._prefetch if lost(k[1])]:
-            self._prefetch.pop(key).cancel()
+            self._prefetch.pop(key)[0].cancel()
 
     async def _fetch_log_tail(self, key: str, pod: Dict[str, Any], want: List[Dict[str, Any]], waited: bool) -> None:
         from .gpu.logtail import fetch_api_tail
@@ -1070,8 +1096,8 @@ class Supervisor:
         try:
             # the owned-columns write needs only the stage; the full-row upsert (reference
             # UpsertCheckpoint of the deep copy) needs every column
-            pre = self._prefetch.pop((r.algorithm, r.request_id), None) if self._prefetch else None
-            if pre is not None and not pre.cancelled() and (not pre.done() or pre.exception() is None):
+            pre = self._take_prefetch((r.algorithm, r.request_id)) if self._prefetch else None
+            if pre is not None:
                 cp = await pre  # started while the failure waited for its log tail / evidence
                 self.metrics.inc("checkpoint_reads_prefetch_used")
             else:

@@ -575,11 +575,39 @@ def test_prefetched_reads_are_dropped_when_fenced(arun):
             sup._prefetch_read(p)
         sup._prefetch_read(pods[0])  # one read per run
         assert len(sup._prefetch) == 2 and sup.metrics.counter("checkpoint_reads_prefetched") == 2
-        futs = list(sup._prefetch.values())
+        futs = [f for f, _t in sup._prefetch.values()]
         sup.fence()
         assert not sup._prefetch
         await asyncio.sleep(0)
         assert all(f.cancelled() or f.done() for f in futs)
+        await c.stop()
+
+    arun(go(), timeout=30)
+
+
+def test_a_stale_prefetched_read_is_never_used(arun):
+    """A prefetch whose deferral decided nothing is not taken by a later decision of the run
+    once it is older than the longest wait it can overlap: that decision reads again."""
+    from nexus_supervisor_amd.testing.inproc import InProcCluster
+
+    async def go():
+        cfg = _app_cfg()
+        rows = seed_rows()
+        store = MemoryStore(rows)
+        pod = make_pod(rows[1].id, cfg.labels, gpus=1)
+        c = InProcCluster(cfg, store, [pod])
+        await c.start()
+        sup = c.supervisor
+        sup.set_active(True)
+        sup._prefetch_read(pod)
+        key = (rows[1].algorithm, rows[1].id)
+        fut, t0 = sup._prefetch[key]
+        await fut
+        assert sup._take_prefetch(key) is fut  # fresh: taken
+        sup._prefetch_read(pod)
+        fut2, _ = sup._prefetch[key]
+        sup._prefetch[key] = (fut2, t0 - sup._prefetch_ttl - 1.0)  # as if it were old
+        assert sup._take_prefetch(key) is None and key not in sup._prefetch
         await c.stop()
 
     arun(go(), timeout=30)
