@@ -231,7 +231,9 @@ def main(argv=None) -> int:
     visible = [v for v in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if v.strip().isdigit()]
     gpu_index = int(visible[local_rank]) if local_rank < len(visible) else local_rank
     try:
-        placed = affinity.apply(affinity.plan(args.cpu_affinity, gpu_index))
+        # the host is shared: leave out the cores another tenant keeps busy right now
+        busy = affinity.cpu_busy(0.25) if args.cpu_affinity != "none" else None
+        placed = affinity.apply(affinity.plan(args.cpu_affinity, gpu_index, busy=busy))
     except OSError as exc:  # a restricted sandbox: keep the scheduler's placement
         print(f"[bench] cpu affinity not applied: {exc}", file=sys.stderr)
         placed = None

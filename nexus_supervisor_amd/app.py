@@ -467,7 +467,8 @@ def main(argv=None) -> int:
         from .utils import affinity
 
         try:  # before any worker process starts: they inherit it
-            placed = affinity.apply(affinity.plan(rt.cpu_affinity, 0, min_cpus=rt.worker_processes + 1))
+            placed = affinity.apply(affinity.plan(rt.cpu_affinity, 0, min_cpus=rt.worker_processes + 1,
+                                                  busy=affinity.cpu_busy(0.25)))
         except OSError as exc:
             log.error(exc, "cpu placement not applied")
         else:

@@ -11,11 +11,12 @@ sibling halves a core's throughput.
 :func:`plan` picks one NUMA node (the GPU's, or node 0), and within it one hardware
 thread per physical core (``numa-cores``) or every thread (``numa``).  It intersects
 that with what the process may already use (a cgroup cpuset or the kubelet's static CPU
-manager).  :func:`apply` sets it on the calling process; children inherit it over fork
-and exec.  A plan smaller than ``min_cpus`` is not applied: a tight pod cpuset is
-already the operator's placement.
+manager), and can leave out the cores other tenants keep busy right now (:func:`cpu_busy`).
+:func:`apply` sets it on the calling process; children inherit it over fork and exec.  A
+plan smaller than ``min_cpus`` is not applied: a tight pod cpuset is already the
+operator's placement.
 
-Everything is read from sysfs, before the process touches a GPU.
+Everything is read from sysfs and ``/proc/stat``, before the process touches a GPU.
 """
 from __future__ import annotations
 
@@ -85,10 +86,47 @@ def first_threads(cpus: List[int], sys_root: str = SYS) -> List[int]:
     return out
 
 
+def cpu_busy(interval: float = 0.25, proc_root: str = "/proc") -> Dict[int, float]:
+    """Each CPU's busy share over ``interval`` seconds (``/proc/stat``: everything but idle
+    and iowait) — what other tenants of a shared host are running where."""
+    import time
+
+    def snap() -> Dict[int, tuple]:
+        out = {}
+        text = _read(os.path.join(proc_root, "stat")) or ""
+        for line in text.splitlines():
+            if line.startswith("cpu") and line[3:4].isdigit():
+                parts = line.split()
+                v = [int(x) for x in parts[1:]]
+                idle = v[3] + (v[4] if len(v) > 4 else 0)
+                out[int(parts[0][3:])] = (sum(v) - idle, sum(v))
+        return out
+
+    a = snap()
+    time.sleep(interval)
+    b = snap()
+    busy = {}
+    for c, (bb, bt) in b.items():
+        ab, at = a.get(c, (bb, bt))
+        busy[c] = (bb - ab) / (bt - at) if bt > at else 0.0
+    return busy
+
+
+def _siblings(c: int, sys_root: str) -> List[int]:
+    sib = _read(os.path.join(sys_root, "devices", "system", "cpu", f"cpu{c}", "topology", "thread_siblings_list"))
+    return parse_cpulist(sib) if sib else [c]
+
+
 def plan(mode: str = "auto", gpu_index: int = 0, allowed: Optional[Set[int]] = None, min_cpus: int = 16,
-         sys_root: str = SYS) -> Optional[Dict[str, object]]:
+         sys_root: str = SYS, busy: Optional[Dict[int, float]] = None,
+         busy_max: float = 0.5) -> Optional[Dict[str, object]]:
     """The CPU set for ``mode`` (None: leave placement alone).  ``auto`` is ``numa-cores``
-    when that leaves at least ``min_cpus`` CPUs, else ``numa``, else nothing."""
+    when that leaves at least ``min_cpus`` CPUs, else ``numa``, else nothing.
+
+    With ``busy`` (:func:`cpu_busy`, a shared host's current load per CPU), ``numa-cores``
+    leaves out the physical cores another tenant keeps busy (both threads together at or
+    over ``busy_max``) while ``min_cpus`` remain: those cores would run the replica at SMT
+    speed.  The summary records how many were left out."""
     if mode not in MODES:
         raise ValueError(f"cpu affinity mode must be one of {MODES}, not {mode!r}")
     if mode == "none":
@@ -103,8 +141,15 @@ def plan(mode: str = "auto", gpu_index: int = 0, allowed: Optional[Set[int]] = N
     tries = ["numa-cores", "numa"] if mode == "auto" else [mode]
     for m in tries:
         sel = first_threads(cpus, sys_root) if m == "numa-cores" else cpus
-        if len(sel) >= min_cpus:
-            return {"mode": m, "node": node, "cpus": sel}
+        if len(sel) < min_cpus:
+            continue
+        out: Dict[str, object] = {"mode": m, "node": node, "cpus": sel}
+        if busy is not None and m == "numa-cores":
+            quiet = [c for c in sel if sum(busy.get(x, 0.0) for x in _siblings(c, sys_root)) < busy_max]
+            if len(quiet) >= min_cpus:
+                out["cpus"] = quiet
+                out["busy_cores_skipped"] = len(sel) - len(quiet)
+        return out
     return None
 
 
@@ -115,4 +160,7 @@ def apply(p: Optional[Dict[str, object]]) -> Optional[Dict[str, object]]:
         return None
     cpus = list(p["cpus"])  # type: ignore[arg-type]
     os.sched_setaffinity(0, cpus)
-    return {"mode": p["mode"], "node": p["node"], "cpus": len(cpus)}
+    out = {"mode": p["mode"], "node": p["node"], "cpus": len(cpus)}
+    if "busy_cores_skipped" in p:
+        out["busy_cores_skipped"] = p["busy_cores_skipped"]
+    return out

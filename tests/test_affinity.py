@@ -73,3 +73,30 @@ def test_apply_restricts_this_process():
         assert affinity.apply(None) is None
     finally:
         os.sched_setaffinity(0, before)
+
+
+def test_busy_cores_are_left_out_while_enough_remain(box):
+    # core 1 (cpus 1 + 9) is busy on one thread, core 2 on both together, core 3 quiet
+    busy = {1: 0.9, 9: 0.0, 2: 0.3, 10: 0.3, 0: 0.1, 8: 0.1}
+    p = affinity.plan("numa-cores", gpu_index=0, allowed=set(range(16)), min_cpus=2, sys_root=box, busy=busy)
+    assert p["cpus"] == [0, 3] and p["busy_cores_skipped"] == 2
+    assert affinity.apply(None) is None
+    # too few quiet cores: the whole node, nothing skipped
+    p = affinity.plan("numa-cores", gpu_index=0, allowed=set(range(16)), min_cpus=3, sys_root=box, busy=busy)
+    assert p["cpus"] == [0, 1, 2, 3] and "busy_cores_skipped" not in p
+
+
+def test_cpu_busy_reads_proc_stat(tmp_path):
+    import threading
+
+    stat = tmp_path / "stat"
+    stat.write_text("cpu  10 0 10 100 0 0 0 0 0 0\ncpu0 5 0 5 50 0 0 0 0 0 0\ncpu1 5 0 5 50 0 0 0 0 0 0\n")
+
+    def later():
+        stat.write_text("cpu  30 0 10 120 0 0 0 0 0 0\ncpu0 25 0 5 50 0 0 0 0 0 0\ncpu1 5 0 5 70 0 0 0 0 0 0\n")
+
+    t = threading.Timer(0.05, later)
+    t.start()
+    busy = affinity.cpu_busy(0.2, proc_root=str(tmp_path))
+    t.join()
+    assert busy == {0: 1.0, 1: 0.0}
