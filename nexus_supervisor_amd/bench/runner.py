@@ -426,6 +426,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
     tracker = Tracker()
     sampler = None
     agent = None
+    beat = None
     try:
         await harness.start()
         sup = harness.supervisor
@@ -469,7 +470,21 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 for st in sts:
                     await finish(st)
 
+        phase = {"name": "warmup", "t0": time.monotonic()}
+
+        async def heartbeat() -> None:
+            # a progress line every 15 s on stderr: long runs (a soak of hundreds of steps, a
+            # read-back of a million rows) stay visibly alive to whatever supervises them
+            import sys as _sys
+
+            while True:
+                await asyncio.sleep(15.0)
+                print(f"[bench] {phase['name']} {time.monotonic() - phase['t0']:.0f}s: {len(done_at)} timed steps "
+                      f"done, {tracker.failures} failures acked", file=_sys.stderr, flush=True)
+
+        beat = asyncio.ensure_future(heartbeat())
         await run_steps(cfg.warmup)
+        phase.update(name="timed", t0=time.monotonic())
         gc.collect()
         tracker.errors = tracker.wrong_stage = 0
         tracker.wrong_examples.clear()
@@ -610,6 +625,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                             # default pods: the agent read their OOM text from the node's logs
                             "agent_log_reads": int(sum(v for k, v in am.items() if k.endswith("agent_log_reads_total"))),
                             "supervisor_log_fetches": int(sup.metrics.counter("decisions_deferred_for_log_tail"))}
+        phase.update(name="readback", t0=time.monotonic())
         readback = await _read_back(harness, tracker)
         attribution = None
         if cfg.node and oom_phase is not None:
@@ -619,6 +635,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
         if cfg.probe_events > 0:
             before = _stage_counts(sup)
             slow0 = _slow_snapshot(sup)
+            phase.update(name="probe", t0=time.monotonic())
             probe = await _latency_probe(harness, tracker, cfg)
             if sync is not None:
                 await sync()
@@ -629,6 +646,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 if slow:  # NEXUS_SLOW_CALLBACK_MS: what held a loop during the probe
                     probe["slow_callbacks"] = slow
     finally:
+        if beat is not None:
+            beat.cancel()
         if sampler is not None:
             sampler.stop()
         if agent is not None:
