@@ -56,14 +56,14 @@ def make_shard_leases(cfg: SupervisorConfig, kube, on_change, metrics, on_renewe
 
 def build_factory(cfg: SupervisorConfig, client) -> InformerFactory:
     from .kube.client import KubeListWatch
-    from .parallel.sharding import ShardSet, watch_selector
+    from .parallel.sharding import ShardSet, watch_field_selector, watch_selector
 
     ns = cfg.resource_namespace
     owned = ShardSet.from_config(cfg).owned  # static: {shard-index}; lease: none until a lease is won
 
     def lw(kind: str):
         return KubeListWatch(client, kind, ns, label_selector=watch_selector(cfg, kind, owned),
-                             watch_timeout=int(cfg.watch_timeout))
+                             field_selector=watch_field_selector(cfg, kind), watch_timeout=int(cfg.watch_timeout))
 
     return InformerFactory(lw, resync_period=cfg.resync_period)
 

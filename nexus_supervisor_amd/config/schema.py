@@ -380,6 +380,9 @@ class SupervisorConfig:
     resync_period: float = field(default=30.0, metadata=_k("resync-period", "duration"))  # informer resync
     # server-side label selector on the Pod/Job informers (only Nexus runs are cached)
     informer_label_selector: bool = field(default=True, metadata=_k("informer-label-selector"))
+    # server-side field selector on the Event informer: reason!=<each Normal start/stop reason
+    # no rule reads> (Scheduled, Pulling, Pulled, Created, Killing, SuccessfulCreate, ...)
+    informer_event_noise_selector: bool = field(default=True, metadata=_k("informer-event-noise-selector"))
     watch_timeout: float = field(default=300.0, metadata=_k("watch-timeout", "duration"))  # server-side watch timeout
     # client-side API flow control (client-go rest.Config QPS / Burst): a token bucket in
     # front of every API request of a replica (Job DELETEs, pods/log reads, Events, LIST /

@@ -75,6 +75,18 @@ def watch_selector(cfg, kind: str, owned: Optional[Iterable[int]] = None) -> str
     return ",".join(parts)
 
 
+def watch_field_selector(cfg, kind: str) -> str:
+    """The server-side field selector of a replica's ``kind`` watch: on Events
+    (``informer-event-noise-selector``), ``reason!=…`` for the start/stop reasons no rule
+    reads (:func:`..classify.classifier.event_field_selector`).  The reference watches
+    every Event of the namespace (``/root/reference/services/supervisor.go:73-75``)."""
+    if kind != "Event" or not getattr(cfg, "informer_event_noise_selector", False):
+        return ""
+    from ..classify.classifier import event_field_selector
+
+    return event_field_selector(cfg.gpu.gpu_resource_name)
+
+
 def kube_name(obj) -> str:
     return ((obj or {}).get("metadata") or {}).get("name", "")
 

@@ -137,12 +137,15 @@ class WatchHub:
     def _path_params(self, kind: str) -> Tuple[str, Dict[str, str]]:
         from ..kube.client import resource_path
 
-        from .sharding import watch_selector
+        from .sharding import watch_field_selector, watch_selector
 
         params: Dict[str, str] = {}
         sel = watch_selector(self.cfg, kind, self.owned)
         if sel:
             params["labelSelector"] = sel
+        fsel = watch_field_selector(self.cfg, kind)
+        if fsel:
+            params["fieldSelector"] = fsel
         return resource_path(kind, self.cfg.resource_namespace), params
 
     async def _route(self, ki: int, outs: List[bytes], ftype: int, prefix: bytes = b"") -> None:

@@ -129,6 +129,60 @@ def test_rest_semantics(arun):
     arun(go())
 
 
+def test_event_noise_selector_on_list_and_watch(arun):
+    """``informer-event-noise-selector``: the Event list/watch of a replica (and of the
+    parent's watch hub) carries ``reason!=…`` for the start/stop reasons no rule reads, so
+    the server never sends them; every reason a rule reads still arrives."""
+    from nexus_supervisor_amd.app import build_factory
+    from nexus_supervisor_amd.classify.classifier import EVENT_NOISE_REASONS, event_field_selector, event_reasons_read
+    from nexus_supervisor_amd.parallel.sharding import watch_field_selector
+    from nexus_supervisor_amd.parallel.watchhub import WatchHub
+
+    sel = event_field_selector()
+    read = event_reasons_read()
+    assert sel and all(f"reason!={r}" in sel.split(",") for r in EVENT_NOISE_REASONS if r not in read)
+    assert not any(t.split("!=")[1] in read for t in sel.split(","))
+    assert watch_field_selector(_cfg(), "Pod") == "" and watch_field_selector(_cfg(), "Event") == sel
+    assert watch_field_selector(_cfg(**{"informer-event-noise-selector": False}), "Event") == ""
+    hub = WatchHub(_cfg(), None, 1, send=lambda *a: None, buffered=lambda w: 0, drain=lambda w: None)
+    assert hub._path_params("Event")[1]["fieldSelector"] == sel
+    assert "fieldSelector" not in hub._path_params("Pod")[1]
+
+    kept = ["Started", "BackOff", "Failed", "FailedScheduling", "OutOfamd.com/gpu", "Evicted", "SomethingNew"]
+    noise = list(EVENT_NOISE_REASONS)
+
+    async def go():
+        with KubeSim() as sim:
+            ctl = SimControl(sim.url)
+            c = KubeClient(KubeConfig(sim.url))
+            await ctl.apply([("ADDED", make_event("Pod", f"p{i}", r)) for i, r in enumerate(kept[:3] + noise[:4])])
+            lw = build_factory(_cfg(), c)._lw_for("Event")  # the single-process replica's Event source
+            assert isinstance(lw, KubeListWatch) and lw.field_selector == sel
+            items, rv = await lw.list()
+            assert sorted(i["reason"] for i in items) == sorted(kept[:3])
+            seen = []
+
+            async def watch():
+                async for t, o in lw.watch(rv):
+                    seen.append(o["reason"])
+
+            task = asyncio.ensure_future(watch())
+            await asyncio.sleep(0.2)
+            await ctl.apply([("ADDED", make_event("Pod", f"q{i}", r)) for i, r in enumerate(noise + kept[3:])])
+            for _ in range(100):
+                if len(seen) >= len(kept) - 3:
+                    break
+                await asyncio.sleep(0.05)
+            await asyncio.sleep(0.2)
+            task.cancel()
+            await asyncio.gather(task, return_exceptions=True)
+            assert sorted(seen) == sorted(kept[3:])
+            await c.close()
+            await ctl.close()
+
+    arun(go(), timeout=60)
+
+
 def test_resource_versions_spliced_consistently(arun):
     """Fully-formed objects are stored by splicing the new resourceVersion into the client's
     text (no re-serialisation): every stored / streamed copy must still be valid JSON with

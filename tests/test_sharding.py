@@ -375,7 +375,12 @@ def test_shard_leases_with_worker_processes_and_watch_hub(arun, tmp_path):
                 cfg = _cfg(ident, {"cql-store-type": "scylla", "kube-config-path": str(kc),
                                    "scylla-cql-store": {"hosts": f"127.0.0.1:{srv.port}"},
                                    "runtime": {"worker-processes": 2},
-                                   "sharding": {"shards": 2, "mode": "lease", "replicas": 2}})
+                                   "sharding": {"shards": 2, "mode": "lease", "replicas": 2},
+                                   # leases long enough that a loaded host (the worker processes
+                                   # and xdist peers) does not lapse them mid-test: each lapse
+                                   # re-lists both hubs and the runs wait on the new owner
+                                   "leader-election": {"identity": ident, "lease-duration": _ms(2400),
+                                                       "renew-deadline": _ms(1600), "retry-period": _ms(200)}})
                 app = ShardedApplication(cfg)
                 await app.start()
                 apps[ident] = app
