@@ -137,12 +137,12 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-BENCH_WORKERS_KNEE = 6
+BENCH_WORKERS_KNEE = 7
 
 
 def auto_procs(local_world: int) -> int:
     """Shard-worker processes per replica: the rank's CPU share minus 4 (simulated
-    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 6].
+    apiserver, CQL server, bench driver + watch hub, cluster process), within [1, 7].
 
     The rule, measured: add workers while they buy throughput the box resolves without
     raising the CPU per failure, and keep the single-threaded apiserver simulator clear of
@@ -155,7 +155,11 @@ def auto_procs(local_world: int) -> int:
     (profiles/r3_cpu_ab/, profiles/r4_sweep/): past six the CPU per failure rises 15-40 %
     while the throughput gain stays inside the box-to-box spread.  On the compiled hot path
     (profiles/r4_procs_ab_compiled/, same box, interleaved, probe on): 6 workers 38.5k at
-    115 µs, 8 workers 42.3k at 145 µs — +10 % throughput for +26 % CPU per failure."""
+    115 µs, 8 workers 42.3k at 145 µs — +10 % throughput for +26 % CPU per failure.
+    Round 6, lifecycle workload, the Event watch's noise selector and NUMA placement
+    (profiles/r6/bench_r6{p,q,r}_*, interleaved on three boxes, probe off): 6 workers 21.4-22.9k
+    at 251-268 µs, 7 workers 23.2-24.1k at 257-261 µs (+6 %), 8 workers 22.5-24.2k at 249-271 µs
+    with the workers at 0.68-0.72 of a core — past seven the simulator paces the line."""
     from nexus_supervisor_amd.utils.cpus import cpu_share
 
     return max(1, min(BENCH_WORKERS_KNEE, int(cpu_share() / max(local_world, 1)) - 4))
