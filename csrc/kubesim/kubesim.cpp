@@ -94,7 +94,8 @@ namespace {
 // ------------------------------------------------------------ CPU sampler (diagnostics)
 // NEXUS_KUBESIM_PROF=<file>: SIGPROF every 1 ms of process CPU time records the stack;
 // at exit every sample is written as "module+offset" frames (leaf first), one line per
-// sample, for tools/native_prof.py to symbolise.  Off unless the variable is set.
+// sample, for tools/native_prof.py to symbolise (the last 128k samples: older ones are
+// overwritten).  Off unless the variable is set.
 namespace prof {
 constexpr int kMaxSamples = 1 << 17;
 constexpr int kDepth = 12;
@@ -106,8 +107,8 @@ pthread_t g_loop;
 std::string g_path;
 
 void on_sigprof(int) {
-  int i = g_n.fetch_add(1, std::memory_order_relaxed);
-  if (i >= kMaxSamples) return;
+  // a ring: a long run keeps its last kMaxSamples samples (the timed steps, not the setup)
+  int i = g_n.fetch_add(1, std::memory_order_relaxed) & (kMaxSamples - 1);
   g_helper[i] = pthread_equal(pthread_self(), g_loop) ? 0 : 1;
   g_depth[i] = static_cast<unsigned char>(backtrace(g_frames[i], kDepth));
 }
