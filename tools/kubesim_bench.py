@@ -111,7 +111,7 @@ async def main(argv=None):
                       "threads": st.get("threads"),
                       "wall_s": round(t1 - t0, 2), "watch_bytes": counter[0], "watchers_per_kind": args.watchers,
                       "sim": {k: st.get(k) for k in ("requests", "deleted", "applied", "sends")},
-                      "us_per_failure": {k[:-3]: round((st.get(k, 0) - st0.get(k, 0)) / 1000 / n, 2) for k in st if k.endswith("_ns")}}))
+                      "us_per_failure": {k[:-3]: round((st.get(k, 0) - st0.get(k, 0)) / 1000 / n, 2) for k in st if k.endswith("_ns") and isinstance(st[k], (int, float))}}))
 
 
 if __name__ == "__main__":
