@@ -45,6 +45,10 @@ from aiohttp import web
 # event loop, so a whole 20k-line step in one request would hold every watch flush, Job
 # DELETE and pods/log answer for its duration (tens of ms); chunks interleave with them
 APPLY_CHUNK = int(os.environ.get("NEXUS_BENCH_APPLY_CHUNK", "1024"))
+# chunks sent ahead of their answers on the generator's apply connection (HTTP/1.1
+# pipelining; 1 = one request per round trip): the apply port then never idles between two
+# chunks of a step waiting for this process to read an answer and send the next
+APPLY_DEPTH = int(os.environ.get("NEXUS_BENCH_APPLY_DEPTH", "3"))
 
 
 async def amain(args) -> None:
@@ -69,6 +73,9 @@ async def amain(args) -> None:
 
     async def apply_chunks(bodies):
         """Apply pre-encoded chunks in order; the step's push time is the first commit."""
+        if APPLY_DEPTH > 1:
+            docs = await simctl.apply_pipelined(list(bodies), APPLY_DEPTH)
+            return docs[0]["t_push"] if docs else time.monotonic()
         t = None
         for b in bodies:
             doc = await simctl.apply_raw(b)
@@ -78,11 +85,8 @@ async def amain(args) -> None:
     async def apply(events):
         """Commit watch traffic to the API server; returns the commit (push) time."""
         if simctl is not None:
-            t = None
-            for i in range(0, len(events), APPLY_CHUNK):
-                doc = await simctl.apply(events[i:i + APPLY_CHUNK])
-                t = doc["t_push"] if t is None else t
-            return t if t is not None else time.monotonic()
+            return await apply_chunks([encode_events(events[i:i + APPLY_CHUNK])
+                                       for i in range(0, len(events), APPLY_CHUNK)])
         t = time.monotonic()
         for i, (etype, obj) in enumerate(events):
             api.apply(etype, obj, copy_obj=False)

@@ -136,6 +136,7 @@ class SimControl:
         self.url = url.rstrip("/")
         self.apply_url = (apply_url or url).rstrip("/")
         self._s = None
+        self._streams: List[Any] = []  # idle pipelined apply connections: (reader, writer)
 
     async def _session(self):
         if self._s is None:
@@ -165,6 +166,55 @@ class SimControl:
                 raise RuntimeError(f"/sim/apply: {r.status} {doc}")
             return doc
 
+    async def apply_pipelined(self, bodies: List[bytes], depth: int = 3) -> List[Dict[str, Any]]:
+        """``apply_raw`` for every body, in order, over one keep-alive connection with up to
+        ``depth`` requests sent ahead of their answers (HTTP/1.1 pipelining).  The apply port
+        reads a connection's requests one after another, so the order of commits is the
+        order of ``bodies``; what pipelining removes is the port idling on the generator's
+        round trip between two chunks of a step.  Returns each body's answer."""
+        import asyncio
+
+        if not bodies:
+            return []
+        if self._streams:  # one call owns a connection: concurrent callers (slots) never share one
+            reader, writer = self._streams.pop()
+        else:
+            host, port = self.apply_url.split("//", 1)[1].rsplit(":", 1)
+            reader, writer = await asyncio.open_connection(host, int(port))
+        head = b"POST /sim/apply HTTP/1.1\r\nHost: sim\r\nContent-Type: application/x-ndjson\r\nContent-Length: %d\r\n\r\n"
+        out: List[Dict[str, Any]] = []
+        sent = 0
+        try:
+            while sent < min(depth, len(bodies)):
+                writer.write(head % len(bodies[sent]))
+                writer.write(bodies[sent])
+                sent += 1
+            await writer.drain()
+            for _ in range(len(bodies)):
+                hdr = await reader.readuntil(b"\r\n\r\n")
+                status = int(hdr.split(b" ", 2)[1])
+                clen = 0
+                for ln in hdr.split(b"\r\n")[1:]:
+                    k, _, v = ln.partition(b":")
+                    if k.strip().lower() == b"content-length":
+                        clen = int(v)
+                doc = json.loads(await reader.readexactly(clen)) if clen else {}
+                if status != 200:
+                    raise RuntimeError(f"/sim/apply: {status} {doc}")
+                out.append(doc)
+                if sent < len(bodies):
+                    writer.write(head % len(bodies[sent]))
+                    writer.write(bodies[sent])
+                    sent += 1
+                    await writer.drain()
+        except BaseException:
+            # a broken or abandoned exchange: answers still owed on this connection would
+            # be read as the next call's
+            writer.close()
+            raise
+        self._streams.append((reader, writer))
+        return out
+
     async def _post(self, path: str, kind: str = "") -> None:
         s = await self._session()
         async with s.post(self.url + path, params={"kind": kind} if kind else None) as r:
@@ -185,3 +235,6 @@ class SimControl:
         if self._s is not None:
             await self._s.close()
             self._s = None
+        for _, writer in self._streams:
+            writer.close()
+        self._streams.clear()

@@ -183,6 +183,48 @@ def test_event_noise_selector_on_list_and_watch(arun):
     arun(go(), timeout=60)
 
 
+def test_pipelined_applies_commit_in_order(arun):
+    """``SimControl.apply_pipelined``: chunks sent ahead of their answers on one apply
+    connection commit in the order given (a watch sees ADDED, MODIFIED, DELETED, ADDED of
+    one pod in that order), and concurrent callers each get a connection of their own."""
+    from nexus_supervisor_amd.testing.kubesim import encode_events
+
+    async def go():
+        labels = _cfg().labels
+        with KubeSim(apply_threads=2) as sim:
+            ctl = SimControl(sim.url, sim.apply_url)
+            c = KubeClient(KubeConfig(sim.url))
+            rv = str((await ctl.stats())["rv"])
+            seen = []
+
+            async def watch():
+                async for t, o in c.watch("Pod", "nexus", rv, timeout_seconds=10):
+                    seen.append((t, o["metadata"]["name"], (o.get("status") or {}).get("phase")))
+
+            task = asyncio.ensure_future(watch())
+            await asyncio.sleep(0.2)
+            p = make_pod("x", labels)
+            q = dict(p, status={"phase": "Failed"})
+            others = [[encode_events([("ADDED", make_pod(f"o{k}-{i}", labels))]) for i in range(20)] for k in range(2)]
+            bodies = [encode_events(b) for b in ([("ADDED", p)], [("MODIFIED", q)], [("DELETED", q)], [("ADDED", p)])]
+            docs, *rest = await asyncio.gather(ctl.apply_pipelined(bodies, depth=3),
+                                               *(ctl.apply_pipelined(o, depth=4) for o in others))
+            assert [d["applied"] for d in docs] == [1, 1, 1, 1] and all(len(r) == 20 for r in rest)
+            assert len(ctl._streams) >= 2  # the concurrent calls did not share a connection
+            for _ in range(100):
+                if len(seen) >= 4 + 40:
+                    break
+                await asyncio.sleep(0.05)
+            task.cancel()
+            await asyncio.gather(task, return_exceptions=True)
+            mine = [(t, ph) for t, n, ph in seen if n == p["metadata"]["name"]]
+            assert [t for t, _ in mine] == ["ADDED", "MODIFIED", "DELETED", "ADDED"]
+            await c.close()
+            await ctl.close()
+
+    arun(go(), timeout=60)
+
+
 def test_resource_versions_spliced_consistently(arun):
     """Fully-formed objects are stored by splicing the new resourceVersion into the client's
     text (no re-serialisation): every stored / streamed copy must still be valid JSON with
