@@ -20,6 +20,8 @@
 //   PATCH  …/{plural}/{name}          JSON merge patch
 //   DELETE …/{plural}/{name}          delete; Background/Foreground propagation deletes the
 //                                      Job's pods (batch.kubernetes.io/job-name) like the GC
+//                                      (--async-gc: Background's pods after the answer, on a
+//                                      GC thread, as kube-controller-manager's GC does)
 //   POST   /sim/apply[?expire=1]      bulk NDJSON {"type": ADDED|MODIFIED|DELETED, "object": …}
 //                                      (the benchmark's cluster generator); answers the
 //                                      CLOCK_MONOTONIC commit time of the batch; expire=1
@@ -178,6 +180,11 @@ struct Options {
   // <root>/<ns>_<pod>_<uid>/<container>/<restart>.log in the CRI format, for a node agent
   // process reading the node's logs (the deployed default-pod path); empty = off
   std::string log_root;
+  // Background propagation as the kube-controller-manager's garbage collector does it: the
+  // Job DELETE is answered at once and the Job's pods are deleted afterwards, on a GC thread
+  // of the simulator's (the loop then answers DELETEs without the pod cascade); off = the
+  // pods go inside the DELETE, before its answer
+  bool async_gc = false;
 } g_opt;
 
 int64_t mono_ns() {
@@ -643,6 +650,10 @@ std::atomic<int64_t> g_rv{1000};
 // commits a bulk apply: both take g_store_mu for every touch.  The loop holds it while it
 // handles requests and timers, never across epoll_wait, recv or a watch's sendmsg.
 std::mutex g_store_mu;
+// --async-gc: pods of Jobs deleted with Background propagation, (namespace, name), waiting for
+// the GC thread; guarded by g_store_mu
+std::deque<std::pair<std::string, std::string>> g_gc;
+std::condition_variable g_gc_cv;
 
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, applied = 0, throttled = 0, delayed = 0;
@@ -654,6 +665,8 @@ struct Stats {
   int64_t prepare_ns = 0;  // the parallel part of apply_ns (wall time)
   int64_t store_ns = 0;    // time g_store_mu was held (loop + apply thread): the serial part
   std::atomic<int64_t> apply_thread_ns{0};  // the apply port's busy time (reading, applying), all connections
+  int64_t gc_ns = 0;   // the GC thread's busy time (--async-gc; under the store lock)
+  uint64_t gc_pods = 0;
   uint64_t commit_parallel = 0;  // bulk-apply chunks committed per kind on threads
 } g_stats;
 
@@ -1373,7 +1386,12 @@ bool remove(int kind, std::string_view ns, std::string_view name, std::string_vi
       // take the job's pod set out of the index (the pods' own unindexing then finds
       // nothing to do) instead of copying every name
       auto node = g_pods_by_job.extract(pit);
-      for (auto& p : node.mapped()) remove(K_POD, o.ns, p, propagation);
+      if (g_opt.async_gc && propagation == "Background") {
+        for (auto& p : node.mapped()) g_gc.emplace_back(o.ns, p);
+        g_gc_cv.notify_one();
+      } else {
+        for (auto& p : node.mapped()) remove(K_POD, o.ns, p, propagation);
+      }
     }
   }
   return true;
@@ -2091,6 +2109,8 @@ void handle(Conn& c, Request& r) {
                       ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
                       ",\"store_ns\":" + std::to_string(g_stats.store_ns) +
                       ",\"apply_thread_ns\":" + std::to_string(g_stats.apply_thread_ns.load()) +
+                      ",\"gc_ns\":" + std::to_string(g_stats.gc_ns) + ",\"gc_pods\":" + std::to_string(g_stats.gc_pods) +
+                      ",\"gc_pending\":" + std::to_string(g_gc.size()) +
                       ",\"apply_conn_ns\":{";
       {
         std::lock_guard<std::mutex> lk(g_apply_conn_mu);
@@ -2300,6 +2320,32 @@ void on_signal(int) { g_stop.store(1); }
 // takes the store lock.  The loop port still accepts /sim/apply (on the loop).
 int g_wake_fd = -1;  // eventfd: an apply committed watch lines the loop must send
 
+// --async-gc: deletes the queued pods of Background-deleted Jobs, up to 256 per hold of the
+// store lock (the loop and the apply port get it between batches), then wakes the loop to
+// send the DELETED lines
+void gc_thread() {
+  std::unique_lock<std::mutex> lk(g_store_mu);
+  while (!g_stop) {
+    if (g_gc.empty()) {
+      g_gc_cv.wait_for(lk, std::chrono::milliseconds(100));
+      continue;
+    }
+    int64_t t0 = mono_ns();
+    for (int n = 0; n < 256 && !g_gc.empty(); ++n) {
+      std::pair<std::string, std::string> p = std::move(g_gc.front());
+      g_gc.pop_front();
+      if (remove(K_POD, p.first, p.second, "Background")) ++g_stats.gc_pods;
+    }
+    int64_t dt = mono_ns() - t0;
+    g_stats.gc_ns += dt;
+    g_stats.store_ns += dt;
+    lk.unlock();
+    uint64_t one = 1;
+    if (write(g_wake_fd, &one, sizeof one) < 0) { /* the loop wakes within 100 ms anyway */ }
+    lk.lock();
+  }
+}
+
 void apply_conn(int fd) {
   const int conn_id = ++g_apply_conn_seq;
   std::string in;
@@ -2397,7 +2443,7 @@ void apply_server(int afd) {
 void usage() {
   fprintf(stderr,
           "nexus-kubesim [--host H] [--port P] [--ready-file F] [--history N] [--bookmark-ms MS] [--token T]\n"
-          "              [--flush-threads N] [--apply-threads N] [--api-latency-us US] [--write-qps Q] [--write-burst B]\n"
+          "              [--flush-threads N] [--apply-threads N] [--async-gc] [--api-latency-us US] [--write-qps Q] [--write-burst B]\n"
           "              [--throttle-deletes N] [--retry-after S] [--log-root DIR]\n");
 }
 
@@ -2422,6 +2468,7 @@ int main(int argc, char** argv) {
     else if (a == "--token") g_opt.token = next();
     else if (a == "--flush-threads") g_opt.flush_threads = std::max(1, atoi(next().c_str()));
     else if (a == "--apply-threads") g_opt.apply_threads = std::max(1, std::min(16, atoi(next().c_str())));
+    else if (a == "--async-gc") g_opt.async_gc = true;
     else if (a == "--api-latency-us") g_opt.api_latency_us = std::max(0L, atol(next().c_str()));
     else if (a == "--write-qps") g_opt.write_qps = atof(next().c_str());
     else if (a == "--write-burst") g_opt.write_burst = atoi(next().c_str());
@@ -2530,6 +2577,8 @@ int main(int argc, char** argv) {
   g_flush_pool.start(g_opt.flush_threads);
   g_apply_pool.start(g_opt.apply_threads);
   std::thread(apply_server, afd).detach();
+  std::thread gc;
+  if (g_opt.async_gc) gc = std::thread(gc_thread);
   std::vector<epoll_event> evs(512);
   int64_t last_tick = mono_ms();
   char buf[1 << 16];
@@ -2653,6 +2702,10 @@ int main(int argc, char** argv) {
   }
   g_flush_pool.stop();
   g_apply_pool.stop();
+  if (gc.joinable()) {
+    g_gc_cv.notify_all();
+    gc.join();
+  }
   for (auto& kv : g_conns) close(kv.first);
   close(lfd);
   prof::dump();

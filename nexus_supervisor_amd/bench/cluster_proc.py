@@ -66,7 +66,10 @@ async def amain(args) -> None:
                       write_qps=args.write_qps, write_burst=args.write_burst,
                       prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "768")),
                       apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "6")),
-                      log_root=args.log_root).start()
+                      log_root=args.log_root,
+                      # Job DELETEs answered before their pods go, as a real API server does (its
+                      # GC deletes them afterwards): the pod cascade is off the simulator's loop
+                      async_gc=os.environ.get("NEXUS_KUBESIM_ASYNC_GC", "1") == "1").start()
         simctl = SimControl(sim.url, sim.apply_url)
     else:
         api = FakeApiServer(history=args.history, bookmark_interval=2.0)

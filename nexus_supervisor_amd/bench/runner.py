@@ -555,7 +555,7 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 # its apply port's, and the store lock's hold time (the loop and the apply port
                 # both commit under it) — the largest is what saturates first
                 share = {k: round((s1.get(f"{k}_ns", 0) - s0.get(f"{k}_ns", 0)) / 1e9 / elapsed, 3)
-                         for k in ("busy", "apply_thread", "store")}
+                         for k in _SIM_SERIAL if k != "gc" or "gc_ns" in s1}
                 c0, c1 = s0.get("apply_conn_ns"), s1.get("apply_conn_ns")
                 if c1:
                     # each apply connection is one thread: the busiest one is the serial part
@@ -564,6 +564,8 @@ async def run_rank(cfg: BenchConfig, barrier_sync: Callable[[], None],
                 cpu["kubesim_loop_util"] = share["busy"]
                 cpu["kubesim_apply_port_util"] = share["apply_thread"]
                 cpu["kubesim_store_util"] = share["store"]
+                if "gc" in share:  # --async-gc: the GC thread deleting the Jobs' pods
+                    cpu["kubesim_gc_util"] = share["gc"]
                 cpu["kubesim_serial_util"] = max(share.values())
         if getattr(harness, "cql_shards", None):
             cpu["cqlsrv_shards"] = harness.cql_shards
@@ -802,7 +804,7 @@ def _by_kind(timed, kinds: Dict[str, str], part_of: Dict[str, Tuple[float, ...]]
     return out
 
 
-_SIM_SERIAL = ("busy", "apply_thread", "store")  # the simulator's single-thread parts (/sim/stats)
+_SIM_SERIAL = ("busy", "apply_thread", "store", "gc")  # the simulator's single-thread parts (/sim/stats)
 _PACING_KEYS = ("parent", "cluster", "cqlsrv", "kubesim") + tuple(f"kubesim_{k}" for k in _SIM_SERIAL)
 
 

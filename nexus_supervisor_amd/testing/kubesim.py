@@ -37,7 +37,7 @@ class KubeSim:
     def __init__(self, *, host: str = "127.0.0.1", port: int = 0, history: int = 400_000, bookmark_ms: int = 1000,
                  token: str = "", flush_threads: int = 1, api_latency_us: int = 0, write_qps: float = 0.0,
                  write_burst: int = 0, throttle_deletes: int = 0, retry_after: int = 1, prefault_mb: int = 0,
-                 apply_threads: int = 1, log_root: str = ""):
+                 apply_threads: int = 1, log_root: str = "", async_gc: bool = False):
         from .._build import binary
 
         self.exe = os.environ.get("NEXUS_KUBESIM_BINARY") or binary("nexus-kubesim")
@@ -52,6 +52,8 @@ class KubeSim:
         self.prefault_mb = prefault_mb  # heap grown and touched at startup (benchmarks)
         self.apply_threads = apply_threads  # threads preparing a /sim/apply chunk's lines
         self.log_root = log_root  # a kubelet's /var/log/pods the LOG lines are also written to
+        # a Background Job DELETE is answered before its pods go (the GC deletes them after)
+        self.async_gc = async_gc
         self.proc: Optional[subprocess.Popen] = None
         self.log_path = os.path.join(self.dir, "server.log")
         self.url = ""
@@ -75,6 +77,8 @@ class KubeSim:
             argv += ["--api-latency-us", str(int(self.api_latency_us))]
         if self.log_root:
             argv += ["--log-root", self.log_root]
+        if self.async_gc:
+            argv += ["--async-gc"]
         if self.write_qps:
             argv += ["--write-qps", str(self.write_qps), "--write-burst", str(int(self.write_burst))]
         if self.throttle_deletes:

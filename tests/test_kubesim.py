@@ -225,6 +225,48 @@ def test_pipelined_applies_commit_in_order(arun):
     arun(go(), timeout=60)
 
 
+def test_async_gc_deletes_a_jobs_pods_after_the_answer(arun):
+    """``--async-gc``: a Background Job DELETE is answered at once and the Job's pods are
+    deleted afterwards on the GC thread (watchers see their DELETED lines); Foreground still
+    deletes the pods before the answer."""
+    async def go():
+        labels = _cfg().labels
+        with KubeSim(async_gc=True) as sim:
+            ctl = SimControl(sim.url)
+            await ctl.apply([("ADDED", o) for r in ("g1", "g2") for o in (make_job(r, labels), make_pod(r, labels))])
+            c = KubeClient(KubeConfig(sim.url))
+            rv = str((await ctl.stats())["rv"])
+            seen = []
+
+            async def watch():
+                async for t, o in c.watch("Pod", "nexus", rv, timeout_seconds=10):
+                    seen.append((t, o["metadata"]["name"]))
+
+            task = asyncio.ensure_future(watch())
+            await asyncio.sleep(0.2)
+            await c.delete_job("nexus", "g1")  # Background
+            for _ in range(100):
+                if ("DELETED", "g1-acdey") in seen:
+                    break
+                await asyncio.sleep(0.02)
+            assert ("DELETED", "g1-acdey") in seen
+            with pytest.raises(NotFound):
+                await c.get("Pod", "nexus", "g1-acdey")
+            st = await ctl.stats()
+            assert st["gc_pods"] == 1 and st["gc_pending"] == 0 and st["gc_ns"] > 0
+            await c.request("DELETE", "/apis/batch/v1/namespaces/nexus/jobs/g2",
+                            body={"kind": "DeleteOptions", "apiVersion": "v1", "propagationPolicy": "Foreground"})
+            with pytest.raises(NotFound):  # gone before the answer
+                await c.get("Pod", "nexus", "g2-acdey")
+            assert (await ctl.stats())["gc_pods"] == 1
+            task.cancel()
+            await asyncio.gather(task, return_exceptions=True)
+            await c.close()
+            await ctl.close()
+
+    arun(go(), timeout=60)
+
+
 def test_resource_versions_spliced_consistently(arun):
     """Fully-formed objects are stored by splicing the new resourceVersion into the client's
     text (no re-serialisation): every stored / streamed copy must still be valid JSON with

@@ -230,7 +230,8 @@ def test_inprocess_extensions_under_sanitizer(sanitize):
 def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
     """``nexus-kubesim`` with apply and fan-out threads: bulk applies of the lifecycle
     workload (lines prepared on threads, kinds committed on threads) while three watches
-    stream and Job DELETEs cascade to their pods on another connection."""
+    stream and Job DELETEs cascade to their pods on another connection (on the GC thread:
+    ``--async-gc``, as the bench runs it)."""
     from nexus_supervisor_amd.bench.workload import Workload
     from nexus_supervisor_amd.kube.client import KubeClient, KubeConfig
     from nexus_supervisor_amd.testing.kubesim import KubeSim, SimControl, encode_events
@@ -238,7 +239,7 @@ def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
     _sanitized(sanitize)
     os.environ["NEXUS_KUBESIM_BINARY"] = os.path.join(_build.BIN, f"nexus-kubesim-{sanitize}")
     try:
-        sim = KubeSim(apply_threads=4, flush_threads=2, history=20_000).start(timeout=30)
+        sim = KubeSim(apply_threads=4, flush_threads=2, history=20_000, async_gc=True).start(timeout=30)
     finally:
         os.environ.pop("NEXUS_KUBESIM_BINARY", None)
     try:
@@ -262,7 +263,8 @@ def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
                 st = wl.step(60)
                 body = encode_events([(t, o) for t, o in st.traffic])
                 lines += body.count(b"\n")
-                await ctl.apply_raw(body)
+                await ctl.apply_pipelined([body[:body.index(b"\n", len(body) // 2) + 1],
+                                           body[body.index(b"\n", len(body) // 2) + 1:]])
                 await asyncio.gather(*(kc.delete_job("nexus", rid) for rid in st.failed))
             for _ in range(200):
                 if seen["Event"] and seen["Pod"] and seen["Job"]:
@@ -284,3 +286,4 @@ def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
     assert not any(r in log for r in _REPORTS), log[-4000:]
     assert all(seen.values()), seen
     assert stats.get("commit_parallel", 0) > 0, stats  # the kinds were committed on threads
+    assert stats.get("gc_pods", 0) > 0, stats  # the deleted Jobs' pods went on the GC thread
