@@ -654,6 +654,9 @@ std::mutex g_store_mu;
 // the GC thread; guarded by g_store_mu
 std::deque<std::pair<std::string, std::string>> g_gc;
 std::condition_variable g_gc_cv;
+// --async-gc: removed objects (their strings, attrs and text references), destroyed on the GC
+// thread outside the lock — the loop answers a Job DELETE without freeing the Job
+std::vector<Obj> g_graves;
 
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, applied = 0, throttled = 0, delayed = 0;
@@ -665,7 +668,7 @@ struct Stats {
   int64_t prepare_ns = 0;  // the parallel part of apply_ns (wall time)
   int64_t store_ns = 0;    // time g_store_mu was held (loop + apply thread): the serial part
   std::atomic<int64_t> apply_thread_ns{0};  // the apply port's busy time (reading, applying), all connections
-  int64_t gc_ns = 0;   // the GC thread's busy time (--async-gc; under the store lock)
+  std::atomic<int64_t> gc_ns{0};  // the GC thread's busy time (--async-gc: pod deletions + frees)
   uint64_t gc_pods = 0;
   uint64_t commit_parallel = 0;  // bulk-apply chunks committed per kind on threads
 } g_stats;
@@ -1394,6 +1397,10 @@ bool remove(int kind, std::string_view ns, std::string_view name, std::string_vi
       }
     }
   }
+  if (g_opt.async_gc) {
+    g_graves.push_back(std::move(o));
+    if (g_graves.size() >= 1024) g_gc_cv.notify_one();
+  }
   return true;
 }
 
@@ -2109,7 +2116,7 @@ void handle(Conn& c, Request& r) {
                       ",\"busy_ns\":" + std::to_string(g_stats.busy_ns) +
                       ",\"store_ns\":" + std::to_string(g_stats.store_ns) +
                       ",\"apply_thread_ns\":" + std::to_string(g_stats.apply_thread_ns.load()) +
-                      ",\"gc_ns\":" + std::to_string(g_stats.gc_ns) + ",\"gc_pods\":" + std::to_string(g_stats.gc_pods) +
+                      ",\"gc_ns\":" + std::to_string(g_stats.gc_ns.load()) + ",\"gc_pods\":" + std::to_string(g_stats.gc_pods) +
                       ",\"gc_pending\":" + std::to_string(g_gc.size()) +
                       ",\"apply_conn_ns\":{";
       {
@@ -2325,23 +2332,29 @@ int g_wake_fd = -1;  // eventfd: an apply committed watch lines the loop must se
 // send the DELETED lines
 void gc_thread() {
   std::unique_lock<std::mutex> lk(g_store_mu);
+  std::vector<Obj> dead;
   while (!g_stop) {
-    if (g_gc.empty()) {
+    if (g_gc.empty() && g_graves.size() < 1024) {
       g_gc_cv.wait_for(lk, std::chrono::milliseconds(100));
-      continue;
+      if (g_gc.empty() && g_graves.empty()) continue;
     }
     int64_t t0 = mono_ns();
+    bool removed = !g_gc.empty();
     for (int n = 0; n < 256 && !g_gc.empty(); ++n) {
       std::pair<std::string, std::string> p = std::move(g_gc.front());
       g_gc.pop_front();
       if (remove(K_POD, p.first, p.second, "Background")) ++g_stats.gc_pods;
     }
-    int64_t dt = mono_ns() - t0;
-    g_stats.gc_ns += dt;
-    g_stats.store_ns += dt;
+    dead.swap(g_graves);
+    int64_t t1 = mono_ns();
+    g_stats.store_ns += t1 - t0;
     lk.unlock();
-    uint64_t one = 1;
-    if (write(g_wake_fd, &one, sizeof one) < 0) { /* the loop wakes within 100 ms anyway */ }
+    if (removed) {
+      uint64_t one = 1;
+      if (write(g_wake_fd, &one, sizeof one) < 0) { /* the loop wakes within 100 ms anyway */ }
+    }
+    dead.clear();  // the frees, outside the store lock
+    g_stats.gc_ns += mono_ns() - t0;
     lk.lock();
   }
 }
