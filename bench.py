@@ -167,7 +167,7 @@ def auto_procs(local_world: int) -> int:
 
 def _harness_bound(cpu) -> dict:
     """Did a harness process limit the run?  The traffic generator by its CPU share, the
-    apiserver simulator by its busiest serial part (event loop, apply port, store lock), the
+    apiserver simulator by its busiest serial part (event loop, apply port, store lock, GC thread), the
     sharded CQL server by its per-shard CPU."""
     util = {k[:-5]: v for k, v in cpu.items() if k in ("kubesim_util", "cqlsrv_util", "cluster_util")}
     limit = dict(util)
@@ -175,7 +175,7 @@ def _harness_bound(cpu) -> dict:
         limit["cqlsrv"] = util["cqlsrv"] / max(1, int(cpu.get("cqlsrv_shards") or 1))
     if "kubesim" in limit and cpu.get("kubesim_serial_util") is not None:
         # the simulator is multi-threaded: its serial parts (event loop, apply port, store
-        # lock), not its process CPU, say whether it saturated
+        # lock, GC thread), not its process CPU, say whether it saturated
         limit["kubesim"] = cpu["kubesim_serial_util"]
     bound = any(v >= 0.9 for v in limit.values())
     out = {"bound": bound, "util": util, "limit_util": {k: round(v, 3) for k, v in limit.items()}}
