@@ -657,6 +657,10 @@ std::condition_variable g_gc_cv;
 // --async-gc: removed objects (their strings, attrs and text references), destroyed on the GC
 // thread outside the lock — the loop answers a Job DELETE without freeing the Job
 std::vector<Obj> g_graves;
+// remove() runs on the loop, the GC thread and a bulk apply's per-kind commit threads (those
+// two at once, under the one store lock the apply thread holds): the graves have a lock of
+// their own
+std::mutex g_graves_mu;
 
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, applied = 0, throttled = 0, delayed = 0;
@@ -1398,6 +1402,7 @@ bool remove(int kind, std::string_view ns, std::string_view name, std::string_vi
     }
   }
   if (g_opt.async_gc) {
+    std::lock_guard<std::mutex> glk(g_graves_mu);
     g_graves.push_back(std::move(o));
     if (g_graves.size() >= 1024) g_gc_cv.notify_one();
   }
@@ -2334,8 +2339,14 @@ void gc_thread() {
   std::unique_lock<std::mutex> lk(g_store_mu);
   std::vector<Obj> dead;
   while (!g_stop) {
-    if (g_gc.empty() && g_graves.size() < 1024) {
+    size_t graves;
+    {
+      std::lock_guard<std::mutex> glk(g_graves_mu);
+      graves = g_graves.size();
+    }
+    if (g_gc.empty() && graves < 1024) {
       g_gc_cv.wait_for(lk, std::chrono::milliseconds(100));
+      std::lock_guard<std::mutex> glk(g_graves_mu);
       if (g_gc.empty() && g_graves.empty()) continue;
     }
     int64_t t0 = mono_ns();
@@ -2345,7 +2356,10 @@ void gc_thread() {
       g_gc.pop_front();
       if (remove(K_POD, p.first, p.second, "Background")) ++g_stats.gc_pods;
     }
-    dead.swap(g_graves);
+    {
+      std::lock_guard<std::mutex> glk(g_graves_mu);
+      dead.swap(g_graves);
+    }
     int64_t t1 = mono_ns();
     g_stats.store_ns += t1 - t0;
     lk.unlock();
