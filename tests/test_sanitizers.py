@@ -239,7 +239,7 @@ def test_kubesim_threaded_apply_under_sanitizer(sanitize, arun):
     _sanitized(sanitize)
     os.environ["NEXUS_KUBESIM_BINARY"] = os.path.join(_build.BIN, f"nexus-kubesim-{sanitize}")
     try:
-        sim = KubeSim(apply_threads=4, flush_threads=2, history=20_000, async_gc=True).start(timeout=30)
+        sim = KubeSim(apply_threads=4, flush_threads=2, history=2_000, async_gc=True).start(timeout=30)  # history overflows: ring pops are buried
     finally:
         os.environ.pop("NEXUS_KUBESIM_BINARY", None)
     try:
