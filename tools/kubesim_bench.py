@@ -71,6 +71,7 @@ async def main(argv=None):
     ap.add_argument("--jobs", type=int, default=10_000)
     ap.add_argument("--watchers", type=int, default=1, help="watch streams per kind (replicas watching the namespace)")
     ap.add_argument("--flush-threads", type=int, default=0, help="simulator fan-out threads (0 = one per watcher, ≤ 8)")
+    ap.add_argument("--async-gc", action="store_true", help="the simulator's GC thread (as the bench runs it)")
     args = ap.parse_args(argv)
     wl = Workload(concurrent_jobs=args.jobs)
     objs, _ = wl.initial()
@@ -78,7 +79,7 @@ async def main(argv=None):
     bodies = [(failed, encode_events(traffic)) for failed, traffic, _ in steps]
     ft = args.flush_threads or max(1, min(8, args.watchers))
     with KubeSim(history=50_000, flush_threads=ft, prefault_mb=int(os.environ.get("NEXUS_KUBESIM_PREFAULT_MB", "0")),
-                 apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "1"))) as sim:
+                 apply_threads=int(os.environ.get("NEXUS_KUBESIM_APPLY_THREADS", "1")), async_gc=args.async_gc) as sim:
         host, port = sim.url.split("//")[1].split(":")
         port = int(port)
         ctl = SimControl(sim.url, sim.apply_url)
