@@ -657,24 +657,10 @@ std::condition_variable g_gc_cv;
 // --async-gc: removed objects (their strings, attrs and text references), destroyed on the GC
 // thread outside the lock — the loop answers a Job DELETE without freeing the Job
 std::vector<Obj> g_graves;
-// ... and watch-history entries that fell off the ring (often the last reference to an
-// object's text), likewise freed on the GC thread instead of under the store lock
-std::vector<Hist> g_hist_graves;
-// the loop, the GC thread and a bulk apply's per-kind commit threads (two at once, under the
-// one store lock the apply thread holds) all bury: the graves have a lock of their own, taken
-// once per 64 burials of a thread
+// remove() runs on the loop, the GC thread and a bulk apply's per-kind commit threads (those
+// two at once, under the one store lock the apply thread holds): the graves have a lock of
+// their own
 std::mutex g_graves_mu;
-
-template <typename T>
-void bury(T&& v, std::vector<T>& global) {
-  thread_local std::vector<T> batch;
-  batch.push_back(std::move(v));
-  if (batch.size() < 64) return;
-  std::lock_guard<std::mutex> glk(g_graves_mu);
-  for (auto& x : batch) global.push_back(std::move(x));
-  batch.clear();
-  if (global.size() >= 4096) g_gc_cv.notify_one();
-}
 
 struct Stats {
   uint64_t requests = 0, watch_requests = 0, applied = 0, throttled = 0, delayed = 0;
@@ -746,7 +732,6 @@ void record(int kind, const char* etype, const Obj& o, int64_t new_rv = 0) {
   ks.history.push_back(Hist{rv, o.ns, lp, o.attrs});
   while (ks.history.size() > g_opt.history) {
     ks.compacted = ks.history.front().rv;
-    if (g_opt.async_gc) bury(std::move(ks.history.front()), g_hist_graves);
     ks.history.pop_front();
   }
   for (Watch* w : ks.watchers)
@@ -1233,12 +1218,8 @@ bool commit(Prep& p) {
     index_pod(o, true);
   }
   record(p.kind, prev ? "MODIFIED" : "ADDED", o);
-  if (prev) {
-    if (g_opt.async_gc) bury(std::move(it->second), g_graves);  // the replaced version
-    it->second = std::move(o);
-  } else {
-    ks.objs.emplace(okey(p.r.ns, p.r.name), std::move(o));
-  }
+  if (prev) it->second = std::move(o);
+  else ks.objs.emplace(okey(p.r.ns, p.r.name), std::move(o));
   return true;
 }
 
@@ -1420,7 +1401,11 @@ bool remove(int kind, std::string_view ns, std::string_view name, std::string_vi
       }
     }
   }
-  if (g_opt.async_gc) bury(std::move(o), g_graves);
+  if (g_opt.async_gc) {
+    std::lock_guard<std::mutex> glk(g_graves_mu);
+    g_graves.push_back(std::move(o));
+    if (g_graves.size() >= 1024) g_gc_cv.notify_one();
+  }
   return true;
 }
 
@@ -2353,17 +2338,16 @@ int g_wake_fd = -1;  // eventfd: an apply committed watch lines the loop must se
 void gc_thread() {
   std::unique_lock<std::mutex> lk(g_store_mu);
   std::vector<Obj> dead;
-  std::vector<Hist> dead_hist;
   while (!g_stop) {
     size_t graves;
     {
       std::lock_guard<std::mutex> glk(g_graves_mu);
-      graves = g_graves.size() + g_hist_graves.size();
+      graves = g_graves.size();
     }
-    if (g_gc.empty() && graves < 4096) {
+    if (g_gc.empty() && graves < 1024) {
       g_gc_cv.wait_for(lk, std::chrono::milliseconds(100));
       std::lock_guard<std::mutex> glk(g_graves_mu);
-      if (g_gc.empty() && g_graves.empty() && g_hist_graves.empty()) continue;
+      if (g_gc.empty() && g_graves.empty()) continue;
     }
     int64_t t0 = mono_ns();
     bool removed = !g_gc.empty();
@@ -2375,7 +2359,6 @@ void gc_thread() {
     {
       std::lock_guard<std::mutex> glk(g_graves_mu);
       dead.swap(g_graves);
-      dead_hist.swap(g_hist_graves);
     }
     int64_t t1 = mono_ns();
     g_stats.store_ns += t1 - t0;
@@ -2385,7 +2368,6 @@ void gc_thread() {
       if (write(g_wake_fd, &one, sizeof one) < 0) { /* the loop wakes within 100 ms anyway */ }
     }
     dead.clear();  // the frees, outside the store lock
-    dead_hist.clear();
     g_stats.gc_ns += mono_ns() - t0;
     lk.lock();
   }
