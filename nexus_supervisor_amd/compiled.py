@@ -69,7 +69,6 @@ MODULES = (
     "nexus_supervisor_amd.store.base",
     "nexus_supervisor_amd.parallel.sharding",
     "nexus_supervisor_amd.parallel.workers",
-    "nexus_supervisor_amd.gpu.agent",  # the node agent: annotates every failed pod of its node
 )
 
 _LOADED: List[str] = []
