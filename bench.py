@@ -59,7 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--workers", type=int, default=256)
     ap.add_argument("--procs", type=int, default=0,
                     help="supervisor shard-worker processes per replica (runtime.worker-processes; wire transport); "
-                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 6 (the measured "
+                         "0 = auto: the rank's CPU share minus 4 for the harness, at most 7 (the measured "
                          "knee: auto_procs)")
     ap.add_argument("--inflight", type=int, default=4, help="steps pushed ahead of acknowledgement")
     ap.add_argument("--no-pregen", action="store_true",
